@@ -1,0 +1,394 @@
+/*
+ * koord_gpu.h — C-ABI of the MI355X batched Filter/Score engine for koord-scheduler.
+ *
+ * This is the drop-in boundary between the (Go) koord-scheduler plugins and the
+ * HIP engine.  Every entry point takes plain pointers and sizes; no torch / HIP
+ * types appear in the signatures (streams are passed as opaque `void*`).
+ *
+ * Which reference surface each entry replaces (paths relative to the reference
+ * repository PeterChg/koordinator @ 2025-01-12):
+ *
+ *   kg_engine_create        plugin construction: loadaware.New (pkg/scheduler/plugins/loadaware/load_aware.go:76-110),
+ *                           NodeResourcesFit (upstream k8s v1.24.15 noderesources.NewFit; profile
+ *                           config/manager/scheduler-config.yaml:17-31)
+ *   kg_build_pod_rows       PreFilter-time pod preprocessing: NodeResourcesFit computePodResourceRequest
+ *                           (in-repo mirror reservation/transformer.go:316-346), estimator.EstimatePod
+ *                           (loadaware/estimator/default_estimator.go:57-108), GetPodPriorityClassWithDefault
+ *                           (apis/extension/priority_utils.go:26-47), isDaemonSetPod (loadaware/helper.go:189-196)
+ *   kg_build_node_rows      snapshot ingest of NodeInfo + NodeMetric + podAssignCache: the node-only parts of
+ *                           LoadAware.Filter (load_aware.go:123-254) and LoadAware.Score (load_aware.go:269-376),
+ *                           EstimateNode (default_estimator.go:110-129)
+ *   kg_snapshot_upsert      informer/event feeders: podAssignCache.OnAdd/OnUpdate/OnDelete
+ *                           (loadaware/pod_assign_cache.go:82-117), upstream Cache.UpdateSnapshot
+ *   kg_eval                 per-(pod,node) hot loops: framework.FilterPlugin.Filter and ScorePlugin.Score of
+ *                           LoadAwareScheduling (load_aware.go:123, :269) and NodeResourcesFit (upstream
+ *                           fitsRequest / LeastAllocated), plus the per-pod max of upstream selectHost
+ *   kg_place                the sequential scheduling cycle (upstream scheduleOne → Filter → Score → selectHost →
+ *                           Reserve) for a queue of pods, with Reserve deltas of LoadAware.Reserve
+ *                           (load_aware.go:260-267) and NodeInfo.AddPod (mirror reservation/transformer.go:293-306)
+ *   kg_commit               one Reserve (AssumePod + LoadAware.Reserve) of a pod on a node
+ *
+ * Units follow k8s Quantity conversions used by the plugins: cpu-like resources
+ * (KG_RES_CPU) in milli-units (Quantity.MilliValue), every other resource in
+ * base units (Quantity.Value).  batch-cpu / mid-cpu are stored as their Value()
+ * (the reference encodes them in milli-cores already).
+ *
+ * Error model: every function returns kg_status (0 = ok, < 0 = error); the
+ * message of the last error of an engine is available from kg_last_error().
+ * Threading: one engine = one HIP stream; calls on one engine must be serialized
+ * by the caller (the Go side holds a mutex), results are plain host memory.
+ */
+#ifndef KOORD_GPU_H
+#define KOORD_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KG_ABI_VERSION 1
+
+/* ------------------------------------------------------------------ */
+/* status codes                                                          */
+/* ------------------------------------------------------------------ */
+typedef int32_t kg_status;
+#define KG_OK 0
+#define KG_ERR_INVALID_ARG (-1)
+#define KG_ERR_HIP (-2)
+#define KG_ERR_UNSUPPORTED (-3)
+#define KG_ERR_RANGE (-4)
+#define KG_ERR_STATE (-5)
+
+/* upstream framework.Code values used in filter results */
+#define KG_CODE_SUCCESS 0
+#define KG_CODE_ERROR 1
+#define KG_CODE_UNSCHEDULABLE 2
+#define KG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE 3
+
+/* ------------------------------------------------------------------ */
+/* resources                                                             */
+/* ------------------------------------------------------------------ */
+#define KG_NUM_RES 8
+enum kg_resource {
+    KG_RES_CPU = 0,               /* "cpu"                         MilliValue */
+    KG_RES_MEMORY = 1,            /* "memory"                      Value      */
+    KG_RES_EPHEMERAL_STORAGE = 2, /* "ephemeral-storage"           Value      */
+    KG_RES_BATCH_CPU = 3,         /* "kubernetes.io/batch-cpu"     Value      */
+    KG_RES_BATCH_MEMORY = 4,      /* "kubernetes.io/batch-memory"  Value      */
+    KG_RES_MID_CPU = 5,           /* "kubernetes.io/mid-cpu"       Value      */
+    KG_RES_MID_MEMORY = 6,        /* "kubernetes.io/mid-memory"    Value      */
+    KG_RES_EXTENDED = 7           /* one extended resource, e.g. "example.com/gpu" Value */
+};
+/* resources that upstream schedutil.IsScalarResourceName() treats as scalar */
+#define KG_SCALAR_RES_MASK 0xF8u
+
+/* A corev1.ResourceList restricted to the resources above: `present` is the
+ * key set (bit r ⇔ key r exists in the map), v[r] the converted value. */
+typedef struct kg_resource_list {
+    int64_t v[KG_NUM_RES];
+    uint32_t present;
+    uint32_t _pad;
+} kg_resource_list;
+
+/* ------------------------------------------------------------------ */
+/* enums                                                                 */
+/* ------------------------------------------------------------------ */
+enum kg_priority_class { /* apis/extension/priority.go:28-34 */
+    KG_PRIO_NONE = 0,
+    KG_PRIO_PROD = 1,
+    KG_PRIO_MID = 2,
+    KG_PRIO_BATCH = 3,
+    KG_PRIO_FREE = 4
+};
+enum kg_qos_class { /* apis/extension/qos.go */
+    KG_QOS_NONE = 0,
+    KG_QOS_LSE = 1,
+    KG_QOS_LSR = 2,
+    KG_QOS_LS = 3,
+    KG_QOS_BE = 4,
+    KG_QOS_SYSTEM = 5
+};
+enum kg_kube_qos { /* corev1.PodQOSClass */
+    KG_KUBE_QOS_UNSET = 0,
+    KG_KUBE_QOS_GUARANTEED = 1,
+    KG_KUBE_QOS_BURSTABLE = 2,
+    KG_KUBE_QOS_BESTEFFORT = 3
+};
+enum kg_aggregation_type { /* apis/extension AggregationType */
+    KG_AGG_UNSET = 0, /* "" */
+    KG_AGG_AVG = 1,
+    KG_AGG_P50 = 2,
+    KG_AGG_P90 = 3,
+    KG_AGG_P95 = 4,
+    KG_AGG_P99 = 5
+};
+#define KG_NUM_AGG_TYPES 6
+
+enum kg_scoring_strategy {
+    KG_STRATEGY_LEAST_ALLOCATED = 0,
+    KG_STRATEGY_MOST_ALLOCATED = 1
+};
+
+#define KG_PLUGIN_FIT 0x1u       /* NodeResourcesFit       */
+#define KG_PLUGIN_LOADAWARE 0x2u /* LoadAwareScheduling    */
+
+/* ------------------------------------------------------------------ */
+/* engine configuration = plugin args (pkg/scheduler/apis/config/types.go)  */
+/* ------------------------------------------------------------------ */
+typedef struct kg_config {
+    int32_t abi_version;       /* must be KG_ABI_VERSION */
+    uint32_t enabled_plugins;  /* KG_PLUGIN_* : enabled at Filter AND Score */
+    int32_t weight_fit;        /* profile score weight of NodeResourcesFit    */
+    int32_t weight_loadaware;  /* profile score weight of LoadAwareScheduling */
+
+    /* NodeResourcesFitArgs.ScoringStrategy (upstream v1.24.15) */
+    int32_t fit_strategy;                  /* kg_scoring_strategy */
+    int32_t _pad0;
+    int64_t fit_resource_weight[KG_NUM_RES]; /* 0 ⇔ resource not listed */
+
+    /* LoadAwareSchedulingArgs (types.go:30-76) */
+    int32_t la_filter_expired_node_metrics;   /* *FilterExpiredNodeMetrics (nil ⇒ 0) */
+    int32_t la_has_expiration;                /* NodeMetricExpirationSeconds != nil  */
+    int64_t la_expiration_seconds;
+    int64_t la_resource_weight[KG_NUM_RES];   /* ResourceWeights (0 ⇔ absent) */
+    int64_t la_scaling_factor[KG_NUM_RES];    /* EstimatedScalingFactors (missing key ⇒ 0) */
+    kg_resource_list la_usage_thresholds;     /* UsageThresholds */
+    kg_resource_list la_prod_usage_thresholds;/* ProdUsageThresholds */
+    int32_t la_score_according_prod_usage;    /* ScoreAccordingProdUsage */
+    int32_t la_has_aggregated;                /* Aggregated != nil */
+    kg_resource_list la_agg_usage_thresholds; /* Aggregated.UsageThresholds */
+    int32_t la_agg_usage_type;                /* Aggregated.UsageAggregationType */
+    int32_t la_agg_score_type;                /* Aggregated.ScoreAggregationType */
+    int64_t la_agg_usage_duration_ns;         /* Aggregated.UsageAggregatedDuration (0 ⇒ max) */
+    int64_t la_agg_score_duration_ns;         /* Aggregated.ScoreAggregatedDuration (0 ⇒ max) */
+
+    /* engine knobs */
+    int32_t device;            /* HIP device ordinal */
+    int32_t place_chunk;       /* pods per refresh in kg_place (0 ⇒ default 64) */
+} kg_config;
+
+/* ------------------------------------------------------------------ */
+/* object-level specs (what the Go plugin reads from its informers)        */
+/* ------------------------------------------------------------------ */
+typedef struct kg_container {
+    kg_resource_list requests;
+    kg_resource_list limits;
+} kg_container;
+
+typedef struct kg_pod_spec {
+    int32_t first_container, n_containers;      /* into kg_cluster_view.containers */
+    int32_t first_init_container, n_init_containers;
+    kg_resource_list overhead;                  /* present == 0 ⇔ Spec.Overhead == nil */
+    int32_t has_priority;                       /* Spec.Priority != nil */
+    int32_t priority;
+    int32_t label_priority_class;               /* -1 label absent, else kg_priority_class of the label value */
+    int32_t label_qos;                          /* -1 label absent, else kg_qos_class of the label value */
+    int32_t status_qos;                         /* kg_kube_qos of Status.QOSClass (UNSET ⇒ computed) */
+    int32_t is_daemonset;                       /* an OwnerReference of Kind DaemonSet */
+    int32_t is_terminated;                      /* util.IsPodTerminated */
+    int32_t _pad;
+    int64_t name_id;                            /* identity of namespace/name */
+} kg_pod_spec;
+
+typedef struct kg_aggregated_usage { /* slov1alpha1.AggregatedUsage */
+    int64_t duration_ns;
+    kg_resource_list usage[KG_NUM_AGG_TYPES];   /* map[AggregationType]ResourceMap */
+} kg_aggregated_usage;
+
+typedef struct kg_pod_metric { /* slov1alpha1.PodMetricInfo */
+    int64_t name_id;      /* namespace/name */
+    int32_t lister_pod;   /* index of the pod in kg_cluster_view.pods, -1 ⇔ podLister NotFound */
+    int32_t _pad;
+    kg_resource_list usage;
+} kg_pod_metric;
+
+typedef struct kg_assigned_pod { /* podAssignCache item */
+    int32_t pod;          /* index into kg_cluster_view.pods */
+    int32_t _pad;
+    int64_t timestamp_ns;
+} kg_assigned_pod;
+
+typedef struct kg_node_spec {
+    /* framework.NodeInfo */
+    kg_resource_list allocatable;   /* Allocatable (scalar keys = ScalarResources keys) */
+    kg_resource_list requested;     /* Requested */
+    int64_t nonzero_requested[2];   /* NonZeroRequested cpu, memory */
+    int32_t allowed_pods;           /* Allocatable.AllowedPodNumber */
+    int32_t pod_count;              /* len(NodeInfo.Pods) */
+    /* annotation node.koordinator.sh/raw-allocatable: 0 absent, 1 present, -1 unparsable */
+    int32_t raw_allocatable_state;
+    /* annotation scheduling.koordinator.sh/usage-thresholds: 0 absent, 1 present, -1 unparsable */
+    int32_t custom_thresholds_state;
+    kg_resource_list raw_allocatable;
+    kg_resource_list custom_usage_thresholds;
+    kg_resource_list custom_prod_usage_thresholds;
+    int32_t custom_has_aggregated;          /* AggregatedUsage != nil */
+    int32_t custom_agg_usage_type;
+    kg_resource_list custom_agg_usage_thresholds;
+    int64_t custom_agg_duration_ns;         /* 0 ⇔ nil/zero */
+    /* NodeMetric (nodeMetricLister.Get(node.Name)) */
+    int32_t has_node_metric;                /* 0 ⇔ NotFound */
+    int32_t has_update_time;                /* Status.UpdateTime != nil */
+    int64_t update_time_ns;
+    int32_t has_report_interval;            /* Spec.CollectPolicy.ReportIntervalSeconds != nil */
+    int32_t has_node_metric_info;           /* Status.NodeMetric != nil */
+    int64_t report_interval_seconds;
+    kg_resource_list node_usage;            /* Status.NodeMetric.NodeUsage */
+    int32_t first_aggregated, n_aggregated; /* Status.NodeMetric.AggregatedNodeUsages */
+    int32_t first_pod_metric, n_pod_metric; /* Status.PodsMetric */
+    int32_t first_assigned, n_assigned;     /* podAssignCache.podInfoItems[node] */
+} kg_node_spec;
+
+typedef struct kg_cluster_view {
+    const kg_pod_spec *pods;                 int32_t n_pods;       int32_t _p0;
+    const kg_container *containers;          int32_t n_containers; int32_t _p1;
+    const kg_node_spec *nodes;               int32_t n_nodes;      int32_t _p2;
+    const kg_aggregated_usage *aggregated;   int32_t n_aggregated; int32_t _p3;
+    const kg_pod_metric *pod_metrics;        int32_t n_pod_metrics; int32_t _p4;
+    const kg_assigned_pod *assigned;         int32_t n_assigned;   int32_t _p5;
+} kg_cluster_view;
+
+/* ------------------------------------------------------------------ */
+/* engine rows (pod-only / node-only precompute; what the kernels read)    */
+/* ------------------------------------------------------------------ */
+#define KG_POD_HAS_REQUEST 0x1u    /* Fit: request not all-zero (fit.go fitsRequest early return) */
+#define KG_POD_DAEMONSET 0x2u      /* LoadAware.Filter passes (load_aware.go:129) */
+#define KG_POD_PROD 0x4u           /* GetPodPriorityClassWithDefault == koord-prod */
+#define KG_POD_LA_PROD_SCORE 0x8u  /* prodPod && ScoreAccordingProdUsage (load_aware.go:291) */
+#define KG_POD_VALID 0x80000000u
+
+typedef struct kg_pod_row {
+    int64_t request[KG_NUM_RES];        /* Fit PreFilter request (computePodResourceRequest) */
+    int64_t fit_score_request[KG_NUM_RES]; /* Fit score pod request per resource (nonzero cpu/mem) */
+    int64_t nonzero_request[2];         /* schedutil.GetNonzeroRequests sum (AssumePod NonZeroRequested delta) */
+    int64_t la_estimate[2];             /* EstimatePod(pod)[cpu], [memory] */
+    uint32_t request_present;           /* ScalarResources key set of the Fit request */
+    uint32_t flags;                     /* KG_POD_* */
+} kg_pod_row;
+
+#define KG_NODE_VALID 0x1u
+#define KG_NODE_HAS_METRIC 0x2u          /* nodeMetricLister found the NodeMetric */
+#define KG_NODE_HAS_UPDATE_TIME 0x4u     /* Status.UpdateTime != nil */
+#define KG_NODE_LA_PASS_NONPROD 0x8u     /* threshold check result for non-prod pods */
+#define KG_NODE_LA_PASS_PROD 0x10u       /* threshold check result for prod pods */
+#define KG_NODE_LA_AGG_MISSING 0x20u     /* score aggregation requested but not reported (info) */
+
+typedef struct kg_node_row {
+    int64_t alloc[KG_NUM_RES];          /* NodeInfo.Allocatable */
+    int64_t requested[KG_NUM_RES];      /* NodeInfo.Requested */
+    int64_t nonzero_requested[2];       /* NodeInfo.NonZeroRequested */
+    int64_t la_alloc[2];                /* EstimateNode(node)[cpu], [memory] */
+    int64_t la_used[2][2];              /* [nonProd, prod][cpu, memory]: assigned-pod estimates + usage term */
+    int64_t metric_update_ns;           /* NodeMetric Status.UpdateTime */
+    int32_t pod_count;
+    int32_t allowed_pods;
+    uint32_t alloc_present;             /* Allocatable.ScalarResources key set */
+    uint32_t flags;                     /* KG_NODE_* */
+} kg_node_row;
+
+/* ------------------------------------------------------------------ */
+/* engine                                                                 */
+/* ------------------------------------------------------------------ */
+typedef struct kg_engine kg_engine;
+
+/* Output of kg_eval (matrix mode).  Any pointer may be NULL (not produced).
+ * Columns cover the evaluated node range [B, E) (the shard; the whole snapshot by default),
+ * W = ceil((E - B) / 64), column c ⇔ node B + c:
+ *   mask     [P][W] uint64: bit (c % 64) of word c/64 ⇔ pod p feasible on node B + c
+ *            (AND of every enabled Filter plugin)
+ *   scores   [P][64·W][2] uint8: {NodeResourcesFit score, LoadAwareScheduling score} ∈ [0,100]
+ *            (0 where a plugin is disabled; row stride 64·W pairs)
+ *   top1     [P] uint64: (total+1) << 32 | (0xFFFFFFFF − node) of the best feasible node,
+ *            total = Σ weight·score, ties → lowest node index; 0 ⇔ no feasible node
+ * When out_on_device != 0 the pointers are device pointers on the engine's device
+ * (results stay resident; no copy back). */
+typedef struct kg_eval_out {
+    uint64_t *mask;
+    uint8_t *scores;
+    uint64_t *top1;
+    int32_t out_on_device;
+    int32_t _pad;
+} kg_eval_out;
+
+int32_t kg_abi_version(void);
+/* sizeof() of every ABI struct, in the order of kg_struct_id, for binding checks */
+enum kg_struct_id {
+    KG_SID_RESOURCE_LIST = 0, KG_SID_CONFIG, KG_SID_CONTAINER, KG_SID_POD_SPEC,
+    KG_SID_AGGREGATED_USAGE, KG_SID_POD_METRIC, KG_SID_ASSIGNED_POD, KG_SID_NODE_SPEC,
+    KG_SID_CLUSTER_VIEW, KG_SID_POD_ROW, KG_SID_NODE_ROW, KG_SID_EVAL_OUT, KG_SID_COUNT
+};
+int64_t kg_struct_size(int32_t sid);
+
+/* Fill a config with the v1beta2 defaults (pkg/scheduler/apis/config/v1beta2/defaults.go:32-137)
+ * and NodeResourcesFit LeastAllocated cpu:1 memory:1, both plugins enabled with weight 1. */
+void kg_config_default(kg_config *cfg);
+/* Shipped profile overrides (config/manager/scheduler-config.yaml:17-45). */
+void kg_config_shipped_profile(kg_config *cfg);
+kg_status kg_config_validate(const kg_config *cfg, char *err, int32_t err_len);
+
+/* Host-side row builders (pure CPU, no GPU needed). */
+kg_status kg_build_pod_rows(const kg_config *cfg, const kg_cluster_view *view,
+                            const int32_t *pod_index, int32_t n, kg_pod_row *out);
+kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view,
+                             const int32_t *node_index, int32_t n, kg_node_row *out);
+/* Reserve delta (AssumePod + LoadAware.Reserve) applied to a host-side row. */
+kg_status kg_row_commit(const kg_config *cfg, kg_node_row *node, const kg_pod_row *pod);
+
+/* Engine lifecycle. */
+kg_status kg_engine_create(const kg_config *cfg, kg_engine **out);
+void kg_engine_destroy(kg_engine *eng);
+const char *kg_last_error(const kg_engine *eng);
+kg_status kg_set_stream(kg_engine *eng, void *hip_stream); /* NULL ⇒ engine-owned stream */
+kg_status kg_sync(kg_engine *eng);
+
+/* Node snapshot (HBM-resident). */
+kg_status kg_snapshot_reset(kg_engine *eng, int32_t n_nodes);
+kg_status kg_snapshot_upsert(kg_engine *eng, const int32_t *node_index, const kg_node_row *rows, int32_t n);
+kg_status kg_snapshot_remove(kg_engine *eng, int32_t node_index);
+kg_status kg_snapshot_download(kg_engine *eng, int32_t first, int32_t n, kg_node_row *out);
+/* Restrict kg_eval/kg_place evaluation to nodes [begin, end) (node sharding across GPUs);
+ * node indices stay global.  begin must be a multiple of 512. */
+kg_status kg_set_shard(kg_engine *eng, int32_t begin, int32_t end);
+
+/* Pod batch (uploaded once; HBM-resident until replaced). */
+kg_status kg_pods_set(kg_engine *eng, const kg_pod_row *pods, int32_t n_pods);
+
+/* Matrix mode: every (pod, node) Filter+Score of the uploaded batch against the snapshot. */
+kg_status kg_eval(kg_engine *eng, int64_t now_ns, const kg_eval_out *out);
+
+/* Placement mode: schedule the uploaded batch in queue order exactly like the sequential
+ * cycle (Filter all nodes → Score → argmax, lowest index on ties → Reserve), committing
+ * each placement to the snapshot.  out_node[p] = node or −1, out_score[p] = total score
+ * (−1 when unschedulable). */
+kg_status kg_place(kg_engine *eng, int64_t now_ns, int32_t *out_node, int64_t *out_score);
+
+/* Multi-GPU building blocks of kg_place (see koordinator_amd/dist.py):
+ * chunk_eval writes per-(pod, 512-node tile) partial keys of the shard for pods
+ * [pod_begin, pod_begin+n) into partial_dev ([n][tiles_total] uint32, tile index global);
+ * chunk_resolve commits those pods sequentially given the partials of ALL tiles. */
+int32_t kg_num_tiles(const kg_engine *eng);
+kg_status kg_place_chunk_eval(kg_engine *eng, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev);
+kg_status kg_place_chunk_resolve(kg_engine *eng, int64_t now_ns, int32_t pod_begin, int32_t n,
+                                 const uint32_t *partial_dev, int32_t *out_node_dev, int64_t *out_score_dev);
+
+/* Single Reserve on the device snapshot (pod = index in the uploaded batch). */
+kg_status kg_commit(kg_engine *eng, int32_t pod, int32_t node);
+
+/* Measurement: when on, every k_eval launch (kg_eval, kg_place_chunk_eval) is bracketed by a
+ * pair of HIP events on the engine stream (ring of 256).  kg_eval_kernel_times writes the
+ * durations (ms) of the last min(n, recorded) launches, oldest first, and returns that count
+ * (< 0 on error). */
+kg_status kg_set_profiling(kg_engine *eng, int32_t on);
+int32_t kg_eval_kernel_times(kg_engine *eng, float *ms, int32_t n);
+
+/* Helpers for consumers of matrix-mode output. */
+static inline int kg_mask_test(const uint64_t *mask, int32_t n_nodes, int32_t p, int32_t n) {
+    int32_t words = (n_nodes + 63) / 64;
+    return (int)((mask[(int64_t)p * words + n / 64] >> (n % 64)) & 1u);
+}
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KOORD_GPU_H */

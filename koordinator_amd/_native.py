@@ -1,0 +1,184 @@
+"""ctypes binding of ``libkoordgpu.so`` (the C-ABI in ``include/koord_gpu.h``).
+
+numpy structured dtypes mirror every ABI struct; ``check_abi()`` compares their sizes with
+``kg_struct_size`` so a layout drift fails loudly.  The library is built in-tree by
+``koordinator_amd/build.py``; there is no fallback: importing the engine without the library
+raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ENGINE_SO = os.path.join(_HERE, "lib", "libkoordgpu.so")
+
+ABI_VERSION = 1
+NUM_RES = 8
+(RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
+ RES_EXTENDED) = range(8)
+PRIO_NONE, PRIO_PROD, PRIO_MID, PRIO_BATCH, PRIO_FREE = range(5)
+QOS_NONE, QOS_LSE, QOS_LSR, QOS_LS, QOS_BE, QOS_SYSTEM = range(6)
+KUBE_QOS_UNSET, KUBE_QOS_GUARANTEED, KUBE_QOS_BURSTABLE, KUBE_QOS_BESTEFFORT = range(4)
+AGG_UNSET, AGG_AVG, AGG_P50, AGG_P90, AGG_P95, AGG_P99 = range(6)
+NUM_AGG_TYPES = 6
+STRATEGY_LEAST_ALLOCATED, STRATEGY_MOST_ALLOCATED = 0, 1
+PLUGIN_FIT, PLUGIN_LOADAWARE = 0x1, 0x2
+
+POD_HAS_REQUEST, POD_DAEMONSET, POD_PROD, POD_LA_PROD_SCORE, POD_VALID = 0x1, 0x2, 0x4, 0x8, 0x80000000
+NODE_VALID, NODE_HAS_METRIC, NODE_HAS_UPDATE_TIME, NODE_LA_PASS_NONPROD, NODE_LA_PASS_PROD = 0x1, 0x2, 0x4, 0x8, 0x10
+
+CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE, CODE_UNSCHEDULABLE_AND_UNRESOLVABLE = 0, 1, 2, 3
+TILE = 512
+
+RESOURCE_LIST = np.dtype([("v", "<i8", (NUM_RES,)), ("present", "<u4"), ("_pad", "<u4")], align=True)
+
+CONFIG = np.dtype([
+    ("abi_version", "<i4"), ("enabled_plugins", "<u4"), ("weight_fit", "<i4"), ("weight_loadaware", "<i4"),
+    ("fit_strategy", "<i4"), ("_pad0", "<i4"), ("fit_resource_weight", "<i8", (NUM_RES,)),
+    ("la_filter_expired_node_metrics", "<i4"), ("la_has_expiration", "<i4"), ("la_expiration_seconds", "<i8"),
+    ("la_resource_weight", "<i8", (NUM_RES,)), ("la_scaling_factor", "<i8", (NUM_RES,)),
+    ("la_usage_thresholds", RESOURCE_LIST), ("la_prod_usage_thresholds", RESOURCE_LIST),
+    ("la_score_according_prod_usage", "<i4"), ("la_has_aggregated", "<i4"),
+    ("la_agg_usage_thresholds", RESOURCE_LIST), ("la_agg_usage_type", "<i4"), ("la_agg_score_type", "<i4"),
+    ("la_agg_usage_duration_ns", "<i8"), ("la_agg_score_duration_ns", "<i8"),
+    ("device", "<i4"), ("place_chunk", "<i4"),
+], align=True)
+
+CONTAINER = np.dtype([("requests", RESOURCE_LIST), ("limits", RESOURCE_LIST)], align=True)
+
+POD_SPEC = np.dtype([
+    ("first_container", "<i4"), ("n_containers", "<i4"), ("first_init_container", "<i4"), ("n_init_containers", "<i4"),
+    ("overhead", RESOURCE_LIST), ("has_priority", "<i4"), ("priority", "<i4"), ("label_priority_class", "<i4"),
+    ("label_qos", "<i4"), ("status_qos", "<i4"), ("is_daemonset", "<i4"), ("is_terminated", "<i4"), ("_pad", "<i4"),
+    ("name_id", "<i8"),
+], align=True)
+
+AGGREGATED_USAGE = np.dtype([("duration_ns", "<i8"), ("usage", RESOURCE_LIST, (NUM_AGG_TYPES,))], align=True)
+POD_METRIC = np.dtype([("name_id", "<i8"), ("lister_pod", "<i4"), ("_pad", "<i4"), ("usage", RESOURCE_LIST)], align=True)
+ASSIGNED_POD = np.dtype([("pod", "<i4"), ("_pad", "<i4"), ("timestamp_ns", "<i8")], align=True)
+
+NODE_SPEC = np.dtype([
+    ("allocatable", RESOURCE_LIST), ("requested", RESOURCE_LIST), ("nonzero_requested", "<i8", (2,)),
+    ("allowed_pods", "<i4"), ("pod_count", "<i4"), ("raw_allocatable_state", "<i4"), ("custom_thresholds_state", "<i4"),
+    ("raw_allocatable", RESOURCE_LIST), ("custom_usage_thresholds", RESOURCE_LIST),
+    ("custom_prod_usage_thresholds", RESOURCE_LIST), ("custom_has_aggregated", "<i4"), ("custom_agg_usage_type", "<i4"),
+    ("custom_agg_usage_thresholds", RESOURCE_LIST), ("custom_agg_duration_ns", "<i8"),
+    ("has_node_metric", "<i4"), ("has_update_time", "<i4"), ("update_time_ns", "<i8"),
+    ("has_report_interval", "<i4"), ("has_node_metric_info", "<i4"), ("report_interval_seconds", "<i8"),
+    ("node_usage", RESOURCE_LIST), ("first_aggregated", "<i4"), ("n_aggregated", "<i4"),
+    ("first_pod_metric", "<i4"), ("n_pod_metric", "<i4"), ("first_assigned", "<i4"), ("n_assigned", "<i4"),
+], align=True)
+
+POD_ROW = np.dtype([
+    ("request", "<i8", (NUM_RES,)), ("fit_score_request", "<i8", (NUM_RES,)), ("nonzero_request", "<i8", (2,)),
+    ("la_estimate", "<i8", (2,)), ("request_present", "<u4"), ("flags", "<u4"),
+], align=True)
+
+NODE_ROW = np.dtype([
+    ("alloc", "<i8", (NUM_RES,)), ("requested", "<i8", (NUM_RES,)), ("nonzero_requested", "<i8", (2,)),
+    ("la_alloc", "<i8", (2,)), ("la_used", "<i8", (2, 2)), ("metric_update_ns", "<i8"),
+    ("pod_count", "<i4"), ("allowed_pods", "<i4"), ("alloc_present", "<u4"), ("flags", "<u4"),
+], align=True)
+
+STRUCT_IDS = [RESOURCE_LIST, CONFIG, CONTAINER, POD_SPEC, AGGREGATED_USAGE, POD_METRIC, ASSIGNED_POD, NODE_SPEC,
+              None, POD_ROW, NODE_ROW, None]
+
+
+class ClusterView(ctypes.Structure):
+    _fields_ = [
+        ("pods", ctypes.c_void_p), ("n_pods", ctypes.c_int32), ("_p0", ctypes.c_int32),
+        ("containers", ctypes.c_void_p), ("n_containers", ctypes.c_int32), ("_p1", ctypes.c_int32),
+        ("nodes", ctypes.c_void_p), ("n_nodes", ctypes.c_int32), ("_p2", ctypes.c_int32),
+        ("aggregated", ctypes.c_void_p), ("n_aggregated", ctypes.c_int32), ("_p3", ctypes.c_int32),
+        ("pod_metrics", ctypes.c_void_p), ("n_pod_metrics", ctypes.c_int32), ("_p4", ctypes.c_int32),
+        ("assigned", ctypes.c_void_p), ("n_assigned", ctypes.c_int32), ("_p5", ctypes.c_int32),
+    ]
+
+
+class EvalOut(ctypes.Structure):
+    _fields_ = [("mask", ctypes.c_void_p), ("scores", ctypes.c_void_p), ("top1", ctypes.c_void_p),
+                ("out_on_device", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+
+
+def ptr(a) -> ctypes.c_void_p:
+    if a is None:
+        return ctypes.c_void_p(0)
+    if isinstance(a, int):
+        return ctypes.c_void_p(a)
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def make_view(pods, containers, nodes, aggregated, pod_metrics, assigned) -> ClusterView:
+    v = ClusterView()
+    for name, arr in (("pods", pods), ("containers", containers), ("nodes", nodes), ("aggregated", aggregated),
+                      ("pod_metrics", pod_metrics), ("assigned", assigned)):
+        assert arr.flags["C_CONTIGUOUS"]
+        setattr(v, name, arr.ctypes.data if len(arr) else 0)
+    v.n_pods, v.n_containers, v.n_nodes = len(pods), len(containers), len(nodes)
+    v.n_aggregated, v.n_pod_metrics, v.n_assigned = len(aggregated), len(pod_metrics), len(assigned)
+    v._keep = (pods, containers, nodes, aggregated, pod_metrics, assigned)
+    return v
+
+
+EXPORTED = [
+    "kg_abi_version", "kg_struct_size", "kg_config_default", "kg_config_shipped_profile", "kg_config_validate",
+    "kg_build_pod_rows", "kg_build_node_rows", "kg_row_commit", "kg_engine_create", "kg_engine_destroy",
+    "kg_last_error", "kg_set_stream", "kg_sync", "kg_snapshot_reset", "kg_snapshot_upsert", "kg_snapshot_remove",
+    "kg_snapshot_download", "kg_set_shard", "kg_pods_set", "kg_eval", "kg_place", "kg_num_tiles",
+    "kg_place_chunk_eval", "kg_place_chunk_resolve", "kg_commit", "kg_set_profiling", "kg_eval_kernel_times",
+]
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load the in-tree engine library; raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(ENGINE_SO):
+        raise RuntimeError(f"{ENGINE_SO} is missing: build it with `python koordinator_amd/build.py` "
+                           "(there is no CPU fallback for the engine)")
+    L = ctypes.CDLL(ENGINE_SO)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    sig = {
+        "kg_abi_version": (i32, []), "kg_struct_size": (i64, [i32]),
+        "kg_config_default": (None, [vp]), "kg_config_shipped_profile": (None, [vp]),
+        "kg_config_validate": (i32, [vp, ctypes.c_char_p, i32]),
+        "kg_build_pod_rows": (i32, [vp, vp, vp, i32, vp]), "kg_build_node_rows": (i32, [vp, vp, vp, i32, vp]),
+        "kg_row_commit": (i32, [vp, vp, vp]),
+        "kg_engine_create": (i32, [vp, ctypes.POINTER(vp)]), "kg_engine_destroy": (None, [vp]),
+        "kg_last_error": (ctypes.c_char_p, [vp]), "kg_set_stream": (i32, [vp, vp]), "kg_sync": (i32, [vp]),
+        "kg_snapshot_reset": (i32, [vp, i32]), "kg_snapshot_upsert": (i32, [vp, vp, vp, i32]),
+        "kg_snapshot_remove": (i32, [vp, i32]), "kg_snapshot_download": (i32, [vp, i32, i32, vp]),
+        "kg_set_shard": (i32, [vp, i32, i32]), "kg_pods_set": (i32, [vp, vp, i32]),
+        "kg_eval": (i32, [vp, i64, vp]), "kg_place": (i32, [vp, i64, vp, vp]), "kg_num_tiles": (i32, [vp]),
+        "kg_place_chunk_eval": (i32, [vp, i64, i32, i32, vp]),
+        "kg_place_chunk_resolve": (i32, [vp, i64, i32, i32, vp, vp, vp]),
+        "kg_commit": (i32, [vp, i32, i32]),
+        "kg_set_profiling": (i32, [vp, i32]), "kg_eval_kernel_times": (i32, [vp, vp, i32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    check_abi(L)
+    return L
+
+
+def check_abi(L=None) -> None:
+    L = L or lib()
+    if L.kg_abi_version() != ABI_VERSION:
+        raise RuntimeError("engine ABI version mismatch")
+    for sid, dt in enumerate(STRUCT_IDS):
+        if dt is None:
+            continue
+        got = L.kg_struct_size(sid)
+        if got != dt.itemsize:
+            raise RuntimeError(f"struct id {sid}: C size {got} != numpy {dt.itemsize}")
+    if L.kg_struct_size(8) != ctypes.sizeof(ClusterView) or L.kg_struct_size(11) != ctypes.sizeof(EvalOut):
+        raise RuntimeError("view/eval_out struct size mismatch")

@@ -1,0 +1,77 @@
+"""In-tree build of the native pieces (no JIT, no site-packages install).
+
+* ``koordinator_amd/lib/libkoordgpu.so`` — the engine: HIP kernels for gfx950 + host row
+  builders, exporting the C-ABI declared in ``include/koord_gpu.h``.
+* ``oracle/build/libkoordoracle.so`` — the CPU restatement used as the parity checker
+  (test infrastructure; never loaded by the product path).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "koordinator_amd", "csrc")
+LIB_DIR = os.path.join(ROOT, "koordinator_amd", "lib")
+ENGINE_SO = os.path.join(LIB_DIR, "libkoordgpu.so")
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "build", "libkoordoracle.so")
+
+ARCH = os.environ.get("KG_OFFLOAD_ARCH", "gfx950")
+
+
+def _run(cmd: list[str]) -> None:
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _newer(target: str, sources: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def engine_sources() -> list[str]:
+    names = ["kg_engine.hip", "kg_host.cpp", "kg_common.h", "kg_host.h"]
+    return [os.path.join(CSRC, n) for n in names] + [os.path.join(ROOT, "include", "koord_gpu.h")]
+
+
+def build_engine(force: bool = False) -> str:
+    os.makedirs(LIB_DIR, exist_ok=True)
+    if not force and not _newer(ENGINE_SO, engine_sources()):
+        return ENGINE_SO
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    common = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
+    host_obj = os.path.join(obj_dir, "kg_host.o")
+    _run(["g++", *common, "-c", os.path.join(CSRC, "kg_host.cpp"), "-o", host_obj])
+    dev_obj = os.path.join(obj_dir, "kg_engine.o")
+    _run([hipcc, *common, f"--offload-arch={ARCH}", "-c", os.path.join(CSRC, "kg_engine.hip"), "-o", dev_obj])
+    tmp = ENGINE_SO + ".tmp"
+    _run([hipcc, "-shared", f"--offload-arch={ARCH}", dev_obj, host_obj, "-o", tmp])
+    os.replace(tmp, ENGINE_SO)
+    return ENGINE_SO
+
+
+def build_oracle(force: bool = False) -> str:
+    src = os.path.join(ORACLE_DIR, "koord_oracle.c")
+    os.makedirs(os.path.dirname(ORACLE_SO), exist_ok=True)
+    if not force and not _newer(ORACLE_SO, [src, os.path.join(ROOT, "include", "koord_gpu.h")]):
+        return ORACLE_SO
+    tmp = ORACLE_SO + ".tmp"
+    _run(["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-ffp-contract=off", "-Wall", src, "-o", tmp, "-lm", "-lpthread"])
+    os.replace(tmp, ORACLE_SO)
+    return ORACLE_SO
+
+
+def build_all(force: bool = False) -> None:
+    build_oracle(force)
+    build_engine(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,85 @@
+"""Plugin args → ``kg_config`` (pkg/scheduler/apis/config/types.go:30-114).
+
+``load_aware_args(...)`` mirrors v1beta2.SetDefaults_LoadAwareSchedulingArgs
+(pkg/scheduler/apis/config/v1beta2/defaults.go:78-100): a map given explicitly replaces the
+default map as a whole (UsageThresholds, ResourceWeights), EstimatedScalingFactors is merged
+key by key, and nil pointers get their defaults.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import _native as nat
+from .objects import AGG, RES
+
+DEFAULT_USAGE_THRESHOLDS = {"cpu": 65, "memory": 95}
+DEFAULT_RESOURCE_WEIGHTS = {"cpu": 1, "memory": 1}
+DEFAULT_SCALING_FACTORS = {"cpu": 85, "memory": 70}
+
+
+def _rl(d: Optional[Dict[str, int]]) -> np.ndarray:
+    out = np.zeros((), dtype=nat.RESOURCE_LIST)
+    for k, v in (d or {}).items():
+        out["v"][RES[k]] = int(v)
+        out["present"] |= np.uint32(1 << RES[k])
+    return out
+
+
+def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_fit: int = 1,
+                weight_loadaware: int = 1, fit_strategy: str = "LeastAllocated",
+                fit_resources: Optional[Dict[str, int]] = None,
+                filter_expired_node_metrics: Optional[bool] = None,
+                node_metric_expiration_seconds: Optional[int] = None,
+                resource_weights: Optional[Dict[str, int]] = None,
+                usage_thresholds: Optional[Dict[str, int]] = None,
+                prod_usage_thresholds: Optional[Dict[str, int]] = None,
+                score_according_prod_usage: bool = False,
+                estimated_scaling_factors: Optional[Dict[str, int]] = None,
+                aggregated: Optional[dict] = None,
+                device: int = 0, place_chunk: int = 64) -> np.ndarray:
+    c = np.zeros((), dtype=nat.CONFIG)
+    c["abi_version"] = nat.ABI_VERSION
+    bits = 0
+    for p in plugins:
+        bits |= {"NodeResourcesFit": nat.PLUGIN_FIT, "LoadAwareScheduling": nat.PLUGIN_LOADAWARE}[p]
+    c["enabled_plugins"] = bits
+    c["weight_fit"] = weight_fit
+    c["weight_loadaware"] = weight_loadaware
+    c["fit_strategy"] = {"LeastAllocated": nat.STRATEGY_LEAST_ALLOCATED,
+                         "MostAllocated": nat.STRATEGY_MOST_ALLOCATED}[fit_strategy]
+    for k, w in (fit_resources or {"cpu": 1, "memory": 1}).items():
+        c["fit_resource_weight"][RES[k]] = w
+    # SetDefaults_LoadAwareSchedulingArgs
+    c["la_filter_expired_node_metrics"] = int(True if filter_expired_node_metrics is None else filter_expired_node_metrics)
+    c["la_has_expiration"] = 1
+    c["la_expiration_seconds"] = 180 if node_metric_expiration_seconds is None else node_metric_expiration_seconds
+    for k, w in (resource_weights or DEFAULT_RESOURCE_WEIGHTS).items():
+        c["la_resource_weight"][RES[k]] = w
+    c["la_usage_thresholds"] = _rl(usage_thresholds if usage_thresholds else DEFAULT_USAGE_THRESHOLDS)
+    c["la_prod_usage_thresholds"] = _rl(prod_usage_thresholds)
+    sf = dict(estimated_scaling_factors or {})
+    for k, v in DEFAULT_SCALING_FACTORS.items():
+        sf.setdefault(k, v)
+    for k, v in sf.items():
+        c["la_scaling_factor"][RES[k]] = v
+    c["la_score_according_prod_usage"] = int(score_according_prod_usage)
+    if aggregated is not None:
+        c["la_has_aggregated"] = 1
+        c["la_agg_usage_thresholds"] = _rl(aggregated.get("usageThresholds"))
+        c["la_agg_usage_type"] = AGG[aggregated.get("usageAggregationType", "")]
+        c["la_agg_score_type"] = AGG[aggregated.get("scoreAggregationType", "")]
+        c["la_agg_usage_duration_ns"] = int(aggregated.get("usageAggregatedDuration", 0) * 10**9)
+        c["la_agg_score_duration_ns"] = int(aggregated.get("scoreAggregatedDuration", 0) * 10**9)
+    c["device"] = device
+    c["place_chunk"] = place_chunk
+    return c
+
+
+def shipped_profile(**kw) -> np.ndarray:
+    """config/manager/scheduler-config.yaml:17-45 (Fit scores batch resources too)."""
+    base = dict(fit_resources={"cpu": 1, "memory": 1, "kubernetes.io/batch-cpu": 1, "kubernetes.io/batch-memory": 1},
+                filter_expired_node_metrics=False, node_metric_expiration_seconds=300)
+    base.update(kw)
+    return make_config(**base)

@@ -1,0 +1,836 @@
+// kg_engine.hip — HBM-resident node snapshot + CDNA4 Filter/Score kernels behind the C-ABI.
+//
+// Hot kernel k_eval (matrix mode, reference hot loops #1 Filter and #2 Score of
+// upstream findNodesThatPassFilters / prioritizeNodes over LoadAwareScheduling
+// load_aware.go:123-335 and NodeResourcesFit):
+//   * one node per thread, a 512-node tile per workgroup (8 waves); the node's derived
+//     planes are loaded once into registers and reused for every pod of the workgroup's
+//     pod range (node bytes are read once per pod range, not once per pair);
+//   * the pod row is wave-uniform → scalar loads (SMEM) and scalar branches on its masks;
+//   * per pair: the Fit filter as int64 compares, LoadAware filter as precomputed node bits,
+//     each LR score as one fp64 FMA + cvt (exactness argument in kg_common.h);
+//   * outputs: a feasibility bit plane written from the wave ballot (one 8-B word per
+//     64 nodes), the u8 score pair {Fit, LoadAware} per pair as one u16 store per lane
+//     (128 B contiguous per wave), and per (pod, tile) the best (total, lowest node) key
+//     from a DPP wave max + an LDS combine across the 8 waves.
+// No MFMA: nothing here is a dense contraction; the roofline is HBM bytes (or VALU issue).
+//
+// Placement mode (sequential scheduling cycle, upstream scheduleOne → selectHost → Reserve):
+// pods are processed in chunks; k_eval writes per-(pod, tile) partial keys against the
+// snapshot at chunk start, then one workgroup (k_resolve) walks the chunk in queue order:
+// a tile's partial is still exact if its best node was not touched by an earlier pod of the
+// chunk; touched nodes are re-scored; tiles whose best node was touched are re-scanned; the
+// winner is committed to the canonical row and its planes re-derived on the device.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "kg_common.h"
+#include "kg_host.h"
+
+#define KG_WAVES_PER_TILE (KG_TILE / 64)
+#define KG_POD_CHUNK 64          // pods between two LDS partial combines in k_eval
+#define KG_RESOLVE_THREADS 1024
+#define KG_MAX_CHUNK 1024        // max pods per resolve call (touched-list capacity)
+#define KG_MAX_TILES 4096        // max tiles per snapshot in k_resolve (2M nodes)
+
+// ---------------------------------------------------------------------------------------
+// wave reductions
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t dpp_max_step(uint32_t v, int ctrl_sel) {
+    uint32_t o;
+    switch (ctrl_sel) {  // old = 0 is the identity of unsigned max
+        case 0: o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false); break;  // row_shr:1
+        case 1: o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false); break;  // row_shr:2
+        case 2: o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false); break;  // row_shr:4
+        case 3: o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false); break;  // row_shr:8
+        case 4: o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); break;  // row_bcast:15
+        default: o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); break; // row_bcast:31
+    }
+    return v > o ? v : o;
+}
+
+// max over the 64 lanes, result valid in lane 63 (returned as a wave-uniform value)
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = dpp_max_step(v, 0);
+    v = dpp_max_step(v, 1);
+    v = dpp_max_step(v, 2);
+    v = dpp_max_step(v, 3);
+    v = dpp_max_step(v, 4);
+    v = dpp_max_step(v, 5);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) {
+        unsigned long long o = __shfl_xor(v, off, 64);
+        v = v > o ? v : o;
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// per-lane node registers and the pair evaluation
+// ---------------------------------------------------------------------------------------
+struct NodeRegs {
+    int64_t free_[KG_NUM_RES];
+    double fit_R[KG_NUM_RES];
+    double fit_F[KG_NUM_RES];
+    double la_R[2];
+    double la_F[2][2];
+    uint32_t fit_mask;
+    uint32_t df;
+    bool ok_np, ok_p, ok_ds;   // node-only filter outcome for non-prod / prod / daemonset pods
+    bool la_valid;
+};
+
+// batch-level union masks: which planes the pods of this launch need
+struct BatchMasks {
+    uint32_t cmp;   // Fit filter compares
+    uint32_t fit;   // Fit score resources
+};
+
+__device__ __forceinline__ void load_node(const kg_consts &c, const kg_planes &pl, int64_t i, bool in_range,
+                                          const BatchMasks &bm, int64_t now_ns, NodeRegs &n) {
+    const int64_t cap = pl.cap;
+    uint32_t df = in_range ? pl.dflags[i] : 0u;
+    n.df = df;
+#pragma unroll
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        n.free_[r] = 0;
+        n.fit_R[r] = 0.0;
+        n.fit_F[r] = 0.0;
+        if (in_range && ((bm.cmp >> r) & 1u)) n.free_[r] = pl.free_[r * cap + i];
+        if (in_range && ((bm.fit >> r) & 1u)) {
+            n.fit_R[r] = pl.fit_R[r * cap + i];
+            n.fit_F[r] = pl.fit_F[r * cap + i];
+        }
+    }
+    n.fit_mask = in_range ? pl.fit_mask[i] : 0u;
+    bool expired = false;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        n.la_R[r] = 0.0;
+        n.la_F[0][r] = 0.0;
+        n.la_F[1][r] = 0.0;
+    }
+    if (c.plugins & KG_PLUGIN_LOADAWARE) {
+        int64_t upd = in_range ? pl.metric_ns[i] : 0;
+        expired = kg_metric_expired(c, df, upd, now_ns);
+        if (in_range) {
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                n.la_R[r] = pl.la_R[r * cap + i];
+                n.la_F[0][r] = pl.la_F[(0 * 2 + r) * cap + i];
+                n.la_F[1][r] = pl.la_F[(1 * 2 + r) * cap + i];
+            }
+        }
+    }
+    bool base = (df & KGD_VALID) != 0;
+    if (c.plugins & KG_PLUGIN_FIT) base = base && !(df & KGD_PODS_FULL);
+    n.ok_ds = base;
+    if (c.plugins & KG_PLUGIN_LOADAWARE) {
+        n.ok_np = base && kg_la_pass(c, df, expired, 0);
+        n.ok_p = base && kg_la_pass(c, df, expired, 1);
+        n.la_valid = kg_la_valid(c, df, expired);
+    } else {
+        n.ok_np = n.ok_p = base;
+        n.la_valid = false;
+    }
+}
+
+__device__ __forceinline__ int lr_q(double neg_pr, double R, double F) {
+    int q = (int)__builtin_fma(neg_pr, R, F);
+    return q > 0 ? q : 0;
+}
+
+// Fast-path evaluation of one pair. Returns feasibility; fit/la scores in [0,100].
+__device__ __forceinline__ bool eval_fast(const kg_consts &c, const kg_pod_dev &p, const NodeRegs &n, uint32_t &fit,
+                                          uint32_t &la) {
+    const uint32_t pf = p.flags;
+    bool ok = (pf & KG_POD_DAEMONSET) ? n.ok_ds : ((pf & KG_POD_PROD) ? n.ok_p : n.ok_np);
+    fit = 0;
+    la = 0;
+    if (c.plugins & KG_PLUGIN_FIT) {
+        const uint32_t over = ((p.zero_native_mask & 1u) ? KGD_OVER_CPU : 0u) |
+                              ((p.zero_native_mask & 2u) ? KGD_OVER_MEM : 0u) |
+                              ((p.zero_native_mask & 4u) ? KGD_OVER_EPH : 0u);
+        ok = ok && !(n.df & over);
+#pragma unroll
+        for (int r = 0; r < KG_NUM_RES; r++)
+            if ((p.cmp_mask >> r) & 1u) ok = ok && (p.req[r] <= n.free_[r]);
+        uint32_t s = 0;
+#pragma unroll
+        for (int r = 0; r < KG_NUM_RES; r++) {
+            if ((p.fit_mask >> r) & 1u) {
+                int q = lr_q(p.fit_pr[r], n.fit_R[r], n.fit_F[r]);
+                if (c.fit_most) q = q < 100 ? q : 100;
+                s += (uint32_t)(c.fit_w[r] * q);
+            }
+        }
+        if ((n.fit_mask & p.fit_mask) == p.fit_mask) {
+            fit = __umulhi(s << 1, p.fit_magic);
+        } else {
+            uint32_t w = 0;
+#pragma unroll
+            for (int r = 0; r < KG_NUM_RES; r++)
+                if (((n.fit_mask & p.fit_mask) >> r) & 1u) w += (uint32_t)c.fit_w[r];
+            fit = w ? s / w : 0u;
+        }
+    }
+    if (c.plugins & KG_PLUGIN_LOADAWARE) {
+        const int v = (pf & KG_POD_LA_PROD_SCORE) ? 1 : 0;
+        const int q0 = lr_q(p.la_est[0], n.la_R[0], n.la_F[v][0]);
+        const int q1 = lr_q(p.la_est[1], n.la_R[1], n.la_F[v][1]);
+        const uint32_t s = (uint32_t)(c.la_w[0] * q0 + c.la_w[1] * q1);
+        la = n.la_valid ? __umulhi(s << 1, c.la_magic) : 0u;
+    }
+    return ok;
+}
+
+__device__ __forceinline__ bool eval_pair(const kg_consts &c, const kg_planes &pl, const kg_pod_dev &p,
+                                          const NodeRegs &n, int64_t node, int64_t now_ns, uint32_t &fit, uint32_t &la) {
+    if (n.df & KGD_SLOW) {
+        bool feas;
+        kg_pair_exact(c, pl.rows[node], n.df, p, now_ns, feas, fit, la);
+        return feas;
+    }
+    return eval_fast(c, p, n, fit, la);
+}
+
+__device__ __forceinline__ uint32_t total_of(const kg_consts &c, uint32_t fit, uint32_t la) {
+    return (uint32_t)c.weight_fit * fit + (uint32_t)c.weight_la * la;
+}
+
+// ---------------------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------------------
+__global__ void k_upsert(kg_consts c, kg_planes pl, const kg_node_row *__restrict__ staged,
+                         const int32_t *__restrict__ idx, int32_t n) {
+    int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    int64_t i = idx[k];
+    pl.rows[i] = staged[k];
+    kg_finalize_node(c, pl, i);
+}
+
+__global__ void k_finalize_range(kg_consts c, kg_planes pl, int64_t begin, int64_t end) {
+    int64_t i = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= end) return;
+    kg_finalize_node(c, pl, i);
+}
+
+struct EvalArgs {
+    const kg_pod_dev *pods;  // batch base
+    int32_t pod_begin;       // first pod of this launch (batch index)
+    int32_t n_pods;          // pods in this launch
+    int32_t pods_per_block;
+    int32_t tile_begin;      // first global tile of the shard
+    int64_t node_end;        // shard end (exclusive, global index)
+    int64_t col_begin;       // first node of the output columns (shard begin)
+    int32_t tiles_total;     // partial row stride
+    int32_t mask_words;      // mask row stride (words)
+    int64_t score_stride;    // score row stride (pairs)
+    int64_t now_ns;
+    BatchMasks bm;
+    uint64_t *mask;          // [n_pods][mask_words] (row 0 = pod_begin)
+    uint16_t *scores;        // [n_pods][score_stride]
+    uint32_t *partials;      // [n_pods][tiles_total]
+};
+
+template <bool WRITE_MASK, bool WRITE_SCORES, bool SLOW>
+__device__ __forceinline__ void eval_loop(const kg_consts &c, const kg_planes &pl, const EvalArgs &a, const NodeRegs &n,
+                                          int64_t node, int p0, int p1, uint32_t (*lds)[KG_WAVES_PER_TILE]) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const uint32_t local_key = (uint32_t)(KG_TILE - 1 - tid);
+    for (int p = p0; p < p1; p++) {
+        const kg_pod_dev &pd = a.pods[a.pod_begin + p];
+        uint32_t fit, la;
+        bool feas = SLOW ? eval_pair(c, pl, pd, n, node, a.now_ns, fit, la) : eval_fast(c, pd, n, fit, la);
+        if (WRITE_SCORES) {
+            if (node < a.node_end) a.scores[(int64_t)p * a.score_stride + (node - a.col_begin)] = (uint16_t)(fit | (la << 8));
+        }
+        if (WRITE_MASK) {
+            unsigned long long b = __ballot(feas);
+            if (lane == 0) a.mask[(int64_t)p * a.mask_words + ((node - a.col_begin) >> 6)] = b;
+        }
+        uint32_t key = feas ? ((total_of(c, fit, la) + 1u) << 9) | local_key : 0u;
+        key = wave_max_u32(key);
+        if (lane == 0) lds[p - p0][wave] = key;
+    }
+}
+
+template <bool WRITE_MASK, bool WRITE_SCORES>
+__global__ __launch_bounds__(KG_TILE) void k_eval(kg_consts c, kg_planes pl, EvalArgs a) {
+    __shared__ uint32_t lds[2][KG_POD_CHUNK][KG_WAVES_PER_TILE];
+    const int tid = threadIdx.x;
+    const int tile = a.tile_begin + blockIdx.x;
+    const int64_t node = (int64_t)tile * KG_TILE + tid;
+    const bool in_range = node < a.node_end;
+    NodeRegs n;
+    load_node(c, pl, node, in_range, a.bm, a.now_ns, n);
+    const bool slow = __any((n.df & KGD_SLOW) != 0);  // wave-uniform
+    const int pb = blockIdx.y * a.pods_per_block;
+    const int pe = min(pb + a.pods_per_block, a.n_pods);
+    int buf = 0;
+    for (int p0 = pb; p0 < pe; p0 += KG_POD_CHUNK, buf ^= 1) {
+        const int p1 = min(p0 + KG_POD_CHUNK, pe);
+        if (slow) eval_loop<WRITE_MASK, WRITE_SCORES, true>(c, pl, a, n, node, p0, p1, lds[buf]);
+        else eval_loop<WRITE_MASK, WRITE_SCORES, false>(c, pl, a, n, node, p0, p1, lds[buf]);
+        __syncthreads();
+        if (tid < p1 - p0) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int w = 0; w < KG_WAVES_PER_TILE; w++) m = m > lds[buf][tid][w] ? m : lds[buf][tid][w];
+            a.partials[(int64_t)(p0 + tid) * a.tiles_total + tile] = m;
+        }
+        // the double buffer makes a second barrier unnecessary: the next chunk writes the other buffer
+    }
+}
+
+__device__ __forceinline__ unsigned long long decode_partial(uint32_t k, int tile) {
+    if (k == 0) return 0ull;
+    const uint32_t node = (uint32_t)tile * KG_TILE + (KG_TILE - 1) - (k & (KG_TILE - 1));
+    return ((unsigned long long)(k >> 9) << 32) | (0xFFFFFFFFull - node);
+}
+
+// per-pod max over the tile partials → (total+1) << 32 | (0xFFFFFFFF − node)
+__global__ void k_top1(const uint32_t *__restrict__ partials, int32_t tiles, int32_t n_pods,
+                       unsigned long long *__restrict__ out) {
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wave >= n_pods) return;
+    unsigned long long best = 0;
+    for (int t = lane; t < tiles; t += 64) {
+        unsigned long long k = decode_partial(partials[(int64_t)wave * tiles + t], t);
+        best = best > k ? best : k;
+    }
+    best = wave_max_u64(best);
+    if (lane == 0) out[wave] = best;
+}
+
+__device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, const kg_pod_dev &p, int64_t node,
+                                       int64_t n_nodes, int64_t now_ns) {
+    if (node < 0 || node >= n_nodes) return 0ull;
+    NodeRegs n;
+    BatchMasks bm{0xFFu, 0xFFu};
+    load_node(c, pl, node, true, bm, now_ns, n);
+    uint32_t fit, la;
+    if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
+    return ((unsigned long long)(total_of(c, fit, la) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
+}
+
+// Sequential commit of pods [pod_begin, pod_begin + n) given their per-tile partial keys.
+__global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_planes pl,
+                                                                const kg_pod_dev *__restrict__ pods, int32_t pod_begin,
+                                                                int32_t n, const uint32_t *partials, int32_t tiles_total,
+                                                                int64_t n_nodes, int64_t now_ns, int32_t *out_node,
+                                                                int64_t *out_score) {
+    __shared__ int32_t touched[KG_MAX_CHUNK];
+    __shared__ int32_t rescan[KG_MAX_TILES];
+    __shared__ unsigned long long red[KG_RESOLVE_THREADS / 64];
+    __shared__ int32_t n_touched, n_rescan;
+    const int tid = threadIdx.x;
+    if (tid == 0) n_touched = 0;
+    for (int j = 0; j < n; j++) {
+        if (tid == 0) n_rescan = 0;
+        __syncthreads();
+        const kg_pod_dev &pd = pods[pod_begin + j];
+        unsigned long long best = 0;
+        const int nt = n_touched;
+        for (int t = tid; t < tiles_total; t += KG_RESOLVE_THREADS) {
+            const unsigned long long k = decode_partial(partials[(int64_t)j * tiles_total + t], t);
+            if (!k) continue;
+            const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
+            bool hit = false;
+            for (int q = 0; q < nt; q++) hit |= touched[q] == node;
+            if (hit) rescan[atomicAdd(&n_rescan, 1)] = t;
+            else best = best > k ? best : k;
+        }
+        for (int q = tid; q < nt; q += KG_RESOLVE_THREADS) {
+            const unsigned long long k = pair_key(c, pl, pd, touched[q], n_nodes, now_ns);
+            best = best > k ? best : k;
+        }
+        __syncthreads();
+        const int nr = n_rescan;
+        for (int q = tid; q < nr * KG_TILE; q += KG_RESOLVE_THREADS) {
+            const int64_t node = (int64_t)rescan[q / KG_TILE] * KG_TILE + (q % KG_TILE);
+            const unsigned long long k = pair_key(c, pl, pd, node, n_nodes, now_ns);
+            best = best > k ? best : k;
+        }
+        best = wave_max_u64(best);
+        if ((tid & 63) == 0) red[tid >> 6] = best;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long w = 0;
+            for (int q = 0; q < KG_RESOLVE_THREADS / 64; q++) w = w > red[q] ? w : red[q];
+            if (w) {
+                const int32_t node = (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull));
+                kg_apply_commit(pl.rows[node], pd);
+                kg_finalize_node(c, pl, node);
+                bool seen = false;
+                for (int q = 0; q < n_touched; q++) seen |= touched[q] == node;
+                if (!seen) touched[n_touched++] = node;
+                out_node[j] = node;
+                out_score[j] = (int64_t)(w >> 32) - 1;
+            } else {
+                out_node[j] = -1;
+                out_score[j] = -1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_commit_one(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t pod, int32_t node) {
+    kg_apply_commit(pl.rows[node], pods[pod]);
+    kg_finalize_node(c, pl, node);
+}
+
+// ---------------------------------------------------------------------------------------
+// engine
+// ---------------------------------------------------------------------------------------
+struct kg_engine {
+    kg_config cfg;
+    kg_consts consts;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    kg_planes pl{};
+    void *plane_mem = nullptr;
+    int64_t n_nodes = 0;
+    int64_t shard_begin = 0, shard_end = 0;
+    kg_pod_dev *pods = nullptr;
+    int32_t n_pods = 0, pods_cap = 0;
+    BatchMasks bm{0, 0};
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    bool profiling = false;
+    static constexpr int kRing = 256;   // event pairs: one per profiled k_eval launch
+    hipEvent_t ev0[kRing] = {}, ev1[kRing] = {};
+    int64_t ev_count = 0;               // launches recorded since kg_set_profiling
+    std::string err;
+};
+
+namespace {
+
+kg_status set_err(kg_engine *e, kg_status code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (e) e->err = buf;
+    return code;
+}
+
+#define HIP_TRY(e, expr)                                                                         \
+    do {                                                                                         \
+        hipError_t _st = (expr);                                                                 \
+        if (_st != hipSuccess) return set_err(e, KG_ERR_HIP, "%s: %s", #expr, hipGetErrorString(_st)); \
+    } while (0)
+
+kg_status ensure_scratch(kg_engine *e, size_t bytes) {
+    if (e->scratch_bytes >= bytes) return KG_OK;
+    if (e->scratch) HIP_TRY(e, hipFree(e->scratch));
+    e->scratch = nullptr;
+    e->scratch_bytes = 0;
+    HIP_TRY(e, hipMalloc(&e->scratch, bytes));
+    e->scratch_bytes = bytes;
+    return KG_OK;
+}
+
+int64_t tiles_total(const kg_engine *e) { return e->pl.cap / KG_TILE; }
+
+int pods_per_block_for(int64_t n_pods, int64_t tiles) {
+    const int64_t target_blocks = 2048;
+    int64_t ppb = (n_pods * tiles + target_blocks - 1) / target_blocks;
+    ppb = (ppb + KG_POD_CHUNK - 1) / KG_POD_CHUNK * KG_POD_CHUNK;
+    if (ppb < KG_POD_CHUNK) ppb = KG_POD_CHUNK;
+    if (ppb > 4096) ppb = 4096;
+    return (int)ppb;
+}
+
+kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
+                      uint32_t *partials) {
+    if (n <= 0) return KG_OK;
+    const int64_t shard_tiles = (e->shard_end - e->shard_begin + KG_TILE - 1) / KG_TILE;
+    if (shard_tiles <= 0) return KG_OK;
+    EvalArgs a;
+    a.pods = e->pods;
+    a.pod_begin = pod_begin;
+    a.n_pods = n;
+    a.pods_per_block = pods_per_block_for(n, shard_tiles);
+    a.tile_begin = (int32_t)(e->shard_begin / KG_TILE);
+    a.node_end = e->shard_end;
+    a.tiles_total = (int32_t)tiles_total(e);
+    a.col_begin = e->shard_begin;
+    a.mask_words = (int32_t)((e->shard_end - e->shard_begin + 63) / 64);
+    a.score_stride = (e->shard_end - e->shard_begin + 63) / 64 * 64;
+    a.now_ns = now_ns;
+    a.bm = e->bm;
+    a.mask = mask;
+    a.scores = scores;
+    a.partials = partials;
+    dim3 grid((unsigned)shard_tiles, (unsigned)((n + a.pods_per_block - 1) / a.pods_per_block));
+    if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
+    if (mask && scores) hipLaunchKernelGGL((k_eval<true, true>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a);
+    else if (mask) hipLaunchKernelGGL((k_eval<true, false>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a);
+    else if (scores) hipLaunchKernelGGL((k_eval<false, true>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a);
+    else hipLaunchKernelGGL((k_eval<false, false>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a);
+    HIP_TRY(e, hipGetLastError());
+    if (e->profiling) {
+        HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
+        e->ev_count++;
+    }
+    return KG_OK;
+}
+
+kg_status check_engine(kg_engine *e) {
+    if (!e) return KG_ERR_INVALID_ARG;
+    HIP_TRY(e, hipSetDevice(e->device));
+    return KG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
+    if (!out) return KG_ERR_INVALID_ARG;
+    *out = nullptr;
+    char msg[256] = {0};
+    kg_status st = kg_config_validate(cfg, msg, sizeof(msg));
+    if (st != KG_OK) {
+        fprintf(stderr, "kg_engine_create: %s\n", msg);
+        return st;
+    }
+    kg_engine *e = new kg_engine();
+    e->cfg = *cfg;
+    kg_consts_from_config(*cfg, e->consts);
+    e->device = cfg->device;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= e->device || e->device < 0) {
+        fprintf(stderr, "kg_engine_create: no HIP device %d (found %d)\n", e->device, ndev);
+        delete e;
+        return KG_ERR_HIP;
+    }
+    if (hipSetDevice(e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return KG_ERR_HIP;
+    }
+    e->own_stream = true;
+    *out = e;
+    return KG_OK;
+}
+
+void kg_engine_destroy(kg_engine *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->plane_mem) (void)hipFree(e->plane_mem);
+    if (e->pods) (void)hipFree(e->pods);
+    if (e->scratch) (void)hipFree(e->scratch);
+    if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+    for (int k = 0; k < kg_engine::kRing; k++) {
+        if (e->ev0[k]) (void)hipEventDestroy(e->ev0[k]);
+        if (e->ev1[k]) (void)hipEventDestroy(e->ev1[k]);
+    }
+    delete e;
+}
+
+const char *kg_last_error(const kg_engine *e) { return e ? e->err.c_str() : "null engine"; }
+
+kg_status kg_set_stream(kg_engine *e, void *s) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (e->own_stream) HIP_TRY(e, hipStreamDestroy(e->stream));
+    if (s) {
+        e->stream = (hipStream_t)s;
+        e->own_stream = false;
+    } else {
+        HIP_TRY(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        e->own_stream = true;
+    }
+    return KG_OK;
+}
+
+kg_status kg_sync(kg_engine *e) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return KG_OK;
+}
+
+kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (n_nodes < 0) return set_err(e, KG_ERR_INVALID_ARG, "negative node count");
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (e->plane_mem) HIP_TRY(e, hipFree(e->plane_mem));
+    e->plane_mem = nullptr;
+    const int64_t cap = ((int64_t)n_nodes + KG_TILE - 1) / KG_TILE * KG_TILE + (n_nodes == 0 ? KG_TILE : 0);
+    if (cap / KG_TILE > KG_MAX_TILES) return set_err(e, KG_ERR_RANGE, "too many nodes (max %d)", KG_MAX_TILES * KG_TILE);
+    char *p = nullptr;
+    auto carve = [&](size_t bytes) {
+        char *r = p;
+        p += (bytes + 255) / 256 * 256;
+        return r;
+    };
+    size_t total = 0;
+    const size_t sizes[] = {sizeof(kg_node_row) * (size_t)cap, (size_t)KG_NUM_RES * 8 * cap, (size_t)KG_NUM_RES * 8 * cap,
+                            (size_t)KG_NUM_RES * 8 * cap, 2 * 8 * (size_t)cap, 4 * 8 * (size_t)cap, 8 * (size_t)cap,
+                            4 * (size_t)cap, 4 * (size_t)cap};
+    for (size_t s : sizes) total += (s + 255) / 256 * 256;
+    HIP_TRY(e, hipMalloc(&e->plane_mem, total));
+    HIP_TRY(e, hipMemsetAsync(e->plane_mem, 0, total, e->stream));
+    p = (char *)e->plane_mem;
+    e->pl.rows = (kg_node_row *)carve(sizes[0]);
+    e->pl.free_ = (int64_t *)carve(sizes[1]);
+    e->pl.fit_R = (double *)carve(sizes[2]);
+    e->pl.fit_F = (double *)carve(sizes[3]);
+    e->pl.la_R = (double *)carve(sizes[4]);
+    e->pl.la_F = (double *)carve(sizes[5]);
+    e->pl.metric_ns = (int64_t *)carve(sizes[6]);
+    e->pl.dflags = (uint32_t *)carve(sizes[7]);
+    e->pl.fit_mask = (uint32_t *)carve(sizes[8]);
+    e->pl.cap = cap;
+    e->n_nodes = n_nodes;
+    e->shard_begin = 0;
+    e->shard_end = n_nodes;
+    hipLaunchKernelGGL(k_finalize_range, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, e->stream, e->consts, e->pl,
+                       (int64_t)0, cap);
+    HIP_TRY(e, hipGetLastError());
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return KG_OK;
+}
+
+kg_status kg_snapshot_upsert(kg_engine *e, const int32_t *node_index, const kg_node_row *rows, int32_t n) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (n < 0 || (n > 0 && (!node_index || !rows))) return set_err(e, KG_ERR_INVALID_ARG, "bad upsert arguments");
+    if (n == 0) return KG_OK;
+    if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised (kg_snapshot_reset)");
+    for (int32_t k = 0; k < n; k++)
+        if (node_index[k] < 0 || node_index[k] >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "node index %d out of range", node_index[k]);
+    const size_t rb = sizeof(kg_node_row) * (size_t)n, ib = sizeof(int32_t) * (size_t)n;
+    st = ensure_scratch(e, rb + ib + 256);
+    if (st) return st;
+    char *s = (char *)e->scratch;
+    HIP_TRY(e, hipMemcpyAsync(s, rows, rb, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(s + (rb + 255) / 256 * 256, node_index, ib, hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(k_upsert, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->consts, e->pl,
+                       (const kg_node_row *)s, (const int32_t *)(s + (rb + 255) / 256 * 256), n);
+    HIP_TRY(e, hipGetLastError());
+    HIP_TRY(e, hipStreamSynchronize(e->stream));  // staging buffer reuse
+    return KG_OK;
+}
+
+kg_status kg_snapshot_remove(kg_engine *e, int32_t node_index) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (node_index < 0 || node_index >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "node index out of range");
+    kg_node_row row;
+    memset(&row, 0, sizeof(row));  // flags = 0 → invalid, never feasible
+    return kg_snapshot_upsert(e, &node_index, &row, 1);
+}
+
+kg_status kg_snapshot_download(kg_engine *e, int32_t first, int32_t n, kg_node_row *out) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (first < 0 || n < 0 || first + (int64_t)n > e->n_nodes || (n > 0 && !out)) return set_err(e, KG_ERR_RANGE, "bad download range");
+    if (n == 0) return KG_OK;
+    HIP_TRY(e, hipMemcpyAsync(out, e->pl.rows + first, sizeof(kg_node_row) * (size_t)n, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return KG_OK;
+}
+
+kg_status kg_set_shard(kg_engine *e, int32_t begin, int32_t end) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (begin < 0 || end < begin || end > e->n_nodes || begin % KG_TILE) return set_err(e, KG_ERR_RANGE, "bad shard [%d,%d)", begin, end);
+    e->shard_begin = begin;
+    e->shard_end = end;
+    return KG_OK;
+}
+
+int32_t kg_num_tiles(const kg_engine *e) { return e ? (int32_t)tiles_total(e) : 0; }
+
+kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (n < 0 || (n > 0 && !rows)) return set_err(e, KG_ERR_INVALID_ARG, "bad pod batch");
+    std::vector<kg_pod_dev> dev((size_t)n);
+    BatchMasks bm{0, 0};
+    for (int32_t i = 0; i < n; i++) {
+        if (!kg_pod_row_in_bounds(rows[i])) return set_err(e, KG_ERR_RANGE, "pod %d: request outside the engine bounds", i);
+        kg_pod_dev_from_row(e->cfg, rows[i], dev[i]);
+        bm.cmp |= dev[i].cmp_mask;
+        bm.fit |= dev[i].fit_mask;
+    }
+    if (!(e->cfg.enabled_plugins & KG_PLUGIN_FIT)) bm.cmp = bm.fit = 0;
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (n > e->pods_cap) {
+        if (e->pods) HIP_TRY(e, hipFree(e->pods));
+        e->pods = nullptr;
+        e->pods_cap = 0;
+        HIP_TRY(e, hipMalloc(&e->pods, sizeof(kg_pod_dev) * (size_t)n));
+        e->pods_cap = n;
+    }
+    if (n) HIP_TRY(e, hipMemcpyAsync(e->pods, dev.data(), sizeof(kg_pod_dev) * (size_t)n, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->n_pods = n;
+    e->bm = bm;
+    return KG_OK;
+}
+
+kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (!out) return set_err(e, KG_ERR_INVALID_ARG, "null output");
+    if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised");
+    const int32_t P = e->n_pods;
+    const int64_t T = tiles_total(e);
+    const int64_t width = e->shard_end - e->shard_begin;
+    const size_t mask_b = (size_t)P * (size_t)((width + 63) / 64) * 8;
+    const size_t score_b = (size_t)P * (size_t)((width + 63) / 64 * 64) * 2;
+    const size_t part_b = (size_t)P * (size_t)T * 4;
+    const size_t top_b = (size_t)P * 8;
+    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+    const bool dev = out->out_on_device != 0;
+    size_t need = up(part_b) + up(top_b);
+    if (!dev) need += (out->mask ? up(mask_b) : 0) + (out->scores ? up(score_b) : 0);
+    st = ensure_scratch(e, need + 256);
+    if (st) return st;
+    char *s = (char *)e->scratch;
+    uint32_t *part = (uint32_t *)s;
+    unsigned long long *top = (unsigned long long *)(s + up(part_b));
+    char *q = s + up(part_b) + up(top_b);
+    uint64_t *mask = nullptr;
+    uint16_t *scores = nullptr;
+    if (out->mask) {
+        if (dev) mask = out->mask;
+        else { mask = (uint64_t *)q; q += up(mask_b); }
+    }
+    if (out->scores) {
+        if (dev) scores = (uint16_t *)out->scores;
+        else { scores = (uint16_t *)q; q += up(score_b); }
+    }
+    HIP_TRY(e, hipMemsetAsync(part, 0, part_b, e->stream));
+    st = launch_eval(e, now_ns, 0, P, mask, scores, part);
+    if (st) return st;
+    if (out->top1) {
+        unsigned long long *dst = dev ? (unsigned long long *)out->top1 : top;
+        if (P > 0) {
+            hipLaunchKernelGGL(k_top1, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, e->stream, part, (int32_t)T, P, dst);
+            HIP_TRY(e, hipGetLastError());
+        }
+        if (!dev && P > 0) HIP_TRY(e, hipMemcpyAsync(out->top1, top, top_b, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (!dev) {
+        if (out->mask && P > 0) HIP_TRY(e, hipMemcpyAsync(out->mask, mask, mask_b, hipMemcpyDeviceToHost, e->stream));
+        if (out->scores && P > 0) HIP_TRY(e, hipMemcpyAsync(out->scores, scores, score_b, hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+    }
+    return KG_OK;
+}
+
+kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (pod_begin < 0 || n < 0 || pod_begin + (int64_t)n > e->n_pods || (n > 0 && !partial_dev))
+        return set_err(e, KG_ERR_RANGE, "bad chunk");
+    HIP_TRY(e, hipMemsetAsync(partial_dev, 0, (size_t)n * (size_t)tiles_total(e) * 4, e->stream));
+    return launch_eval(e, now_ns, pod_begin, n, nullptr, nullptr, partial_dev);
+}
+
+kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, const uint32_t *partial_dev,
+                                 int32_t *out_node_dev, int64_t *out_score_dev) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (pod_begin < 0 || n < 0 || n > KG_MAX_CHUNK || pod_begin + (int64_t)n > e->n_pods)
+        return set_err(e, KG_ERR_RANGE, "bad chunk");
+    if (n == 0) return KG_OK;
+    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream, e->consts, e->pl, e->pods, pod_begin, n,
+                       partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev);
+    HIP_TRY(e, hipGetLastError());
+    return KG_OK;
+}
+
+kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (!out_node || !out_score) return set_err(e, KG_ERR_INVALID_ARG, "null outputs");
+    if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised");
+    if (e->shard_begin != 0 || e->shard_end != e->n_nodes)
+        return set_err(e, KG_ERR_STATE, "kg_place runs on the whole snapshot; use the chunk API for shards");
+    const int32_t P = e->n_pods;
+    if (P == 0) return KG_OK;
+    int32_t chunk = e->cfg.place_chunk > 0 ? e->cfg.place_chunk : 64;
+    if (chunk > KG_MAX_CHUNK) chunk = KG_MAX_CHUNK;
+    const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4;
+    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+    st = ensure_scratch(e, up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + 256);
+    if (st) return st;
+    char *s = (char *)e->scratch;
+    uint32_t *part = (uint32_t *)s;
+    int32_t *dnode = (int32_t *)(s + up(part_b));
+    int64_t *dscore = (int64_t *)(s + up(part_b) + up((size_t)P * 4));
+    for (int32_t b = 0; b < P; b += chunk) {
+        const int32_t n = P - b < chunk ? P - b : chunk;
+        st = kg_place_chunk_eval(e, now_ns, b, n, part);
+        if (st) return st;
+        st = kg_place_chunk_resolve(e, now_ns, b, n, part, dnode + b, dscore + b);
+        if (st) return st;
+    }
+    HIP_TRY(e, hipMemcpyAsync(out_node, dnode, (size_t)P * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(out_score, dscore, (size_t)P * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return KG_OK;
+}
+
+kg_status kg_set_profiling(kg_engine *e, int32_t on) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (on && !e->ev0[0]) {
+        for (int k = 0; k < kg_engine::kRing; k++) {
+            HIP_TRY(e, hipEventCreate(&e->ev0[k]));
+            HIP_TRY(e, hipEventCreate(&e->ev1[k]));
+        }
+    }
+    e->profiling = on != 0;
+    e->ev_count = 0;
+    return KG_OK;
+}
+
+int32_t kg_eval_kernel_times(kg_engine *e, float *ms, int32_t n) {
+    if (check_engine(e) != KG_OK || !ms || n < 0) return KG_ERR_INVALID_ARG;
+    if (!e->profiling) return set_err(e, KG_ERR_STATE, "profiling is off");
+    const int64_t have = e->ev_count < kg_engine::kRing ? e->ev_count : kg_engine::kRing;
+    const int32_t k = n < have ? n : (int32_t)have;
+    for (int32_t j = 0; j < k; j++) {
+        const int64_t slot = (e->ev_count - k + j) % kg_engine::kRing;
+        HIP_TRY(e, hipEventSynchronize(e->ev1[slot]));
+        HIP_TRY(e, hipEventElapsedTime(&ms[j], e->ev0[slot], e->ev1[slot]));
+    }
+    return k;
+}
+
+kg_status kg_commit(kg_engine *e, int32_t pod, int32_t node) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (pod < 0 || pod >= e->n_pods || node < 0 || node >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "bad commit");
+    hipLaunchKernelGGL(k_commit_one, dim3(1), dim3(1), 0, e->stream, e->consts, e->pl, e->pods, pod, node);
+    HIP_TRY(e, hipGetLastError());
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return KG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,189 @@
+"""Python handle on the HIP engine (``libkoordgpu.so``), used by the plugin mirror, tests and bench."""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _native as nat
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def _check(st: int, eng: Optional["Engine"] = None, what: str = "") -> None:
+    if st != 0:
+        msg = nat.lib().kg_last_error(eng._h).decode() if eng is not None and eng._h else ""
+        raise EngineError(f"{what} failed with status {st}: {msg}")
+
+
+def build_pod_rows(cfg: np.ndarray, view, pod_index: Sequence[int]) -> np.ndarray:
+    idx = np.ascontiguousarray(pod_index, dtype=np.int32)
+    out = np.zeros(len(idx), dtype=nat.POD_ROW)
+    _check(nat.lib().kg_build_pod_rows(nat.ptr(cfg), ctypes.byref(view.c_view), nat.ptr(idx), len(idx), nat.ptr(out)),
+           what="kg_build_pod_rows")
+    return out
+
+
+def build_node_rows(cfg: np.ndarray, view, node_index: Optional[Sequence[int]] = None) -> np.ndarray:
+    n = len(view.nodes)
+    idx = np.arange(n, dtype=np.int32) if node_index is None else np.ascontiguousarray(node_index, dtype=np.int32)
+    out = np.zeros(len(idx), dtype=nat.NODE_ROW)
+    _check(nat.lib().kg_build_node_rows(nat.ptr(cfg), ctypes.byref(view.c_view), nat.ptr(idx), len(idx), nat.ptr(out)),
+           what="kg_build_node_rows")
+    return out
+
+
+def row_commit(cfg: np.ndarray, node_row: np.ndarray, pod_row: np.ndarray) -> None:
+    _check(nat.lib().kg_row_commit(nat.ptr(cfg), nat.ptr(node_row), nat.ptr(pod_row)), what="kg_row_commit")
+
+
+class Engine:
+    """One engine = one GPU, one HIP stream, one HBM-resident node snapshot."""
+
+    def __init__(self, cfg: np.ndarray):
+        self.cfg = cfg.copy()
+        self._h = ctypes.c_void_p()
+        _check(nat.lib().kg_engine_create(nat.ptr(self.cfg), ctypes.byref(self._h)), what="kg_engine_create")
+        self.n_nodes = 0
+        self.n_pods = 0
+
+    # lifecycle --------------------------------------------------------------------------
+    def close(self) -> None:
+        if self._h:
+            nat.lib().kg_engine_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_stream(self, stream_ptr: int) -> None:
+        _check(nat.lib().kg_set_stream(self._h, ctypes.c_void_p(stream_ptr)), self, "kg_set_stream")
+
+    def sync(self) -> None:
+        _check(nat.lib().kg_sync(self._h), self, "kg_sync")
+
+    # snapshot ---------------------------------------------------------------------------
+    def load_snapshot(self, rows: np.ndarray) -> None:
+        rows = np.ascontiguousarray(rows, dtype=nat.NODE_ROW)
+        _check(nat.lib().kg_snapshot_reset(self._h, len(rows)), self, "kg_snapshot_reset")
+        self.n_nodes = len(rows)
+        self.shard = (0, len(rows))
+        self.upsert(np.arange(len(rows), dtype=np.int32), rows)
+
+    def upsert(self, idx, rows: np.ndarray) -> None:
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        rows = np.ascontiguousarray(rows, dtype=nat.NODE_ROW)
+        _check(nat.lib().kg_snapshot_upsert(self._h, nat.ptr(idx), nat.ptr(rows), len(idx)), self, "kg_snapshot_upsert")
+
+    def remove(self, i: int) -> None:
+        _check(nat.lib().kg_snapshot_remove(self._h, int(i)), self, "kg_snapshot_remove")
+
+    def download(self, first: int = 0, n: Optional[int] = None) -> np.ndarray:
+        n = self.n_nodes - first if n is None else n
+        out = np.zeros(n, dtype=nat.NODE_ROW)
+        _check(nat.lib().kg_snapshot_download(self._h, first, n, nat.ptr(out)), self, "kg_snapshot_download")
+        return out
+
+    def set_shard(self, begin: int, end: int) -> None:
+        _check(nat.lib().kg_set_shard(self._h, begin, end), self, "kg_set_shard")
+        self.shard = (begin, end)
+
+    def set_profiling(self, on: bool = True) -> None:
+        _check(nat.lib().kg_set_profiling(self._h, int(on)), self, "kg_set_profiling")
+
+    def eval_kernel_times(self, n: int = 256) -> np.ndarray:
+        """Durations (ms) of the last ≤ n profiled k_eval launches, oldest first."""
+        ms = np.zeros(n, dtype=np.float32)
+        k = nat.lib().kg_eval_kernel_times(self._h, nat.ptr(ms), n)
+        if k < 0:
+            _check(k, self, "kg_eval_kernel_times")
+        return ms[:k].astype(np.float64)
+
+    @property
+    def num_tiles(self) -> int:
+        return nat.lib().kg_num_tiles(self._h)
+
+    # pods -------------------------------------------------------------------------------
+    def set_pods(self, rows: np.ndarray) -> None:
+        rows = np.ascontiguousarray(rows, dtype=nat.POD_ROW)
+        _check(nat.lib().kg_pods_set(self._h, nat.ptr(rows), len(rows)), self, "kg_pods_set")
+        self.n_pods = len(rows)
+
+    # evaluation -------------------------------------------------------------------------
+    @property
+    def mask_words(self) -> int:
+        return (self.shard[1] - self.shard[0] + 63) // 64
+
+    @property
+    def score_stride(self) -> int:
+        return self.mask_words * 64
+
+    def eval(self, now_ns: int, mask: bool = True, scores: bool = True, top1: bool = True) -> dict:
+        """Matrix mode into host arrays: mask [P][words] u64, scores [P][stride][2] u8, top1 [P] u64."""
+        P = self.n_pods
+        res = {}
+        out = nat.EvalOut()
+        if mask:
+            res["mask"] = np.zeros((P, self.mask_words), dtype=np.uint64)
+            out.mask = res["mask"].ctypes.data
+        if scores:
+            res["scores"] = np.zeros((P, self.score_stride, 2), dtype=np.uint8)
+            out.scores = res["scores"].ctypes.data
+        if top1:
+            res["top1"] = np.zeros(P, dtype=np.uint64)
+            out.top1 = res["top1"].ctypes.data
+        out.out_on_device = 0
+        _check(nat.lib().kg_eval(self._h, int(now_ns), ctypes.byref(out)), self, "kg_eval")
+        return res
+
+    def eval_device(self, now_ns: int, mask_ptr: int = 0, scores_ptr: int = 0, top1_ptr: int = 0) -> None:
+        out = nat.EvalOut()
+        out.mask, out.scores, out.top1, out.out_on_device = mask_ptr or None, scores_ptr or None, top1_ptr or None, 1
+        _check(nat.lib().kg_eval(self._h, int(now_ns), ctypes.byref(out)), self, "kg_eval")
+
+    def place(self, now_ns: int):
+        P = self.n_pods
+        nodes = np.zeros(P, dtype=np.int32)
+        scores = np.zeros(P, dtype=np.int64)
+        _check(nat.lib().kg_place(self._h, int(now_ns), nat.ptr(nodes), nat.ptr(scores)), self, "kg_place")
+        return nodes, scores
+
+    def chunk_eval(self, now_ns: int, pod_begin: int, n: int, partial_ptr: int) -> None:
+        _check(nat.lib().kg_place_chunk_eval(self._h, int(now_ns), pod_begin, n, ctypes.c_void_p(partial_ptr)), self,
+               "kg_place_chunk_eval")
+
+    def chunk_resolve(self, now_ns: int, pod_begin: int, n: int, partial_ptr: int, node_ptr: int,
+                      score_ptr: int) -> None:
+        _check(nat.lib().kg_place_chunk_resolve(self._h, int(now_ns), pod_begin, n, ctypes.c_void_p(partial_ptr),
+                                                ctypes.c_void_p(node_ptr), ctypes.c_void_p(score_ptr)), self,
+               "kg_place_chunk_resolve")
+
+    def commit(self, pod: int, node: int) -> None:
+        _check(nat.lib().kg_commit(self._h, pod, node), self, "kg_commit")
+
+
+def decode_top1(keys: np.ndarray):
+    """(total+1) << 32 | (0xFFFFFFFF − node) → (node or −1, total or −1)."""
+    keys = np.asarray(keys, dtype=np.uint64)
+    ok = keys != 0
+    node = np.where(ok, (np.uint64(0xFFFFFFFF) - (keys & np.uint64(0xFFFFFFFF))).astype(np.int64), -1)
+    total = np.where(ok, (keys >> np.uint64(32)).astype(np.int64) - 1, -1)
+    return node, total
+
+
+def unpack_mask(mask: np.ndarray, n_nodes: int) -> np.ndarray:
+    """[P][words] u64 → [P][n_nodes] bool."""
+    b = np.unpackbits(mask.view(np.uint8), axis=1, bitorder="little")
+    return b[:, :n_nodes].astype(bool)

@@ -1,0 +1,363 @@
+"""Object model of the inputs the koord-scheduler plugins read, and its flattening into the
+C structs of ``include/koord_gpu.h`` (``kg_cluster_view``).
+
+This is the Python face of the drop-in boundary: a Go shim builds the same structs from its
+informer objects (corev1.Pod / corev1.Node / NodeInfo / slov1alpha1.NodeMetric and the
+LoadAware podAssignCache).  Quantities follow k8s ``resource.Quantity``: cpu is stored as
+``MilliValue()``, everything else as ``Value()`` (rounded up, as Quantity does).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+import re
+from fractions import Fraction
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as nat
+
+RES = {
+    "cpu": nat.RES_CPU,
+    "memory": nat.RES_MEMORY,
+    "ephemeral-storage": nat.RES_EPHEMERAL_STORAGE,
+    "kubernetes.io/batch-cpu": nat.RES_BATCH_CPU,
+    "kubernetes.io/batch-memory": nat.RES_BATCH_MEMORY,
+    "kubernetes.io/mid-cpu": nat.RES_MID_CPU,
+    "kubernetes.io/mid-memory": nat.RES_MID_MEMORY,
+    "example.com/gpu": nat.RES_EXTENDED,
+}
+BATCH_CPU = "kubernetes.io/batch-cpu"
+BATCH_MEMORY = "kubernetes.io/batch-memory"
+
+PRIORITY_CLASS = {"koord-prod": nat.PRIO_PROD, "koord-mid": nat.PRIO_MID, "koord-batch": nat.PRIO_BATCH,
+                  "koord-free": nat.PRIO_FREE}
+QOS_CLASS = {"LSE": nat.QOS_LSE, "LSR": nat.QOS_LSR, "LS": nat.QOS_LS, "BE": nat.QOS_BE, "SYSTEM": nat.QOS_SYSTEM}
+KUBE_QOS = {"": nat.KUBE_QOS_UNSET, "Guaranteed": nat.KUBE_QOS_GUARANTEED, "Burstable": nat.KUBE_QOS_BURSTABLE,
+            "BestEffort": nat.KUBE_QOS_BESTEFFORT}
+AGG = {"": nat.AGG_UNSET, "avg": nat.AGG_AVG, "p50": nat.AGG_P50, "p90": nat.AGG_P90, "p95": nat.AGG_P95,
+       "p99": nat.AGG_P99}
+
+PRIORITY_PROD_MAX, PRIORITY_PROD_MIN = 9999, 9000
+PRIORITY_MID_MAX, PRIORITY_MID_MIN = 7999, 7000
+PRIORITY_BATCH_MAX, PRIORITY_BATCH_MIN = 5999, 5000
+PRIORITY_FREE_MAX, PRIORITY_FREE_MIN = 3999, 3000
+
+_SUFFIX = {
+    "": 1, "m": Fraction(1, 1000), "k": 10**3, "M": 10**6, "G": 10**9, "T": 10**12, "P": 10**15, "E": 10**18,
+    "Ki": 2**10, "Mi": 2**20, "Gi": 2**30, "Ti": 2**40, "Pi": 2**50, "Ei": 2**60,
+}
+_QRE = re.compile(r"^([+-]?[0-9.]+)([eE][+-]?[0-9]+)?([a-zA-Z]*)$")
+
+
+def parse_quantity(s) -> Fraction:
+    """resource.MustParse → exact rational value in base units."""
+    if isinstance(s, (int, Fraction)):
+        return Fraction(s)
+    m = _QRE.match(str(s).strip())
+    if not m:
+        raise ValueError(f"bad quantity {s!r}")
+    num, exp, suf = m.groups()
+    v = Fraction(num)
+    if exp:
+        v *= Fraction(10) ** int(exp[1:])
+    if suf not in _SUFFIX:
+        raise ValueError(f"bad quantity suffix {s!r}")
+    return v * _SUFFIX[suf]
+
+
+def quantity_value(name: str, q) -> int:
+    """getResourceValue semantics: MilliValue for cpu, Value otherwise (ceil, as Quantity)."""
+    v = parse_quantity(q)
+    if name == "cpu":
+        v *= 1000
+    return int(math.ceil(v))
+
+
+def resource_list(d: Optional[Dict[str, object]]) -> np.ndarray:
+    out = np.zeros((), dtype=nat.RESOURCE_LIST)
+    for k, q in (d or {}).items():
+        r = RES[k]
+        out["v"][r] = quantity_value(k, q)
+        out["present"] |= np.uint32(1 << r)
+    return out
+
+
+@dataclasses.dataclass
+class Container:
+    requests: Dict[str, object] = dataclasses.field(default_factory=dict)
+    limits: Dict[str, object] = dataclasses.field(default_factory=dict)
+
+
+@dataclasses.dataclass
+class Pod:
+    namespace: str = "default"
+    name: str = ""
+    containers: List[Container] = dataclasses.field(default_factory=list)
+    init_containers: List[Container] = dataclasses.field(default_factory=list)
+    overhead: Optional[Dict[str, object]] = None
+    priority: Optional[int] = None
+    labels: Dict[str, str] = dataclasses.field(default_factory=dict)
+    qos_status: str = ""
+    daemonset: bool = False
+    terminated: bool = False
+    node_name: str = ""
+
+    @property
+    def key(self) -> str:
+        return f"{self.namespace}/{self.name}"
+
+
+@dataclasses.dataclass
+class Node:
+    name: str
+    allocatable: Dict[str, object] = dataclasses.field(default_factory=dict)
+    pods: int = 110
+    annotations_raw_allocatable: Optional[Dict[str, object]] = None   # node.koordinator.sh/raw-allocatable
+    custom_usage_thresholds: Optional[Dict[str, int]] = None          # scheduling.koordinator.sh/usage-thresholds
+    custom_prod_usage_thresholds: Optional[Dict[str, int]] = None
+    custom_aggregated: Optional[dict] = None   # {"usageThresholds": {...}, "usageAggregationType": "p95", "usageAggregatedDuration": seconds}
+
+
+@dataclasses.dataclass
+class NodeMetric:
+    update_time_s: Optional[float] = None             # Status.UpdateTime as seconds relative to `now` (None ⇒ nil)
+    report_interval_s: Optional[int] = None           # Spec.CollectPolicy.ReportIntervalSeconds
+    node_usage: Optional[Dict[str, object]] = None    # None ⇒ Status.NodeMetric == nil
+    aggregated: List[dict] = dataclasses.field(default_factory=list)  # [{"duration": s, "usage": {"p95": {...}}}]
+    pods_metric: List[dict] = dataclasses.field(default_factory=list)  # [{"namespace","name","usage": {...}}]
+
+
+class Cluster:
+    """Holds objects and flattens them into the C arrays of a ``kg_cluster_view``."""
+
+    def __init__(self, now_ns: int = 1_700_000_000 * 10**9):
+        self.now_ns = int(now_ns)
+        self.nodes: List[Node] = []
+        self.node_info: Dict[str, dict] = {}
+        self.metrics: Dict[str, NodeMetric] = {}
+        self.lister_pods: Dict[str, Pod] = {}
+        self.assigned: Dict[str, List[tuple]] = {}
+        self._names: Dict[str, int] = {}
+
+    # -- building -------------------------------------------------------------------------
+    def add_node(self, node: Node, requested: Optional[Dict[str, object]] = None,
+                 nonzero_requested: Optional[Dict[str, object]] = None, pod_count: int = 0) -> "Cluster":
+        self.nodes.append(node)
+        self.node_info[node.name] = {"requested": requested or {}, "nonzero": nonzero_requested, "pods": pod_count}
+        return self
+
+    def add_node_with_pods(self, node: Node, pods: Sequence[Pod]) -> "Cluster":
+        """NodeInfo built from pods (framework.NewNodeInfo(pods...))."""
+        req: Dict[str, int] = {}
+        nz = [0, 0]
+        for p in pods:
+            row = pod_request(p)
+            for k, r in RES.items():
+                if row["request"][r] or (r in (0, 1, 2)):
+                    req[k] = req.get(k, 0) + int(row["request"][r])
+            nz[0] += int(row["nonzero"][0])
+            nz[1] += int(row["nonzero"][1])
+        self.nodes.append(node)
+        self.node_info[node.name] = {"requested_raw": req, "nonzero_raw": nz, "pods": len(pods)}
+        return self
+
+    def set_metric(self, node_name: str, m: NodeMetric) -> "Cluster":
+        self.metrics[node_name] = m
+        return self
+
+    def add_lister_pod(self, pod: Pod) -> "Cluster":
+        self.lister_pods[pod.key] = pod
+        return self
+
+    def assign(self, node_name: str, pod: Pod, age_s: float) -> "Cluster":
+        """podAssignCache entry with timestamp now − age_s."""
+        self.assigned.setdefault(node_name, []).append((pod, age_s))
+        return self
+
+    def name_id(self, key: str) -> int:
+        return self._names.setdefault(key, len(self._names) + 1)
+
+    # -- flattening -----------------------------------------------------------------------
+    def view(self, extra_pods: Sequence[Pod] = ()) -> "FlatView":
+        fv = FlatView(self)
+        for p in self.lister_pods.values():
+            fv.pod_index(p)
+        for p in extra_pods:
+            fv.pod_index(p)
+        nodes = np.zeros(len(self.nodes), dtype=nat.NODE_SPEC)
+        for i, n in enumerate(self.nodes):
+            ns = nodes[i]
+            ns["allocatable"] = resource_list(n.allocatable)
+            info = self.node_info[n.name]
+            if "requested_raw" in info:
+                rl = np.zeros((), dtype=nat.RESOURCE_LIST)
+                for k, v in info["requested_raw"].items():
+                    rl["v"][RES[k]] = v
+                    rl["present"] |= np.uint32(1 << RES[k])
+                ns["requested"] = rl
+                ns["nonzero_requested"] = info["nonzero_raw"]
+            else:
+                ns["requested"] = resource_list(info["requested"])
+                nz = info["nonzero"]
+                if nz is None:
+                    ns["nonzero_requested"] = [ns["requested"]["v"][0], ns["requested"]["v"][1]]
+                else:
+                    ns["nonzero_requested"] = [quantity_value("cpu", nz.get("cpu", 0)),
+                                               quantity_value("memory", nz.get("memory", 0))]
+            ns["pod_count"] = info["pods"]
+            ns["allowed_pods"] = n.pods
+            if n.annotations_raw_allocatable is not None:
+                ns["raw_allocatable_state"] = 1
+                ns["raw_allocatable"] = resource_list(n.annotations_raw_allocatable)
+            if (n.custom_usage_thresholds or n.custom_prod_usage_thresholds or n.custom_aggregated) is not None:
+                ns["custom_thresholds_state"] = 1
+                ns["custom_usage_thresholds"] = _thresholds(n.custom_usage_thresholds)
+                ns["custom_prod_usage_thresholds"] = _thresholds(n.custom_prod_usage_thresholds)
+                if n.custom_aggregated is not None:
+                    ca = n.custom_aggregated
+                    ns["custom_has_aggregated"] = 1
+                    ns["custom_agg_usage_type"] = AGG[ca.get("usageAggregationType", "")]
+                    ns["custom_agg_usage_thresholds"] = _thresholds(ca.get("usageThresholds"))
+                    ns["custom_agg_duration_ns"] = int(ca.get("usageAggregatedDuration", 0) * 10**9)
+            m = self.metrics.get(n.name)
+            if m is not None:
+                ns["has_node_metric"] = 1
+                if m.update_time_s is not None:
+                    ns["has_update_time"] = 1
+                    ns["update_time_ns"] = self.now_ns + int(round(m.update_time_s * 10**9))
+                if m.report_interval_s is not None:
+                    ns["has_report_interval"] = 1
+                    ns["report_interval_seconds"] = m.report_interval_s
+                if m.node_usage is not None:
+                    ns["has_node_metric_info"] = 1
+                    ns["node_usage"] = resource_list(m.node_usage)
+                ns["first_aggregated"] = len(fv.aggregated)
+                for a in m.aggregated:
+                    rec = np.zeros((), dtype=nat.AGGREGATED_USAGE)
+                    rec["duration_ns"] = int(a["duration"] * 10**9)
+                    for t, u in a["usage"].items():
+                        rec["usage"][AGG[t]] = resource_list(u)
+                    fv.aggregated.append(rec)
+                ns["n_aggregated"] = len(m.aggregated)
+                ns["first_pod_metric"] = len(fv.pod_metrics)
+                for pm in m.pods_metric:
+                    rec = np.zeros((), dtype=nat.POD_METRIC)
+                    key = f"{pm.get('namespace', 'default')}/{pm['name']}"
+                    rec["name_id"] = self.name_id(key)
+                    lp = self.lister_pods.get(key)
+                    rec["lister_pod"] = fv.pod_index(lp) if lp is not None else -1
+                    rec["usage"] = resource_list(pm["usage"])
+                    fv.pod_metrics.append(rec)
+                ns["n_pod_metric"] = len(m.pods_metric)
+            ns["first_assigned"] = len(fv.assigned)
+            for pod, age in self.assigned.get(n.name, []):
+                rec = np.zeros((), dtype=nat.ASSIGNED_POD)
+                rec["pod"] = fv.pod_index(pod)
+                rec["timestamp_ns"] = self.now_ns - int(round(age * 10**9))
+                fv.assigned.append(rec)
+            ns["n_assigned"] = len(self.assigned.get(n.name, []))
+        fv.nodes = nodes
+        return fv.finish()
+
+
+def _thresholds(d: Optional[Dict[str, int]]) -> np.ndarray:
+    out = np.zeros((), dtype=nat.RESOURCE_LIST)
+    for k, v in (d or {}).items():
+        out["v"][RES[k]] = int(v)
+        out["present"] |= np.uint32(1 << RES[k])
+    return out
+
+
+def pod_spec_record(p: Pod, containers: list, name_id: int) -> np.ndarray:
+    rec = np.zeros((), dtype=nat.POD_SPEC)
+    rec["first_container"] = len(containers)
+    for c in p.containers:
+        containers.append((resource_list(c.requests), resource_list(c.limits)))
+    rec["n_containers"] = len(p.containers)
+    rec["first_init_container"] = len(containers)
+    for c in p.init_containers:
+        containers.append((resource_list(c.requests), resource_list(c.limits)))
+    rec["n_init_containers"] = len(p.init_containers)
+    if p.overhead is not None:
+        rec["overhead"] = resource_list(p.overhead)
+    if p.priority is not None:
+        rec["has_priority"] = 1
+        rec["priority"] = p.priority
+    pc = p.labels.get("koordinator.sh/priority-class")
+    rec["label_priority_class"] = -1 if pc is None else PRIORITY_CLASS.get(pc, nat.PRIO_NONE)
+    q = p.labels.get("koordinator.sh/qosClass")
+    rec["label_qos"] = -1 if q is None else QOS_CLASS.get(q, nat.QOS_NONE)
+    rec["status_qos"] = KUBE_QOS[p.qos_status]
+    rec["is_daemonset"] = int(p.daemonset)
+    rec["is_terminated"] = int(p.terminated)
+    rec["name_id"] = name_id
+    return rec
+
+
+def pod_request(p: Pod) -> dict:
+    """Fit request / nonzero request of a pod (for NodeInfo built from pods)."""
+    req = np.zeros(nat.NUM_RES, dtype=np.int64)
+    for c in p.containers:
+        rl = resource_list(c.requests)
+        for r in range(nat.NUM_RES):
+            if rl["present"] >> r & 1:
+                req[r] += rl["v"][r]
+    nz = [0, 0]
+    for c in p.containers:
+        rl = resource_list(c.requests)
+        nz[0] += int(rl["v"][0]) if rl["present"] & 1 else 100
+        nz[1] += int(rl["v"][1]) if rl["present"] & 2 else 200 * 1024 * 1024
+    return {"request": req, "nonzero": nz}
+
+
+class FlatView:
+    """Owns the numpy arrays behind one ``kg_cluster_view``."""
+
+    def __init__(self, cluster: Cluster):
+        self.cluster = cluster
+        self._pods: List[np.ndarray] = []
+        self._containers: list = []
+        self._index: Dict[int, int] = {}
+        self.aggregated: List[np.ndarray] = []
+        self.pod_metrics: List[np.ndarray] = []
+        self.assigned: List[np.ndarray] = []
+        self.nodes = None
+
+    def pod_index(self, p: Pod) -> int:
+        k = id(p)
+        if k not in self._index:
+            self._index[k] = len(self._pods)
+            self._pods.append(pod_spec_record(p, self._containers, self.cluster.name_id(p.key)))
+        return self._index[k]
+
+    def finish(self) -> "FlatView":
+        self.pods = _stack(self._pods, nat.POD_SPEC)
+        cont = np.zeros(len(self._containers), dtype=nat.CONTAINER)
+        for i, (rq, lm) in enumerate(self._containers):
+            cont[i]["requests"] = rq
+            cont[i]["limits"] = lm
+        self.containers = cont
+        self.aggregated_arr = _stack(self.aggregated, nat.AGGREGATED_USAGE)
+        self.pod_metrics_arr = _stack(self.pod_metrics, nat.POD_METRIC)
+        self.assigned_arr = _stack(self.assigned, nat.ASSIGNED_POD)
+        self.c_view = nat.make_view(self.pods, self.containers, self.nodes, self.aggregated_arr, self.pod_metrics_arr,
+                                    self.assigned_arr)
+        return self
+
+    def add_pods(self, pods: Sequence[Pod]) -> List[int]:
+        """Append pending pods after finish(); returns their indices."""
+        idx = [self.pod_index(p) for p in pods]
+        return self.refresh(idx)
+
+    def refresh(self, idx):
+        self.finish()
+        return idx
+
+
+def _stack(recs: List[np.ndarray], dtype) -> np.ndarray:
+    out = np.zeros(len(recs), dtype=dtype)
+    for i, r in enumerate(recs):
+        out[i] = r
+    return out

@@ -1,0 +1,744 @@
+/*
+ * koord_oracle.c — CPU restatement of the koord-scheduler Filter/Score path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP engine
+ * (koordinator_amd/csrc).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product path never does.
+ *
+ * It follows the reference (PeterChg/koordinator @ 2025-01-12) object by
+ * object, per (pod, node), without any of the engine's precomputation:
+ *   LoadAwareScheduling  pkg/scheduler/plugins/loadaware/load_aware.go:123-397,
+ *                        helper.go:36-196, estimator/default_estimator.go:57-129
+ *   priority / QoS       apis/extension/priority.go:71-101, priority_utils.go:26-47,
+ *                        qos_utils.go:32-78, resource.go:53-58
+ *   NodeResourcesFit     upstream k8s.io/kubernetes v1.24.15 (module absent here):
+ *                        fit.go computePodResourceRequest/fitsRequest (in-repo mirrors
+ *                        reservation/transformer.go:316-346, reservation/plugin.go:427-476),
+ *                        resource_allocation.go + least_allocated.go / most_allocated.go
+ *                        (in-repo mirrors nodenumaresource/scoring.go:187-226,
+ *                        least_allocated.go:30-58, most_allocated.go:30-62)
+ *   cycle                upstream scheduleOne/findNodesThatFitPod/prioritizeNodes/selectHost
+ *                        with percentageOfNodesToScore = 100 and selectHost's random tie-break
+ *                        replaced by the lowest node index; Reserve =
+ *                        NodeInfo.AddPod (mirror reservation/transformer.go:293-306) +
+ *                        podAssignCache.assign (loadaware/pod_assign_cache.go:53-68).
+ * Parity pinning: the LoadAware Filter/Score known-answer tests of the reference
+ * (load_aware_test.go) are transcribed in tests/golden/; NodeResourcesFit has no
+ * reference test in the tree (parity unpinned beyond its in-repo mirrors).
+ * Built with -ffp-contract=off so float64 expressions round like Go's.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/koord_gpu.h"
+
+#define MAX_NODE_SCORE 100
+
+/* ---------------------------------------------------------------- */
+/* small resource-list helpers (k8s Quantity restricted to int64)     */
+/* ---------------------------------------------------------------- */
+static int is_scalar(int r) { return (KG_SCALAR_RES_MASK >> r) & 1u; }
+static int has(const kg_resource_list *l, int r) { return (l->present >> r) & 1u; }
+static int64_t get(const kg_resource_list *l, int r) { return has(l, r) ? l->v[r] : 0; }
+/* Quantity.MilliValue() of the stored value */
+static int64_t milli(int r, int64_t v) { return r == KG_RES_CPU ? v : v * 1000; }
+static int list_len(const kg_resource_list *l) { return __builtin_popcount(l->present); }
+
+static void rl_add(kg_resource_list *dst, const kg_resource_list *src) { /* quotav1.Add / util.AddResourceList */
+    for (int r = 0; r < KG_NUM_RES; r++)
+        if (has(src, r)) {
+            dst->v[r] = (has(dst, r) ? dst->v[r] : 0) + src->v[r];
+            dst->present |= 1u << r;
+        }
+}
+static void rl_max(kg_resource_list *dst, const kg_resource_list *src) { /* maxResourceList */
+    for (int r = 0; r < KG_NUM_RES; r++)
+        if (has(src, r)) {
+            if (!has(dst, r) || src->v[r] > dst->v[r]) dst->v[r] = src->v[r];
+            dst->present |= 1u << r;
+        }
+}
+
+/* ---------------------------------------------------------------- */
+/* pod classification                                                */
+/* ---------------------------------------------------------------- */
+/* resourceapi.PodRequestsAndLimits (k8s v1.24.15 pkg/api/v1/resource) */
+static void pod_requests_and_limits(const kg_cluster_view *v, const kg_pod_spec *p,
+                                    kg_resource_list *req, kg_resource_list *lim) {
+    memset(req, 0, sizeof(*req));
+    memset(lim, 0, sizeof(*lim));
+    for (int c = 0; c < p->n_containers; c++) {
+        const kg_container *ct = &v->containers[p->first_container + c];
+        rl_add(req, &ct->requests);
+        rl_add(lim, &ct->limits);
+    }
+    for (int c = 0; c < p->n_init_containers; c++) {
+        const kg_container *ct = &v->containers[p->first_init_container + c];
+        rl_max(req, &ct->requests);
+        rl_max(lim, &ct->limits);
+    }
+    if (p->overhead.present) {
+        rl_add(req, &p->overhead);
+        /* limits get overhead only for keys already present in limits */
+        for (int r = 0; r < KG_NUM_RES; r++)
+            if (has(&p->overhead, r) && has(lim, r)) lim->v[r] += p->overhead.v[r];
+    }
+}
+
+/* v1qos.GetPodQOS (k8s v1.24.15 pkg/apis/core/v1/helper/qos) — cpu & memory only */
+static int kube_qos(const kg_cluster_view *v, const kg_pod_spec *p) {
+    if (p->status_qos != KG_KUBE_QOS_UNSET) return p->status_qos;
+    int64_t req[2] = {0, 0}, lim[2] = {0, 0};
+    int req_has[2] = {0, 0}, lim_has[2] = {0, 0};
+    int guaranteed = 1;
+    int total = p->n_containers + p->n_init_containers;
+    for (int i = 0; i < total; i++) {
+        const kg_container *ct = i < p->n_containers ? &v->containers[p->first_container + i]
+                                                     : &v->containers[p->first_init_container + i - p->n_containers];
+        int limits_found = 0;
+        for (int r = 0; r < 2; r++) {
+            if (has(&ct->requests, r) && ct->requests.v[r] > 0) { req[r] += ct->requests.v[r]; req_has[r] = 1; }
+            if (has(&ct->limits, r) && ct->limits.v[r] > 0) { lim[r] += ct->limits.v[r]; lim_has[r] = 1; limits_found |= 1 << r; }
+        }
+        if (limits_found != 3) guaranteed = 0;
+    }
+    if (!req_has[0] && !req_has[1] && !lim_has[0] && !lim_has[1]) return KG_KUBE_QOS_BESTEFFORT;
+    if (guaranteed) {
+        for (int r = 0; r < 2; r++)
+            if (req_has[r] && (!lim_has[r] || lim[r] != req[r])) { guaranteed = 0; break; }
+    }
+    if (guaranteed && (req_has[0] + req_has[1]) == (lim_has[0] + lim_has[1])) return KG_KUBE_QOS_GUARANTEED;
+    return KG_KUBE_QOS_BURSTABLE;
+}
+
+/* GetPodQoSClassWithDefault (qos_utils.go:32-78) */
+static int koord_qos(const kg_cluster_view *v, const kg_pod_spec *p) {
+    if (p->label_qos >= 0 && p->label_qos != KG_QOS_NONE) return p->label_qos;
+    switch (kube_qos(v, p)) {
+    case KG_KUBE_QOS_GUARANTEED: return KG_QOS_LSR; /* QoSClassForGuaranteed */
+    case KG_KUBE_QOS_BURSTABLE: return KG_QOS_LS;
+    case KG_KUBE_QOS_BESTEFFORT: return KG_QOS_BE;
+    }
+    return KG_QOS_NONE;
+}
+
+/* GetPodPriorityClassWithDefault (priority_utils.go:26-47, priority.go:71-101) */
+int kgo_priority_class(const kg_cluster_view *v, const kg_pod_spec *p) {
+    int pc = KG_PRIO_NONE;
+    if (p->label_priority_class >= 0) {
+        pc = p->label_priority_class;
+    } else if (p->has_priority) {
+        int32_t x = p->priority;
+        if (x >= 9000 && x <= 9999) pc = KG_PRIO_PROD;
+        else if (x >= 7000 && x <= 7999) pc = KG_PRIO_MID;
+        else if (x >= 5000 && x <= 5999) pc = KG_PRIO_BATCH;
+        else if (x >= 3000 && x <= 3999) pc = KG_PRIO_FREE;
+        else pc = KG_PRIO_NONE; /* DefaultPriorityClass */
+    }
+    if (pc != KG_PRIO_NONE) return pc;
+    switch (koord_qos(v, p)) {
+    case KG_QOS_SYSTEM: case KG_QOS_LSE: case KG_QOS_LSR: case KG_QOS_LS: return KG_PRIO_PROD;
+    case KG_QOS_BE: return KG_PRIO_BATCH;
+    }
+    return KG_PRIO_NONE;
+}
+
+/* TranslateResourceNameByPriorityClass (resource.go:53-58); -1 ⇔ the empty resource name */
+static int translate(int pc, int r) {
+    if (pc == KG_PRIO_PROD || pc == KG_PRIO_NONE) return r;
+    if (pc == KG_PRIO_BATCH) return r == KG_RES_CPU ? KG_RES_BATCH_CPU : r == KG_RES_MEMORY ? KG_RES_BATCH_MEMORY : -1;
+    if (pc == KG_PRIO_MID) return r == KG_RES_CPU ? KG_RES_MID_CPU : r == KG_RES_MEMORY ? KG_RES_MID_MEMORY : -1;
+    return -1; /* koord-free has no mapping → "" */
+}
+
+/* ---------------------------------------------------------------- */
+/* LoadAwareScheduling                                               */
+/* ---------------------------------------------------------------- */
+/* estimatedUsedByResource (default_estimator.go:73-108) */
+static int64_t estimated_used_by_resource(const kg_resource_list *req, const kg_resource_list *lim, int r,
+                                          int64_t scaling) {
+    if (r < 0) return 0; /* resource "" : both quantities zero, no default branch */
+    int64_t limit = get(lim, r), request = get(req, r);
+    int64_t q;
+    if (limit > request) { scaling = 100; q = limit; } else q = request;
+    if (q == 0) {
+        if (r == KG_RES_CPU || r == KG_RES_BATCH_CPU) return 250;
+        if (r == KG_RES_MEMORY || r == KG_RES_BATCH_MEMORY) return 200LL * 1024 * 1024;
+        return 0;
+    }
+    int64_t est = (int64_t)round((double)q * (double)scaling / 100.0);
+    if (limit > 0 && est > limit) est = limit;
+    return est;
+}
+
+/* EstimatePod (default_estimator.go:57-70): returns values for every weighted resource */
+static void estimate_pod(const kg_config *cfg, const kg_cluster_view *v, const kg_pod_spec *p, int64_t out[KG_NUM_RES],
+                         uint32_t *keys) {
+    kg_resource_list req, lim;
+    pod_requests_and_limits(v, p, &req, &lim);
+    int pc = kgo_priority_class(v, p);
+    *keys = 0;
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        out[r] = 0;
+        if (cfg->la_resource_weight[r] == 0) continue;
+        out[r] = estimated_used_by_resource(&req, &lim, translate(pc, r), cfg->la_scaling_factor[r]);
+        *keys |= 1u << r;
+    }
+}
+
+/* EstimateNode (default_estimator.go:110-129) */
+static void estimate_node(const kg_node_spec *n, kg_resource_list *out) {
+    *out = n->allocatable;
+    if (n->raw_allocatable_state != 1 || n->raw_allocatable.present == 0) return;
+    int equal = n->raw_allocatable.present == n->allocatable.present;
+    for (int r = 0; equal && r < KG_NUM_RES; r++)
+        if (has(&n->raw_allocatable, r) && n->raw_allocatable.v[r] != n->allocatable.v[r]) equal = 0;
+    if (equal) return;
+    for (int r = 0; r < KG_NUM_RES; r++)
+        if (has(&n->raw_allocatable, r)) { out->v[r] = n->raw_allocatable.v[r]; out->present |= 1u << r; }
+}
+
+/* isNodeMetricExpired (helper.go:36-41) */
+static int metric_expired(const kg_node_spec *n, int64_t exp_s, int64_t now_ns) {
+    return !n->has_update_time || (exp_s > 0 && now_ns - n->update_time_ns >= exp_s * 1000000000LL);
+}
+
+/* getTargetAggregatedUsage (helper.go:58-90); NULL ⇔ nil */
+static const kg_resource_list *target_aggregated_usage(const kg_cluster_view *v, const kg_node_spec *n,
+                                                       int64_t duration_ns, int type) {
+    if (!n->has_node_metric_info || n->n_aggregated == 0) return NULL;
+    const kg_aggregated_usage *a = &v->aggregated[n->first_aggregated];
+    if (duration_ns == 0) {
+        int64_t maxd = 0;
+        int maxi = 0;
+        for (int i = 0; i < n->n_aggregated; i++)
+            if (a[i].duration_ns > maxd) { maxd = a[i].duration_ns; maxi = i; }
+        const kg_resource_list *u = &a[maxi].usage[type];
+        return list_len(u) > 0 ? u : NULL;
+    }
+    for (int i = 0; i < n->n_aggregated; i++)
+        if (a[i].duration_ns == duration_ns) {
+            const kg_resource_list *u = &a[i].usage[type];
+            if (list_len(u) > 0) return u;
+        }
+    return NULL;
+}
+
+typedef struct {
+    kg_resource_list usage, prod;
+    int has_agg;
+    kg_resource_list agg_thr;
+    int agg_type;
+    int64_t agg_duration_ns;
+} filter_profile;
+
+static int filter_with_aggregation(const kg_config *c) {
+    return c->la_has_aggregated && list_len(&c->la_agg_usage_thresholds) > 0 && c->la_agg_usage_type != KG_AGG_UNSET;
+}
+
+/* generateUsageThresholdsFilterProfile (helper.go:102-140) */
+static void filter_profile_of(const kg_config *c, const kg_node_spec *n, filter_profile *fp) {
+    memset(fp, 0, sizeof(*fp));
+    if (n->custom_thresholds_state == -1) { /* unmarshal error */
+        fp->usage = c->la_usage_thresholds;
+        fp->prod = c->la_prod_usage_thresholds;
+    } else {
+        if (n->custom_thresholds_state == 1) {
+            fp->usage = n->custom_usage_thresholds;
+            fp->prod = n->custom_prod_usage_thresholds;
+            if (n->custom_has_aggregated) {
+                fp->has_agg = 1;
+                fp->agg_thr = n->custom_agg_usage_thresholds;
+                fp->agg_type = n->custom_agg_usage_type;
+                fp->agg_duration_ns = n->custom_agg_duration_ns;
+            }
+        }
+        if (list_len(&fp->usage) == 0) fp->usage = c->la_usage_thresholds;
+        if (list_len(&fp->prod) == 0) fp->prod = c->la_prod_usage_thresholds;
+        if (fp->has_agg && (list_len(&fp->agg_thr) == 0 || fp->agg_type == KG_AGG_UNSET)) fp->has_agg = 0;
+        if (fp->has_agg) return;
+    }
+    if (filter_with_aggregation(c)) {
+        fp->has_agg = 1;
+        fp->agg_thr = c->la_agg_usage_thresholds;
+        fp->agg_type = c->la_agg_usage_type;
+        fp->agg_duration_ns = c->la_agg_usage_duration_ns;
+    }
+}
+
+static int64_t usage_percent(int r, int64_t used, int64_t total) { /* load_aware.go:214,248 */
+    return (int64_t)round((double)milli(r, used) / (double)milli(r, total) * 100.0);
+}
+
+/* filterNodeUsage (load_aware.go:173-224): 1 ⇔ pass */
+static int filter_node_usage(const kg_cluster_view *v, const kg_node_spec *n, const filter_profile *fp) {
+    if (!n->has_node_metric_info) return 1;
+    const kg_resource_list *thr = fp->has_agg ? &fp->agg_thr : &fp->usage;
+    kg_resource_list alloc;
+    estimate_node(n, &alloc);
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        if (!has(thr, r) || thr->v[r] == 0) continue;
+        int64_t total = get(&alloc, r);
+        if (total == 0) continue;
+        const kg_resource_list *nu = fp->has_agg ? target_aggregated_usage(v, n, fp->agg_duration_ns, fp->agg_type)
+                                                 : &n->node_usage;
+        if (!nu) continue;
+        if (usage_percent(r, get(nu, r), total) >= thr->v[r]) return 0;
+    }
+    return 1;
+}
+
+/* buildPodMetricMap (helper.go:153-170): map name → usage, later duplicates overwrite */
+typedef struct { int64_t name; const kg_resource_list *usage; } pm_entry;
+static int build_pod_metric_map(const kg_cluster_view *v, const kg_node_spec *n, int filter_prod, pm_entry *out) {
+    int cnt = 0;
+    for (int i = 0; i < n->n_pod_metric; i++) {
+        const kg_pod_metric *m = &v->pod_metrics[n->first_pod_metric + i];
+        if (m->lister_pod < 0) continue;
+        if (filter_prod && kgo_priority_class(v, &v->pods[m->lister_pod]) != KG_PRIO_PROD) continue;
+        int k;
+        for (k = 0; k < cnt; k++)
+            if (out[k].name == m->name_id) break;
+        out[k].name = m->name_id;
+        out[k].usage = &m->usage;
+        if (k == cnt) cnt++;
+    }
+    return cnt;
+}
+
+/* filterProdUsage (load_aware.go:226-254) */
+static int filter_prod_usage(const kg_cluster_view *v, const kg_node_spec *n, const kg_resource_list *thr) {
+    if (n->n_pod_metric == 0) return 1;
+    pm_entry *pm = (pm_entry *)malloc(sizeof(pm_entry) * (size_t)n->n_pod_metric);
+    int cnt = build_pod_metric_map(v, n, 1, pm);
+    kg_resource_list prod_usage;
+    memset(&prod_usage, 0, sizeof(prod_usage));
+    for (int i = 0; i < cnt; i++) rl_add(&prod_usage, pm[i].usage);
+    free(pm);
+    kg_resource_list alloc;
+    estimate_node(n, &alloc);
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        if (!has(thr, r) || thr->v[r] == 0) continue;
+        int64_t total = get(&alloc, r);
+        if (total == 0) continue;
+        if (usage_percent(r, get(&prod_usage, r), total) >= thr->v[r]) return 0;
+    }
+    return 1;
+}
+
+/* LoadAware.Filter (load_aware.go:123-171): returns framework code */
+int kgo_loadaware_filter(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod,
+                         const kg_node_spec *n, int64_t now_ns) {
+    if (pod->is_daemonset) return KG_CODE_SUCCESS;
+    if (!n->has_node_metric) return KG_CODE_SUCCESS;
+    if (c->la_filter_expired_node_metrics && c->la_has_expiration &&
+        metric_expired(n, c->la_expiration_seconds, now_ns))
+        return KG_CODE_SUCCESS;
+    filter_profile fp;
+    filter_profile_of(c, n, &fp);
+    if (list_len(&fp.prod) > 0 && kgo_priority_class(v, pod) == KG_PRIO_PROD) {
+        if (!filter_prod_usage(v, n, &fp.prod)) return KG_CODE_UNSCHEDULABLE;
+    } else {
+        const kg_resource_list *thr = fp.has_agg ? &fp.agg_thr : &fp.usage;
+        if (list_len(thr) > 0 && !filter_node_usage(v, n, &fp)) return KG_CODE_UNSCHEDULABLE;
+    }
+    return KG_CODE_SUCCESS;
+}
+
+/* an assigned pod of the podAssignCache (original view entries + oracle reservations) */
+typedef struct { const kg_pod_spec *pod; int64_t ts; } assigned_ref;
+
+static int score_with_aggregation(const kg_config *c) { return c->la_has_aggregated && c->la_agg_score_type != KG_AGG_UNSET; }
+
+/* LoadAware.Score (load_aware.go:269-335) + estimatedAssignedPodUsed (:337-376) */
+static int64_t loadaware_score_impl(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod,
+                                    const kg_node_spec *n, const assigned_ref *assigned, int n_assigned,
+                                    int64_t now_ns) {
+    if (!n->has_node_metric) return 0;
+    if (c->la_has_expiration && metric_expired(n, c->la_expiration_seconds, now_ns)) return 0;
+    int prod_pod = kgo_priority_class(v, pod) == KG_PRIO_PROD && c->la_score_according_prod_usage;
+    pm_entry *pm = (pm_entry *)malloc(sizeof(pm_entry) * (size_t)(n->n_pod_metric + 1));
+    int pm_cnt = build_pod_metric_map(v, n, prod_pod, pm);
+
+    int64_t used[KG_NUM_RES];
+    uint32_t keys;
+    estimate_pod(c, v, pod, used, &keys);
+
+    /* estimatedAssignedPodUsed */
+    int64_t update_ns = n->has_update_time ? n->update_time_ns : INT64_MIN; /* zero time.Time */
+    int64_t interval_ns = (n->has_report_interval ? n->report_interval_seconds : 60) * 1000000000LL;
+    const kg_resource_list *agg_score =
+        score_with_aggregation(c) ? target_aggregated_usage(v, n, c->la_agg_score_duration_ns, c->la_agg_score_type) : NULL;
+    int64_t *est_names = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n_assigned + 1));
+    int n_est = 0;
+    for (int i = 0; i < n_assigned; i++) {
+        const kg_pod_spec *ap = assigned[i].pod;
+        if (prod_pod && kgo_priority_class(v, ap) != KG_PRIO_PROD) continue;
+        const kg_resource_list *pu = NULL;
+        for (int k = 0; k < pm_cnt; k++)
+            if (pm[k].name == ap->name_id) pu = pm[k].usage;
+        int64_t ts = assigned[i].ts;
+        int missed = ts > update_ns;                                          /* missedLatestUpdateTime */
+        int in_interval = ts < update_ns && (update_ns - ts) < interval_ns;  /* stillInTheReportInterval */
+        if (pu == NULL || list_len(pu) == 0 || missed || in_interval || (score_with_aggregation(c) && agg_score == NULL)) {
+            int64_t est[KG_NUM_RES];
+            uint32_t ek;
+            estimate_pod(c, v, ap, est, &ek);
+            for (int r = 0; r < KG_NUM_RES; r++) {
+                if (!((ek >> r) & 1u)) continue;
+                int64_t val = est[r];
+                if (pu && has(pu, r) && pu->v[r] > val) val = pu->v[r];
+                used[r] += val;
+            }
+            est_names[n_est++] = ap->name_id;
+        }
+    }
+    /* sumPodUsages (helper.go:172-186) */
+    kg_resource_list pod_usages, est_usages;
+    memset(&pod_usages, 0, sizeof(pod_usages));
+    memset(&est_usages, 0, sizeof(est_usages));
+    for (int k = 0; k < pm_cnt; k++) {
+        int is_est = 0;
+        for (int e = 0; e < n_est; e++)
+            if (est_names[e] == pm[k].name) is_est = 1;
+        rl_add(is_est ? &est_usages : &pod_usages, pm[k].usage);
+    }
+    if (prod_pod) {
+        for (int r = 0; r < KG_NUM_RES; r++)
+            if (has(&pod_usages, r)) used[r] += pod_usages.v[r];
+    } else if (n->has_node_metric_info) {
+        const kg_resource_list *nu = score_with_aggregation(c) ? agg_score : &n->node_usage;
+        if (nu) {
+            for (int r = 0; r < KG_NUM_RES; r++) {
+                if (!has(nu, r)) continue;
+                int64_t q = nu->v[r];
+                int64_t e = get(&est_usages, r);
+                if (e != 0 && q >= e) q -= e;
+                used[r] += q;
+            }
+        }
+    }
+    free(pm);
+    free(est_names);
+
+    kg_resource_list alloc;
+    estimate_node(n, &alloc);
+    /* loadAwareSchedulingScorer (load_aware.go:378-397) */
+    int64_t score = 0, wsum = 0;
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        int64_t w = c->la_resource_weight[r];
+        if (w == 0) continue;
+        int64_t cap = get(&alloc, r), req = used[r], s;
+        if (cap == 0 || req > cap) s = 0;
+        else s = ((cap - req) * MAX_NODE_SCORE) / cap;
+        score += s * w;
+        wsum += w;
+    }
+    return wsum ? score / wsum : 0;
+}
+
+static int gather_assigned(const kg_cluster_view *v, const kg_node_spec *n, assigned_ref *out) {
+    for (int i = 0; i < n->n_assigned; i++) {
+        const kg_assigned_pod *a = &v->assigned[n->first_assigned + i];
+        out[i].pod = &v->pods[a->pod];
+        out[i].ts = a->timestamp_ns;
+    }
+    return n->n_assigned;
+}
+
+int64_t kgo_loadaware_score(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod,
+                            const kg_node_spec *n, int64_t now_ns) {
+    assigned_ref *a = (assigned_ref *)malloc(sizeof(assigned_ref) * (size_t)(n->n_assigned + 1));
+    int na = gather_assigned(v, n, a);
+    int64_t s = loadaware_score_impl(c, v, pod, n, a, na, now_ns);
+    free(a);
+    return s;
+}
+
+/* ---------------------------------------------------------------- */
+/* NodeResourcesFit (upstream v1.24.15)                              */
+/* ---------------------------------------------------------------- */
+typedef struct { int64_t v[KG_NUM_RES]; uint32_t scalar_keys; } fw_resource; /* framework.Resource */
+
+/* computePodResourceRequest: Σ containers, max init containers, + overhead */
+static void fit_pod_request(const kg_cluster_view *v, const kg_pod_spec *p, fw_resource *out) {
+    memset(out, 0, sizeof(*out));
+    for (int c = 0; c < p->n_containers; c++) {
+        const kg_resource_list *rq = &v->containers[p->first_container + c].requests;
+        for (int r = 0; r < KG_NUM_RES; r++)
+            if (has(rq, r)) { out->v[r] += rq->v[r]; if (is_scalar(r)) out->scalar_keys |= 1u << r; }
+    }
+    for (int c = 0; c < p->n_init_containers; c++) { /* Resource.SetMaxResource */
+        const kg_resource_list *rq = &v->containers[p->first_init_container + c].requests;
+        for (int r = 0; r < KG_NUM_RES; r++) {
+            if (!has(rq, r)) continue;
+            if (is_scalar(r)) {
+                if (!((out->scalar_keys >> r) & 1u) || rq->v[r] > out->v[r]) out->v[r] = rq->v[r];
+                out->scalar_keys |= 1u << r;
+            } else if (rq->v[r] > out->v[r]) out->v[r] = rq->v[r];
+        }
+    }
+    if (p->overhead.present)
+        for (int r = 0; r < KG_NUM_RES; r++)
+            if (has(&p->overhead, r)) { out->v[r] += p->overhead.v[r]; if (is_scalar(r)) out->scalar_keys |= 1u << r; }
+}
+
+/* schedutil.GetRequestForResource(resource, &requests, nonZero) */
+static int64_t request_for_resource(int r, const kg_resource_list *rq, int non_zero) {
+    if (r == KG_RES_CPU && !has(rq, r) && non_zero) return 100;
+    if (r == KG_RES_MEMORY && !has(rq, r) && non_zero) return 200LL * 1024 * 1024;
+    return get(rq, r);
+}
+
+/* calculatePodResourceRequest (resource_allocation.go, v1.24.15) */
+static int64_t fit_score_pod_request(const kg_cluster_view *v, const kg_pod_spec *p, int r) {
+    int64_t pr = 0;
+    for (int c = 0; c < p->n_containers; c++)
+        pr += request_for_resource(r, &v->containers[p->first_container + c].requests, 1);
+    for (int c = 0; c < p->n_init_containers; c++) {
+        int64_t x = request_for_resource(r, &v->containers[p->first_init_container + c].requests, 1);
+        if (pr < x) pr = x;
+    }
+    /* upstream adds quantity.Value() here, i.e. whole cores (rounded up) for cpu */
+    if (p->overhead.present && has(&p->overhead, r))
+        pr += r == KG_RES_CPU ? (p->overhead.v[r] + 999) / 1000 : p->overhead.v[r];
+    return pr;
+}
+
+/* NodeResourcesFit.Filter → fitsRequest: returns framework code */
+int kgo_fit_filter(const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n) {
+    if (n->pod_count + 1 > n->allowed_pods) return KG_CODE_UNSCHEDULABLE;
+    fw_resource req;
+    fit_pod_request(v, pod, &req);
+    if (req.v[KG_RES_CPU] == 0 && req.v[KG_RES_MEMORY] == 0 && req.v[KG_RES_EPHEMERAL_STORAGE] == 0 && req.scalar_keys == 0)
+        return KG_CODE_SUCCESS;
+    for (int r = 0; r < 3; r++)
+        if (req.v[r] > get(&n->allocatable, r) - get(&n->requested, r)) return KG_CODE_UNSCHEDULABLE;
+    for (int r = 3; r < KG_NUM_RES; r++)
+        if (((req.scalar_keys >> r) & 1u) && req.v[r] > get(&n->allocatable, r) - get(&n->requested, r))
+            return KG_CODE_UNSCHEDULABLE;
+    return KG_CODE_SUCCESS;
+}
+
+/* NodeResourcesFit.Score (LeastAllocated / MostAllocated) */
+int64_t kgo_fit_score(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n) {
+    int64_t score = 0, wsum = 0;
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        int64_t w = c->fit_resource_weight[r];
+        if (w == 0) continue;
+        int64_t pr = fit_score_pod_request(v, pod, r);
+        if (pr == 0 && is_scalar(r)) continue;
+        int64_t alloc, req;
+        if (r == KG_RES_CPU || r == KG_RES_MEMORY) {
+            alloc = get(&n->allocatable, r);
+            req = n->nonzero_requested[r] + pr;
+        } else if (r == KG_RES_EPHEMERAL_STORAGE) {
+            alloc = get(&n->allocatable, r);
+            req = get(&n->requested, r) + pr;
+        } else if (has(&n->allocatable, r)) {
+            alloc = n->allocatable.v[r];
+            req = get(&n->requested, r) + pr;
+        } else {
+            alloc = 0; req = 0;
+        }
+        if (alloc == 0) continue;
+        int64_t s;
+        if (c->fit_strategy == KG_STRATEGY_MOST_ALLOCATED) {
+            int64_t q = req > alloc ? alloc : req;
+            s = q * MAX_NODE_SCORE / alloc;
+        } else {
+            s = req > alloc ? 0 : ((alloc - req) * MAX_NODE_SCORE) / alloc;
+        }
+        score += s * w;
+        wsum += w;
+    }
+    return wsum ? score / wsum : 0;
+}
+
+/* ---------------------------------------------------------------- */
+/* combined per-pair evaluation and the sequential reference cycle    */
+/* ---------------------------------------------------------------- */
+typedef struct {
+    kg_node_spec spec;        /* mutable NodeInfo copy */
+    assigned_ref *assigned;   /* podAssignCache items of this node */
+    int n_assigned, cap_assigned;
+} node_state;
+
+static int pair_feasible(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n,
+                         int64_t now_ns) {
+    if ((c->enabled_plugins & KG_PLUGIN_FIT) && kgo_fit_filter(v, pod, n) != KG_CODE_SUCCESS) return 0;
+    if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && kgo_loadaware_filter(c, v, pod, n, now_ns) != KG_CODE_SUCCESS) return 0;
+    return 1;
+}
+
+/* Matrix mode oracle: feasibility + per-plugin scores of every pair.
+ * mask[p*N+n] ∈ {0,1}; fit/la [p*N+n] (0 where the plugin is disabled). */
+int kgo_eval_matrix_range(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P,
+                          int32_t node_begin, int32_t node_end, int64_t now_ns, uint8_t *mask, uint8_t *fit,
+                          uint8_t *la) {
+    const int32_t W = node_end - node_begin;
+    for (int32_t p = 0; p < P; p++) {
+        const kg_pod_spec *pod = &v->pods[pod_index[p]];
+        for (int32_t j = node_begin; j < node_end; j++) {
+            const kg_node_spec *n = &v->nodes[j];
+            int64_t o = (int64_t)p * W + (j - node_begin);
+            mask[o] = (uint8_t)pair_feasible(c, v, pod, n, now_ns);
+            fit[o] = (c->enabled_plugins & KG_PLUGIN_FIT) ? (uint8_t)kgo_fit_score(c, v, pod, n) : 0;
+            la[o] = (c->enabled_plugins & KG_PLUGIN_LOADAWARE) ? (uint8_t)kgo_loadaware_score(c, v, pod, n, now_ns) : 0;
+        }
+    }
+    return 0;
+}
+
+int kgo_eval_matrix(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P,
+                    int64_t now_ns, uint8_t *mask, uint8_t *fit, uint8_t *la) {
+    return kgo_eval_matrix_range(c, v, pod_index, P, 0, v->n_nodes, now_ns, mask, fit, la);
+}
+
+/* Sequential reference cycle over pod_index[0..P) in queue order.
+ * out_node[p] = chosen node or -1; out_score[p] = weighted total or -1. */
+int kgo_schedule(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
+                 int32_t *out_node, int64_t *out_score) {
+    int32_t N = v->n_nodes;
+    node_state *st = (node_state *)calloc((size_t)N, sizeof(node_state));
+    kg_cluster_view vv = *v;
+    for (int32_t j = 0; j < N; j++) {
+        st[j].spec = v->nodes[j];
+        st[j].cap_assigned = v->nodes[j].n_assigned + 4;
+        st[j].assigned = (assigned_ref *)malloc(sizeof(assigned_ref) * (size_t)st[j].cap_assigned);
+        st[j].n_assigned = gather_assigned(v, &v->nodes[j], st[j].assigned);
+    }
+    for (int32_t p = 0; p < P; p++) {
+        const kg_pod_spec *pod = &v->pods[pod_index[p]];
+        int64_t best = -1;
+        int32_t best_n = -1;
+        for (int32_t j = 0; j < N; j++) {
+            const kg_node_spec *n = &st[j].spec;
+            if (!pair_feasible(c, &vv, pod, n, now_ns)) continue;
+            int64_t total = 0;
+            if (c->enabled_plugins & KG_PLUGIN_FIT) total += c->weight_fit * kgo_fit_score(c, &vv, pod, n);
+            if (c->enabled_plugins & KG_PLUGIN_LOADAWARE)
+                total += c->weight_loadaware *
+                         loadaware_score_impl(c, &vv, pod, n, st[j].assigned, st[j].n_assigned, now_ns);
+            if (total > best) { best = total; best_n = j; }
+        }
+        out_node[p] = best_n;
+        out_score[p] = best;
+        if (best_n < 0) continue;
+        /* Reserve: AssumePod → NodeInfo.AddPod (calculateResource) */
+        node_state *s = &st[best_n];
+        fw_resource req;
+        fit_pod_request(&vv, pod, &req);
+        for (int r = 0; r < KG_NUM_RES; r++) {
+            if (r < 3 || ((req.scalar_keys >> r) & 1u)) {
+                s->spec.requested.v[r] = get(&s->spec.requested, r) + req.v[r];
+                if (r >= 3) s->spec.requested.present |= 1u << r;
+            }
+        }
+        s->spec.requested.present |= 0x7u;
+        for (int r = 0; r < 2; r++) {
+            int64_t nz = 0;
+            for (int k = 0; k < pod->n_containers; k++)
+                nz += request_for_resource(r, &v->containers[pod->first_container + k].requests, 1);
+            for (int k = 0; k < pod->n_init_containers; k++) {
+                int64_t x = request_for_resource(r, &v->containers[pod->first_init_container + k].requests, 1);
+                if (x > nz) nz = x;
+            }
+            if (pod->overhead.present && has(&pod->overhead, r)) nz += pod->overhead.v[r];
+            s->spec.nonzero_requested[r] += nz;
+        }
+        s->spec.pod_count += 1;
+        /* LoadAware.Reserve → podAssignCache.assign(nodeName, pod) with timestamp now */
+        if (!pod->is_terminated) {
+            if (s->n_assigned == s->cap_assigned) {
+                s->cap_assigned *= 2;
+                s->assigned = (assigned_ref *)realloc(s->assigned, sizeof(assigned_ref) * (size_t)s->cap_assigned);
+            }
+            s->assigned[s->n_assigned].pod = pod;
+            s->assigned[s->n_assigned].ts = now_ns;
+            s->n_assigned++;
+        }
+    }
+    for (int32_t j = 0; j < N; j++) free(st[j].assigned);
+    free(st);
+    return 0;
+}
+
+int kgo_abi_version(void) { return KG_ABI_VERSION; }
+
+/* ---------------------------------------------------------------- */
+/* CPU baseline: the reference's Parallelizer fan-out                */
+/* (pkg/util/parallelize/parallelism.go:27-49 = upstream             */
+/* workqueue.ParallelizeUntil with chunk = max(1, min(√n, n/W+1)))   */
+/* over nodes, one pod at a time, Filter then Score on every node.   */
+/* ---------------------------------------------------------------- */
+#include <pthread.h>
+
+typedef struct {
+    const kg_config *c;
+    const kg_cluster_view *v;
+    const kg_pod_spec *pod;
+    int64_t now_ns;
+    int32_t n, chunk;
+    int32_t next; /* atomic work counter */
+    int64_t *best;  /* per worker best key */
+} par_job;
+
+typedef struct { par_job *job; int w; } par_arg;
+
+static void *par_worker(void *arg) {
+    par_arg *a = (par_arg *)arg;
+    par_job *j = a->job;
+    int64_t best = -1;
+    for (;;) {
+        int32_t s = __atomic_fetch_add(&j->next, j->chunk, __ATOMIC_RELAXED);
+        if (s >= j->n) break;
+        int32_t e = s + j->chunk < j->n ? s + j->chunk : j->n;
+        for (int32_t k = s; k < e; k++) {
+            const kg_node_spec *nd = &j->v->nodes[k];
+            if (!pair_feasible(j->c, j->v, j->pod, nd, j->now_ns)) continue;
+            int64_t total = 0;
+            if (j->c->enabled_plugins & KG_PLUGIN_FIT) total += j->c->weight_fit * kgo_fit_score(j->c, j->v, j->pod, nd);
+            if (j->c->enabled_plugins & KG_PLUGIN_LOADAWARE)
+                total += j->c->weight_loadaware * kgo_loadaware_score(j->c, j->v, j->pod, nd, j->now_ns);
+            int64_t key = ((total + 1) << 32) | (int64_t)(0xFFFFFFFFu - (uint32_t)k);
+            if (key > best) best = key;
+        }
+    }
+    j->best[a->w] = best;
+    return NULL;
+}
+
+/* Evaluates every (pod, node) pair of pod_index[0..P) with `workers` threads; writes the best
+ * key per pod (same encoding as the engine's top1: (total+1)<<32 | (0xFFFFFFFF−node), 0 ⇔ none). */
+int kgo_eval_parallel(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P,
+                      int64_t now_ns, int32_t workers, uint64_t *top1) {
+    if (workers < 1) workers = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)workers);
+    par_arg *args = (par_arg *)malloc(sizeof(par_arg) * (size_t)workers);
+    int64_t *best = (int64_t *)malloc(sizeof(int64_t) * (size_t)workers);
+    int32_t n = v->n_nodes;
+    int32_t chunk = (int32_t)sqrt((double)n);
+    if (n / workers + 1 < chunk) chunk = n / workers + 1;
+    if (chunk < 1) chunk = 1;
+    for (int32_t p = 0; p < P; p++) {
+        par_job job = {c, v, &v->pods[pod_index[p]], now_ns, n, chunk, 0, best};
+        for (int w = 0; w < workers; w++) {
+            args[w].job = &job;
+            args[w].w = w;
+            pthread_create(&th[w], NULL, par_worker, &args[w]);
+        }
+        int64_t b = -1;
+        for (int w = 0; w < workers; w++) {
+            pthread_join(th[w], NULL);
+            if (best[w] > b) b = best[w];
+        }
+        top1[p] = b < 0 ? 0 : (uint64_t)b;
+    }
+    free(th);
+    free(args);
+    free(best);
+    return 0;
+}

@@ -1,0 +1,113 @@
+"""ctypes binding of oracle/build/libkoordoracle.so (test infrastructure only)."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(_HERE, "build", "libkoordoracle.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            raise RuntimeError(f"{ORACLE_SO} missing: run `python koordinator_amd/build.py`")
+        L = ctypes.CDLL(ORACLE_SO)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.kgo_loadaware_filter.restype = ctypes.c_int
+        L.kgo_loadaware_filter.argtypes = [vp, vp, vp, vp, i64]
+        L.kgo_loadaware_score.restype = i64
+        L.kgo_loadaware_score.argtypes = [vp, vp, vp, vp, i64]
+        L.kgo_fit_filter.restype = ctypes.c_int
+        L.kgo_fit_filter.argtypes = [vp, vp, vp]
+        L.kgo_fit_score.restype = i64
+        L.kgo_fit_score.argtypes = [vp, vp, vp, vp]
+        L.kgo_eval_matrix.restype = ctypes.c_int
+        L.kgo_eval_matrix.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
+        L.kgo_schedule.restype = ctypes.c_int
+        L.kgo_schedule.argtypes = [vp, vp, vp, i32, i64, vp, vp]
+        L.kgo_priority_class.restype = ctypes.c_int
+        L.kgo_priority_class.argtypes = [vp, vp]
+        _lib = L
+    return _lib
+
+
+def _pod(view, i):
+    return ctypes.c_void_p(view.pods.ctypes.data + i * view.pods.dtype.itemsize)
+
+
+def _node(view, j):
+    return ctypes.c_void_p(view.nodes.ctypes.data + j * view.nodes.dtype.itemsize)
+
+
+def _cfg(cfg):
+    return ctypes.c_void_p(cfg.ctypes.data)
+
+
+def la_filter(cfg, view, pod_i, node_j, now_ns) -> int:
+    return lib().kgo_loadaware_filter(_cfg(cfg), ctypes.byref(view.c_view), _pod(view, pod_i), _node(view, node_j), now_ns)
+
+
+def la_score(cfg, view, pod_i, node_j, now_ns) -> int:
+    return lib().kgo_loadaware_score(_cfg(cfg), ctypes.byref(view.c_view), _pod(view, pod_i), _node(view, node_j), now_ns)
+
+
+def fit_filter(view, pod_i, node_j) -> int:
+    return lib().kgo_fit_filter(ctypes.byref(view.c_view), _pod(view, pod_i), _node(view, node_j))
+
+
+def fit_score(cfg, view, pod_i, node_j) -> int:
+    return lib().kgo_fit_score(_cfg(cfg), ctypes.byref(view.c_view), _pod(view, pod_i), _node(view, node_j))
+
+
+def priority_class(view, pod_i) -> int:
+    return lib().kgo_priority_class(ctypes.byref(view.c_view), _pod(view, pod_i))
+
+
+def eval_matrix(cfg, view, pod_index, now_ns):
+    idx = np.ascontiguousarray(pod_index, dtype=np.int32)
+    P, N = len(idx), len(view.nodes)
+    mask = np.zeros((P, N), np.uint8)
+    fit = np.zeros((P, N), np.uint8)
+    la = np.zeros((P, N), np.uint8)
+    lib().kgo_eval_matrix(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, P, now_ns, mask.ctypes.data,
+                          fit.ctypes.data, la.ctypes.data)
+    return mask.astype(bool), fit, la
+
+
+def schedule(cfg, view, pod_index, now_ns):
+    idx = np.ascontiguousarray(pod_index, dtype=np.int32)
+    nodes = np.zeros(len(idx), np.int32)
+    scores = np.zeros(len(idx), np.int64)
+    lib().kgo_schedule(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, len(idx), now_ns, nodes.ctypes.data,
+                       scores.ctypes.data)
+    return nodes, scores
+
+
+def eval_matrix_range(cfg, view, pod_index, node_begin, node_end, now_ns):
+    idx = np.ascontiguousarray(pod_index, dtype=np.int32)
+    P, W = len(idx), node_end - node_begin
+    mask = np.zeros((P, W), np.uint8)
+    fit = np.zeros((P, W), np.uint8)
+    la = np.zeros((P, W), np.uint8)
+    L = lib()
+    L.kgo_eval_matrix_range.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32] * 3 + [ctypes.c_int64] + [ctypes.c_void_p] * 3
+    L.kgo_eval_matrix_range(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, P, node_begin, node_end, now_ns,
+                            mask.ctypes.data, fit.ctypes.data, la.ctypes.data)
+    return mask.astype(bool), fit, la
+
+
+def eval_parallel(cfg, view, pod_index, now_ns, workers=16):
+    """Parallelizer-faithful CPU baseline: best key per pod, `workers` threads over nodes."""
+    idx = np.ascontiguousarray(pod_index, dtype=np.int32)
+    top = np.zeros(len(idx), np.uint64)
+    L = lib()
+    L.kgo_eval_parallel.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+                                                            ctypes.c_void_p]
+    L.kgo_eval_parallel(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, len(idx), now_ns, workers,
+                        top.ctypes.data)
+    return top

@@ -1,0 +1,150 @@
+"""Parity of the HIP engine (through the C-ABI) against the CPU oracle and the reference KATs."""
+import numpy as np
+import pytest
+
+from kat import case_cluster, load
+from koordinator_amd import engine, synth
+from koordinator_amd.config import make_config, shipped_profile
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+DOC = load("loadaware_kat.json")
+
+
+def _engine_for(cfg, view, pod_index):
+    eng = engine.Engine(cfg)
+    eng.load_snapshot(engine.build_node_rows(cfg, view))
+    eng.set_pods(engine.build_pod_rows(cfg, view, pod_index))
+    return eng
+
+
+@pytest.mark.parametrize("case", DOC["score_cases"], ids=lambda c: c["name"])
+def test_kat_loadaware_score(case):
+    cfg, view, pi, cl = case_cluster(DOC, case, "pod")
+    with _engine_for(cfg, view, [pi]) as eng:
+        res = eng.eval(cl.now_ns)
+    assert int(res["scores"][0, 0, 1]) == case["want"]
+
+
+@pytest.mark.parametrize("case", DOC["filter_cases"], ids=lambda c: c["name"])
+def test_kat_loadaware_filter(case):
+    cfg, view, pi, cl = case_cluster(DOC, case, "test_pod")
+    cfg["enabled_plugins"] = 0x2  # LoadAwareScheduling only, like the reference test framework
+    with _engine_for(cfg, view, [pi]) as eng:
+        res = eng.eval(cl.now_ns)
+    feasible = bool(res["mask"][0, 0] & np.uint64(1))
+    assert feasible == (case["want"] == 0)
+
+
+def _check_matrix(cfg, view, pod_index, now_ns):
+    N = len(view.nodes)
+    with _engine_for(cfg, view, pod_index) as eng:
+        res = eng.eval(now_ns)
+    m_ref, fit_ref, la_ref = oracle.eval_matrix(cfg, view, pod_index, now_ns)
+    mask = engine.unpack_mask(res["mask"], N)
+    np.testing.assert_array_equal(mask, m_ref)
+    np.testing.assert_array_equal(res["scores"][:, :N, 0], fit_ref)
+    np.testing.assert_array_equal(res["scores"][:, :N, 1], la_ref)
+    total = int(cfg["weight_fit"]) * fit_ref.astype(np.int64) + int(cfg["weight_loadaware"]) * la_ref.astype(np.int64)
+    total = np.where(m_ref, total, -1)
+    best = total.argmax(axis=1)  # lowest index among ties
+    node, tot = engine.decode_top1(res["top1"])
+    want_node = np.where(total.max(axis=1) >= 0, best, -1)
+    np.testing.assert_array_equal(node, want_node)
+    np.testing.assert_array_equal(tot, total.max(axis=1))
+
+
+@pytest.mark.parametrize("profile", ["default", "shipped", "most"])
+def test_matrix_parity_config1_shape(profile):
+    cl = synth.make_cluster(5_000, 96, seed=11)
+    cfg = {"default": make_config, "shipped": shipped_profile,
+           "most": lambda: make_config(fit_strategy="MostAllocated",
+                                       fit_resources={"cpu": 2, "memory": 1, "kubernetes.io/batch-cpu": 3})}[profile]()
+    _check_matrix(cfg, cl, np.arange(96), cl.now_ns)
+
+
+@pytest.mark.parametrize("n_nodes", [1, 63, 64, 511, 513, 1500])
+def test_matrix_parity_ragged_node_counts(n_nodes):
+    cl = synth.make_cluster(n_nodes, 70, seed=n_nodes)
+    _check_matrix(shipped_profile(), cl, np.arange(70), cl.now_ns)
+
+
+def test_matrix_slow_path_huge_nodes():
+    """Nodes beyond the fp64 fast-path bounds (cap >= 2^41 B) take the exact int64 path."""
+    cl = synth.make_cluster(700, 40, seed=5)
+    big = np.arange(0, 700, 7)
+    cl.nodes["allocatable"]["v"][big, 1] = (1 << 43) + 12345
+    cl.nodes["requested"]["v"][big, 1] = (1 << 42) + 777
+    cl.nodes["nonzero_requested"][big, 1] = (1 << 42) + 777
+    cl = synth.SynthView(cl.pods, cl.containers, cl.nodes, cl.now_ns)
+    _check_matrix(shipped_profile(), cl, np.arange(40), cl.now_ns)
+
+
+def test_matrix_daemonset_and_prod_score_variant():
+    cl = synth.make_cluster(1_000, 64, seed=9)
+    cl.pods["is_daemonset"][::5] = 1
+    cl = synth.SynthView(cl.pods, cl.containers, cl.nodes, cl.now_ns)
+    cfg = shipped_profile(score_according_prod_usage=True, prod_usage_thresholds={"cpu": 40})
+    _check_matrix(cfg, cl, np.arange(64), cl.now_ns)
+
+
+def test_empty_pod_batch():
+    cl = synth.make_cluster(600, 1, seed=3)
+    cfg = shipped_profile()
+    with _engine_for(cfg, cl, []) as eng:
+        res = eng.eval(cl.now_ns)
+        assert res["mask"].shape[0] == 0
+        nodes, scores = eng.place(cl.now_ns)
+        assert len(nodes) == 0
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 64])
+def test_placement_matches_sequential_cycle(chunk):
+    cl = synth.make_cluster(3_000, 400, seed=21)
+    cfg = shipped_profile(place_chunk=chunk)
+    idx = np.arange(400)
+    with _engine_for(cfg, cl, idx) as eng:
+        nodes, scores = eng.place(cl.now_ns)
+        after = eng.download()
+    ref_nodes, ref_scores = oracle.schedule(cfg, cl, idx, cl.now_ns)
+    np.testing.assert_array_equal(nodes, ref_nodes)
+    np.testing.assert_array_equal(scores, ref_scores)
+    # snapshot rows after the commits equal host-side Reserve deltas
+    rows = engine.build_node_rows(cfg, cl)
+    prow = engine.build_pod_rows(cfg, cl, idx)
+    for p, n in enumerate(nodes):
+        if n >= 0:
+            engine.row_commit(cfg, rows[n:n + 1], prow[p:p + 1])
+    np.testing.assert_array_equal(after, rows)
+
+
+def test_placement_tight_cluster_with_unschedulable_pods():
+    """Few small nodes: pods run out of room, later pods become unschedulable (−1)."""
+    cl = synth.make_cluster(40, 300, seed=33, no_metric_frac=0.3)
+    cfg = shipped_profile(place_chunk=32)
+    idx = np.arange(300)
+    with _engine_for(cfg, cl, idx) as eng:
+        nodes, scores = eng.place(cl.now_ns)
+    ref_nodes, ref_scores = oracle.schedule(cfg, cl, idx, cl.now_ns)
+    assert (ref_nodes == -1).any()
+    np.testing.assert_array_equal(nodes, ref_nodes)
+    np.testing.assert_array_equal(scores, ref_scores)
+
+
+def test_snapshot_upsert_remove_and_commit():
+    cl = synth.make_cluster(2_000, 50, seed=8)
+    cfg = shipped_profile()
+    idx = np.arange(50)
+    rows = engine.build_node_rows(cfg, cl)
+    with _engine_for(cfg, cl, idx) as eng:
+        eng.remove(17)
+        eng.commit(3, 99)
+        res = eng.eval(cl.now_ns)
+        got = eng.download()
+    prow = engine.build_pod_rows(cfg, cl, idx)
+    engine.row_commit(cfg, rows[99:100], prow[3:4])
+    np.testing.assert_array_equal(got[99], rows[99])
+    assert got[17]["flags"] == 0
+    mask = engine.unpack_mask(res["mask"], 2000)
+    assert not mask[:, 17].any()
