@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ENGINE_SO = os.path.join(_HERE, "lib", "libkoordgpu.so")
+ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
 ABI_VERSION = 1
 NUM_RES = 8

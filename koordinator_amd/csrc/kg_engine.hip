@@ -81,12 +81,15 @@ struct NodeRegs {
     double fit_R[KG_NUM_RES];
     double fit_F[KG_NUM_RES];
     double la_R[2];
-    double la_F[2][2];
+    double la_F0[2];           // LoadAware offset, non-prod usage variant
+    double la_F1[2];           // LoadAware offset, prod usage variant
     uint32_t fit_mask;
     uint32_t df;
-    bool ok_np, ok_p, ok_ds;   // node-only filter outcome for non-prod / prod / daemonset pods
+    uint32_t ok_bits;          // bit 0: non-prod pod passes node-only filters, bit 1: prod pod, bit 2: daemonset
     bool la_valid;
 };
+// pods select their node-only filter bit with a uniform shift: no per-lane select of addresses
+#define KG_OKBIT_SHIFT(pf) (((pf) & KG_POD_DAEMONSET) ? 2u : (((pf) & KG_POD_PROD) ? 1u : 0u))
 
 // batch-level union masks: which planes the pods of this launch need
 struct BatchMasks {
@@ -115,8 +118,8 @@ __device__ __forceinline__ void load_node(const kg_consts &c, const kg_planes &p
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         n.la_R[r] = 0.0;
-        n.la_F[0][r] = 0.0;
-        n.la_F[1][r] = 0.0;
+        n.la_F0[r] = 0.0;
+        n.la_F1[r] = 0.0;
     }
     if (c.plugins & KG_PLUGIN_LOADAWARE) {
         int64_t upd = in_range ? pl.metric_ns[i] : 0;
@@ -125,22 +128,23 @@ __device__ __forceinline__ void load_node(const kg_consts &c, const kg_planes &p
 #pragma unroll
             for (int r = 0; r < 2; r++) {
                 n.la_R[r] = pl.la_R[r * cap + i];
-                n.la_F[0][r] = pl.la_F[(0 * 2 + r) * cap + i];
-                n.la_F[1][r] = pl.la_F[(1 * 2 + r) * cap + i];
+                n.la_F0[r] = pl.la_F[(0 * 2 + r) * cap + i];
+                n.la_F1[r] = pl.la_F[(1 * 2 + r) * cap + i];
             }
         }
     }
     bool base = (df & KGD_VALID) != 0;
     if (c.plugins & KG_PLUGIN_FIT) base = base && !(df & KGD_PODS_FULL);
-    n.ok_ds = base;
+    uint32_t ok = base ? 4u : 0u;
     if (c.plugins & KG_PLUGIN_LOADAWARE) {
-        n.ok_np = base && kg_la_pass(c, df, expired, 0);
-        n.ok_p = base && kg_la_pass(c, df, expired, 1);
+        ok |= (base && kg_la_pass(c, df, expired, 0)) ? 1u : 0u;
+        ok |= (base && kg_la_pass(c, df, expired, 1)) ? 2u : 0u;
         n.la_valid = kg_la_valid(c, df, expired);
     } else {
-        n.ok_np = n.ok_p = base;
+        ok |= base ? 3u : 0u;
         n.la_valid = false;
     }
+    n.ok_bits = ok;
 }
 
 __device__ __forceinline__ int lr_q(double neg_pr, double R, double F) {
@@ -152,7 +156,7 @@ __device__ __forceinline__ int lr_q(double neg_pr, double R, double F) {
 __device__ __forceinline__ bool eval_fast(const kg_consts &c, const kg_pod_dev &p, const NodeRegs &n, uint32_t &fit,
                                           uint32_t &la) {
     const uint32_t pf = p.flags;
-    bool ok = (pf & KG_POD_DAEMONSET) ? n.ok_ds : ((pf & KG_POD_PROD) ? n.ok_p : n.ok_np);
+    bool ok = (n.ok_bits >> KG_OKBIT_SHIFT(pf)) & 1u;
     fit = 0;
     la = 0;
     if (c.plugins & KG_PLUGIN_FIT) {
@@ -183,9 +187,10 @@ __device__ __forceinline__ bool eval_fast(const kg_consts &c, const kg_pod_dev &
         }
     }
     if (c.plugins & KG_PLUGIN_LOADAWARE) {
-        const int v = (pf & KG_POD_LA_PROD_SCORE) ? 1 : 0;
-        const int q0 = lr_q(p.la_est[0], n.la_R[0], n.la_F[v][0]);
-        const int q1 = lr_q(p.la_est[1], n.la_R[1], n.la_F[v][1]);
+        // the variant is pod-uniform: select with a ternary (a runtime index would push NodeRegs to scratch)
+        const bool prod = (pf & KG_POD_LA_PROD_SCORE) != 0;
+        const int q0 = lr_q(p.la_est[0], n.la_R[0], prod ? n.la_F1[0] : n.la_F0[0]);
+        const int q1 = lr_q(p.la_est[1], n.la_R[1], prod ? n.la_F1[1] : n.la_F0[1]);
         const uint32_t s = (uint32_t)(c.la_w[0] * q0 + c.la_w[1] * q1);
         la = n.la_valid ? __umulhi(s << 1, c.la_magic) : 0u;
     }
@@ -225,8 +230,6 @@ __global__ void k_finalize_range(kg_consts c, kg_planes pl, int64_t begin, int64
 }
 
 struct EvalArgs {
-    const kg_pod_dev *pods;  // batch base
-    int32_t pod_begin;       // first pod of this launch (batch index)
     int32_t n_pods;          // pods in this launch
     int32_t pods_per_block;
     int32_t tile_begin;      // first global tile of the shard
@@ -237,28 +240,35 @@ struct EvalArgs {
     int64_t score_stride;    // score row stride (pairs)
     int64_t now_ns;
     BatchMasks bm;
-    uint64_t *mask;          // [n_pods][mask_words] (row 0 = pod_begin)
-    uint16_t *scores;        // [n_pods][score_stride]
-    uint32_t *partials;      // [n_pods][tiles_total]
 };
 
 template <bool WRITE_MASK, bool WRITE_SCORES, bool SLOW>
-__device__ __forceinline__ void eval_loop(const kg_consts &c, const kg_planes &pl, const EvalArgs &a, const NodeRegs &n,
-                                          int64_t node, int p0, int p1, uint32_t (*lds)[KG_WAVES_PER_TILE]) {
+__device__ __forceinline__ void eval_loop(const kg_consts &c, const kg_planes &pl, const EvalArgs &a,
+                                          const kg_pod_dev *__restrict__ pods, uint64_t *__restrict__ mask,
+                                          uint16_t *__restrict__ scores, const NodeRegs &n, int64_t node, int p0,
+                                          int p1, uint32_t (*lds)[KG_WAVES_PER_TILE]) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const uint32_t local_key = (uint32_t)(KG_TILE - 1 - tid);
     for (int p = p0; p < p1; p++) {
-        const kg_pod_dev &pd = a.pods[a.pod_begin + p];
+        const kg_pod_dev &pd = pods[p];
         uint32_t fit, la;
         bool feas = SLOW ? eval_pair(c, pl, pd, n, node, a.now_ns, fit, la) : eval_fast(c, pd, n, fit, la);
         if (WRITE_SCORES) {
-            if (node < a.node_end) a.scores[(int64_t)p * a.score_stride + (node - a.col_begin)] = (uint16_t)(fit | (la << 8));
+            if (node < a.node_end) scores[(int64_t)p * a.score_stride + (node - a.col_begin)] = (uint16_t)(fit | (la << 8));
         }
         if (WRITE_MASK) {
             unsigned long long b = __ballot(feas);
-            if (lane == 0) a.mask[(int64_t)p * a.mask_words + ((node - a.col_begin) >> 6)] = b;
+#ifdef KG_DEBUG_EVAL
+            if (blockIdx.x == 0 && wave == 0 && lane < 3 && p < 3)
+                printf("blk(%d,%d) p=%d lane=%d feas=%d okds=%d oknp=%d okp=%d df=%x f0=%ld f1=%ld f3=%ld f4=%ld ballot=%llx cmp=%x over=%x\n",
+                       blockIdx.x, blockIdx.y, p, lane, (int)feas, (int)n.ok_ds, (int)n.ok_np, (int)n.ok_p, n.df,
+                       (long)n.free_[0], (long)n.free_[1], (long)n.free_[3], (long)n.free_[4], b, pd.cmp_mask, pd.zero_native_mask);
+#endif
+            // lane 0 holds the wave's first node: waves wholly past the shard end must not store
+            // (their word index would run into the next row)
+            if (lane == 0 && node < a.node_end) mask[(int64_t)p * a.mask_words + ((node - a.col_begin) >> 6)] = b;
         }
         uint32_t key = feas ? ((total_of(c, fit, la) + 1u) << 9) | local_key : 0u;
         key = wave_max_u32(key);
@@ -267,7 +277,9 @@ __device__ __forceinline__ void eval_loop(const kg_consts &c, const kg_planes &p
 }
 
 template <bool WRITE_MASK, bool WRITE_SCORES>
-__global__ __launch_bounds__(KG_TILE) void k_eval(kg_consts c, kg_planes pl, EvalArgs a) {
+__global__ __launch_bounds__(KG_TILE) void k_eval(kg_consts c, kg_planes pl, EvalArgs a,
+                                                  const kg_pod_dev *__restrict__ pods, uint64_t *__restrict__ mask,
+                                                  uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
     __shared__ uint32_t lds[2][KG_POD_CHUNK][KG_WAVES_PER_TILE];
     const int tid = threadIdx.x;
     const int tile = a.tile_begin + blockIdx.x;
@@ -281,14 +293,14 @@ __global__ __launch_bounds__(KG_TILE) void k_eval(kg_consts c, kg_planes pl, Eva
     int buf = 0;
     for (int p0 = pb; p0 < pe; p0 += KG_POD_CHUNK, buf ^= 1) {
         const int p1 = min(p0 + KG_POD_CHUNK, pe);
-        if (slow) eval_loop<WRITE_MASK, WRITE_SCORES, true>(c, pl, a, n, node, p0, p1, lds[buf]);
-        else eval_loop<WRITE_MASK, WRITE_SCORES, false>(c, pl, a, n, node, p0, p1, lds[buf]);
+        if (slow) eval_loop<WRITE_MASK, WRITE_SCORES, true>(c, pl, a, pods, mask, scores, n, node, p0, p1, lds[buf]);
+        else eval_loop<WRITE_MASK, WRITE_SCORES, false>(c, pl, a, pods, mask, scores, n, node, p0, p1, lds[buf]);
         __syncthreads();
         if (tid < p1 - p0) {
             uint32_t m = 0;
 #pragma unroll
             for (int w = 0; w < KG_WAVES_PER_TILE; w++) m = m > lds[buf][tid][w] ? m : lds[buf][tid][w];
-            a.partials[(int64_t)(p0 + tid) * a.tiles_total + tile] = m;
+            partials[(int64_t)(p0 + tid) * a.tiles_total + tile] = m;
         }
         // the double buffer makes a second barrier unnecessary: the next chunk writes the other buffer
     }
@@ -463,8 +475,6 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     const int64_t shard_tiles = (e->shard_end - e->shard_begin + KG_TILE - 1) / KG_TILE;
     if (shard_tiles <= 0) return KG_OK;
     EvalArgs a;
-    a.pods = e->pods;
-    a.pod_begin = pod_begin;
     a.n_pods = n;
     a.pods_per_block = pods_per_block_for(n, shard_tiles);
     a.tile_begin = (int32_t)(e->shard_begin / KG_TILE);
@@ -475,15 +485,13 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     a.score_stride = (e->shard_end - e->shard_begin + 63) / 64 * 64;
     a.now_ns = now_ns;
     a.bm = e->bm;
-    a.mask = mask;
-    a.scores = scores;
-    a.partials = partials;
+    const kg_pod_dev *pods = e->pods + pod_begin;
     dim3 grid((unsigned)shard_tiles, (unsigned)((n + a.pods_per_block - 1) / a.pods_per_block));
     if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
-    if (mask && scores) hipLaunchKernelGGL((k_eval<true, true>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a);
-    else if (mask) hipLaunchKernelGGL((k_eval<true, false>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a);
-    else if (scores) hipLaunchKernelGGL((k_eval<false, true>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a);
-    else hipLaunchKernelGGL((k_eval<false, false>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a);
+    if (mask && scores) hipLaunchKernelGGL((k_eval<true, true>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a, pods, mask, scores, partials);
+    else if (mask) hipLaunchKernelGGL((k_eval<true, false>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a, pods, mask, scores, partials);
+    else if (scores) hipLaunchKernelGGL((k_eval<false, true>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a, pods, mask, scores, partials);
+    else hipLaunchKernelGGL((k_eval<false, false>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a, pods, mask, scores, partials);
     HIP_TRY(e, hipGetLastError());
     if (e->profiling) {
         HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));

@@ -121,9 +121,9 @@ def test_placement_matches_sequential_cycle(chunk):
 
 def test_placement_tight_cluster_with_unschedulable_pods():
     """Few small nodes: pods run out of room, later pods become unschedulable (−1)."""
-    cl = synth.make_cluster(40, 300, seed=33, no_metric_frac=0.3)
+    cl = synth.make_cluster(10, 1200, seed=33, no_metric_frac=0.3)
     cfg = shipped_profile(place_chunk=32)
-    idx = np.arange(300)
+    idx = np.arange(1200)
     with _engine_for(cfg, cl, idx) as eng:
         nodes, scores = eng.place(cl.now_ns)
     ref_nodes, ref_scores = oracle.schedule(cfg, cl, idx, cl.now_ns)
