@@ -75,7 +75,28 @@ struct kg_consts {
     int32_t la_wsum;
     int32_t la_filter_expired;
     int32_t la_has_exp;
+    int32_t la_shift;            // log2 Σ la_w when a power of two, else 0xFF
+    float la_rcp;                // 1 / Σ la_w
     int64_t la_exp_ns;
+};
+
+#define KG_NEUTRAL_REQ INT64_MIN  // request that passes every Fit compare
+
+// per-pod data of the hot kernel (k_eval_hot), over S resource "slots" (the launch's resource
+// profile maps slot s → resource id).  Read as whole 64-byte blocks with s_load_dwordx16.
+#define KG_HOT_PROD 0x1u             // flags: LoadAware prod-usage variant
+#define KG_HOT_CMP_SHIFT 8           // flags bits 8..15: slot s is compared by the Fit filter
+#define KG_HOT_FIT_SHIFT 16          // flags bits 16..23: slot s is scored by NodeResourcesFit
+template <int S>
+struct alignas(64) kg_pod_hot_t {
+    int64_t req[S];        // Fit filter request; KG_NEUTRAL_REQ where the slot is not compared
+    double fit_pr[S];      // signed fma operand (−pr LeastAllocated, +pr MostAllocated); 0 if not scored
+    double la_est[2];      // −EstimatePod (cpu, memory)
+    uint32_t fit_w[S];     // Fit weight of the slot for this pod (0 ⇔ not scored)
+    uint32_t okshift;      // node filter bit: variant (0 non-prod, 1 prod, 2 daemonset) + 3·has_request
+    uint32_t fit_shift;    // log2 W when W is a power of two (W = Σ fit_w), else 0xFF
+    float fit_rcp;         // 1 / W
+    uint32_t flags;        // KG_HOT_*
 };
 
 struct kg_planes {

@@ -229,80 +229,257 @@ __global__ void k_finalize_range(kg_consts c, kg_planes pl, int64_t begin, int64
     kg_finalize_node(c, pl, i);
 }
 
-struct EvalArgs {
-    int32_t n_pods;          // pods in this launch
+// ---------------------------------------------------------------------------------------
+// hot kernel: S resource slots per launch, branch-free per pair
+// ---------------------------------------------------------------------------------------
+// The host maps slot s → resource id per pod batch (KG_PROF_*: cpu+memory, + batch-cpu/memory,
+// or all 8) and builds kg_pod_hot_t<S> rows.  Per pair and slot: one int64 compare (Fit filter)
+// and one fp64 FMA + cvt (least-requested score); node-only filter outcomes are six wave
+// lane-masks selected per pod by a scalar index.
+typedef uint32_t kg_u32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint32_t cvt_u32_sat(double x) {
+    uint32_t r;  // v_cvt_u32_f64 clamps negatives to 0 (and truncates toward zero)
+    asm volatile("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// s / W, exact for s < 2^16 and W ≤ 2^11: a shift when every W of the launch is a power of two
+// (POW2), else fma with 1/W + 2^-12 (|s·RN(1/W) − s/W| ≤ 100·2^-23 ≪ 2^-12 < 1/W − 2^-12)
+template <bool POW2>
+__device__ __forceinline__ uint32_t div_w(uint32_t s, uint32_t shift, float rcp) {
+    if (POW2) return s >> shift;
+    return (uint32_t)__builtin_fmaf((float)s, rcp, 0x1p-12f);
+}
+
+// whole-row scalar load: the row is wave-uniform and read-only → s_load_dwordx16 per 64 B
+template <int S>
+__device__ __forceinline__ kg_pod_hot_t<S> load_pod(const kg_pod_hot_t<S> *__restrict__ p) {
+    constexpr int NB = sizeof(kg_pod_hot_t<S>) / 64;
+    union U {
+        kg_u32x16 v[NB];
+        kg_pod_hot_t<S> h;
+        __device__ U() {}
+    } u;
+    const kg_u32x16 *src = reinterpret_cast<const kg_u32x16 *>(p);
+#pragma unroll
+    for (int i = 0; i < NB; i++) u.v[i] = src[i];
+    return u.h;
+}
+
+struct HotArgs {
+    int32_t n_pods;
     int32_t pods_per_block;
-    int32_t tile_begin;      // first global tile of the shard
-    int64_t node_end;        // shard end (exclusive, global index)
-    int64_t col_begin;       // first node of the output columns (shard begin)
-    int32_t tiles_total;     // partial row stride
-    int32_t mask_words;      // mask row stride (words)
-    int64_t score_stride;    // score row stride (pairs)
+    int32_t tile_begin;
+    int32_t tiles_total;
+    int64_t node_end;
+    int64_t col_begin;
+    int64_t score_stride;
+    int32_t mask_words;
+    uint32_t fit_cap;        // 100 for MostAllocated (clamp), 0xFFFFFFFF for LeastAllocated (no-op)
+    int32_t slot_res[8];     // resource id of each slot (−1 unused)
     int64_t now_ns;
-    BatchMasks bm;
 };
 
-template <bool WRITE_MASK, bool WRITE_SCORES, bool SLOW>
-__device__ __forceinline__ void eval_loop(const kg_consts &c, const kg_planes &pl, const EvalArgs &a,
-                                          const kg_pod_dev *__restrict__ pods, uint64_t *__restrict__ mask,
-                                          uint16_t *__restrict__ scores, const NodeRegs &n, int64_t node, int p0,
-                                          int p1, uint32_t (*lds)[KG_WAVES_PER_TILE]) {
+// FAST = both plugins on, LeastAllocated, every divisor a power of two, plugin weights 1 (checked on
+// the host); otherwise the generic path handles MostAllocated clamps, other divisors and weights.
+template <int S, bool FAST, bool LA_PROD, bool FULL, bool OUT>
+__device__ __forceinline__ void hot_loop(const kg_consts &c, const HotArgs &a, const kg_pod_hot_t<S> *__restrict__ pods,
+                                         uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
+                                         const int64_t (&fr)[S], const double (&R)[S], const double (&F)[S],
+                                         const double (&laR)[2], const double (&laF0)[2], const double (&laF1)[2],
+                                         uint32_t okbits, uint32_t node_slot_mask, int64_t node, int p0,
+                                         int p1, uint32_t *kbuf) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const uint32_t local_key = (uint32_t)(KG_TILE - 1 - tid);
+    const uint32_t key_base = (uint32_t)(KG_TILE + KG_TILE - 1 - tid);  // + (tot << 9) = ((tot+1) << 9) | local
+    const bool store_lane = node < a.node_end;
+    const bool fit_on = FAST || (c.plugins & KG_PLUGIN_FIT);
+    const bool la_on = FAST || (c.plugins & KG_PLUGIN_LOADAWARE);
+    uint16_t *srow = scores + (node - a.col_begin);
+    uint64_t *mrow = mask + ((node - a.col_begin) >> 6);
     for (int p = p0; p < p1; p++) {
-        const kg_pod_dev &pd = pods[p];
-        uint32_t fit, la;
-        bool feas = SLOW ? eval_pair(c, pl, pd, n, node, a.now_ns, fit, la) : eval_fast(c, pd, n, fit, la);
-        if (WRITE_SCORES) {
-            if (node < a.node_end) scores[(int64_t)p * a.score_stride + (node - a.col_begin)] = (uint16_t)(fit | (la << 8));
+        const kg_pod_hot_t<S> pd = load_pod<S>(pods + p);
+        // node-only filter outcome as a lane mask, chosen by a scalar select chain
+        bool ok = (okbits >> pd.okshift) & 1u;
+        uint32_t fit = 0;
+        if (fit_on) {
+#pragma unroll
+            for (int s = 0; s < S; s++) {
+                if (s >= 2 && !((pd.flags >> (KG_HOT_CMP_SHIFT + s)) & 1u)) continue;  // uniform
+                ok &= pd.req[s] <= fr[s];
+            }
+            uint32_t sum = 0;
+#pragma unroll
+            for (int s = 0; s < S; s++) {
+                if (s >= 2 && !((pd.flags >> (KG_HOT_FIT_SHIFT + s)) & 1u)) continue;  // uniform
+                uint32_t q = cvt_u32_sat(__builtin_fma(pd.fit_pr[s], R[s], F[s]));
+                if (!FAST) q = q < a.fit_cap ? q : a.fit_cap;  // MostAllocated clamp
+                sum = __umul24(pd.fit_w[s], q) + sum;
+            }
+            const uint32_t pmask = (pd.flags >> KG_HOT_FIT_SHIFT) & 0xFFu;
+            if (FULL || (node_slot_mask & pmask) == pmask) {
+                fit = FAST ? sum >> pd.fit_shift : div_w<false>(sum, pd.fit_shift, pd.fit_rcp);
+            } else {  // the node lacks a resource the pod scores (no allocatable): its weight drops out
+                uint32_t w = 0;
+#pragma unroll
+                for (int s = 0; s < S; s++) w += ((node_slot_mask & pmask) >> s & 1u) ? pd.fit_w[s] : 0u;
+                fit = w ? sum / w : 0u;
+            }
         }
-        if (WRITE_MASK) {
-            unsigned long long b = __ballot(feas);
-#ifdef KG_DEBUG_EVAL
-            if (blockIdx.x == 0 && wave == 0 && lane < 3 && p < 3)
-                printf("blk(%d,%d) p=%d lane=%d feas=%d okds=%d oknp=%d okp=%d df=%x f0=%ld f1=%ld f3=%ld f4=%ld ballot=%llx cmp=%x over=%x\n",
-                       blockIdx.x, blockIdx.y, p, lane, (int)feas, (int)n.ok_ds, (int)n.ok_np, (int)n.ok_p, n.df,
-                       (long)n.free_[0], (long)n.free_[1], (long)n.free_[3], (long)n.free_[4], b, pd.cmp_mask, pd.zero_native_mask);
-#endif
+        uint32_t la = 0;
+        if (la_on) {
+            const bool prod = LA_PROD && (pd.flags & KG_HOT_PROD);
+            const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la_est[0], laR[0], prod ? laF1[0] : laF0[0]));
+            const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la_est[1], laR[1], prod ? laF1[1] : laF0[1]));
+            const uint32_t sum = __umul24((uint32_t)c.la_w[0], q0) + __umul24((uint32_t)c.la_w[1], q1);
+            la = FAST ? sum >> c.la_shift : div_w<false>(sum, (uint32_t)c.la_shift, c.la_rcp);
+        }
+        if (OUT) {
+            if (store_lane) srow[(int64_t)p * a.score_stride] = (uint16_t)(fit | (la << 8));
+            const unsigned long long b = __ballot(ok);
             // lane 0 holds the wave's first node: waves wholly past the shard end must not store
-            // (their word index would run into the next row)
-            if (lane == 0 && node < a.node_end) mask[(int64_t)p * a.mask_words + ((node - a.col_begin) >> 6)] = b;
+            if (lane == 0 && store_lane) mrow[(int64_t)p * a.mask_words] = b;
         }
-        uint32_t key = feas ? ((total_of(c, fit, la) + 1u) << 9) | local_key : 0u;
-        key = wave_max_u32(key);
-        if (lane == 0) lds[p - p0][wave] = key;
+        uint32_t tot;
+        if (FAST) tot = fit + la;
+        else tot = __umul24((uint32_t)c.weight_fit, fit) + __umul24((uint32_t)c.weight_la, la);
+        // per-lane key into LDS; the workgroup reduces 16 pods at a time (cheaper than a wave max per pod)
+        kbuf[(p - p0) * KG_TILE + tid] = ok ? (tot << 9) + key_base : 0u;
     }
 }
 
-template <bool WRITE_MASK, bool WRITE_SCORES>
-__global__ __launch_bounds__(KG_TILE) void k_eval(kg_consts c, kg_planes pl, EvalArgs a,
-                                                  const kg_pod_dev *__restrict__ pods, uint64_t *__restrict__ mask,
-                                                  uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
-    __shared__ uint32_t lds[2][KG_POD_CHUNK][KG_WAVES_PER_TILE];
+#define KG_KCHUNK 16   // pods per LDS key buffer
+
+template <int S, bool FAST, bool LA_PROD, bool OUT>
+__global__ __launch_bounds__(KG_TILE) void k_eval_hot(kg_consts c, kg_planes pl, HotArgs a,
+                                                      const kg_pod_hot_t<S> *__restrict__ pods,
+                                                      uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
+                                                      uint32_t *__restrict__ partials) {
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_KCHUNK * KG_TILE];
     const int tid = threadIdx.x;
     const int tile = a.tile_begin + blockIdx.x;
     const int64_t node = (int64_t)tile * KG_TILE + tid;
     const bool in_range = node < a.node_end;
-    NodeRegs n;
-    load_node(c, pl, node, in_range, a.bm, a.now_ns, n);
-    const bool slow = __any((n.df & KGD_SLOW) != 0);  // wave-uniform
+    const int64_t cap = pl.cap;
+    // ---- node registers (loaded once, reused for every pod of the block) ----
+    const uint32_t df = in_range ? pl.dflags[node] : 0u;
+    const bool slow = (df & KGD_SLOW) != 0;
+    const uint32_t nfm = in_range ? pl.fit_mask[node] : 0u;
+    int64_t fr[S];
+    double R[S], F[S];
+    uint32_t node_slot_mask = 0, slot_natives = 0;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        const int r = a.slot_res[s];
+        fr[s] = 0;
+        R[s] = 0.0;
+        F[s] = 0.0;
+        if (r >= 0) {
+            if (r < 3) slot_natives |= 1u << r;
+            if (in_range) fr[s] = pl.free_[r * cap + node];
+            if (in_range && !slow) {
+                R[s] = pl.fit_R[r * cap + node];
+                F[s] = pl.fit_F[r * cap + node];
+            }
+            if ((nfm >> r) & 1u) node_slot_mask |= 1u << s;
+        }
+    }
+    double laR[2] = {0.0, 0.0}, laF0[2] = {0.0, 0.0}, laF1[2] = {0.0, 0.0};
+    bool expired = false;
+    if (c.plugins & KG_PLUGIN_LOADAWARE) {
+        expired = kg_metric_expired(c, df, in_range ? pl.metric_ns[node] : 0, a.now_ns);
+        if (in_range && !slow && kg_la_valid(c, df, expired)) {  // invalid NodeMetric ⇒ score 0 via R = F = 0
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                laR[r] = pl.la_R[r * cap + node];
+                laF0[r] = pl.la_F[(0 * 2 + r) * cap + node];
+                if (LA_PROD) laF1[r] = pl.la_F[(1 * 2 + r) * cap + node];
+            }
+        }
+    }
+    // node-only filter outcomes: bit (variant + 3·has_request), variant 0 non-prod, 1 prod, 2 daemonset
+    bool base = (df & KGD_VALID) && !slow;
+    if (c.plugins & KG_PLUGIN_FIT) base = base && !(df & KGD_PODS_FULL);
+    bool over = false;  // a zero request of a native resource without a slot still fails an overcommitted node
+    if (c.plugins & KG_PLUGIN_FIT) {
+        if (!(slot_natives & 1u)) over |= (df & KGD_OVER_CPU) != 0;
+        if (!(slot_natives & 2u)) over |= (df & KGD_OVER_MEM) != 0;
+        if (!(slot_natives & 4u)) over |= (df & KGD_OVER_EPH) != 0;
+    }
+    uint32_t okbits = 0;
+#pragma unroll
+    for (int v = 0; v < 3; v++) {
+        bool okv = base;
+        if ((c.plugins & KG_PLUGIN_LOADAWARE) && v < 2) okv = okv && kg_la_pass(c, df, expired, v);
+        okbits |= (okv ? 1u : 0u) << v;
+        okbits |= (okv && !over ? 1u : 0u) << (v + 3);
+    }
+    uint32_t all_slots = 0;
+#pragma unroll
+    for (int s = 0; s < S; s++) all_slots |= (a.slot_res[s] >= 0) ? (1u << s) : 0u;
+    const bool full = __all(((node_slot_mask & all_slots) == all_slots) || !in_range);
     const int pb = blockIdx.y * a.pods_per_block;
     const int pe = min(pb + a.pods_per_block, a.n_pods);
-    int buf = 0;
-    for (int p0 = pb; p0 < pe; p0 += KG_POD_CHUNK, buf ^= 1) {
-        const int p1 = min(p0 + KG_POD_CHUNK, pe);
-        if (slow) eval_loop<WRITE_MASK, WRITE_SCORES, true>(c, pl, a, pods, mask, scores, n, node, p0, p1, lds[buf]);
-        else eval_loop<WRITE_MASK, WRITE_SCORES, false>(c, pl, a, pods, mask, scores, n, node, p0, p1, lds[buf]);
+    // reduction geometry: thread t reduces 16 consecutive keys of pod (t >> 5), then 32 lanes combine
+    const int rj = tid >> 5, rg = tid & 31;
+    for (int p0 = pb; p0 < pe; p0 += KG_KCHUNK) {
+        const int p1 = min(p0 + KG_KCHUNK, pe);
+        if (full)
+            hot_loop<S, FAST, LA_PROD, true, OUT>(c, a, pods, mask, scores, fr, R, F, laR, laF0, laF1, okbits,
+                                                  node_slot_mask, node, p0, p1, kbuf);
+        else
+            hot_loop<S, FAST, LA_PROD, false, OUT>(c, a, pods, mask, scores, fr, R, F, laR, laF0, laF1, okbits,
+                                                   node_slot_mask, node, p0, p1, kbuf);
         __syncthreads();
-        if (tid < p1 - p0) {
-            uint32_t m = 0;
+        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * KG_TILE + rg * 16);
+        uint32_t mx = 0;
 #pragma unroll
-            for (int w = 0; w < KG_WAVES_PER_TILE; w++) m = m > lds[buf][tid][w] ? m : lds[buf][tid][w];
-            partials[(int64_t)(p0 + tid) * a.tiles_total + tile] = m;
+        for (int k = 0; k < 4; k++) {
+            const uint4 v = src[k];
+            const uint32_t a0 = v.x > v.y ? v.x : v.y, a1 = v.z > v.w ? v.z : v.w;
+            const uint32_t a2 = a0 > a1 ? a0 : a1;
+            mx = mx > a2 ? mx : a2;
         }
-        // the double buffer makes a second barrier unnecessary: the next chunk writes the other buffer
+        // max over the 32 lanes of this half-wave (rows 0-1 / 2-3): row_shr 1,2,4,8 then row_bcast:15
+        mx = dpp_max_step(mx, 0);
+        mx = dpp_max_step(mx, 1);
+        mx = dpp_max_step(mx, 2);
+        mx = dpp_max_step(mx, 3);
+        mx = dpp_max_step(mx, 4);
+        if (rg == 31 && rj < p1 - p0) partials[(int64_t)(p0 + rj) * a.tiles_total + tile] = mx;
+        __syncthreads();
+    }
+}
+
+// Slow nodes (outside the fp64 exactness bounds) come out of k_eval_hot as infeasible with
+// zero scores; k_slow_list collects them and k_fix_slow re-evaluates those pairs exactly.
+__global__ void k_slow_list(const uint32_t *__restrict__ dflags, int64_t begin, int64_t end, int32_t *__restrict__ list,
+                            int32_t *__restrict__ count) {
+    const int64_t i = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < end && (dflags[i] & KGD_SLOW) && (dflags[i] & KGD_VALID)) list[atomicAdd(count, 1)] = (int32_t)i;
+}
+
+__global__ void k_fix_slow(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t n_pods,
+                           const int32_t *__restrict__ list, const int32_t *__restrict__ count, int64_t col_begin,
+                           int32_t mask_words, int64_t score_stride, int32_t tiles_total, int64_t now_ns,
+                           unsigned long long *mask, uint16_t *scores, uint32_t *partials) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pods) return;
+    const int32_t n = *count;
+    for (int32_t k = 0; k < n; k++) {
+        const int64_t node = list[k];
+        bool feas;
+        uint32_t fit, la;
+        kg_pair_exact(c, pl.rows[node], pl.dflags[node], pods[p], now_ns, feas, fit, la);
+        const int64_t col = node - col_begin;
+        if (scores) scores[(int64_t)p * score_stride + col] = (uint16_t)(fit | (la << 8));
+        if (feas) {
+            if (mask) atomicOr(&mask[(int64_t)p * mask_words + (col >> 6)], 1ull << (col & 63));
+            const uint32_t tot = (uint32_t)c.weight_fit * fit + (uint32_t)c.weight_la * la;
+            const uint32_t key = ((tot + 1u) << 9) | (uint32_t)(KG_TILE - 1 - (node % KG_TILE));
+            atomicMax(&partials[(int64_t)p * tiles_total + node / KG_TILE], key);
+        }
     }
 }
 
@@ -418,9 +595,17 @@ struct kg_engine {
     void *plane_mem = nullptr;
     int64_t n_nodes = 0;
     int64_t shard_begin = 0, shard_end = 0;
-    kg_pod_dev *pods = nullptr;
+    kg_pod_dev *pods = nullptr;     // generic per-pod rows (exact path, placement resolve)
+    void *hot = nullptr;            // hot-kernel per-pod rows: kg_pod_hot_t<nslot>[n]
+    int32_t nslot = 2;              // resource slots of the batch's profile (2, 4 or 8)
+    int32_t slot_res[8] = {0, 1, -1, -1, -1, -1, -1, -1};
     int32_t n_pods = 0, pods_cap = 0;
+    size_t hot_bytes = 0;
     BatchMasks bm{0, 0};
+    bool la_prod = false;           // some pod of the batch scores with the prod-usage variant
+    bool pow2 = true;               // every Fit / LoadAware weight sum of the batch is a power of two
+    int32_t *slow_list = nullptr;   // [cap] nodes outside the fast-path bounds (rebuilt per eval)
+    int32_t *slow_count = nullptr;
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
     bool profiling = false;
@@ -469,34 +654,71 @@ int pods_per_block_for(int64_t n_pods, int64_t tiles) {
     return (int)ppb;
 }
 
+template <int S, bool FAST, bool LA_PROD>
+void launch_hot_div(kg_engine *e, dim3 grid, const HotArgs &a, int32_t pod_begin, uint64_t *mask, uint16_t *scores,
+                    uint32_t *partials) {
+    const kg_pod_hot_t<S> *pods = reinterpret_cast<const kg_pod_hot_t<S> *>(e->hot) + pod_begin;
+    if (mask)
+        hipLaunchKernelGGL((k_eval_hot<S, FAST, LA_PROD, true>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a,
+                           pods, mask, scores, partials);
+    else
+        hipLaunchKernelGGL((k_eval_hot<S, FAST, LA_PROD, false>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a,
+                           pods, mask, scores, partials);
+}
+
+template <int S>
+void launch_hot(kg_engine *e, dim3 grid, const HotArgs &a, int32_t pod_begin, uint64_t *mask, uint16_t *scores,
+                uint32_t *partials) {
+    const kg_consts &c = e->consts;
+    const bool fast = e->pow2 && !c.fit_most && c.weight_fit == 1 && c.weight_la == 1 &&
+                      (c.plugins & (KG_PLUGIN_FIT | KG_PLUGIN_LOADAWARE)) == (KG_PLUGIN_FIT | KG_PLUGIN_LOADAWARE);
+    if (e->la_prod) {
+        if (fast) launch_hot_div<S, true, true>(e, grid, a, pod_begin, mask, scores, partials);
+        else launch_hot_div<S, false, true>(e, grid, a, pod_begin, mask, scores, partials);
+    } else {
+        if (fast) launch_hot_div<S, true, false>(e, grid, a, pod_begin, mask, scores, partials);
+        else launch_hot_div<S, false, false>(e, grid, a, pod_begin, mask, scores, partials);
+    }
+}
+
+// mask and scores are both produced or both omitted (the host path provides scratch for a missing one)
 kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
                       uint32_t *partials) {
     if (n <= 0) return KG_OK;
+    if ((mask == nullptr) != (scores == nullptr)) return set_err(e, KG_ERR_INVALID_ARG, "mask and scores go together");
     const int64_t shard_tiles = (e->shard_end - e->shard_begin + KG_TILE - 1) / KG_TILE;
     if (shard_tiles <= 0) return KG_OK;
-    EvalArgs a;
+    HotArgs a;
     a.n_pods = n;
     a.pods_per_block = pods_per_block_for(n, shard_tiles);
     a.tile_begin = (int32_t)(e->shard_begin / KG_TILE);
-    a.node_end = e->shard_end;
     a.tiles_total = (int32_t)tiles_total(e);
+    a.node_end = e->shard_end;
     a.col_begin = e->shard_begin;
     a.mask_words = (int32_t)((e->shard_end - e->shard_begin + 63) / 64);
     a.score_stride = (e->shard_end - e->shard_begin + 63) / 64 * 64;
+    a.fit_cap = e->consts.fit_most ? 100u : 0xFFFFFFFFu;
+    for (int s = 0; s < 8; s++) a.slot_res[s] = s < e->nslot ? e->slot_res[s] : -1;
     a.now_ns = now_ns;
-    a.bm = e->bm;
-    const kg_pod_dev *pods = e->pods + pod_begin;
     dim3 grid((unsigned)shard_tiles, (unsigned)((n + a.pods_per_block - 1) / a.pods_per_block));
     if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
-    if (mask && scores) hipLaunchKernelGGL((k_eval<true, true>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a, pods, mask, scores, partials);
-    else if (mask) hipLaunchKernelGGL((k_eval<true, false>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a, pods, mask, scores, partials);
-    else if (scores) hipLaunchKernelGGL((k_eval<false, true>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a, pods, mask, scores, partials);
-    else hipLaunchKernelGGL((k_eval<false, false>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a, pods, mask, scores, partials);
+    if (e->nslot == 2) launch_hot<2>(e, grid, a, pod_begin, mask, scores, partials);
+    else if (e->nslot == 4) launch_hot<4>(e, grid, a, pod_begin, mask, scores, partials);
+    else launch_hot<8>(e, grid, a, pod_begin, mask, scores, partials);
     HIP_TRY(e, hipGetLastError());
     if (e->profiling) {
         HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
         e->ev_count++;
     }
+    // exact re-evaluation of the (rare) nodes outside the fp64 fast-path bounds
+    const int64_t width = e->shard_end - e->shard_begin;
+    HIP_TRY(e, hipMemsetAsync(e->slow_count, 0, sizeof(int32_t), e->stream));
+    hipLaunchKernelGGL(k_slow_list, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, e->stream, e->pl.dflags,
+                       e->shard_begin, e->shard_end, e->slow_list, e->slow_count);
+    hipLaunchKernelGGL(k_fix_slow, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->consts, e->pl,
+                       e->pods + pod_begin, n, e->slow_list, e->slow_count, e->shard_begin, a.mask_words, a.score_stride,
+                       a.tiles_total, now_ns, (unsigned long long *)mask, scores, partials);
+    HIP_TRY(e, hipGetLastError());
     return KG_OK;
 }
 
@@ -544,6 +766,7 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->plane_mem) (void)hipFree(e->plane_mem);
     if (e->pods) (void)hipFree(e->pods);
+    if (e->hot) (void)hipFree(e->hot);
     if (e->scratch) (void)hipFree(e->scratch);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     for (int k = 0; k < kg_engine::kRing; k++) {
@@ -595,7 +818,7 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
     size_t total = 0;
     const size_t sizes[] = {sizeof(kg_node_row) * (size_t)cap, (size_t)KG_NUM_RES * 8 * cap, (size_t)KG_NUM_RES * 8 * cap,
                             (size_t)KG_NUM_RES * 8 * cap, 2 * 8 * (size_t)cap, 4 * 8 * (size_t)cap, 8 * (size_t)cap,
-                            4 * (size_t)cap, 4 * (size_t)cap};
+                            4 * (size_t)cap, 4 * (size_t)cap, 4 * (size_t)cap, 256};
     for (size_t s : sizes) total += (s + 255) / 256 * 256;
     HIP_TRY(e, hipMalloc(&e->plane_mem, total));
     HIP_TRY(e, hipMemsetAsync(e->plane_mem, 0, total, e->stream));
@@ -609,6 +832,8 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
     e->pl.metric_ns = (int64_t *)carve(sizes[6]);
     e->pl.dflags = (uint32_t *)carve(sizes[7]);
     e->pl.fit_mask = (uint32_t *)carve(sizes[8]);
+    e->slow_list = (int32_t *)carve(sizes[9]);
+    e->slow_count = (int32_t *)carve(sizes[10]);
     e->pl.cap = cap;
     e->n_nodes = n_nodes;
     e->shard_begin = 0;
@@ -677,25 +902,61 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     if (n < 0 || (n > 0 && !rows)) return set_err(e, KG_ERR_INVALID_ARG, "bad pod batch");
     std::vector<kg_pod_dev> dev((size_t)n);
     BatchMasks bm{0, 0};
+    bool la_prod = false, pow2 = true;
+    uint32_t need = 0;
     for (int32_t i = 0; i < n; i++) {
         if (!kg_pod_row_in_bounds(rows[i])) return set_err(e, KG_ERR_RANGE, "pod %d: request outside the engine bounds", i);
         kg_pod_dev_from_row(e->cfg, rows[i], dev[i]);
         bm.cmp |= dev[i].cmp_mask;
         bm.fit |= dev[i].fit_mask;
+        la_prod |= (rows[i].flags & KG_POD_LA_PROD_SCORE) != 0;
+        pow2 &= dev[i].fit_w == 0 || (dev[i].fit_w & (dev[i].fit_w - 1)) == 0;
     }
     if (!(e->cfg.enabled_plugins & KG_PLUGIN_FIT)) bm.cmp = bm.fit = 0;
+    if (!(e->cfg.enabled_plugins & KG_PLUGIN_LOADAWARE)) la_prod = false;
+    pow2 &= e->consts.la_shift != 0xFF || !(e->cfg.enabled_plugins & KG_PLUGIN_LOADAWARE);
+    // resource profile: the smallest slot set covering every resource the batch compares or scores
+    int32_t nslot;
+    int32_t slot_res[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    std::vector<char> hot;
+    auto build = [&](auto tag, int ns, const int32_t *map) {
+        using H = decltype(tag);
+        nslot = ns;
+        for (int s = 0; s < ns; s++) slot_res[s] = map[s];
+        hot.assign(sizeof(H) * (size_t)n, 0);
+        need = 0;
+        for (int32_t i = 0; i < n; i++) need |= kg_pod_hot_from_row(e->cfg, rows[i], slot_res, ((H *)hot.data())[i]);
+    };
+    static const int32_t native_map[2] = {KG_RES_CPU, KG_RES_MEMORY};
+    static const int32_t coloc_map[4] = {KG_RES_CPU, KG_RES_MEMORY, KG_RES_BATCH_CPU, KG_RES_BATCH_MEMORY};
+    static const int32_t all_map[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+    build(kg_pod_hot_t<2>(), 2, native_map);
+    if (need & ~0x3u) build(kg_pod_hot_t<4>(), 4, coloc_map);
+    if (need & ~0x1Bu) build(kg_pod_hot_t<8>(), 8, all_map);
     HIP_TRY(e, hipStreamSynchronize(e->stream));
-    if (n > e->pods_cap) {
+    if (n > e->pods_cap || hot.size() > e->hot_bytes) {
         if (e->pods) HIP_TRY(e, hipFree(e->pods));
+        if (e->hot) HIP_TRY(e, hipFree(e->hot));
         e->pods = nullptr;
+        e->hot = nullptr;
         e->pods_cap = 0;
-        HIP_TRY(e, hipMalloc(&e->pods, sizeof(kg_pod_dev) * (size_t)n));
+        e->hot_bytes = 0;
+        HIP_TRY(e, hipMalloc(&e->pods, sizeof(kg_pod_dev) * (size_t)(n > 0 ? n : 1)));
+        HIP_TRY(e, hipMalloc(&e->hot, sizeof(kg_pod_hot_t<8>) * (size_t)(n > 0 ? n : 1)));
         e->pods_cap = n;
+        e->hot_bytes = sizeof(kg_pod_hot_t<8>) * (size_t)(n > 0 ? n : 1);
     }
-    if (n) HIP_TRY(e, hipMemcpyAsync(e->pods, dev.data(), sizeof(kg_pod_dev) * (size_t)n, hipMemcpyHostToDevice, e->stream));
+    if (n) {
+        HIP_TRY(e, hipMemcpyAsync(e->pods, dev.data(), sizeof(kg_pod_dev) * (size_t)n, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(e, hipMemcpyAsync(e->hot, hot.data(), hot.size(), hipMemcpyHostToDevice, e->stream));
+    }
     HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->nslot = nslot;
+    for (int s = 0; s < 8; s++) e->slot_res[s] = slot_res[s];
     e->n_pods = n;
     e->bm = bm;
+    e->la_prod = la_prod;
+    e->pow2 = pow2;
     return KG_OK;
 }
 
@@ -713,8 +974,11 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     const size_t top_b = (size_t)P * 8;
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
     const bool dev = out->out_on_device != 0;
-    size_t need = up(part_b) + up(top_b);
-    if (!dev) need += (out->mask ? up(mask_b) : 0) + (out->scores ? up(score_b) : 0);
+    // the hot kernel writes the mask and the scores together: stage whichever is not a device output
+    const bool planes = out->mask || out->scores;
+    const bool stage_mask = planes && (!dev || !out->mask);
+    const bool stage_scores = planes && (!dev || !out->scores);
+    size_t need = up(part_b) + up(top_b) + (stage_mask ? up(mask_b) : 0) + (stage_scores ? up(score_b) : 0);
     st = ensure_scratch(e, need + 256);
     if (st) return st;
     char *s = (char *)e->scratch;
@@ -723,13 +987,11 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     char *q = s + up(part_b) + up(top_b);
     uint64_t *mask = nullptr;
     uint16_t *scores = nullptr;
-    if (out->mask) {
-        if (dev) mask = out->mask;
-        else { mask = (uint64_t *)q; q += up(mask_b); }
-    }
-    if (out->scores) {
-        if (dev) scores = (uint16_t *)out->scores;
-        else { scores = (uint16_t *)q; q += up(score_b); }
+    if (planes) {
+        if (stage_mask) { mask = (uint64_t *)q; q += up(mask_b); }
+        else mask = out->mask;
+        if (stage_scores) { scores = (uint16_t *)q; q += up(score_b); }
+        else scores = (uint16_t *)out->scores;
     }
     HIP_TRY(e, hipMemsetAsync(part, 0, part_b, e->stream));
     st = launch_eval(e, now_ns, 0, P, mask, scores, part);

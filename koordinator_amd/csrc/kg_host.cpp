@@ -527,6 +527,9 @@ void kg_consts_from_config(const kg_config &c, kg_consts &k) {
     k.la_w[1] = (int32_t)c.la_resource_weight[1];
     k.la_wsum = k.la_w[0] + k.la_w[1];
     k.la_magic = k.la_wsum ? (uint32_t)((0x80000000ULL + (uint64_t)k.la_wsum - 1) / (uint64_t)k.la_wsum) : 0;
+    k.la_shift = 0xFF;
+    if (k.la_wsum > 0 && (k.la_wsum & (k.la_wsum - 1)) == 0) k.la_shift = __builtin_ctz((unsigned)k.la_wsum);
+    k.la_rcp = k.la_wsum ? 1.0f / (float)k.la_wsum : 0.0f;
     k.la_filter_expired = c.la_filter_expired_node_metrics;
     k.la_has_exp = c.la_has_expiration;
     k.la_exp_ns = c.la_has_expiration ? c.la_expiration_seconds * 1000000000LL : 0;
@@ -566,6 +569,57 @@ void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &
     d.la_est_i[0] = row.la_estimate[0];
     d.la_est_i[1] = row.la_estimate[1];
 }
+
+template <int S>
+uint32_t kg_pod_hot_from_row(const kg_config &c, const kg_pod_row &row, const int32_t *slot_res, kg_pod_hot_t<S> &h) {
+    memset(&h, 0, sizeof(h));
+    const bool hr = (row.flags & KG_POD_HAS_REQUEST) != 0;
+    const bool fit_on = (c.enabled_plugins & KG_PLUGIN_FIT) != 0;
+    // resources that need a slot: natives with a non-zero request and scalar keys (a zero native
+    // request only fails an overcommitted node, which the kernel folds into the node filter bits),
+    // and every resource the pod scores
+    uint32_t need = 0, fit_mask = 0, w = 0;
+    if (fit_on && hr) {
+        for (int r = 0; r < 3; r++)
+            if (row.request[r] != 0) need |= 1u << r;
+        need |= row.request_present & KG_SCALAR_RES_MASK;
+    }
+    for (int r = 0; fit_on && r < KG_NUM_RES; r++) {
+        if (c.fit_resource_weight[r] <= 0) continue;
+        if (scalar_res(r) && row.fit_score_request[r] == 0) continue;
+        fit_mask |= 1u << r;
+        w += (uint32_t)c.fit_resource_weight[r];
+    }
+    need |= fit_mask;
+    uint32_t flags = (row.flags & KG_POD_LA_PROD_SCORE) ? KG_HOT_PROD : 0u;
+    for (int s = 0; s < S; s++) {
+        const int r = slot_res[s];
+        h.req[s] = KG_NEUTRAL_REQ;
+        if (r < 0) continue;
+        // natives are compared once the pod requests anything; scalars only when the key is present
+        if (fit_on && hr && (r < 3 || bit(row.request_present, r))) {
+            h.req[s] = row.request[r];
+            flags |= 1u << (KG_HOT_CMP_SHIFT + s);
+        }
+        if (bit(fit_mask, r)) {
+            h.fit_w[s] = (uint32_t)c.fit_resource_weight[r];
+            const double pr = (double)row.fit_score_request[r];
+            h.fit_pr[s] = c.fit_strategy == KG_STRATEGY_MOST_ALLOCATED ? pr : -pr;
+            flags |= 1u << (KG_HOT_FIT_SHIFT + s);
+        }
+    }
+    h.fit_shift = (w > 0 && (w & (w - 1)) == 0) ? (uint32_t)__builtin_ctz(w) : (w == 0 ? 0u : 0xFFu);
+    h.fit_rcp = w ? 1.0f / (float)w : 0.0f;
+    h.la_est[0] = -(double)row.la_estimate[0];
+    h.la_est[1] = -(double)row.la_estimate[1];
+    const uint32_t variant = (row.flags & KG_POD_DAEMONSET) ? 2u : (row.flags & KG_POD_PROD) ? 1u : 0u;
+    h.okshift = variant + (hr && fit_on ? 3u : 0u);
+    h.flags = flags;
+    return need;
+}
+template uint32_t kg_pod_hot_from_row<2>(const kg_config &, const kg_pod_row &, const int32_t *, kg_pod_hot_t<2> &);
+template uint32_t kg_pod_hot_from_row<4>(const kg_config &, const kg_pod_row &, const int32_t *, kg_pod_hot_t<4> &);
+template uint32_t kg_pod_hot_from_row<8>(const kg_config &, const kg_pod_row &, const int32_t *, kg_pod_hot_t<8> &);
 
 bool kg_pod_row_in_bounds(const kg_pod_row &row) {
     for (int r = 0; r < KG_NUM_RES; r++)

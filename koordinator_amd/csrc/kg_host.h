@@ -5,3 +5,7 @@
 void kg_consts_from_config(const kg_config &c, kg_consts &k);
 void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &d);
 bool kg_pod_row_in_bounds(const kg_pod_row &row);
+// Fills the S-slot hot row (slot s ↔ resource slot_res[s]) and returns the pod's resources that
+// need a slot (compared or scored), so the caller can check the profile covers them.
+template <int S>
+uint32_t kg_pod_hot_from_row(const kg_config &c, const kg_pod_row &row, const int32_t *slot_res, kg_pod_hot_t<S> &h);
