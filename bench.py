@@ -45,6 +45,21 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(kernel_prefix: str = "k_eval"):
+    """HBM bytes per launch of the hot kernel from the committed rocprofv3 PMC passes of this same
+    command (profiles/<CURRENT>/summary.json, written by tools/summarize_profile.py), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "CURRENT")) as f:
+            tag = f.read().strip()
+        with open(os.path.join(ROOT, "profiles", tag, "summary.json")) as f:
+            s = json.load(f)
+        if not s.get("hbm_traffic_per_launch") or kernel_prefix not in (s.get("hot_kernel") or {}).get("name", ""):
+            return None, None
+        return s["hbm_traffic_per_launch"]["total_bytes"], f"profiles/{tag}"
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -159,6 +174,7 @@ def main():
                                   f"Parallelizer-faithful {workers}-thread node fan-out (oracle/koord_oracle.c "
                                   f"kgo_eval_parallel), {tc:.1f}s on {cpu_model()}"}
 
+    traffic, traffic_src = pmc_traffic()
     if rank == 0:
         line = {
             "metric": "pod×node Filter+Score evals/sec (LoadAwareScheduling + NodeResourcesFit, matrix mode)",
@@ -177,7 +193,9 @@ def main():
                                    "args, outputs: feasibility bits + Fit/LoadAware u8 scores + per-pod top-1",
                        "pods": P, "nodes_per_gpu": N, "parallelism": f"node-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK, 4),
+                         "traffic": None if traffic is None else int(traffic), "traffic_unit": "bytes per launch (PMC)",
+                         "traffic_source": traffic_src,
                          "kernel": "k_eval", "kernel_ms": round(k_ms, 4),
                          "algorithmic_bytes_per_launch": int(algo_bytes)},
             "cpu_baseline": cpu_baseline,

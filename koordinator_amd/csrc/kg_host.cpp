@@ -384,8 +384,9 @@ kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
     }
     if (fw > 600 || lw > 600) return fail("resource weight sum too large (max 600)");
     if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && lw == 0) return fail("LoadAwareScheduling needs resourceWeights");
-    if (c->weight_fit < 0 || c->weight_loadaware < 0 || c->weight_fit > 100000 || c->weight_loadaware > 100000)
-        return fail("plugin weight out of range");
+    // totals are packed as ((total + 1) << 10) | node into 32-bit per-tile keys: 100·Σweights < 2^22
+    if (c->weight_fit < 0 || c->weight_loadaware < 0 || (int64_t)c->weight_fit + c->weight_loadaware > 40000)
+        return fail("plugin weight out of range (each >= 0, sum <= 40000)");
     if (c->fit_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->fit_strategy != KG_STRATEGY_MOST_ALLOCATED)
         return fail("unsupported NodeResourcesFit scoring strategy");
     return KG_OK;
