@@ -31,7 +31,7 @@ POD_HAS_REQUEST, POD_DAEMONSET, POD_PROD, POD_LA_PROD_SCORE, POD_VALID = 0x1, 0x
 NODE_VALID, NODE_HAS_METRIC, NODE_HAS_UPDATE_TIME, NODE_LA_PASS_NONPROD, NODE_LA_PASS_PROD = 0x1, 0x2, 0x4, 0x8, 0x10
 
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE, CODE_UNSCHEDULABLE_AND_UNRESOLVABLE = 0, 1, 2, 3
-TILE = 512
+TILE = 1024
 
 RESOURCE_LIST = np.dtype([("v", "<i8", (NUM_RES,)), ("present", "<u4"), ("_pad", "<u4")], align=True)
 

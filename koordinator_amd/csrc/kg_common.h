@@ -29,7 +29,9 @@
 #define KG_HD inline
 #endif
 
-#define KG_TILE 512                 // nodes per eval workgroup (one node per thread)
+#define KG_TILE 1024                // nodes per eval workgroup / per-pod partial key (two nodes per lane)
+#define KG_TILE_SHIFT 10            // log2 KG_TILE: partial key = ((total + 1) << 10) | (1023 − local node)
+#define KG_BLOCK 512                // threads per eval workgroup
 #define KG_EPS 0x1p-42
 #define KG_CAP_LIMIT (1LL << 41)    // fast-path bound on every divisor
 #define KG_VAL_LIMIT (1LL << 50)    // fast-path bound on every numerator term
@@ -82,7 +84,7 @@ struct kg_consts {
 
 #define KG_NEUTRAL_REQ INT64_MIN  // request that passes every Fit compare
 
-// per-pod data of the hot kernel (k_eval_hot), over S resource "slots" (the launch's resource
+// per-pod data of the hot kernel (k_eval2), over S resource "slots" (the launch's resource
 // profile maps slot s → resource id).  Read as whole 64-byte blocks with s_load_dwordx16.
 #define KG_HOT_PROD 0x1u             // flags: LoadAware prod-usage variant
 #define KG_HOT_CMP_SHIFT 8           // flags bits 8..15: slot s is compared by the Fit filter
@@ -97,6 +99,46 @@ struct alignas(64) kg_pod_hot_t {
     uint32_t fit_shift;    // log2 W when W is a power of two (W = Σ fit_w), else 0xFF
     float fit_rcp;         // 1 / W
     uint32_t flags;        // KG_HOT_*
+};
+
+// ---- class-specialised matrix mode (k_eval3) ---------------------------------------------
+// Pods of a batch that compare the same resources in the Fit filter, score the same resources,
+// take the same node-filter variant and the same LoadAware usage variant form a class.  Within a
+// class every per-pair branch is a compile-time constant: NC compared resources (int64), NF scored
+// resources (fp64 fma), padded to 2 or 4.  Rows are stored class after class (queue order inside a
+// class) and carry their output offsets.
+#define KG_CLS_MAX 16                // classes per batch on the specialised path
+template <int NC, int NF>
+struct alignas(64) kg_pod_cls_t {
+    int64_t req[NC];       // Fit filter request of the compared resources (INT64_MIN pads)
+    double pr[NF];         // signed Fit pod request of the scored resources (0 pads)
+    double la[2];          // −EstimatePod (cpu, memory)
+    int64_t score_off;     // output row × score stride (elements)
+    int32_t mask_off;      // output row × mask words
+    int32_t row;           // output row (partial keys)
+};
+
+struct kg_cls_desc {
+    int32_t kind;          // 0: (2,2)  1: (2,4)  2: (4,2)  3: (4,4)   (NC, NF)
+    int32_t first;         // first row of the class in the class-sorted pod array
+    int32_t count;
+    int32_t cmp_res[4];    // resource of each compared slot (−1 pad)
+    int32_t fit_res[4];    // resource of each scored slot (−1 pad)
+    uint32_t fit_w[4];     // Fit weight of each scored slot (0 pad)
+    uint32_t fit_shift;    // log2 Σ fit_w (a power of two on this path)
+    uint32_t node_ok_sel;  // node filter bit: variant (0 non-prod, 1 prod, 2 daemonset) + 3·has_request
+    uint32_t la_variant;   // 0 non-prod usage, 1 prod usage (ScoreAccordingProdUsage)
+    uint32_t over_mask;    // natives with a zero request on a pod with requests: fail an overcommitted node
+    int64_t row_bytes;     // sizeof(kg_pod_cls_t<NC, NF>)
+    int64_t rows_offset;   // byte offset of the class's rows in the row buffer
+};
+
+// one workgroup row of the launch grid: a pod range of one class
+struct kg_cls_work {
+    int32_t cls;
+    int32_t begin;         // [begin, end) within the class
+    int32_t end;
+    int32_t _pad;
 };
 
 struct kg_planes {

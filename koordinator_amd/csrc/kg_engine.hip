@@ -26,13 +26,13 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <map>
 #include <string>
 #include <vector>
 
 #include "kg_common.h"
 #include "kg_host.h"
 
-#define KG_WAVES_PER_TILE (KG_TILE / 64)
 #define KG_POD_CHUNK 64          // pods between two LDS partial combines in k_eval
 #define KG_RESOLVE_THREADS 1024
 #define KG_MAX_CHUNK 1024        // max pods per resolve call (touched-list capacity)
@@ -279,126 +279,60 @@ struct HotArgs {
     uint32_t fit_cap;        // 100 for MostAllocated (clamp), 0xFFFFFFFF for LeastAllocated (no-op)
     int32_t slot_res[8];     // resource id of each slot (−1 unused)
     int64_t now_ns;
+    uint32_t ablate;         // TEMP experiment bits
 };
 
-// FAST = both plugins on, LeastAllocated, every divisor a power of two, plugin weights 1 (checked on
-// the host); otherwise the generic path handles MostAllocated clamps, other divisors and weights.
-template <int S, bool FAST, bool LA_PROD, bool FULL, bool OUT>
-__device__ __forceinline__ void hot_loop(const kg_consts &c, const HotArgs &a, const kg_pod_hot_t<S> *__restrict__ pods,
-                                         uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
-                                         const int64_t (&fr)[S], const double (&R)[S], const double (&F)[S],
-                                         const double (&laR)[2], const double (&laF0)[2], const double (&laF1)[2],
-                                         uint32_t okbits, uint32_t node_slot_mask, int64_t node, int p0,
-                                         int p1, uint32_t *kbuf) {
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const uint32_t key_base = (uint32_t)(KG_TILE + KG_TILE - 1 - tid);  // + (tot << 9) = ((tot+1) << 9) | local
-    const bool store_lane = node < a.node_end;
-    const bool fit_on = FAST || (c.plugins & KG_PLUGIN_FIT);
-    const bool la_on = FAST || (c.plugins & KG_PLUGIN_LOADAWARE);
-    uint16_t *srow = scores + (node - a.col_begin);
-    uint64_t *mrow = mask + ((node - a.col_begin) >> 6);
-    for (int p = p0; p < p1; p++) {
-        const kg_pod_hot_t<S> pd = load_pod<S>(pods + p);
-        // node-only filter outcome as a lane mask, chosen by a scalar select chain
-        bool ok = (okbits >> pd.okshift) & 1u;
-        uint32_t fit = 0;
-        if (fit_on) {
-#pragma unroll
-            for (int s = 0; s < S; s++) {
-                if (s >= 2 && !((pd.flags >> (KG_HOT_CMP_SHIFT + s)) & 1u)) continue;  // uniform
-                ok &= pd.req[s] <= fr[s];
-            }
-            uint32_t sum = 0;
-#pragma unroll
-            for (int s = 0; s < S; s++) {
-                if (s >= 2 && !((pd.flags >> (KG_HOT_FIT_SHIFT + s)) & 1u)) continue;  // uniform
-                uint32_t q = cvt_u32_sat(__builtin_fma(pd.fit_pr[s], R[s], F[s]));
-                if (!FAST) q = q < a.fit_cap ? q : a.fit_cap;  // MostAllocated clamp
-                sum = __umul24(pd.fit_w[s], q) + sum;
-            }
-            const uint32_t pmask = (pd.flags >> KG_HOT_FIT_SHIFT) & 0xFFu;
-            if (FULL || (node_slot_mask & pmask) == pmask) {
-                fit = FAST ? sum >> pd.fit_shift : div_w<false>(sum, pd.fit_shift, pd.fit_rcp);
-            } else {  // the node lacks a resource the pod scores (no allocatable): its weight drops out
-                uint32_t w = 0;
-#pragma unroll
-                for (int s = 0; s < S; s++) w += ((node_slot_mask & pmask) >> s & 1u) ? pd.fit_w[s] : 0u;
-                fit = w ? sum / w : 0u;
-            }
-        }
-        uint32_t la = 0;
-        if (la_on) {
-            const bool prod = LA_PROD && (pd.flags & KG_HOT_PROD);
-            const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la_est[0], laR[0], prod ? laF1[0] : laF0[0]));
-            const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la_est[1], laR[1], prod ? laF1[1] : laF0[1]));
-            const uint32_t sum = __umul24((uint32_t)c.la_w[0], q0) + __umul24((uint32_t)c.la_w[1], q1);
-            la = FAST ? sum >> c.la_shift : div_w<false>(sum, (uint32_t)c.la_shift, c.la_rcp);
-        }
-        if (OUT) {
-            if (store_lane) srow[(int64_t)p * a.score_stride] = (uint16_t)(fit | (la << 8));
-            const unsigned long long b = __ballot(ok);
-            // lane 0 holds the wave's first node: waves wholly past the shard end must not store
-            if (lane == 0 && store_lane) mrow[(int64_t)p * a.mask_words] = b;
-        }
-        uint32_t tot;
-        if (FAST) tot = fit + la;
-        else tot = __umul24((uint32_t)c.weight_fit, fit) + __umul24((uint32_t)c.weight_la, la);
-        // per-lane key into LDS; the workgroup reduces 16 pods at a time (cheaper than a wave max per pod)
-        kbuf[(p - p0) * KG_TILE + tid] = ok ? (tot << 9) + key_base : 0u;
-    }
-}
+// ---------------------------------------------------------------------------------------
+// v2: two nodes per lane (a 1024-node tile per 512-thread workgroup)
+// ---------------------------------------------------------------------------------------
+// per-lane registers of one node
+template <int S, bool LA_PROD>
+struct HotNode {
+    int64_t fr[S];          // Allocatable − Requested per slot (Fit filter)
+    double R[S], F[S];      // Fit least/most-requested fma operands per slot
+    double laR[2], laF0[2], laF1[2];
+    uint32_t okbits;        // node-only filter outcome per pod variant (bit variant + 3·has_request)
+    uint32_t slot_mask;     // slots the node contributes to the Fit score
+};
 
-#define KG_KCHUNK 16   // pods per LDS key buffer
-
-template <int S, bool FAST, bool LA_PROD, bool OUT>
-__global__ __launch_bounds__(KG_TILE) void k_eval_hot(kg_consts c, kg_planes pl, HotArgs a,
-                                                      const kg_pod_hot_t<S> *__restrict__ pods,
-                                                      uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
-                                                      uint32_t *__restrict__ partials) {
-    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_KCHUNK * KG_TILE];
-    const int tid = threadIdx.x;
-    const int tile = a.tile_begin + blockIdx.x;
-    const int64_t node = (int64_t)tile * KG_TILE + tid;
-    const bool in_range = node < a.node_end;
+template <int S, bool LA_PROD>
+__device__ __forceinline__ void load_hot_node(const kg_consts &c, const kg_planes &pl, const HotArgs &a, int64_t node,
+                                              uint32_t slot_natives, HotNode<S, LA_PROD> &n) {
     const int64_t cap = pl.cap;
-    // ---- node registers (loaded once, reused for every pod of the block) ----
+    const bool in_range = node < a.node_end;   // nodes past the shard end are never feasible
     const uint32_t df = in_range ? pl.dflags[node] : 0u;
     const bool slow = (df & KGD_SLOW) != 0;
     const uint32_t nfm = in_range ? pl.fit_mask[node] : 0u;
-    int64_t fr[S];
-    double R[S], F[S];
-    uint32_t node_slot_mask = 0, slot_natives = 0;
+    n.slot_mask = 0;
 #pragma unroll
     for (int s = 0; s < S; s++) {
         const int r = a.slot_res[s];
-        fr[s] = 0;
-        R[s] = 0.0;
-        F[s] = 0.0;
+        n.fr[s] = 0;
+        n.R[s] = 0.0;
+        n.F[s] = 0.0;
         if (r >= 0) {
-            if (r < 3) slot_natives |= 1u << r;
-            if (in_range) fr[s] = pl.free_[r * cap + node];
+            if (in_range) n.fr[s] = pl.free_[r * cap + node];
             if (in_range && !slow) {
-                R[s] = pl.fit_R[r * cap + node];
-                F[s] = pl.fit_F[r * cap + node];
+                n.R[s] = pl.fit_R[r * cap + node];
+                n.F[s] = pl.fit_F[r * cap + node];
             }
-            if ((nfm >> r) & 1u) node_slot_mask |= 1u << s;
+            if ((nfm >> r) & 1u) n.slot_mask |= 1u << s;
         }
     }
-    double laR[2] = {0.0, 0.0}, laF0[2] = {0.0, 0.0}, laF1[2] = {0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 2; r++) n.laR[r] = n.laF0[r] = n.laF1[r] = 0.0;
     bool expired = false;
     if (c.plugins & KG_PLUGIN_LOADAWARE) {
         expired = kg_metric_expired(c, df, in_range ? pl.metric_ns[node] : 0, a.now_ns);
         if (in_range && !slow && kg_la_valid(c, df, expired)) {  // invalid NodeMetric ⇒ score 0 via R = F = 0
 #pragma unroll
             for (int r = 0; r < 2; r++) {
-                laR[r] = pl.la_R[r * cap + node];
-                laF0[r] = pl.la_F[(0 * 2 + r) * cap + node];
-                if (LA_PROD) laF1[r] = pl.la_F[(1 * 2 + r) * cap + node];
+                n.laR[r] = pl.la_R[r * cap + node];
+                n.laF0[r] = pl.la_F[(0 * 2 + r) * cap + node];
+                if (LA_PROD) n.laF1[r] = pl.la_F[(1 * 2 + r) * cap + node];
             }
         }
     }
-    // node-only filter outcomes: bit (variant + 3·has_request), variant 0 non-prod, 1 prod, 2 daemonset
     bool base = (df & KGD_VALID) && !slow;
     if (c.plugins & KG_PLUGIN_FIT) base = base && !(df & KGD_PODS_FULL);
     bool over = false;  // a zero request of a native resource without a slot still fails an overcommitted node
@@ -415,24 +349,134 @@ __global__ __launch_bounds__(KG_TILE) void k_eval_hot(kg_consts c, kg_planes pl,
         okbits |= (okv ? 1u : 0u) << v;
         okbits |= (okv && !over ? 1u : 0u) << (v + 3);
     }
-    uint32_t all_slots = 0;
+    n.okbits = okbits;
+}
+
+// One (pod, node) pair on the fast path: feasibility, Fit and LoadAware scores.
+template <int S, bool FAST, bool LA_PROD, bool FULL>
+__device__ __forceinline__ bool eval_hot(const kg_consts &c, const HotArgs &a, const kg_pod_hot_t<S> &pd,
+                                         const HotNode<S, LA_PROD> &n, uint32_t &fit, uint32_t &la) {
+    bool ok = (n.okbits >> pd.okshift) & 1u;
+    fit = 0;
+    if (FAST || (c.plugins & KG_PLUGIN_FIT)) {
 #pragma unroll
-    for (int s = 0; s < S; s++) all_slots |= (a.slot_res[s] >= 0) ? (1u << s) : 0u;
-    const bool full = __all(((node_slot_mask & all_slots) == all_slots) || !in_range);
+        for (int s = 0; s < S; s++) {
+            if (s >= 2 && !((pd.flags >> (KG_HOT_CMP_SHIFT + s)) & 1u)) continue;  // uniform
+            ok &= pd.req[s] <= n.fr[s];
+        }
+        uint32_t sum = 0;
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            if (s >= 2 && !((pd.flags >> (KG_HOT_FIT_SHIFT + s)) & 1u)) continue;  // uniform
+            uint32_t q = cvt_u32_sat(__builtin_fma(pd.fit_pr[s], n.R[s], n.F[s]));
+            if (!FAST) q = q < a.fit_cap ? q : a.fit_cap;  // MostAllocated clamp
+            sum = __umul24(pd.fit_w[s], q) + sum;
+        }
+        const uint32_t pmask = (pd.flags >> KG_HOT_FIT_SHIFT) & 0xFFu;
+        if (FULL || (n.slot_mask & pmask) == pmask) {
+            fit = FAST ? sum >> pd.fit_shift : div_w<false>(sum, pd.fit_shift, pd.fit_rcp);
+        } else {  // the node lacks a resource the pod scores (no allocatable): its weight drops out
+            uint32_t w = 0;
+#pragma unroll
+            for (int s = 0; s < S; s++) w += ((n.slot_mask & pmask) >> s & 1u) ? pd.fit_w[s] : 0u;
+            fit = w ? sum / w : 0u;
+        }
+    }
+    la = 0;
+    if (FAST || (c.plugins & KG_PLUGIN_LOADAWARE)) {
+        const bool prod = LA_PROD && (pd.flags & KG_HOT_PROD);
+        const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la_est[0], n.laR[0], prod ? n.laF1[0] : n.laF0[0]));
+        const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la_est[1], n.laR[1], prod ? n.laF1[1] : n.laF0[1]));
+        const uint32_t sum = __umul24((uint32_t)c.la_w[0], q0) + __umul24((uint32_t)c.la_w[1], q1);
+        la = FAST ? sum >> c.la_shift : div_w<false>(sum, (uint32_t)c.la_shift, c.la_rcp);
+    }
+    return ok;
+}
+
+// Pods [p0, p1) against the lane's two nodes (n0 = wave base + lane, n1 = n0 + 64).
+// seg0 / seg1: the wave's two 64-node segments lie inside the output rows (wave-uniform).
+template <int S, bool FAST, bool LA_PROD, bool FULL, bool OUT>
+__device__ __forceinline__ void hot_loop2(const kg_consts &c, const HotArgs &a, const kg_pod_hot_t<S> *__restrict__ pods,
+                                          uint64_t *__restrict__ mrow, uint16_t *__restrict__ srow,
+                                          const HotNode<S, LA_PROD> &n0, const HotNode<S, LA_PROD> &n1,
+                                          uint32_t kb0, uint32_t kb1, int mask_lanes, bool seg0, bool seg1, int p0,
+                                          int p1, uint32_t *kbuf) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    for (int p = p0; p < p1; p++) {
+        const kg_pod_hot_t<S> pd = load_pod<S>(pods + p);
+        uint32_t fit0, la0, fit1, la1;
+        const bool ok0 = eval_hot<S, FAST, LA_PROD, FULL>(c, a, pd, n0, fit0, la0);
+        const bool ok1 = eval_hot<S, FAST, LA_PROD, FULL>(c, a, pd, n1, fit1, la1);
+        if (OUT) {
+            uint16_t *s = srow + (int64_t)p * a.score_stride;
+            if (seg0) s[0] = (uint16_t)(fit0 | (la0 << 8));
+            if (seg1) s[64] = (uint16_t)(fit1 | (la1 << 8));
+            const unsigned long long b0 = __ballot(ok0), b1 = __ballot(ok1);
+            if (lane < mask_lanes) mrow[(int64_t)p * a.mask_words + lane] = lane ? b1 : b0;
+        }
+        uint32_t tot0, tot1;
+        if (FAST) {
+            tot0 = fit0 + la0;
+            tot1 = fit1 + la1;
+        } else {
+            tot0 = __umul24((uint32_t)c.weight_fit, fit0) + __umul24((uint32_t)c.weight_la, la0);
+            tot1 = __umul24((uint32_t)c.weight_fit, fit1) + __umul24((uint32_t)c.weight_la, la1);
+        }
+        const uint32_t k0 = ok0 ? (tot0 << KG_TILE_SHIFT) + kb0 : 0u;
+        const uint32_t k1 = ok1 ? (tot1 << KG_TILE_SHIFT) + kb1 : 0u;
+        kbuf[(p - p0) * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
+    }
+}
+
+#define KG_KCHUNK 16   // pods per LDS key buffer
+
+template <int S, bool FAST, bool LA_PROD, bool OUT>
+__global__ __launch_bounds__(KG_BLOCK) void k_eval2(kg_consts c, kg_planes pl, HotArgs a,
+                                                    const kg_pod_hot_t<S> *__restrict__ pods,
+                                                    uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
+                                                    uint32_t *__restrict__ partials) {
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_KCHUNK * KG_BLOCK];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tile = a.tile_begin + blockIdx.x;
+    const int64_t wave_base = (int64_t)tile * KG_TILE + wave * 128;   // first node of the wave
+    const int64_t node0 = wave_base + lane, node1 = node0 + 64;
+    uint32_t slot_natives = 0, all_slots = 0;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        const int r = a.slot_res[s];
+        if (r >= 0 && r < 3) slot_natives |= 1u << r;
+        all_slots |= (r >= 0) ? (1u << s) : 0u;
+    }
+    HotNode<S, LA_PROD> n0, n1;
+    load_hot_node<S, LA_PROD>(c, pl, a, node0, slot_natives, n0);
+    load_hot_node<S, LA_PROD>(c, pl, a, node1, slot_natives, n1);
+    const bool full = __all(((n0.slot_mask & all_slots) == all_slots || node0 >= a.node_end) &&
+                            ((n1.slot_mask & all_slots) == all_slots || node1 >= a.node_end));
+    // output columns: a 64-node segment is written iff it lies inside the padded row (wave-uniform)
+    const int64_t col0 = wave_base - a.col_begin;
+    const bool seg0 = col0 < a.score_stride, seg1 = col0 + 64 < a.score_stride;
+    const int mask_lanes = seg1 ? 2 : seg0 ? 1 : 0;
+    uint16_t *srow = scores + col0 + lane;
+    uint64_t *mrow = mask + (col0 >> 6);
+    // key = ((tot + 1) << 10) | (1023 − local node) ⇒ max = best total, then lowest node
+    const uint32_t local0 = (uint32_t)(wave * 128 + lane);
+    const uint32_t kb0 = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0, kb1 = kb0 - 64;
     const int pb = blockIdx.y * a.pods_per_block;
     const int pe = min(pb + a.pods_per_block, a.n_pods);
-    // reduction geometry: thread t reduces 16 consecutive keys of pod (t >> 5), then 32 lanes combine
     const int rj = tid >> 5, rg = tid & 31;
     for (int p0 = pb; p0 < pe; p0 += KG_KCHUNK) {
         const int p1 = min(p0 + KG_KCHUNK, pe);
         if (full)
-            hot_loop<S, FAST, LA_PROD, true, OUT>(c, a, pods, mask, scores, fr, R, F, laR, laF0, laF1, okbits,
-                                                  node_slot_mask, node, p0, p1, kbuf);
+            hot_loop2<S, FAST, LA_PROD, true, OUT>(c, a, pods, mrow, srow, n0, n1, kb0, kb1, mask_lanes, seg0, seg1,
+                                                   p0, p1, kbuf);
         else
-            hot_loop<S, FAST, LA_PROD, false, OUT>(c, a, pods, mask, scores, fr, R, F, laR, laF0, laF1, okbits,
-                                                   node_slot_mask, node, p0, p1, kbuf);
+            hot_loop2<S, FAST, LA_PROD, false, OUT>(c, a, pods, mrow, srow, n0, n1, kb0, kb1, mask_lanes, seg0, seg1,
+                                                    p0, p1, kbuf);
         __syncthreads();
-        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * KG_TILE + rg * 16);
+        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * KG_BLOCK + rg * 16);
         uint32_t mx = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -441,7 +485,6 @@ __global__ __launch_bounds__(KG_TILE) void k_eval_hot(kg_consts c, kg_planes pl,
             const uint32_t a2 = a0 > a1 ? a0 : a1;
             mx = mx > a2 ? mx : a2;
         }
-        // max over the 32 lanes of this half-wave (rows 0-1 / 2-3): row_shr 1,2,4,8 then row_bcast:15
         mx = dpp_max_step(mx, 0);
         mx = dpp_max_step(mx, 1);
         mx = dpp_max_step(mx, 2);
@@ -452,7 +495,240 @@ __global__ __launch_bounds__(KG_TILE) void k_eval_hot(kg_consts c, kg_planes pl,
     }
 }
 
-// Slow nodes (outside the fp64 exactness bounds) come out of k_eval_hot as infeasible with
+// ---------------------------------------------------------------------------------------
+// k_eval3: class-specialised matrix mode (one launch; each workgroup = one 1024-node tile × a pod
+// range of ONE class, so every per-pair branch is resolved at compile time or per workgroup)
+// ---------------------------------------------------------------------------------------
+template <int NC, int NF>
+struct ClsNode {
+    int64_t fr[NC];        // Allocatable − Requested of the compared resources
+    double R[NF], F[NF];   // Fit fma operands of the scored resources
+    double laR[2], laF[2]; // LoadAware fma operands (the class's usage variant)
+    uint32_t w;            // Σ Fit weights of the scored resources the node has
+    bool ok;               // node-only filters for the class (valid, pods, overcommit, LoadAware thresholds)
+};
+
+template <int NC, int NF, bool FIT_ON, bool LA_ON>
+__device__ __forceinline__ void load_cls_node(const kg_consts &c, const kg_planes &pl, const kg_cls_desc &d,
+                                              int64_t node, int64_t node_end, int64_t now_ns, ClsNode<NC, NF> &n) {
+    const int64_t cap = pl.cap;
+    const bool in_range = node < node_end;
+    const uint32_t df = in_range ? pl.dflags[node] : 0u;
+    const bool slow = (df & KGD_SLOW) != 0;
+    const uint32_t nfm = in_range ? pl.fit_mask[node] : 0u;
+#pragma unroll
+    for (int k = 0; k < NC; k++) {
+        const int r = d.cmp_res[k];
+        n.fr[k] = (r >= 0 && in_range) ? pl.free_[r * cap + node] : 0;
+    }
+    n.w = 0;
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+        const int r = d.fit_res[f];
+        const bool use = FIT_ON && r >= 0 && in_range && !slow;
+        n.R[f] = use ? pl.fit_R[r * cap + node] : 0.0;
+        n.F[f] = use ? pl.fit_F[r * cap + node] : 0.0;
+        if (FIT_ON && r >= 0 && ((nfm >> r) & 1u)) n.w += d.fit_w[f];
+    }
+    bool expired = false;
+#pragma unroll
+    for (int r = 0; r < 2; r++) n.laR[r] = n.laF[r] = 0.0;
+    if (LA_ON) {
+        expired = kg_metric_expired(c, df, in_range ? pl.metric_ns[node] : 0, now_ns);
+        if (in_range && !slow && kg_la_valid(c, df, expired)) {  // invalid NodeMetric ⇒ score 0 via R = F = 0
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                n.laR[r] = pl.la_R[r * cap + node];
+                n.laF[r] = pl.la_F[(d.la_variant * 2 + r) * cap + node];
+            }
+        }
+    }
+    const uint32_t variant = d.node_ok_sel % 3u;
+    bool ok = (df & KGD_VALID) && !slow;
+    if (FIT_ON) {
+        ok = ok && !(df & KGD_PODS_FULL);
+        const uint32_t over = ((d.over_mask & 1u) ? KGD_OVER_CPU : 0u) | ((d.over_mask & 2u) ? KGD_OVER_MEM : 0u) |
+                              ((d.over_mask & 4u) ? KGD_OVER_EPH : 0u);
+        ok = ok && !(df & over);
+    }
+    if (LA_ON && variant < 2) ok = ok && kg_la_pass(c, df, expired, (int)variant);
+    n.ok = ok;
+}
+
+template <int NC, int NF>
+__device__ __forceinline__ kg_pod_cls_t<NC, NF> load_cls_row(const kg_pod_cls_t<NC, NF> *__restrict__ p) {
+    constexpr int NB = sizeof(kg_pod_cls_t<NC, NF>) / 64;
+    union U {
+        kg_u32x16 v[NB];
+        kg_pod_cls_t<NC, NF> h;
+        __device__ U() {}
+    } u;
+    const kg_u32x16 *src = reinterpret_cast<const kg_u32x16 *>(p);
+#pragma unroll
+    for (int i = 0; i < NB; i++) u.v[i] = src[i];
+    return u.h;
+}
+
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool FULL>
+__device__ __forceinline__ bool cls_pair(const kg_consts &c, const kg_cls_desc &d, const kg_pod_cls_t<NC, NF> &pd,
+                                         const ClsNode<NC, NF> &n, uint32_t &fit, uint32_t &la) {
+    bool ok = n.ok;
+#pragma unroll
+    for (int k = 0; k < NC; k++) ok &= pd.req[k] <= n.fr[k];
+    fit = 0;
+    if (FIT_ON) {
+        uint32_t sum = 0;
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n.R[f], n.F[f]));
+            if (MOST) q = q < 100u ? q : 100u;
+            sum = __umul24(d.fit_w[f], q) + sum;
+        }
+        if (FULL) fit = sum >> d.fit_shift;
+        else fit = n.w ? sum / n.w : 0u;  // the node lacks a scored resource: its weight drops out
+    }
+    la = 0;
+    if (LA_ON) {
+        const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la[0], n.laR[0], n.laF[0]));
+        const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la[1], n.laR[1], n.laF[1]));
+        la = (__umul24((uint32_t)c.la_w[0], q0) + __umul24((uint32_t)c.la_w[1], q1)) >> c.la_shift;
+    }
+    return ok;
+}
+
+// Pods [p0, p1) of one class against the lane's two nodes; rows come from the LDS chunk buffer.
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1>
+__device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> &n0,
+                                         const ClsNode<NC, NF> &n1, const char *lrows, int p0, int p1,
+                                         uint64_t *__restrict__ mask, uint16_t *__restrict__ scores, uint32_t scol,
+                                         int32_t mcol, bool seg0, bool seg1, int mask_lanes, uint32_t kb0,
+                                         uint32_t kb1, uint32_t *kbuf) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    for (int p = p0; p < p1; p++) {
+        const kg_pod_cls_t<NC, NF> pd =
+            *reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(lrows + (p - p0) * (int)sizeof(kg_pod_cls_t<NC, NF>));
+        uint32_t fit0, la0, fit1, la1;
+        const bool ok0 = cls_pair<NC, NF, MOST, FIT_ON, LA_ON, FULL>(c, d, pd, n0, fit0, la0);
+        const bool ok1 = cls_pair<NC, NF, MOST, FIT_ON, LA_ON, FULL>(c, d, pd, n1, fit1, la1);
+        if (OUT) {
+            uint16_t *srow = scores + pd.score_off;
+            if (seg0) srow[scol] = (uint16_t)(fit0 | (la0 << 8));
+            if (seg1) srow[scol + 64] = (uint16_t)(fit1 | (la1 << 8));
+            const unsigned long long b0 = __ballot(ok0), b1 = __ballot(ok1);
+            if (lane < mask_lanes) mask[pd.mask_off + mcol] = lane ? b1 : b0;
+        }
+        uint32_t tot0, tot1;
+        if (W1) {
+            tot0 = fit0 + la0;
+            tot1 = fit1 + la1;
+        } else {
+            tot0 = __umul24((uint32_t)c.weight_fit, fit0) + __umul24((uint32_t)c.weight_la, la0);
+            tot1 = __umul24((uint32_t)c.weight_fit, fit1) + __umul24((uint32_t)c.weight_la, la1);
+        }
+        const uint32_t k0 = ok0 ? (tot0 << KG_TILE_SHIFT) + kb0 : 0u;
+        const uint32_t k1 = ok1 ? (tot1 << KG_TILE_SHIFT) + kb1 : 0u;
+        kbuf[(p - p0) * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
+    }
+}
+
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1>
+__device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
+                                          const kg_cls_work &w, const char *__restrict__ rows_base,
+                                          uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
+                                          uint32_t *__restrict__ partials, uint32_t *kbuf, char *lrows) {
+    constexpr int RB = (int)sizeof(kg_pod_cls_t<NC, NF>);
+    constexpr int CHUNK_DW = KG_KCHUNK * RB / 4;          // dwords of one chunk of rows (≤ KG_BLOCK)
+    static_assert(CHUNK_DW <= KG_BLOCK, "one dword per thread stages a chunk");
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tile = a.tile_begin + blockIdx.x;
+    const int64_t wave_base = (int64_t)tile * KG_TILE + wave * 128;
+    ClsNode<NC, NF> n0, n1;
+    load_cls_node<NC, NF, FIT_ON, LA_ON>(c, pl, d, wave_base + lane, a.node_end, a.now_ns, n0);
+    load_cls_node<NC, NF, FIT_ON, LA_ON>(c, pl, d, wave_base + 64 + lane, a.node_end, a.now_ns, n1);
+    const uint32_t W = 1u << d.fit_shift;
+    const bool full = !FIT_ON || __all((n0.w == W || wave_base + lane >= a.node_end) &&
+                                       (n1.w == W || wave_base + 64 + lane >= a.node_end));
+    const int64_t col0 = wave_base - a.col_begin;
+    const bool seg0 = col0 < a.score_stride, seg1 = col0 + 64 < a.score_stride;
+    const int mask_lanes = seg1 ? 2 : seg0 ? 1 : 0;
+    const uint32_t scol = (uint32_t)col0 + (uint32_t)lane;        // score column of n0
+    const int32_t mcol = (int32_t)(col0 >> 6) + lane;              // mask word of lane 0 / 1
+    const uint32_t local0 = (uint32_t)(wave * 128 + lane);
+    const uint32_t kb0 = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0, kb1 = kb0 - 64;
+    // pod rows are staged chunk by chunk into LDS (double buffer); the next chunk's global load is
+    // in flight while the current chunk is evaluated, so no pod pays a memory round trip
+    const uint32_t *gsrc = reinterpret_cast<const uint32_t *>(rows_base + d.rows_offset);
+    const int64_t last_dw = (int64_t)w.end * (RB / 4) - 1;        // stay inside the class's rows
+    uint32_t *lbuf = reinterpret_cast<uint32_t *>(lrows);
+    if (tid < CHUNK_DW) {
+        const int64_t src = (int64_t)w.begin * (RB / 4) + tid;
+        lbuf[tid] = gsrc[src < last_dw ? src : last_dw];
+    }
+    __syncthreads();
+    const int rj = tid >> 5, rg = tid & 31;
+    int buf = 0;
+    for (int p0 = w.begin; p0 < w.end; p0 += KG_KCHUNK) {
+        const int p1 = min(p0 + KG_KCHUNK, w.end);
+        uint32_t staged = 0;
+        const bool more = p1 < w.end;
+        if (more && tid < CHUNK_DW) {
+            const int64_t src = (int64_t)p1 * (RB / 4) + tid;
+            staged = gsrc[src < last_dw ? src : last_dw];
+        }
+        const char *cur = lrows + buf * (KG_KCHUNK * RB);
+        if (full)
+            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, true, W1>(c, d, n0, n1, cur, p0, p1, mask, scores, scol, mcol, seg0,
+                                                                 seg1, mask_lanes, kb0, kb1, kbuf);
+        else
+            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, false, W1>(c, d, n0, n1, cur, p0, p1, mask, scores, scol, mcol,
+                                                                  seg0, seg1, mask_lanes, kb0, kb1, kbuf);
+        if (more && tid < CHUNK_DW) lbuf[(buf ^ 1) * (KG_KCHUNK * RB / 4) + tid] = staged;
+        __syncthreads();
+        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * KG_BLOCK + rg * 16);
+        uint32_t mx = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 v = src[k];
+            const uint32_t a0 = v.x > v.y ? v.x : v.y, a1 = v.z > v.w ? v.z : v.w;
+            const uint32_t a2 = a0 > a1 ? a0 : a1;
+            mx = mx > a2 ? mx : a2;
+        }
+        mx = dpp_max_step(mx, 0);
+        mx = dpp_max_step(mx, 1);
+        mx = dpp_max_step(mx, 2);
+        mx = dpp_max_step(mx, 3);
+        mx = dpp_max_step(mx, 4);
+        if (rg == 31 && rj < p1 - p0) {
+            const int32_t row = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[rj].row;
+            partials[(int64_t)row * a.tiles_total + tile] = mx;
+        }
+        __syncthreads();
+        buf ^= 1;
+    }
+}
+
+template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1>
+__global__ __launch_bounds__(KG_BLOCK) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
+                                                    const kg_cls_desc *__restrict__ descs,
+                                                    const kg_cls_work *__restrict__ work,
+                                                    const char *__restrict__ rows, uint64_t *__restrict__ mask,
+                                                    uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_KCHUNK * KG_BLOCK];
+    __shared__ __attribute__((aligned(64))) char lrows[2 * KG_KCHUNK * 128];
+    const kg_cls_work w = work[blockIdx.y];
+    const kg_cls_desc d = descs[w.cls];
+    switch (d.kind) {
+        case 0: cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1>(c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows); break;
+        case 1: cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1>(c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows); break;
+        case 2: cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1>(c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows); break;
+        default: cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1>(c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows); break;
+    }
+}
+
+// Slow nodes (outside the fp64 exactness bounds) come out of k_eval2 as infeasible with
 // zero scores; k_slow_list collects them and k_fix_slow re-evaluates those pairs exactly.
 __global__ void k_slow_list(const uint32_t *__restrict__ dflags, int64_t begin, int64_t end, int32_t *__restrict__ list,
                             int32_t *__restrict__ count) {
@@ -477,7 +753,7 @@ __global__ void k_fix_slow(kg_consts c, kg_planes pl, const kg_pod_dev *__restri
         if (feas) {
             if (mask) atomicOr(&mask[(int64_t)p * mask_words + (col >> 6)], 1ull << (col & 63));
             const uint32_t tot = (uint32_t)c.weight_fit * fit + (uint32_t)c.weight_la * la;
-            const uint32_t key = ((tot + 1u) << 9) | (uint32_t)(KG_TILE - 1 - (node % KG_TILE));
+            const uint32_t key = ((tot + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - (node % KG_TILE));
             atomicMax(&partials[(int64_t)p * tiles_total + node / KG_TILE], key);
         }
     }
@@ -486,7 +762,7 @@ __global__ void k_fix_slow(kg_consts c, kg_planes pl, const kg_pod_dev *__restri
 __device__ __forceinline__ unsigned long long decode_partial(uint32_t k, int tile) {
     if (k == 0) return 0ull;
     const uint32_t node = (uint32_t)tile * KG_TILE + (KG_TILE - 1) - (k & (KG_TILE - 1));
-    return ((unsigned long long)(k >> 9) << 32) | (0xFFFFFFFFull - node);
+    return ((unsigned long long)(k >> KG_TILE_SHIFT) << 32) | (0xFFFFFFFFull - node);
 }
 
 // per-pod max over the tile partials → (total+1) << 32 | (0xFFFFFFFF − node)
@@ -604,6 +880,18 @@ struct kg_engine {
     BatchMasks bm{0, 0};
     bool la_prod = false;           // some pod of the batch scores with the prod-usage variant
     bool pow2 = true;               // every Fit / LoadAware weight sum of the batch is a power of two
+    // class-specialised matrix mode (k_eval3): built from the batch in kg_pods_set, laid out for
+    // the current shard width on the first kg_eval that needs it
+    bool cls_ok = false;                    // every pod of the batch belongs to a specialisable class
+    bool cls_dirty = true;
+    int64_t cls_width = -1, cls_tiles = -1;
+    std::vector<kg_cls_desc> cls_desc;      // host copies
+    std::vector<std::vector<int32_t>> cls_members;   // pod indices (queue order) per class
+    std::vector<kg_pod_row> pod_rows_h;
+    void *cls_mem = nullptr;                // device: descs | work | rows
+    size_t cls_mem_bytes = 0;
+    int32_t cls_nwork = 0;
+    size_t cls_work_off = 0, cls_rows_off = 0;
     int32_t *slow_list = nullptr;   // [cap] nodes outside the fast-path bounds (rebuilt per eval)
     int32_t *slow_count = nullptr;
     void *scratch = nullptr;
@@ -659,10 +947,10 @@ void launch_hot_div(kg_engine *e, dim3 grid, const HotArgs &a, int32_t pod_begin
                     uint32_t *partials) {
     const kg_pod_hot_t<S> *pods = reinterpret_cast<const kg_pod_hot_t<S> *>(e->hot) + pod_begin;
     if (mask)
-        hipLaunchKernelGGL((k_eval_hot<S, FAST, LA_PROD, true>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a,
+        hipLaunchKernelGGL((k_eval2<S, FAST, LA_PROD, true>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts, e->pl, a,
                            pods, mask, scores, partials);
     else
-        hipLaunchKernelGGL((k_eval_hot<S, FAST, LA_PROD, false>), grid, dim3(KG_TILE), 0, e->stream, e->consts, e->pl, a,
+        hipLaunchKernelGGL((k_eval2<S, FAST, LA_PROD, false>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts, e->pl, a,
                            pods, mask, scores, partials);
 }
 
@@ -681,9 +969,206 @@ void launch_hot(kg_engine *e, dim3 grid, const HotArgs &a, int32_t pod_begin, ui
     }
 }
 
+// ---- class-specialised path (k_eval3): host-side class building -------------------------------
+struct ClsKey {
+    uint32_t nzc, zc, fitm, sel, lav;
+    bool operator<(const ClsKey &o) const {
+        if (nzc != o.nzc) return nzc < o.nzc;
+        if (zc != o.zc) return zc < o.zc;
+        if (fitm != o.fitm) return fitm < o.fitm;
+        if (sel != o.sel) return sel < o.sel;
+        return lav < o.lav;
+    }
+};
+
+// The class of a pod: which resources the Fit filter compares (nzc: per-pod values; zc: zero native
+// requests, a node-only overcommit check), which it scores, its node-filter variant and LoadAware
+// usage variant.  False when the pod needs the generic slot kernel.
+bool pod_class(const kg_config &cfg, const kg_pod_row &row, ClsKey &key) {
+    const bool fit_on = (cfg.enabled_plugins & KG_PLUGIN_FIT) != 0;
+    const bool la_on = (cfg.enabled_plugins & KG_PLUGIN_LOADAWARE) != 0;
+    const bool hr = fit_on && (row.flags & KG_POD_HAS_REQUEST);
+    key = ClsKey{0, 0, 0, 0, 0};
+    if (hr) {
+        for (int r = 0; r < 3; r++) (row.request[r] != 0 ? key.nzc : key.zc) |= 1u << r;
+        key.nzc |= row.request_present & KG_SCALAR_RES_MASK;
+    }
+    uint32_t w = 0;
+    if (fit_on) {
+        for (int r = 0; r < KG_NUM_RES; r++) {
+            if (cfg.fit_resource_weight[r] <= 0) continue;
+            if (((KG_SCALAR_RES_MASK >> r) & 1u) && row.fit_score_request[r] == 0) continue;
+            key.fitm |= 1u << r;
+            w += (uint32_t)cfg.fit_resource_weight[r];
+        }
+    }
+    const uint32_t variant = (row.flags & KG_POD_DAEMONSET) ? 2u : (row.flags & KG_POD_PROD) ? 1u : 0u;
+    key.sel = variant + (hr ? 3u : 0u);
+    key.lav = (la_on && (row.flags & KG_POD_LA_PROD_SCORE)) ? 1u : 0u;
+    if (__builtin_popcount(key.nzc) > 4 || __builtin_popcount(key.fitm) > 4) return false;
+    if (w != 0 && (w & (w - 1)) != 0) return false;
+    return true;
+}
+
+void cls_prepare(kg_engine *e) {
+    e->cls_ok = false;
+    e->cls_dirty = true;
+    e->cls_desc.clear();
+    e->cls_members.clear();
+    const bool la_on = (e->cfg.enabled_plugins & KG_PLUGIN_LOADAWARE) != 0;
+    if (la_on && e->consts.la_shift == 0xFF) return;
+    std::map<ClsKey, int> index;
+    std::vector<ClsKey> keys;
+    for (int32_t i = 0; i < (int32_t)e->pod_rows_h.size(); i++) {
+        ClsKey k;
+        if (!pod_class(e->cfg, e->pod_rows_h[i], k)) return;
+        auto it = index.find(k);
+        int c;
+        if (it == index.end()) {
+            if ((int)keys.size() == KG_CLS_MAX) return;
+            c = (int)keys.size();
+            index.emplace(k, c);
+            keys.push_back(k);
+            e->cls_members.emplace_back();
+        } else {
+            c = it->second;
+        }
+        e->cls_members[c].push_back(i);
+    }
+    for (size_t c = 0; c < keys.size(); c++) {
+        const ClsKey &k = keys[c];
+        kg_cls_desc d;
+        memset(&d, 0, sizeof(d));
+        const int nc = __builtin_popcount(k.nzc) <= 2 ? 2 : 4, nf = __builtin_popcount(k.fitm) <= 2 ? 2 : 4;
+        d.kind = (nc == 2 ? 0 : 2) + (nf == 2 ? 0 : 1);
+        d.count = (int32_t)e->cls_members[c].size();
+        int a = 0, b = 0;
+        uint32_t w = 0;
+        for (int s = 0; s < 4; s++) d.cmp_res[s] = d.fit_res[s] = -1;
+        for (int r = 0; r < KG_NUM_RES; r++) {
+            if ((k.nzc >> r) & 1u) d.cmp_res[a++] = r;
+            if ((k.fitm >> r) & 1u) {
+                d.fit_w[b] = (uint32_t)e->cfg.fit_resource_weight[r];
+                w += d.fit_w[b];
+                d.fit_res[b++] = r;
+            }
+        }
+        d.fit_shift = w ? (uint32_t)__builtin_ctz(w) : 0u;
+        d.node_ok_sel = k.sel;
+        d.la_variant = k.lav;
+        d.over_mask = k.zc;
+        d.row_bytes = d.kind == 0 ? (int64_t)sizeof(kg_pod_cls_t<2, 2>) : d.kind == 1 ? (int64_t)sizeof(kg_pod_cls_t<2, 4>)
+                      : d.kind == 2 ? (int64_t)sizeof(kg_pod_cls_t<4, 2>) : (int64_t)sizeof(kg_pod_cls_t<4, 4>);
+        e->cls_desc.push_back(d);
+    }
+    e->cls_ok = true;
+}
+
+template <int NC, int NF>
+void cls_fill_row(const kg_engine *e, const kg_cls_desc &d, const kg_pod_row &r, int32_t row, int64_t stride,
+                  int64_t words, char *dst) {
+    kg_pod_cls_t<NC, NF> h;
+    memset(&h, 0, sizeof(h));
+    const bool most = e->cfg.fit_strategy == KG_STRATEGY_MOST_ALLOCATED;
+    for (int k = 0; k < NC; k++) h.req[k] = d.cmp_res[k] >= 0 ? r.request[d.cmp_res[k]] : KG_NEUTRAL_REQ;
+    for (int f = 0; f < NF; f++) {
+        const double pr = d.fit_res[f] >= 0 ? (double)r.fit_score_request[d.fit_res[f]] : 0.0;
+        h.pr[f] = most ? pr : -pr;
+    }
+    h.la[0] = -(double)r.la_estimate[0];
+    h.la[1] = -(double)r.la_estimate[1];
+    h.score_off = (int64_t)row * stride;
+    h.mask_off = (int32_t)((int64_t)row * words);
+    h.row = row;
+    memcpy(dst, &h, sizeof(h));
+}
+
+// Lay the class rows out for the shard width (output offsets) and the work table for its tiles.
+kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
+    if (!e->cls_dirty && e->cls_width == width && e->cls_tiles == shard_tiles) return KG_OK;
+    const int64_t words = (width + 63) / 64, stride = words * 64;
+    if ((int64_t)e->pod_rows_h.size() * words >= (1LL << 31)) return set_err(e, KG_ERR_RANGE, "mask too large");
+    std::vector<kg_cls_desc> descs = e->cls_desc;
+    std::vector<kg_cls_work> work;
+    size_t rows_bytes = 0;
+    for (size_t c = 0; c < descs.size(); c++) {
+        descs[c].rows_offset = (int64_t)rows_bytes;
+        rows_bytes += (size_t)descs[c].row_bytes * (size_t)descs[c].count;
+        const int32_t n = descs[c].count;
+        const int32_t ppb = pods_per_block_for(n, shard_tiles);
+        for (int32_t b = 0; b < n; b += ppb) work.push_back(kg_cls_work{(int32_t)c, b, b + ppb < n ? b + ppb : n, 0});
+    }
+    std::vector<char> rows(rows_bytes ? rows_bytes : 64, 0);
+    for (size_t c = 0; c < descs.size(); c++) {
+        const kg_cls_desc &d = descs[c];
+        for (int32_t j = 0; j < d.count; j++) {
+            const int32_t i = e->cls_members[c][j];
+            char *dst = rows.data() + d.rows_offset + (size_t)j * (size_t)d.row_bytes;
+            const kg_pod_row &r = e->pod_rows_h[i];
+            if (d.kind == 0) cls_fill_row<2, 2>(e, d, r, i, stride, words, dst);
+            else if (d.kind == 1) cls_fill_row<2, 4>(e, d, r, i, stride, words, dst);
+            else if (d.kind == 2) cls_fill_row<4, 2>(e, d, r, i, stride, words, dst);
+            else cls_fill_row<4, 4>(e, d, r, i, stride, words, dst);
+        }
+    }
+    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t desc_b = sizeof(kg_cls_desc) * KG_CLS_MAX, work_b = sizeof(kg_cls_work) * (work.size() + 1);
+    const size_t need = up(desc_b) + up(work_b) + up(rows.size());
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (need > e->cls_mem_bytes) {
+        if (e->cls_mem) HIP_TRY(e, hipFree(e->cls_mem));
+        e->cls_mem = nullptr;
+        e->cls_mem_bytes = 0;
+        HIP_TRY(e, hipMalloc(&e->cls_mem, need));
+        e->cls_mem_bytes = need;
+    }
+    e->cls_work_off = up(desc_b);
+    e->cls_rows_off = up(desc_b) + up(work_b);
+    char *m = (char *)e->cls_mem;
+    HIP_TRY(e, hipMemcpy(m, descs.data(), sizeof(kg_cls_desc) * descs.size(), hipMemcpyHostToDevice));
+    if (!work.empty()) HIP_TRY(e, hipMemcpy(m + e->cls_work_off, work.data(), sizeof(kg_cls_work) * work.size(), hipMemcpyHostToDevice));
+    HIP_TRY(e, hipMemcpy(m + e->cls_rows_off, rows.data(), rows.size(), hipMemcpyHostToDevice));
+    e->cls_nwork = (int32_t)work.size();
+    e->cls_width = width;
+    e->cls_tiles = shard_tiles;
+    e->cls_dirty = false;
+    return KG_OK;
+}
+
+template <bool MOST, bool FIT_ON, bool LA_ON, bool W1>
+void launch_cls4(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint16_t *scores, uint32_t *partials) {
+    const char *m = (const char *)e->cls_mem;
+    const kg_cls_desc *descs = (const kg_cls_desc *)m;
+    const kg_cls_work *work = (const kg_cls_work *)(m + e->cls_work_off);
+    const char *rows = m + e->cls_rows_off;
+    if (mask)
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts, e->pl,
+                           a, descs, work, rows, mask, scores, partials);
+    else
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts, e->pl,
+                           a, descs, work, rows, mask, scores, partials);
+}
+
+template <bool MOST, bool FIT_ON, bool LA_ON>
+void launch_cls3(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint16_t *scores, uint32_t *partials) {
+    // plugin weights 1 (the shipped profile): totals are plain sums
+    if (e->consts.weight_fit == 1 && e->consts.weight_la == 1) launch_cls4<MOST, FIT_ON, LA_ON, true>(e, grid, a, mask, scores, partials);
+    else launch_cls4<MOST, FIT_ON, LA_ON, false>(e, grid, a, mask, scores, partials);
+}
+
+void launch_cls(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint16_t *scores, uint32_t *partials) {
+    const bool most = e->consts.fit_most != 0;
+    const bool fit = (e->consts.plugins & KG_PLUGIN_FIT) != 0, la = (e->consts.plugins & KG_PLUGIN_LOADAWARE) != 0;
+    if (!fit) launch_cls3<false, false, true>(e, grid, a, mask, scores, partials);
+    else if (most && la) launch_cls3<true, true, true>(e, grid, a, mask, scores, partials);
+    else if (most) launch_cls3<true, true, false>(e, grid, a, mask, scores, partials);
+    else if (la) launch_cls3<false, true, true>(e, grid, a, mask, scores, partials);
+    else launch_cls3<false, true, false>(e, grid, a, mask, scores, partials);
+}
+
 // mask and scores are both produced or both omitted (the host path provides scratch for a missing one)
 kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
-                      uint32_t *partials) {
+                      uint32_t *partials, bool use_cls = false) {
     if (n <= 0) return KG_OK;
     if ((mask == nullptr) != (scores == nullptr)) return set_err(e, KG_ERR_INVALID_ARG, "mask and scores go together");
     const int64_t shard_tiles = (e->shard_end - e->shard_begin + KG_TILE - 1) / KG_TILE;
@@ -700,9 +1185,16 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     a.fit_cap = e->consts.fit_most ? 100u : 0xFFFFFFFFu;
     for (int s = 0; s < 8; s++) a.slot_res[s] = s < e->nslot ? e->slot_res[s] : -1;
     a.now_ns = now_ns;
-    dim3 grid((unsigned)shard_tiles, (unsigned)((n + a.pods_per_block - 1) / a.pods_per_block));
+    a.ablate = getenv("KG_ABLATE") ? (uint32_t)atoi(getenv("KG_ABLATE")) : 0u;
+    use_cls = use_cls && e->cls_ok && pod_begin == 0 && n == e->n_pods && !(a.ablate & 16);
+    if (use_cls) {
+        kg_status st = cls_layout(e, e->shard_end - e->shard_begin, shard_tiles);
+        if (st) return st;
+    }
+    dim3 grid((unsigned)shard_tiles, use_cls ? (unsigned)e->cls_nwork : (unsigned)((n + a.pods_per_block - 1) / a.pods_per_block));
     if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
-    if (e->nslot == 2) launch_hot<2>(e, grid, a, pod_begin, mask, scores, partials);
+    if (use_cls) launch_cls(e, grid, a, mask, scores, partials);
+    else if (e->nslot == 2) launch_hot<2>(e, grid, a, pod_begin, mask, scores, partials);
     else if (e->nslot == 4) launch_hot<4>(e, grid, a, pod_begin, mask, scores, partials);
     else launch_hot<8>(e, grid, a, pod_begin, mask, scores, partials);
     HIP_TRY(e, hipGetLastError());
@@ -768,6 +1260,7 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->pods) (void)hipFree(e->pods);
     if (e->hot) (void)hipFree(e->hot);
     if (e->scratch) (void)hipFree(e->scratch);
+    if (e->cls_mem) (void)hipFree(e->cls_mem);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     for (int k = 0; k < kg_engine::kRing; k++) {
         if (e->ev0[k]) (void)hipEventDestroy(e->ev0[k]);
@@ -957,6 +1450,8 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     e->bm = bm;
     e->la_prod = la_prod;
     e->pow2 = pow2;
+    e->pod_rows_h.assign(rows, rows + n);
+    cls_prepare(e);
     return KG_OK;
 }
 
@@ -994,7 +1489,7 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
         else scores = (uint16_t *)out->scores;
     }
     HIP_TRY(e, hipMemsetAsync(part, 0, part_b, e->stream));
-    st = launch_eval(e, now_ns, 0, P, mask, scores, part);
+    st = launch_eval(e, now_ns, 0, P, mask, scores, part, true);
     if (st) return st;
     if (out->top1) {
         unsigned long long *dst = dev ? (unsigned long long *)out->top1 : top;
