@@ -596,28 +596,35 @@ __device__ __forceinline__ bool cls_pair(const kg_consts &c, const kg_cls_desc &
     return ok;
 }
 
+// v_writelane_b32 ×4: lane `lane` of mb[0..3] := the wave-uniform words (no exec change; the
+// lane select goes through M0 because a VOP3 may read only one SGPR)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // M0 is otherwise unused by these kernels (checked in the ISA)
+__device__ __forceinline__ void write_lanes(uint32_t (&mb)[4], uint32_t lane, unsigned long long b0,
+                                            unsigned long long b1) {
+    asm("s_mov_b32 m0, %4\n\ts_nop 0\n\tv_writelane_b32 %0, %5, m0\n\tv_writelane_b32 %1, %6, m0\n\t"
+        "v_writelane_b32 %2, %7, m0\n\tv_writelane_b32 %3, %8, m0"
+        : "+v"(mb[0]), "+v"(mb[1]), "+v"(mb[2]), "+v"(mb[3])
+        : "s"(lane), "s"((uint32_t)b0), "s"((uint32_t)(b0 >> 32)), "s"((uint32_t)b1), "s"((uint32_t)(b1 >> 32))
+        : "m0");
+}
+#pragma clang diagnostic pop
+
 // Pods [p0, p1) of one class against the lane's two nodes; rows come from the LDS chunk buffer.
+// The feasibility ballots of the chunk are collected into lanes (p − p0) of four VGPRs and written
+// once per chunk; EDGE workgroups (the shard's last tile) check that a segment lies in the row.
 template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1>
 __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> &n0,
                                          const ClsNode<NC, NF> &n1, const char *lrows, int p0, int p1,
-                                         uint64_t *__restrict__ mask, uint16_t *__restrict__ scores, uint32_t scol,
-                                         int32_t mcol, bool seg0, bool seg1, int mask_lanes, uint32_t kb0,
-                                         uint32_t kb1, uint32_t *kbuf) {
+                                         uint16_t *__restrict__ scores, uint32_t scol, bool seg0, bool seg1,
+                                         uint32_t kb0, uint32_t kb1, uint32_t *kbuf, uint32_t (&mb)[4]) {
     const int tid = threadIdx.x;
-    const int lane = tid & 63;
     for (int p = p0; p < p1; p++) {
         const kg_pod_cls_t<NC, NF> pd =
             *reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(lrows + (p - p0) * (int)sizeof(kg_pod_cls_t<NC, NF>));
         uint32_t fit0, la0, fit1, la1;
         const bool ok0 = cls_pair<NC, NF, MOST, FIT_ON, LA_ON, FULL>(c, d, pd, n0, fit0, la0);
         const bool ok1 = cls_pair<NC, NF, MOST, FIT_ON, LA_ON, FULL>(c, d, pd, n1, fit1, la1);
-        if (OUT) {
-            uint16_t *srow = scores + pd.score_off;
-            if (seg0) srow[scol] = (uint16_t)(fit0 | (la0 << 8));
-            if (seg1) srow[scol + 64] = (uint16_t)(fit1 | (la1 << 8));
-            const unsigned long long b0 = __ballot(ok0), b1 = __ballot(ok1);
-            if (lane < mask_lanes) mask[pd.mask_off + mcol] = lane ? b1 : b0;
-        }
         uint32_t tot0, tot1;
         if (W1) {
             tot0 = fit0 + la0;
@@ -629,6 +636,12 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
         const uint32_t k0 = ok0 ? (tot0 << KG_TILE_SHIFT) + kb0 : 0u;
         const uint32_t k1 = ok1 ? (tot1 << KG_TILE_SHIFT) + kb1 : 0u;
         kbuf[(p - p0) * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
+        if (OUT) {
+            write_lanes(mb, (uint32_t)(p - p0), __ballot(ok0), __ballot(ok1));
+            uint16_t *srow = scores + pd.score_off;
+            if (seg0) srow[scol] = (uint16_t)(fit0 | (la0 << 8));
+            if (seg1) srow[scol + 64] = (uint16_t)(fit1 | (la1 << 8));
+        }
     }
 }
 
@@ -653,9 +666,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
                                        (n1.w == W || wave_base + 64 + lane >= a.node_end));
     const int64_t col0 = wave_base - a.col_begin;
     const bool seg0 = col0 < a.score_stride, seg1 = col0 + 64 < a.score_stride;
-    const int mask_lanes = seg1 ? 2 : seg0 ? 1 : 0;
     const uint32_t scol = (uint32_t)col0 + (uint32_t)lane;        // score column of n0
-    const int32_t mcol = (int32_t)(col0 >> 6) + lane;              // mask word of lane 0 / 1
     const uint32_t local0 = (uint32_t)(wave * 128 + lane);
     const uint32_t kb0 = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0, kb1 = kb0 - 64;
     // pod rows are staged chunk by chunk into LDS (double buffer); the next chunk's global load is
@@ -667,6 +678,9 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         const int64_t src = (int64_t)w.begin * (RB / 4) + tid;
         lbuf[tid] = gsrc[src < last_dw ? src : last_dw];
     }
+    // every node-plane load has landed before the pod loop: the loop itself then never waits on
+    // vector memory (its stores included)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __syncthreads();
     const int rj = tid >> 5, rg = tid & 31;
     int buf = 0;
@@ -679,12 +693,20 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
             staged = gsrc[src < last_dw ? src : last_dw];
         }
         const char *cur = lrows + buf * (KG_KCHUNK * RB);
+        uint32_t mb[4] = {0u, 0u, 0u, 0u};
         if (full)
-            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, true, W1>(c, d, n0, n1, cur, p0, p1, mask, scores, scol, mcol, seg0,
-                                                                 seg1, mask_lanes, kb0, kb1, kbuf);
+            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, true, W1>(c, d, n0, n1, cur, p0, p1, scores, scol, seg0,
+                                                                       seg1, kb0, kb1, kbuf, mb);
         else
-            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, false, W1>(c, d, n0, n1, cur, p0, p1, mask, scores, scol, mcol,
-                                                                  seg0, seg1, mask_lanes, kb0, kb1, kbuf);
+            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, false, W1>(c, d, n0, n1, cur, p0, p1, scores, scol, seg0,
+                                                                        seg1, kb0, kb1, kbuf, mb);
+        if (OUT && lane < p1 - p0 && seg0) {
+            // lane l writes the two feasibility words of pod p0 + l
+            const kg_pod_cls_t<NC, NF> &pr = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[lane];
+            uint64_t *mw = mask + pr.mask_off + (col0 >> 6);
+            mw[0] = (uint64_t)mb[0] | ((uint64_t)mb[1] << 32);
+            if (seg1) mw[1] = (uint64_t)mb[2] | ((uint64_t)mb[3] << 32);
+        }
         if (more && tid < CHUNK_DW) lbuf[(buf ^ 1) * (KG_KCHUNK * RB / 4) + tid] = staged;
         __syncthreads();
         const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * KG_BLOCK + rg * 16);
