@@ -98,7 +98,10 @@ def main():
     now = cl.now_ns
 
     eng = engine.Engine(cfg)
-    stream = torch.cuda.current_stream(dev)
+    # one dedicated stream for the engine kernels and the torch / RCCL ops around them (the legacy
+    # null stream cannot be shared: kg_set_stream(NULL) means an engine-owned stream)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
     eng.load_snapshot(node_rows)
     eng.set_pods(pod_rows)
@@ -156,7 +159,24 @@ def main():
         tp1 = time.perf_counter()
         placement = {"pods": P, "nodes": N, "seconds": round(tp1 - tp0, 6),
                      "pods_placed_per_s": round(P / (tp1 - tp0), 1), "placed": int((nodes >= 0).sum()),
-                     "chunk": int(cfg["place_chunk"])}
+                     "chunk": int(cfg["place_chunk"]), "mode": "kg_place, one GPU"}
+    elif not args.no_placement:
+        # node-sharded sequential cycle over the union of every rank's shard (replicated snapshot,
+        # per-tile partial keys merged with RCCL all_reduce(MAX), replicated resolve: koordinator_amd/dist.py)
+        from koordinator_amd import dist as kdist
+        all_rows = np.concatenate([engine.build_node_rows(cfg, synth.make_cluster(N, 1, seed=2 + 7919 * r))
+                                   for r in range(world)])
+        deng = kdist.sharded_engine(cfg, all_rows, pod_rows, dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tp0 = time.perf_counter()
+        nodes, tot = kdist.place_sharded(deng, now, dev, chunk=int(cfg["place_chunk"]))
+        dist.barrier()
+        tp1 = time.perf_counter()
+        deng.close()
+        placement = {"pods": P, "nodes": N * world, "seconds": round(tp1 - tp0, 6),
+                     "pods_placed_per_s": round(P / (tp1 - tp0), 1), "placed": int((nodes >= 0).sum()),
+                     "chunk": int(cfg["place_chunk"]), "mode": f"dist.place_sharded over {world} ranks"}
 
     cpu_baseline = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -348,7 +348,7 @@ kg_status kg_snapshot_upsert(kg_engine *eng, const int32_t *node_index, const kg
 kg_status kg_snapshot_remove(kg_engine *eng, int32_t node_index);
 kg_status kg_snapshot_download(kg_engine *eng, int32_t first, int32_t n, kg_node_row *out);
 /* Restrict kg_eval/kg_place evaluation to nodes [begin, end) (node sharding across GPUs);
- * node indices stay global.  begin must be a multiple of 1024. */
+ * node indices stay global.  begin must be a multiple of 1024 unless the shard is empty. */
 kg_status kg_set_shard(kg_engine *eng, int32_t begin, int32_t end);
 
 /* Pod batch (uploaded once; HBM-resident until replaced). */

@@ -1403,7 +1403,7 @@ kg_status kg_snapshot_download(kg_engine *e, int32_t first, int32_t n, kg_node_r
 kg_status kg_set_shard(kg_engine *e, int32_t begin, int32_t end) {
     kg_status st = check_engine(e);
     if (st) return st;
-    if (begin < 0 || end < begin || end > e->n_nodes || begin % KG_TILE) return set_err(e, KG_ERR_RANGE, "bad shard [%d,%d)", begin, end);
+    if (begin < 0 || end < begin || end > e->n_nodes || (begin % KG_TILE && begin != end)) return set_err(e, KG_ERR_RANGE, "bad shard [%d,%d)", begin, end);
     e->shard_begin = begin;
     e->shard_end = end;
     return KG_OK;

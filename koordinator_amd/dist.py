@@ -1,0 +1,139 @@
+"""Node-sharded scheduling across GPUs (one process per GPU, ``torch.distributed``; backend ``nccl``
+is RCCL on ROCm).
+
+SURVEY §8e: every per-pair quantity depends on one pod row and one node row, so the path shards over
+nodes with no data-path collective. The only exchange is the per-pod best-node merge:
+
+* matrix mode (``merge_top1``): each rank evaluates its own node shard and emits one u64 key per pod,
+  ``(total+1) << 32 | (0xFFFFFFFF − global node)``; one ``all_reduce(MAX)`` (equivalently an
+  all-gather of P × 8 B and a max over ranks) gives the highest total, then the lowest node index.
+* placement mode (``place_sharded``): the node snapshot is replicated on every rank (1M nodes × 200 B
+  is 0.2 GB of a 288 GB device). For each chunk of pods in queue order, every rank evaluates only its
+  own tile range (``kg_place_chunk_eval`` on its shard), the per-(pod, 1024-node tile) partial keys are
+  merged with one ``all_reduce(MAX)`` (chunk × tiles × 4 B: 250 KB at 1M nodes and 64 pods), and every
+  rank runs the same deterministic resolve (``kg_place_chunk_resolve``) on identical inputs. The replicas
+  therefore stay identical, and the placements equal the single-GPU ones (and the oracle's sequential
+  cycle).
+
+Keys are unsigned 32/64-bit; ``torch.distributed`` reduces signed integers, so the sign bit is flipped
+before and after the max (an order-preserving map from unsigned to signed).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Protocol, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _native as nat
+
+SIGN32 = -(2**31)
+SIGN64 = -(2**63)
+
+
+def shard_range(n_nodes: int, rank: int, world: int, tile: int = nat.TILE) -> Tuple[int, int]:
+    """Contiguous, tile-aligned node range [begin, end) of `rank` (possibly empty)."""
+    tiles = max(1, math.ceil(n_nodes / tile))
+    per = math.ceil(tiles / world)
+    t0 = min(rank * per, tiles)
+    t1 = min(tiles, t0 + per)
+    if t0 >= t1 or t0 * tile >= n_nodes:
+        return n_nodes, n_nodes          # empty shard (more ranks than tiles)
+    return t0 * tile, min(n_nodes, t1 * tile)
+
+
+def _max_unsigned_(t: torch.Tensor, sign: int, group=None) -> None:
+    t.bitwise_xor_(sign)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    t.bitwise_xor_(sign)
+
+
+def merge_partials_(partial: torch.Tensor, group=None) -> None:
+    """In-place max over ranks of u32 per-(pod, tile) keys held in an int32 tensor."""
+    _max_unsigned_(partial, SIGN32, group)
+
+
+def merge_top1_(keys: torch.Tensor, group=None) -> None:
+    """In-place max over ranks of u64 per-pod keys held in an int64 tensor."""
+    _max_unsigned_(keys, SIGN64, group)
+
+
+class ChunkBackend(Protocol):
+    """What `place_sharded` needs from an engine (the HIP engine implements it through the C-ABI)."""
+
+    n_pods: int
+    num_tiles: int
+
+    def chunk_eval(self, now_ns: int, pod_begin: int, n: int, partial_ptr: int) -> None: ...
+
+    def chunk_resolve(self, now_ns: int, pod_begin: int, n: int, partial_ptr: int, node_ptr: int,
+                      score_ptr: int) -> None: ...
+
+
+def place_sharded(backend: ChunkBackend, now_ns: int, device: torch.device, chunk: int = 64,
+                  group=None) -> Tuple[np.ndarray, np.ndarray]:
+    """Sequential-cycle placement of the backend's pod batch, node-sharded across the group.
+
+    The backend must hold the full (replicated) snapshot with its evaluation restricted to this
+    rank's `shard_range`. Returns (node or −1, total or −1) per pod, identical on every rank."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    P, tiles = backend.n_pods, backend.num_tiles
+    stream = getattr(backend, "torch_stream", None)
+    with torch.cuda.stream(stream) if stream is not None else _nullctx():
+        partial = torch.zeros((max(chunk, 1), tiles), dtype=torch.int32, device=device)
+        nodes = torch.full((max(P, 1),), -1, dtype=torch.int32, device=device)
+        scores = torch.full((max(P, 1),), -1, dtype=torch.int64, device=device)
+        for b in range(0, P, chunk):
+            n = min(chunk, P - b)
+            backend.chunk_eval(now_ns, b, n, partial.data_ptr())
+            if world > 1:
+                merge_partials_(partial[:n], group)
+            backend.chunk_resolve(now_ns, b, n, partial.data_ptr(), nodes.data_ptr() + 4 * b,
+                                  scores.data_ptr() + 8 * b)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        return nodes[:P].cpu().numpy(), scores[:P].cpu().numpy()
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def sharded_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, device: torch.device,
+                   group=None):
+    """A HIP engine on `device` holding the full snapshot, restricted to this rank's node shard.
+
+    The engine is bound to a dedicated torch stream (``eng.torch_stream``); `place_sharded` runs the
+    collectives and tensor ops on that same stream, so engine kernels and merges are ordered. (The
+    legacy null stream cannot be shared: ``kg_set_stream(NULL)`` means an engine-owned stream.)"""
+    from .engine import Engine
+
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    cfg = cfg.copy()
+    cfg["device"] = device.index or 0
+    eng = Engine(cfg)
+    eng.torch_stream = torch.cuda.Stream(device)
+    eng.set_stream(eng.torch_stream.cuda_stream)
+    eng.load_snapshot(node_rows)
+    eng.set_pods(pod_rows)
+    begin, end = shard_range(len(node_rows), rank, world)
+    eng.set_shard(begin, end)
+    return eng
+
+
+def place(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, now_ns: int,
+          device: Optional[torch.device] = None, group=None) -> Tuple[np.ndarray, np.ndarray]:
+    """Convenience wrapper: build the sharded engine, place the batch, release the engine."""
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    eng = sharded_engine(cfg, node_rows, pod_rows, device, group)
+    try:
+        return place_sharded(eng, now_ns, device, chunk=int(cfg["place_chunk"]) or 64, group=group)
+    finally:
+        eng.close()

@@ -1,0 +1,151 @@
+"""Multi-rank (node-sharded) paths, world size 2.
+
+CPU (gloo): the placement protocol of koordinator_amd/dist.py — tile-aligned node shards, the
+per-(pod, tile) partial-key merge over the group and the replicated sequential resolve — driven with the
+numpy mirror of the engine's chunk API (tests/rows_ref.py), must reproduce the oracle's sequential
+cycle; the matrix-mode top-1 merge must equal the single-rank best node.
+
+GPU: two processes share cuda:0 (gloo moves the tensors), each with the HIP engine restricted to its
+shard; placements and merged top-1 keys must equal the oracle.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from koordinator_amd import dist as kdist
+from koordinator_amd import engine, synth
+from koordinator_amd.config import shipped_profile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def test_shard_ranges_cover_the_snapshot():
+    for n in (1, 1023, 1024, 3000, 100_000):
+        for world in (1, 2, 3, 8):
+            rs = [kdist.shard_range(n, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            for (b0, e0), (b1, e1) in zip(rs, rs[1:]):
+                assert e0 == b1
+            assert all((b % 1024 == 0 or b == e) and b <= e for b, e in rs)
+
+
+def _cpu_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, HERE)
+    from oracle import oracle
+    from rows_ref import RowsBackend, rows_eval
+
+    _init(rank, world, port)
+    try:
+        cl = synth.make_cluster(2_600, 90, seed=61, no_metric_frac=0.1)
+        cfg = shipped_profile()
+        idx = np.arange(90)
+        nodes = engine.build_node_rows(cfg, cl)
+        pods = engine.build_pod_rows(cfg, cl, idx)
+        shard = kdist.shard_range(len(nodes), rank, world)
+        # placement: sharded chunk eval + merged partials + replicated resolve
+        be = RowsBackend(cfg, nodes, pods, shard)
+        got_n, got_s = kdist.place_sharded(be, cl.now_ns, torch.device("cpu"), chunk=16)
+        ref_n, ref_s = oracle.schedule(cfg, cl, idx, cl.now_ns)
+        # matrix mode: local best key of the shard, merged across ranks
+        lo, hi = shard
+        m, f, l = rows_eval(cfg, nodes[lo:hi], pods, cl.now_ns)
+        tot = np.where(m, f + l, -1)
+        keys = np.zeros(len(pods), np.uint64)
+        if hi > lo:
+            j = tot.argmax(axis=1)
+            best = tot[np.arange(len(pods)), j]
+            keys = np.where(best >= 0, ((best + 1).astype(np.uint64) << np.uint64(32)) |
+                            (np.uint64(0xFFFFFFFF) - (lo + j).astype(np.uint64)), np.uint64(0))
+        t = torch.from_numpy(keys.view(np.int64).copy())
+        kdist.merge_top1_(t)
+        merged = t.numpy().view(np.uint64)
+        m_all, f_all, l_all = rows_eval(cfg, nodes, pods, cl.now_ns)
+        tot_all = np.where(m_all, f_all + l_all, -1)
+        want = tot_all.argmax(axis=1)
+        got_node = np.where(merged != 0, (0xFFFFFFFF - (merged & np.uint64(0xFFFFFFFF))).astype(np.int64), -1)
+        q.put((rank, np.array_equal(got_n, ref_n) and np.array_equal(got_s, ref_s),
+               np.array_equal(got_node, np.where(tot_all.max(axis=1) >= 0, want, -1))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_placement_protocol_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, placed_ok, top1_ok in res:
+        assert placed_ok, f"rank {rank}: sharded placement differs from the sequential oracle"
+        assert top1_ok, f"rank {rank}: merged top-1 differs from the single-rank best node"
+
+
+def _gpu_worker(rank, world, port, q):
+    from oracle import oracle
+
+    _init(rank, world, port)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        cl = synth.make_cluster(5_000, 300, seed=71)
+        cfg = shipped_profile()
+        idx = np.arange(300)
+        nodes = engine.build_node_rows(cfg, cl)
+        pods = engine.build_pod_rows(cfg, cl, idx)
+        got_n, got_s = kdist.place(cfg, nodes, pods, cl.now_ns, device=dev)
+        ref_n, ref_s = oracle.schedule(cfg, cl, idx, cl.now_ns)
+        # matrix mode on the shard + top-1 merge
+        eng = kdist.sharded_engine(cfg, nodes, pods, dev)
+        with torch.cuda.stream(eng.torch_stream):
+            top1 = torch.zeros(len(idx), dtype=torch.int64, device=dev)
+            eng.eval_device(cl.now_ns, 0, 0, top1.data_ptr())
+            kdist.merge_top1_(top1)
+            torch.cuda.synchronize(dev)
+        node, tot = engine.decode_top1(top1.cpu().numpy().view(np.uint64))
+        eng.close()
+        m, f, l = oracle.eval_matrix(cfg, cl, idx, cl.now_ns)
+        t_ref = np.where(m, f.astype(np.int64) + l, -1)
+        want = np.where(t_ref.max(axis=1) >= 0, t_ref.argmax(axis=1), -1)
+        q.put((rank, np.array_equal(got_n, ref_n) and np.array_equal(got_s, ref_s), np.array_equal(node, want)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_engine_two_ranks_one_gpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=110) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, placed_ok, top1_ok in res:
+        assert placed_ok, f"rank {rank}: sharded placement differs from the sequential oracle"
+        assert top1_ok, f"rank {rank}: merged top-1 differs from the oracle"
