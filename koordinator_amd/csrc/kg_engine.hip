@@ -279,7 +279,6 @@ struct HotArgs {
     uint32_t fit_cap;        // 100 for MostAllocated (clamp), 0xFFFFFFFF for LeastAllocated (no-op)
     int32_t slot_res[8];     // resource id of each slot (−1 unused)
     int64_t now_ns;
-    uint32_t ablate;         // TEMP experiment bits
 };
 
 // ---------------------------------------------------------------------------------------
@@ -1207,8 +1206,7 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     a.fit_cap = e->consts.fit_most ? 100u : 0xFFFFFFFFu;
     for (int s = 0; s < 8; s++) a.slot_res[s] = s < e->nslot ? e->slot_res[s] : -1;
     a.now_ns = now_ns;
-    a.ablate = getenv("KG_ABLATE") ? (uint32_t)atoi(getenv("KG_ABLATE")) : 0u;
-    use_cls = use_cls && e->cls_ok && pod_begin == 0 && n == e->n_pods && !(a.ablate & 16);
+    use_cls = use_cls && e->cls_ok && pod_begin == 0 && n == e->n_pods;
     if (use_cls) {
         kg_status st = cls_layout(e, e->shard_end - e->shard_begin, shard_tiles);
         if (st) return st;
