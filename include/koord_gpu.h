@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 1
+#define KG_ABI_VERSION 2
 
 /* ------------------------------------------------------------------ */
 /* status codes                                                          */
@@ -132,6 +132,17 @@ enum kg_scoring_strategy {
 
 #define KG_PLUGIN_FIT 0x1u       /* NodeResourcesFit       */
 #define KG_PLUGIN_LOADAWARE 0x2u /* LoadAwareScheduling    */
+#define KG_PLUGIN_NUMA 0x4u      /* NodeNUMAResource (zone fit + score; no cpuset binding) */
+
+/* NUMA topology policies (apis/extension/numa_aware.go; node label node.koordinator.sh/numa-topology-policy
+ * or the NodeResourceTopology kubelet policy, pkg/scheduler/plugins/nodenumaresource/util.go:52-58) */
+enum kg_numa_policy {
+    KG_NUMA_NONE = 0,
+    KG_NUMA_BEST_EFFORT = 1,
+    KG_NUMA_RESTRICTED = 2,
+    KG_NUMA_SINGLE_NUMA_NODE = 3
+};
+#define KG_MAX_ZONES 8
 
 /* ------------------------------------------------------------------ */
 /* engine configuration = plugin args (pkg/scheduler/apis/config/types.go)  */
@@ -162,6 +173,14 @@ typedef struct kg_config {
     int32_t la_agg_score_type;                /* Aggregated.ScoreAggregationType */
     int64_t la_agg_usage_duration_ns;         /* Aggregated.UsageAggregatedDuration (0 ⇒ max) */
     int64_t la_agg_score_duration_ns;         /* Aggregated.ScoreAggregatedDuration (0 ⇒ max) */
+
+    /* NodeNUMAResourceArgs (types.go:103-114); both scorers weigh ScoringStrategy.Resources
+     * (nodenumaresource/scoring.go:38,46) */
+    int32_t weight_numa;                      /* profile score weight of NodeNUMAResource */
+    int32_t numa_strategy;                    /* ScoringStrategy.Type (node / allocated-zone score) */
+    int32_t numa_hint_strategy;               /* NUMAScoringStrategy.Type (per-mask hint score) */
+    int32_t _pad1;
+    int64_t numa_resource_weight[KG_NUM_RES]; /* ScoringStrategy.Resources (0 ⇔ absent) */
 
     /* engine knobs */
     int32_t device;            /* HIP device ordinal */
@@ -238,7 +257,22 @@ typedef struct kg_node_spec {
     int32_t first_aggregated, n_aggregated; /* Status.NodeMetric.AggregatedNodeUsages */
     int32_t first_pod_metric, n_pod_metric; /* Status.PodsMetric */
     int32_t first_assigned, n_assigned;     /* podAssignCache.podInfoItems[node] */
+    int32_t numa;                           /* index into kg_cluster_view.numa, −1 ⇔ no topology options */
+    int32_t _pad_numa;
 } kg_node_spec;
+
+/* NodeNUMAResource view of one node: TopologyOptions (nodenumaresource/topology_options.go:90-153)
+ * and the plugin's NodeAllocation (node_allocation.go). */
+typedef struct kg_numa_spec {
+    int32_t policy;                                  /* kg_numa_policy (label, else NRT policy) */
+    int32_t n_zones;                                 /* len(NUMANodeResources) */
+    int32_t zone_id[KG_MAX_ZONES];                   /* NUMANodeResource.Node: the zone's affinity bit (< 64) */
+    kg_resource_list zone_total[KG_MAX_ZONES];       /* NUMANodeResources[i].Resources (before amplification) */
+    kg_resource_list zone_allocated[KG_MAX_ZONES];   /* allocatedResources[zone] (present == 0 ⇔ none) */
+    double cpu_amplification_ratio;                  /* annotation resource-amplification-ratio cpu (≤ 1 ⇔ none) */
+    int32_t cpu_topology_valid;                      /* CPUTopology.IsValid(): Reserve records allocations only then */
+    int32_t _pad;
+} kg_numa_spec;
 
 typedef struct kg_cluster_view {
     const kg_pod_spec *pods;                 int32_t n_pods;       int32_t _p0;
@@ -247,6 +281,7 @@ typedef struct kg_cluster_view {
     const kg_aggregated_usage *aggregated;   int32_t n_aggregated; int32_t _p3;
     const kg_pod_metric *pod_metrics;        int32_t n_pod_metrics; int32_t _p4;
     const kg_assigned_pod *assigned;         int32_t n_assigned;   int32_t _p5;
+    const kg_numa_spec *numa;                int32_t n_numa;       int32_t _p6;
 } kg_cluster_view;
 
 /* ------------------------------------------------------------------ */
@@ -256,6 +291,8 @@ typedef struct kg_cluster_view {
 #define KG_POD_DAEMONSET 0x2u      /* LoadAware.Filter passes (load_aware.go:129) */
 #define KG_POD_PROD 0x4u           /* GetPodPriorityClassWithDefault == koord-prod */
 #define KG_POD_LA_PROD_SCORE 0x8u  /* prodPod && ScoreAccordingProdUsage (load_aware.go:291) */
+#define KG_POD_NUMA_SKIP 0x10u     /* NodeNUMAResource PreFilter skip: all requests zero (plugin.go:225-231) */
+#define KG_POD_NUMA_CPU_BIND 0x20u /* the pod asks for cpuset binding (LSE/LSR prod, plugin.go:232-262): unsupported */
 #define KG_POD_VALID 0x80000000u
 
 typedef struct kg_pod_row {
@@ -265,6 +302,9 @@ typedef struct kg_pod_row {
     int64_t la_estimate[2];             /* EstimatePod(pod)[cpu], [memory] */
     uint32_t request_present;           /* ScalarResources key set of the Fit request */
     uint32_t flags;                     /* KG_POD_* */
+    int64_t numa_request[KG_NUM_RES];   /* PodRequestsAndLimits requests (NodeNUMAResource PreFilter) */
+    uint32_t numa_request_present;      /* key set of those requests */
+    uint32_t _pad;
 } kg_pod_row;
 
 #define KG_NODE_VALID 0x1u
@@ -273,6 +313,8 @@ typedef struct kg_pod_row {
 #define KG_NODE_LA_PASS_NONPROD 0x8u     /* threshold check result for non-prod pods */
 #define KG_NODE_LA_PASS_PROD 0x10u       /* threshold check result for prod pods */
 #define KG_NODE_LA_AGG_MISSING 0x20u     /* score aggregation requested but not reported (info) */
+#define KG_NODE_NUMA_OPTIONS 0x40u       /* the node has NodeNUMAResource topology options */
+#define KG_NODE_NUMA_TOPO_VALID 0x80u    /* CPUTopology valid: Reserve records zone allocations */
 
 typedef struct kg_node_row {
     int64_t alloc[KG_NUM_RES];          /* NodeInfo.Allocatable */
@@ -285,6 +327,15 @@ typedef struct kg_node_row {
     int32_t allowed_pods;
     uint32_t alloc_present;             /* Allocatable.ScalarResources key set */
     uint32_t flags;                     /* KG_NODE_* */
+    /* NodeNUMAResource: zones of cpu (milli, amplified) and memory; zone z = affinity bit zone_id[z] */
+    int32_t numa_policy;                /* kg_numa_policy */
+    int32_t n_zones;                    /* 0 ⇔ no NUMA resources */
+    int32_t zone_id[KG_MAX_ZONES];
+    int64_t zone_total[KG_MAX_ZONES][2];
+    int64_t zone_allocated[KG_MAX_ZONES][2];
+    uint32_t zone_keys;                 /* bit 2z+r: zone z's total has resource r (cpu 0, memory 1) */
+    uint32_t zone_alloc_keys;           /* bit 2z+r: zone z's allocation has resource r */
+    double cpu_amplification_ratio;     /* ≤ 1 ⇔ none */
 } kg_node_row;
 
 /* ------------------------------------------------------------------ */
@@ -299,6 +350,7 @@ typedef struct kg_engine kg_engine;
  *            (AND of every enabled Filter plugin)
  *   scores   [P][64·W][2] uint8: {NodeResourcesFit score, LoadAwareScheduling score} ∈ [0,100]
  *            (0 where a plugin is disabled; row stride 64·W pairs)
+ *   numa_scores [P][64·W] uint8: NodeNUMAResource score (when KG_PLUGIN_NUMA is enabled)
  *   top1     [P] uint64: (total+1) << 32 | (0xFFFFFFFF − node) of the best feasible node,
  *            total = Σ weight·score, ties → lowest node index; 0 ⇔ no feasible node
  * When out_on_device != 0 the pointers are device pointers on the engine's device
@@ -309,6 +361,7 @@ typedef struct kg_eval_out {
     uint64_t *top1;
     int32_t out_on_device;
     int32_t _pad;
+    uint8_t *numa_scores;    /* [P][64·W] NodeNUMAResource score (KG_PLUGIN_NUMA only; may be NULL) */
 } kg_eval_out;
 
 int32_t kg_abi_version(void);
@@ -316,7 +369,7 @@ int32_t kg_abi_version(void);
 enum kg_struct_id {
     KG_SID_RESOURCE_LIST = 0, KG_SID_CONFIG, KG_SID_CONTAINER, KG_SID_POD_SPEC,
     KG_SID_AGGREGATED_USAGE, KG_SID_POD_METRIC, KG_SID_ASSIGNED_POD, KG_SID_NODE_SPEC,
-    KG_SID_CLUSTER_VIEW, KG_SID_POD_ROW, KG_SID_NODE_ROW, KG_SID_EVAL_OUT, KG_SID_COUNT
+    KG_SID_CLUSTER_VIEW, KG_SID_POD_ROW, KG_SID_NODE_ROW, KG_SID_EVAL_OUT, KG_SID_NUMA_SPEC, KG_SID_COUNT
 };
 int64_t kg_struct_size(int32_t sid);
 

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 NUM_RES = 8
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
  RES_EXTENDED) = range(8)
@@ -25,10 +25,14 @@ KUBE_QOS_UNSET, KUBE_QOS_GUARANTEED, KUBE_QOS_BURSTABLE, KUBE_QOS_BESTEFFORT = r
 AGG_UNSET, AGG_AVG, AGG_P50, AGG_P90, AGG_P95, AGG_P99 = range(6)
 NUM_AGG_TYPES = 6
 STRATEGY_LEAST_ALLOCATED, STRATEGY_MOST_ALLOCATED = 0, 1
-PLUGIN_FIT, PLUGIN_LOADAWARE = 0x1, 0x2
+PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA = 0x1, 0x2, 0x4
+NUMA_NONE, NUMA_BEST_EFFORT, NUMA_RESTRICTED, NUMA_SINGLE_NUMA_NODE = range(4)
+MAX_ZONES = 8
 
 POD_HAS_REQUEST, POD_DAEMONSET, POD_PROD, POD_LA_PROD_SCORE, POD_VALID = 0x1, 0x2, 0x4, 0x8, 0x80000000
+POD_NUMA_SKIP, POD_NUMA_CPU_BIND = 0x10, 0x20
 NODE_VALID, NODE_HAS_METRIC, NODE_HAS_UPDATE_TIME, NODE_LA_PASS_NONPROD, NODE_LA_PASS_PROD = 0x1, 0x2, 0x4, 0x8, 0x10
+NODE_NUMA_OPTIONS, NODE_NUMA_TOPO_VALID = 0x40, 0x80
 
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE, CODE_UNSCHEDULABLE_AND_UNRESOLVABLE = 0, 1, 2, 3
 TILE = 1024
@@ -44,6 +48,8 @@ CONFIG = np.dtype([
     ("la_score_according_prod_usage", "<i4"), ("la_has_aggregated", "<i4"),
     ("la_agg_usage_thresholds", RESOURCE_LIST), ("la_agg_usage_type", "<i4"), ("la_agg_score_type", "<i4"),
     ("la_agg_usage_duration_ns", "<i8"), ("la_agg_score_duration_ns", "<i8"),
+    ("weight_numa", "<i4"), ("numa_strategy", "<i4"), ("numa_hint_strategy", "<i4"), ("_pad1", "<i4"),
+    ("numa_resource_weight", "<i8", (NUM_RES,)),
     ("device", "<i4"), ("place_chunk", "<i4"),
 ], align=True)
 
@@ -70,21 +76,32 @@ NODE_SPEC = np.dtype([
     ("has_report_interval", "<i4"), ("has_node_metric_info", "<i4"), ("report_interval_seconds", "<i8"),
     ("node_usage", RESOURCE_LIST), ("first_aggregated", "<i4"), ("n_aggregated", "<i4"),
     ("first_pod_metric", "<i4"), ("n_pod_metric", "<i4"), ("first_assigned", "<i4"), ("n_assigned", "<i4"),
+    ("numa", "<i4"), ("_pad_numa", "<i4"),
+], align=True)
+
+NUMA_SPEC = np.dtype([
+    ("policy", "<i4"), ("n_zones", "<i4"), ("zone_id", "<i4", (MAX_ZONES,)),
+    ("zone_total", RESOURCE_LIST, (MAX_ZONES,)), ("zone_allocated", RESOURCE_LIST, (MAX_ZONES,)),
+    ("cpu_amplification_ratio", "<f8"), ("cpu_topology_valid", "<i4"), ("_pad", "<i4"),
 ], align=True)
 
 POD_ROW = np.dtype([
     ("request", "<i8", (NUM_RES,)), ("fit_score_request", "<i8", (NUM_RES,)), ("nonzero_request", "<i8", (2,)),
     ("la_estimate", "<i8", (2,)), ("request_present", "<u4"), ("flags", "<u4"),
+    ("numa_request", "<i8", (NUM_RES,)), ("numa_request_present", "<u4"), ("_pad", "<u4"),
 ], align=True)
 
 NODE_ROW = np.dtype([
     ("alloc", "<i8", (NUM_RES,)), ("requested", "<i8", (NUM_RES,)), ("nonzero_requested", "<i8", (2,)),
     ("la_alloc", "<i8", (2,)), ("la_used", "<i8", (2, 2)), ("metric_update_ns", "<i8"),
     ("pod_count", "<i4"), ("allowed_pods", "<i4"), ("alloc_present", "<u4"), ("flags", "<u4"),
+    ("numa_policy", "<i4"), ("n_zones", "<i4"), ("zone_id", "<i4", (MAX_ZONES,)),
+    ("zone_total", "<i8", (MAX_ZONES, 2)), ("zone_allocated", "<i8", (MAX_ZONES, 2)),
+    ("zone_keys", "<u4"), ("zone_alloc_keys", "<u4"), ("cpu_amplification_ratio", "<f8"),
 ], align=True)
 
 STRUCT_IDS = [RESOURCE_LIST, CONFIG, CONTAINER, POD_SPEC, AGGREGATED_USAGE, POD_METRIC, ASSIGNED_POD, NODE_SPEC,
-              None, POD_ROW, NODE_ROW, None]
+              None, POD_ROW, NODE_ROW, None, NUMA_SPEC]
 
 
 class ClusterView(ctypes.Structure):
@@ -95,12 +112,13 @@ class ClusterView(ctypes.Structure):
         ("aggregated", ctypes.c_void_p), ("n_aggregated", ctypes.c_int32), ("_p3", ctypes.c_int32),
         ("pod_metrics", ctypes.c_void_p), ("n_pod_metrics", ctypes.c_int32), ("_p4", ctypes.c_int32),
         ("assigned", ctypes.c_void_p), ("n_assigned", ctypes.c_int32), ("_p5", ctypes.c_int32),
+        ("numa", ctypes.c_void_p), ("n_numa", ctypes.c_int32), ("_p6", ctypes.c_int32),
     ]
 
 
 class EvalOut(ctypes.Structure):
     _fields_ = [("mask", ctypes.c_void_p), ("scores", ctypes.c_void_p), ("top1", ctypes.c_void_p),
-                ("out_on_device", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+                ("out_on_device", ctypes.c_int32), ("_pad", ctypes.c_int32), ("numa_scores", ctypes.c_void_p)]
 
 
 def ptr(a) -> ctypes.c_void_p:
@@ -111,15 +129,18 @@ def ptr(a) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
 
 
-def make_view(pods, containers, nodes, aggregated, pod_metrics, assigned) -> ClusterView:
+def make_view(pods, containers, nodes, aggregated, pod_metrics, assigned, numa=None) -> ClusterView:
+    if numa is None:
+        numa = np.zeros(0, dtype=NUMA_SPEC)
     v = ClusterView()
     for name, arr in (("pods", pods), ("containers", containers), ("nodes", nodes), ("aggregated", aggregated),
-                      ("pod_metrics", pod_metrics), ("assigned", assigned)):
+                      ("pod_metrics", pod_metrics), ("assigned", assigned), ("numa", numa)):
         assert arr.flags["C_CONTIGUOUS"]
         setattr(v, name, arr.ctypes.data if len(arr) else 0)
     v.n_pods, v.n_containers, v.n_nodes = len(pods), len(containers), len(nodes)
     v.n_aggregated, v.n_pod_metrics, v.n_assigned = len(aggregated), len(pod_metrics), len(assigned)
-    v._keep = (pods, containers, nodes, aggregated, pod_metrics, assigned)
+    v.n_numa = len(numa)
+    v._keep = (pods, containers, nodes, aggregated, pod_metrics, assigned, numa)
     return v
 
 

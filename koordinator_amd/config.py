@@ -38,12 +38,15 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
                 score_according_prod_usage: bool = False,
                 estimated_scaling_factors: Optional[Dict[str, int]] = None,
                 aggregated: Optional[dict] = None,
+                weight_numa: int = 1, numa_strategy: str = "LeastAllocated",
+                numa_hint_strategy: str = "LeastAllocated", numa_resources: Optional[Dict[str, int]] = None,
                 device: int = 0, place_chunk: int = 64) -> np.ndarray:
     c = np.zeros((), dtype=nat.CONFIG)
     c["abi_version"] = nat.ABI_VERSION
     bits = 0
     for p in plugins:
-        bits |= {"NodeResourcesFit": nat.PLUGIN_FIT, "LoadAwareScheduling": nat.PLUGIN_LOADAWARE}[p]
+        bits |= {"NodeResourcesFit": nat.PLUGIN_FIT, "LoadAwareScheduling": nat.PLUGIN_LOADAWARE,
+                 "NodeNUMAResource": nat.PLUGIN_NUMA}[p]
     c["enabled_plugins"] = bits
     c["weight_fit"] = weight_fit
     c["weight_loadaware"] = weight_loadaware
@@ -72,6 +75,13 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
         c["la_agg_score_type"] = AGG[aggregated.get("scoreAggregationType", "")]
         c["la_agg_usage_duration_ns"] = int(aggregated.get("usageAggregatedDuration", 0) * 10**9)
         c["la_agg_score_duration_ns"] = int(aggregated.get("scoreAggregatedDuration", 0) * 10**9)
+    # NodeNUMAResourceArgs (SetDefaults_NodeNUMAResourceArgs, v1beta2/defaults.go:101-137)
+    strategies = {"LeastAllocated": nat.STRATEGY_LEAST_ALLOCATED, "MostAllocated": nat.STRATEGY_MOST_ALLOCATED}
+    c["weight_numa"] = weight_numa
+    c["numa_strategy"] = strategies[numa_strategy]
+    c["numa_hint_strategy"] = strategies[numa_hint_strategy]
+    for k, w in (numa_resources or {"cpu": 1, "memory": 1}).items():
+        c["numa_resource_weight"][RES[k]] = w
     c["device"] = device
     c["place_chunk"] = place_chunk
     return c

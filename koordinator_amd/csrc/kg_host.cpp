@@ -331,6 +331,7 @@ int64_t kg_struct_size(int32_t sid) {
         case KG_SID_POD_ROW: return sizeof(kg_pod_row);
         case KG_SID_NODE_ROW: return sizeof(kg_node_row);
         case KG_SID_EVAL_OUT: return sizeof(kg_eval_out);
+        case KG_SID_NUMA_SPEC: return sizeof(kg_numa_spec);
     }
     return -1;
 }
@@ -354,6 +355,12 @@ void kg_config_default(kg_config *c) {
     set_thr(c->la_usage_thresholds, KG_RES_MEMORY, 95);
     c->la_scaling_factor[KG_RES_CPU] = 85;
     c->la_scaling_factor[KG_RES_MEMORY] = 70;
+    // SetDefaults_NodeNUMAResourceArgs (v1beta2/defaults.go:101-137): LeastAllocated cpu:1 memory:1 for both
+    c->weight_numa = 1;
+    c->numa_strategy = KG_STRATEGY_LEAST_ALLOCATED;
+    c->numa_hint_strategy = KG_STRATEGY_LEAST_ALLOCATED;
+    c->numa_resource_weight[KG_RES_CPU] = 1;
+    c->numa_resource_weight[KG_RES_MEMORY] = 1;
     c->place_chunk = 64;
 }
 
@@ -373,19 +380,27 @@ kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
     };
     if (!c) return fail("null config");
     if (c->abi_version != KG_ABI_VERSION) return fail("abi_version mismatch");
-    if (c->enabled_plugins & ~(KG_PLUGIN_FIT | KG_PLUGIN_LOADAWARE)) return fail("unsupported plugin bit");
-    int64_t fw = 0, lw = 0;
+    if (c->enabled_plugins & ~(KG_PLUGIN_FIT | KG_PLUGIN_LOADAWARE | KG_PLUGIN_NUMA)) return fail("unsupported plugin bit");
+    int64_t fw = 0, lw = 0, nw = 0;
     for (int r = 0; r < KG_NUM_RES; r++) {
-        if (c->fit_resource_weight[r] < 0 || c->la_resource_weight[r] < 0) return fail("negative resource weight");
+        if (c->fit_resource_weight[r] < 0 || c->la_resource_weight[r] < 0 || c->numa_resource_weight[r] < 0)
+            return fail("negative resource weight");
         fw += c->fit_resource_weight[r];
         lw += c->la_resource_weight[r];
+        nw += c->numa_resource_weight[r];
         if (r >= 2 && c->la_resource_weight[r] != 0)
             return fail("LoadAwareScheduling resourceWeights beyond cpu/memory are not supported by the engine");
     }
-    if (fw > 600 || lw > 600) return fail("resource weight sum too large (max 600)");
+    if (fw > 600 || lw > 600 || nw > 600) return fail("resource weight sum too large (max 600)");
+    if ((c->enabled_plugins & KG_PLUGIN_NUMA) && nw == 0) return fail("NodeNUMAResource needs scoringStrategy resources");
+    if (c->numa_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->numa_strategy != KG_STRATEGY_MOST_ALLOCATED)
+        return fail("unsupported NodeNUMAResource scoring strategy");
+    if (c->numa_hint_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->numa_hint_strategy != KG_STRATEGY_MOST_ALLOCATED)
+        return fail("unsupported NodeNUMAResource NUMA scoring strategy");
     if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && lw == 0) return fail("LoadAwareScheduling needs resourceWeights");
     // totals are packed as ((total + 1) << 10) | node into 32-bit per-tile keys: 100·Σweights < 2^22
-    if (c->weight_fit < 0 || c->weight_loadaware < 0 || (int64_t)c->weight_fit + c->weight_loadaware > 40000)
+    if (c->weight_fit < 0 || c->weight_loadaware < 0 || c->weight_numa < 0 ||
+        (int64_t)c->weight_fit + c->weight_loadaware + ((c->enabled_plugins & KG_PLUGIN_NUMA) ? c->weight_numa : 0) > 40000)
         return fail("plugin weight out of range (each >= 0, sum <= 40000)");
     if (c->fit_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->fit_strategy != KG_STRATEGY_MOST_ALLOCATED)
         return fail("unsupported NodeResourcesFit scoring strategy");
@@ -436,7 +451,23 @@ kg_status kg_build_pod_rows(const kg_config *cfg, const kg_cluster_view *view, c
             if (r < 2) row.nonzero_request[r] = nz;
         }
         estimate_pod(*cfg, pv, row.la_estimate);
+        // NodeNUMAResource PreFilter (plugin.go:219-269): PodRequestsAndLimits requests; skip when all zero
+        {
+            kg_resource_list nreq, nlim;
+            requests_and_limits(pv, nreq, nlim);
+            bool all_zero = true;
+            for (int r = 0; r < KG_NUM_RES; r++) {
+                row.numa_request[r] = val(nreq, r);
+                if (row.numa_request[r] != 0) all_zero = false;
+            }
+            row.numa_request_present = nreq.present;
+            if (all_zero) row.flags |= KG_POD_NUMA_SKIP;
+        }
         const int pc = priority_class_of(pv);
+        // AllowUseCPUSet (util.go:43-50): raw QoS label LSE/LSR and koord-prod; the default bind policy
+        // FullPCPUs (defaults.go:50) then asks for a cpuset whenever cpu is requested
+        if ((pv.p.label_qos == KG_QOS_LSE || pv.p.label_qos == KG_QOS_LSR) && pc == KG_PRIO_PROD && row.numa_request[KG_RES_CPU] > 0)
+            row.flags |= KG_POD_NUMA_CPU_BIND;
         if (pc == KG_PRIO_PROD) row.flags |= KG_POD_PROD;
         if (pc == KG_PRIO_PROD && cfg->la_score_according_prod_usage) row.flags |= KG_POD_LA_PROD_SCORE;
         if (pv.p.is_daemonset) row.flags |= KG_POD_DAEMONSET;
@@ -500,6 +531,34 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
             if (pass_p) row.flags |= KG_NODE_LA_PASS_PROD;
             loadaware_node_term(*cfg, *view, ns, 0, row.la_used[0]);
             loadaware_node_term(*cfg, *view, ns, 1, row.la_used[1]);
+        }
+        // NodeNUMAResource topology options (topology_options.go) with amplified zone cpu
+        // (util.go:62-85 amplifyNUMANodeResources) and the plugin's zone allocations
+        row.cpu_amplification_ratio = 1.0;
+        if (ns.numa >= 0) {
+            if (ns.numa >= view->n_numa) return KG_ERR_RANGE;
+            const kg_numa_spec &nm = view->numa[ns.numa];
+            if (nm.n_zones < 0 || nm.n_zones > KG_MAX_ZONES) return KG_ERR_RANGE;
+            row.flags |= KG_NODE_NUMA_OPTIONS;
+            if (nm.cpu_topology_valid) row.flags |= KG_NODE_NUMA_TOPO_VALID;
+            row.numa_policy = nm.policy;
+            row.n_zones = nm.n_zones;
+            row.cpu_amplification_ratio = nm.cpu_amplification_ratio;
+            for (int z = 0; z < nm.n_zones; z++) {
+                if (nm.zone_id[z] < 0 || nm.zone_id[z] >= 64) return KG_ERR_RANGE;
+                // the engine's zones carry cpu and memory only
+                if ((nm.zone_total[z].present | nm.zone_allocated[z].present) & ~0x3u) return KG_ERR_UNSUPPORTED;
+                row.zone_id[z] = nm.zone_id[z];
+                for (int r = 0; r < 2; r++) {
+                    int64_t t = val(nm.zone_total[z], r);
+                    if (r == KG_RES_CPU && nm.cpu_amplification_ratio > 1.0 && t != 0)
+                        t = (int64_t)ceil((double)t * nm.cpu_amplification_ratio);
+                    row.zone_total[z][r] = t;
+                    row.zone_allocated[z][r] = val(nm.zone_allocated[z], r);
+                    if (bit(nm.zone_total[z].present, r)) row.zone_keys |= 1u << (2 * z + r);
+                    if (bit(nm.zone_allocated[z].present, r)) row.zone_alloc_keys |= 1u << (2 * z + r);
+                }
+            }
         }
     }
     return KG_OK;

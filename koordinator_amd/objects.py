@@ -118,6 +118,33 @@ class Node:
     custom_usage_thresholds: Optional[Dict[str, int]] = None          # scheduling.koordinator.sh/usage-thresholds
     custom_prod_usage_thresholds: Optional[Dict[str, int]] = None
     custom_aggregated: Optional[dict] = None   # {"usageThresholds": {...}, "usageAggregationType": "p95", "usageAggregatedDuration": seconds}
+    # NodeNUMAResource topology options: zones in NodeResourceTopology order
+    numa_policy: str = ""                                   # "", "BestEffort", "Restricted", "SingleNUMANode"
+    numa_zones: Optional[List[Dict[str, object]]] = None    # NUMANodeResources[i].Resources (None ⇔ no options)
+    numa_zone_ids: Optional[List[int]] = None               # NUMANodeResource.Node (default 0..Z-1)
+    numa_allocated: Optional[Dict[int, Dict[str, object]]] = None   # allocatedResources by zone id
+    cpu_amplification_ratio: float = 0.0
+    cpu_topology_valid: bool = True
+
+
+NUMA_POLICY = {"": nat.NUMA_NONE, "BestEffort": nat.NUMA_BEST_EFFORT, "Restricted": nat.NUMA_RESTRICTED,
+               "SingleNUMANode": nat.NUMA_SINGLE_NUMA_NODE}
+
+
+def numa_spec_record(n: "Node") -> np.ndarray:
+    rec = np.zeros((), dtype=nat.NUMA_SPEC)
+    rec["policy"] = NUMA_POLICY[n.numa_policy]
+    zones = n.numa_zones or []
+    ids = n.numa_zone_ids if n.numa_zone_ids is not None else list(range(len(zones)))
+    rec["n_zones"] = len(zones)
+    for z, (zid, res) in enumerate(zip(ids, zones)):
+        rec["zone_id"][z] = zid
+        rec["zone_total"][z] = resource_list(res)
+        if n.numa_allocated and zid in n.numa_allocated:
+            rec["zone_allocated"][z] = resource_list(n.numa_allocated[zid])
+    rec["cpu_amplification_ratio"] = n.cpu_amplification_ratio
+    rec["cpu_topology_valid"] = int(n.cpu_topology_valid)
+    return rec
 
 
 @dataclasses.dataclass
@@ -258,6 +285,10 @@ class Cluster:
                 rec["timestamp_ns"] = self.now_ns - int(round(age * 10**9))
                 fv.assigned.append(rec)
             ns["n_assigned"] = len(self.assigned.get(n.name, []))
+            ns["numa"] = -1
+            if n.numa_zones is not None:
+                ns["numa"] = len(fv.numa)
+                fv.numa.append(numa_spec_record(n))
         fv.nodes = nodes
         return fv.finish()
 
@@ -323,6 +354,7 @@ class FlatView:
         self.aggregated: List[np.ndarray] = []
         self.pod_metrics: List[np.ndarray] = []
         self.assigned: List[np.ndarray] = []
+        self.numa: List[np.ndarray] = []
         self.nodes = None
 
     def pod_index(self, p: Pod) -> int:
@@ -342,8 +374,9 @@ class FlatView:
         self.aggregated_arr = _stack(self.aggregated, nat.AGGREGATED_USAGE)
         self.pod_metrics_arr = _stack(self.pod_metrics, nat.POD_METRIC)
         self.assigned_arr = _stack(self.assigned, nat.ASSIGNED_POD)
+        self.numa_arr = _stack(self.numa, nat.NUMA_SPEC)
         self.c_view = nat.make_view(self.pods, self.containers, self.nodes, self.aggregated_arr, self.pod_metrics_arr,
-                                    self.assigned_arr)
+                                    self.assigned_arr, self.numa_arr)
         return self
 
     def add_pods(self, pods: Sequence[Pod]) -> List[int]:

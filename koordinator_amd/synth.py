@@ -30,19 +30,21 @@ MI = 1 << 20
 class SynthView:
     """Same attribute surface as objects.FlatView (pods, containers, nodes, c_view …)."""
 
-    def __init__(self, pods, containers, nodes, now_ns):
+    def __init__(self, pods, containers, nodes, now_ns, numa=None):
         self.pods = pods
         self.containers = containers
         self.nodes = nodes
         self.aggregated_arr = np.zeros(0, dtype=nat.AGGREGATED_USAGE)
         self.pod_metrics_arr = np.zeros(0, dtype=nat.POD_METRIC)
         self.assigned_arr = np.zeros(0, dtype=nat.ASSIGNED_POD)
+        self.numa_arr = np.zeros(0, dtype=nat.NUMA_SPEC) if numa is None else numa
         self.now_ns = now_ns
         self.c_view = nat.make_view(self.pods, self.containers, self.nodes, self.aggregated_arr, self.pod_metrics_arr,
-                                    self.assigned_arr)
+                                    self.assigned_arr, self.numa_arr)
 
     def subset_nodes(self, begin: int, end: int) -> "SynthView":
-        return SynthView(self.pods, self.containers, np.ascontiguousarray(self.nodes[begin:end]), self.now_ns)
+        nodes = np.ascontiguousarray(self.nodes[begin:end])
+        return SynthView(self.pods, self.containers, nodes, self.now_ns, self.numa_arr)
 
 
 def _rl_fill(arr, r, values, mask=None):
@@ -92,6 +94,7 @@ def make_nodes(n: int, seed: int, now_ns: int = NOW_NS, no_metric_frac: float = 
     usage = nodes["node_usage"]
     _rl_fill(usage, nat.RES_CPU, (cpu * rng.integers(0, 81, n)) // 100)
     _rl_fill(usage, nat.RES_MEMORY, (mem // 100) * rng.integers(0, 91, n))
+    nodes["numa"] = -1
     return nodes
 
 
@@ -128,6 +131,66 @@ def make_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, **k
     nodes = make_nodes(n_nodes, seed, now_ns, **kw)
     pods, cont = make_pods(n_pods, seed)
     return SynthView(pods, cont, nodes, now_ns)
+
+
+def make_numa_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, zones=(4, 6, 8),
+                      ls_frac: float = 0.6) -> SynthView:
+    """BASELINE config 3: nodes with Z ∈ `zones` NUMA zones (equal split of the node's
+    cpu / memory allocatable; zone allocated uniform 0–70 %), policy mix 40 % SingleNUMANode, 30 %
+    Restricted, 30 % None; pods 60 % LS (cpu / memory requests) and 40 % batch (batch-cpu /
+    batch-memory).  Node Requested carries the zone allocations (they are pods on the node)."""
+    rng = np.random.default_rng(seed + 77)
+    nodes = make_nodes(n_nodes, seed, now_ns)
+    cpu = nodes["allocatable"]["v"][:, nat.RES_CPU].copy()
+    mem = nodes["allocatable"]["v"][:, nat.RES_MEMORY].copy()
+    Z = rng.choice(np.array(zones, np.int64), n_nodes)
+    u = rng.random(n_nodes)
+    policy = np.where(u < 0.4, nat.NUMA_SINGLE_NUMA_NODE, np.where(u < 0.7, nat.NUMA_RESTRICTED, nat.NUMA_NONE))
+    numa = np.zeros(n_nodes, dtype=nat.NUMA_SPEC)
+    numa["policy"] = policy
+    numa["n_zones"] = Z
+    numa["cpu_topology_valid"] = 1
+    req_cpu = np.zeros(n_nodes, np.int64)
+    req_mem = np.zeros(n_nodes, np.int64)
+    for z in range(max(zones)):
+        live = z < Z
+        zc = np.where(live, (cpu // Z) // 1000 * 1000, 0)
+        zm = np.where(live, (mem // Z) // (1 << 20) * (1 << 20), 0)
+        ac = (zc * rng.integers(0, 71, n_nodes)) // 100 // 1000 * 1000
+        am = (zm // 100) * rng.integers(0, 71, n_nodes)
+        numa["zone_id"][:, z] = np.where(live, z, 0)
+        _rl_fill(numa["zone_total"][:, z], nat.RES_CPU, zc, live)
+        _rl_fill(numa["zone_total"][:, z], nat.RES_MEMORY, zm, live)
+        _rl_fill(numa["zone_allocated"][:, z], nat.RES_CPU, ac, live)
+        _rl_fill(numa["zone_allocated"][:, z], nat.RES_MEMORY, am, live)
+        req_cpu += np.where(live, ac, 0)
+        req_mem += np.where(live, am, 0)
+    # the zone allocations are pods on the node: NodeInfo.Requested / NonZeroRequested hold them
+    rv = nodes["requested"]["v"]
+    rv[:, nat.RES_CPU] = np.maximum(rv[:, nat.RES_CPU], req_cpu)
+    rv[:, nat.RES_MEMORY] = np.maximum(rv[:, nat.RES_MEMORY], req_mem)
+    nodes["nonzero_requested"][:, 0] = rv[:, nat.RES_CPU]
+    nodes["nonzero_requested"][:, 1] = rv[:, nat.RES_MEMORY]
+    nodes["numa"] = np.arange(n_nodes)
+    pods, cont = make_pods(n_pods, seed)
+    # 60 % LS / 40 % batch mix
+    rng2 = np.random.default_rng(seed + 991)
+    batch = rng2.random(n_pods) >= ls_frac
+    rq, lm = cont["requests"], cont["limits"]
+    cpu_r = np.where(rq["present"] & (1 << nat.RES_CPU), rq["v"][:, nat.RES_CPU], rq["v"][:, nat.RES_BATCH_CPU])
+    mem_r = np.where(rq["present"] & (1 << nat.RES_MEMORY), rq["v"][:, nat.RES_MEMORY], rq["v"][:, nat.RES_BATCH_MEMORY])
+    for arr in (rq, lm):
+        arr["v"][:] = 0
+        arr["present"][:] = 0
+    _rl_fill(rq, nat.RES_CPU, cpu_r, ~batch)
+    _rl_fill(rq, nat.RES_MEMORY, mem_r, ~batch)
+    _rl_fill(lm, nat.RES_CPU, cpu_r, ~batch)
+    _rl_fill(lm, nat.RES_MEMORY, mem_r, ~batch)
+    _rl_fill(rq, nat.RES_BATCH_CPU, cpu_r, batch)
+    _rl_fill(rq, nat.RES_BATCH_MEMORY, mem_r, batch)
+    _rl_fill(lm, nat.RES_BATCH_CPU, cpu_r, batch)
+    _rl_fill(lm, nat.RES_BATCH_MEMORY, mem_r, batch)
+    return SynthView(pods, cont, nodes, now_ns, numa)
 
 
 # BASELINE.json configs (single-GPU bench uses config 2)

@@ -558,26 +558,449 @@ int64_t kgo_fit_score(const kg_config *c, const kg_cluster_view *v, const kg_pod
 }
 
 /* ---------------------------------------------------------------- */
+/* NodeNUMAResource without cpuset binding                            */
+/* pkg/scheduler/plugins/nodenumaresource/{plugin.go:219-419,         */
+/* scoring.go:55-242, resource_manager.go:122-271,418-532,            */
+/* node_allocation.go:155-177, util.go:52-85}, frameworkext/          */
+/* topologymanager/{manager.go:58-120, policy.go:68-224,              */
+/* policy_single_numa_node.go, policy_restricted.go,                  */
+/* policy_best_effort.go}, pkg/util/bitmask/bitmask.go.               */
+/* The reference iterates the per-resource hint lists in Go map order  */
+/* (policy.go:108, random); this restatement fixes the order to the   */
+/* sorted resource names.                               */
+/* ---------------------------------------------------------------- */
+typedef struct { uint64_t mask; int nil; int pref; int64_t score; } numa_hint;
+
+/* resource ids in sorted resource-name order: cpu, ephemeral-storage, example.com/gpu,
+ * kubernetes.io/batch-cpu, batch-memory, mid-cpu, mid-memory, memory */
+static const int kSortedRes[KG_NUM_RES] = {KG_RES_CPU, KG_RES_EPHEMERAL_STORAGE, KG_RES_EXTENDED, KG_RES_BATCH_CPU,
+                                           KG_RES_BATCH_MEMORY, KG_RES_MID_CPU, KG_RES_MID_MEMORY, KG_RES_MEMORY};
+
+static int popcount64(uint64_t m) { return __builtin_popcountll(m); }
+
+/* quotav1.SubtractWithNonNegativeResult: keys of a ∪ b, max(a − b, 0) */
+static void rl_sub_nonneg(const kg_resource_list *a, const kg_resource_list *b, kg_resource_list *out) {
+    memset(out, 0, sizeof(*out));
+    out->present = a->present | b->present;
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        if (!has(out, r)) continue;
+        int64_t x = get(a, r) - get(b, r);
+        out->v[r] = x > 0 ? x : 0;
+    }
+}
+
+/* resourceAllocationScorer.score (scoring.go:187-226) over framework.Resources built from lists */
+static int64_t numa_scorer(const kg_config *c, int strategy, const kg_resource_list *requested,
+                           const kg_resource_list *allocatable, const kg_resource_list *pod) {
+    int64_t score = 0, wsum = 0;
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        int64_t w = c->numa_resource_weight[r];
+        if (w <= 0) continue;
+        int64_t pr = get(pod, r);
+        if (pr == 0 && is_scalar(r)) continue;
+        if (is_scalar(r) && !has(allocatable, r)) continue;
+        int64_t alloc = get(allocatable, r), req = get(requested, r) + pr;
+        if (alloc == 0) continue;
+        int64_t s;
+        if (strategy == KG_STRATEGY_MOST_ALLOCATED) s = ((req > alloc ? alloc : req) * MAX_NODE_SCORE) / alloc;
+        else s = req > alloc ? 0 : ((alloc - req) * MAX_NODE_SCORE) / alloc;
+        score += s * w;
+        wsum += w;
+    }
+    return wsum ? score / wsum : 0;
+}
+
+typedef struct {
+    int n;
+    int id[KG_MAX_ZONES];
+    kg_resource_list total[KG_MAX_ZONES];      /* amplified */
+    kg_resource_list allocated[KG_MAX_ZONES];  /* present == 0 ⇔ no allocation entry */
+    int has_alloc[KG_MAX_ZONES];
+    kg_resource_list avail[KG_MAX_ZONES];
+} numa_zones;
+
+/* TopologyOptions after amplifyNUMANodeResources + NodeAllocation.getAvailableNUMANodeResources */
+static void numa_zones_of(const kg_numa_spec *s, numa_zones *z) {
+    memset(z, 0, sizeof(*z));
+    z->n = s->n_zones;
+    for (int i = 0; i < s->n_zones; i++) {
+        z->id[i] = s->zone_id[i];
+        z->total[i] = s->zone_total[i];
+        if (s->cpu_amplification_ratio > 1.0 && get(&z->total[i], KG_RES_CPU) != 0)
+            z->total[i].v[KG_RES_CPU] = (int64_t)ceil((double)get(&z->total[i], KG_RES_CPU) * s->cpu_amplification_ratio);
+        z->allocated[i] = s->zone_allocated[i];
+        z->has_alloc[i] = s->zone_allocated[i].present != 0;
+        kg_resource_list none;
+        memset(&none, 0, sizeof(none));
+        rl_sub_nonneg(&z->total[i], z->has_alloc[i] ? &z->allocated[i] : &none, &z->avail[i]);
+    }
+}
+
+#define MAX_HINTS 256
+typedef struct {
+    int present;          /* the resource has a hint list in the map */
+    int n;
+    numa_hint h[MAX_HINTS];
+} hint_list;
+
+/* generateResourceHints (resource_manager.go:418-492) + hintsGenerator.generateHints (:499-532) */
+static void numa_generate_hints(const kg_config *c, const numa_zones *z, const kg_resource_list *preq,
+                                hint_list lists[KG_NUM_RES]) {
+    int min_aff[KG_NUM_RES];
+    int total_names[KG_NUM_RES];
+    memset(total_names, 0, sizeof(total_names));
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        lists[r].present = 0;
+        lists[r].n = 0;
+        min_aff[r] = z->n;
+    }
+    /* IterateBitMasks(numaNodes): sizes 1..n, combinations of the zone list in order */
+    int idx[KG_MAX_ZONES];
+    for (int size = 1; size <= z->n; size++) {
+        for (int i = 0; i < size; i++) idx[i] = i;
+        for (;;) {
+            uint64_t mask = 0;
+            kg_resource_list total, avail;
+            memset(&total, 0, sizeof(total));
+            memset(&avail, 0, sizeof(avail));
+            for (int i = 0; i < size; i++) {
+                mask |= 1ull << z->id[idx[i]];
+                rl_add(&avail, &z->avail[idx[i]]);
+                rl_add(&total, &z->total[idx[i]]);
+            }
+            kg_resource_list requested;
+            rl_sub_nonneg(&total, &avail, &requested);
+            int64_t score = numa_scorer(c, c->numa_hint_strategy, &requested, &total, preq);
+            int count = popcount64(mask);
+            /* memory group first, then every other requested resource on its own */
+            for (int pass = 0; pass < 2; pass++) {
+                for (int r = 0; r < KG_NUM_RES; r++) {
+                    if (!has(preq, r)) continue;
+                    int is_mem = r == KG_RES_MEMORY;
+                    if (pass == 0 && !is_mem) continue;
+                    if (pass == 1) {
+                        if (has(&total, r)) total_names[r] = 1;
+                        if (is_mem) continue;
+                    }
+                    if (get(&total, r) < get(preq, r)) continue;
+                    if (count < min_aff[r]) min_aff[r] = count;
+                    if (get(&avail, r) < get(preq, r)) continue;
+                    hint_list *l = &lists[r];
+                    l->present = 1;
+                    if (l->n < MAX_HINTS) {
+                        l->h[l->n].mask = mask;
+                        l->h[l->n].nil = 0;
+                        l->h[l->n].pref = 0;
+                        l->h[l->n].score = score;
+                        l->n++;
+                    }
+                }
+            }
+            /* next combination */
+            int i = size - 1;
+            while (i >= 0 && idx[i] == z->n - size + i) i--;
+            if (i < 0) break;
+            idx[i]++;
+            for (int k = i + 1; k < size; k++) idx[k] = idx[k - 1] + 1;
+        }
+    }
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        if (!has(preq, r)) continue;
+        for (int k = 0; k < lists[r].n; k++) lists[r].h[k].pref = popcount64(lists[r].h[k].mask) == min_aff[r];
+        if (total_names[r]) lists[r].present = 1; /* possibly an empty list */
+    }
+}
+
+/* mergeFilteredHints (policy.go:127-185) over provider lists in order */
+typedef struct { numa_hint best; uint64_t dflt; } merge_state;
+
+static void merge_visit(merge_state *m, const numa_hint *perm, int k) {
+    int pref = 1;
+    uint64_t merged = m->dflt;
+    for (int i = 0; i < k; i++) {
+        merged &= perm[i].nil ? m->dflt : perm[i].mask;
+        if (!perm[i].pref) pref = 0;
+    }
+    if (popcount64(merged) == 0) return;
+    int64_t score = 0;
+    for (int i = 0; i < k; i++)
+        if (!perm[i].nil && perm[i].mask == merged && perm[i].score > score) score = perm[i].score;
+    numa_hint mh = {merged, 0, pref, score};
+    numa_hint *b = &m->best;
+    if (mh.pref && !b->pref) { *b = mh; return; }
+    if (!mh.pref && b->pref) return;
+    int cm = popcount64(mh.mask), cb = popcount64(b->mask);
+    int narrower = cm == cb ? mh.mask < b->mask : cm < cb;
+    if (!narrower) {
+        if (cm == cb && mh.score > b->score) *b = mh;
+        return;
+    }
+    *b = mh;
+}
+
+static void merge_iterate(merge_state *m, numa_hint **lists, const int *lens, int nl, int i, numa_hint *accum) {
+    if (i == nl) {
+        merge_visit(m, accum, nl);
+        return;
+    }
+    for (int j = 0; j < lens[i]; j++) {
+        accum[i] = lists[i][j];
+        merge_iterate(m, lists, lens, nl, i + 1, accum);
+    }
+}
+
+/* policy.Merge over already-filtered provider lists (filterProvidersHints output) */
+static int numa_merge_lists(int policy, uint64_t dflt, numa_hint **plist, int *plen, int nl, numa_hint *best) {
+    static __thread numa_hint filtered[KG_NUM_RES + 8][MAX_HINTS];
+    if (policy == KG_NUMA_SINGLE_NUMA_NODE) {
+        /* filterSingleNumaHints (policy_single_numa_node.go:48-78) */
+        for (int i = 0; i < nl; i++) {
+            int n = 0;
+            for (int j = 0; j < plen[i] && n < MAX_HINTS; j++) {
+                const numa_hint *h = &plist[i][j];
+                if ((h->nil && h->pref) || (!h->nil && popcount64(h->mask) == 1 && h->pref)) filtered[i][n++] = *h;
+            }
+            plist[i] = filtered[i];
+            plen[i] = n;
+        }
+    }
+    merge_state m;
+    m.dflt = dflt;
+    m.best.mask = dflt;
+    m.best.nil = 0;
+    m.best.pref = 0;
+    m.best.score = 0;
+    numa_hint accum[KG_NUM_RES + 8];
+    merge_iterate(&m, plist, plen, nl, 0, accum);
+    *best = m.best;
+    if (policy == KG_NUMA_SINGLE_NUMA_NODE) {
+        if (best->mask == dflt) { best->nil = 1; best->mask = 0; best->score = 0; }
+        return best->pref;
+    }
+    if (policy == KG_NUMA_RESTRICTED) return best->pref;
+    return 1; /* BestEffort */
+}
+
+/* Merge entry for the reference's policy tests: n_lists provider lists (len −1 ⇔ a nil list, i.e. a
+ * provider without hints → {nil, preferred}; len 0 ⇔ an empty list → {nil, not preferred}). */
+int kgo_numa_merge(int policy, const int32_t *numa_nodes, int nn, int n_lists, const int32_t *list_len,
+                   const uint64_t *masks, const int32_t *nils, const int32_t *prefs, const int64_t *scores,
+                   uint64_t *out_mask, int32_t *out_nil, int32_t *out_pref) {
+    static __thread numa_hint store[KG_NUM_RES + 8][MAX_HINTS];
+    numa_hint *plist[KG_NUM_RES + 8];
+    int plen[KG_NUM_RES + 8];
+    uint64_t dflt = 0;
+    for (int i = 0; i < nn; i++) dflt |= 1ull << numa_nodes[i];
+    if (n_lists > KG_NUM_RES + 8) return -1;
+    int k = 0;
+    for (int i = 0; i < n_lists; i++) {
+        plist[i] = store[i];
+        if (list_len[i] <= 0) {
+            store[i][0].nil = 1;
+            store[i][0].mask = 0;
+            store[i][0].pref = list_len[i] < 0;
+            store[i][0].score = 0;
+            plen[i] = 1;
+            continue;
+        }
+        for (int j = 0; j < list_len[i] && j < MAX_HINTS; j++, k++) {
+            store[i][j].mask = masks[k];
+            store[i][j].nil = nils[k];
+            store[i][j].pref = prefs[k];
+            store[i][j].score = scores[k];
+        }
+        plen[i] = list_len[i];
+    }
+    numa_hint best;
+    int admit = numa_merge_lists(policy, dflt, plist, plen, n_lists, &best);
+    *out_mask = best.nil ? 0 : best.mask;
+    *out_nil = best.nil;
+    *out_pref = best.pref;
+    return admit;
+}
+
+/* Admit (manager.go:58-80): returns admit, writes the best hint */
+static int numa_admit(const kg_config *c, const numa_zones *z, int policy, const kg_resource_list *preq, numa_hint *best) {
+    static __thread hint_list lists[KG_NUM_RES];
+    numa_generate_hints(c, z, preq, lists);
+    uint64_t dflt = 0;
+    for (int i = 0; i < z->n; i++) dflt |= 1ull << z->id[i];
+    /* filterProvidersHints (policy.go:94-125), resources in sorted-name order */
+    numa_hint any_pref = {0, 1, 1, 0}, none_possible = {0, 1, 0, 0};
+    numa_hint *plist[KG_NUM_RES];
+    int plen[KG_NUM_RES];
+    int nl = 0, any_list = 0;
+    for (int k = 0; k < KG_NUM_RES; k++) {
+        const hint_list *l = &lists[kSortedRes[k]];
+        if (!l->present) continue;
+        any_list = 1;
+        if (l->n == 0) {
+            plist[nl] = &none_possible;
+            plen[nl++] = 1;
+        } else {
+            plist[nl] = (numa_hint *)l->h;
+            plen[nl++] = l->n;
+        }
+    }
+    if (!any_list) {
+        plist[0] = &any_pref;
+        plen[0] = 1;
+        nl = 1;
+    }
+    return numa_merge_lists(policy, dflt, plist, plen, nl, best);
+}
+
+/* allocateResourcesByHint (resource_manager.go:195-250): 0 on success, zone allocations in out */
+static int numa_allocate(const numa_zones *z, const numa_hint *hint, const kg_resource_list *preq,
+                         kg_resource_list out[KG_MAX_ZONES], int *n_out, int out_zone[KG_MAX_ZONES]) {
+    *n_out = 0;
+    if (hint->nil) return 0;
+    kg_resource_list req = *preq;
+    uint32_t inter = 0;
+    for (int bitn = 0; bitn < 64; bitn++) {
+        if (!((hint->mask >> bitn) & 1ull)) continue;
+        int zi = -1;
+        for (int i = 0; i < z->n; i++)
+            if (z->id[i] == bitn) zi = i;
+        if (zi < 0) continue;
+        kg_resource_list avail = z->avail[zi];
+        kg_resource_list got;
+        memset(&got, 0, sizeof(got));
+        for (int r = 0; r < KG_NUM_RES; r++) {
+            if (!has(&req, r) || !has(&avail, r)) continue;
+            inter |= 1u << r;
+            int64_t a = avail.v[r], q = req.v[r], alloc;
+            if (a > q) { avail.v[r] = a - q; req.v[r] = 0; alloc = q; }
+            else if (a < q) { req.v[r] = q - a; avail.v[r] = 0; alloc = a; }
+            else { req.v[r] = 0; avail.v[r] = 0; alloc = a; }
+            if (alloc != 0) { got.v[r] = alloc; got.present |= 1u << r; }
+        }
+        int nonzero = 0;
+        for (int r = 0; r < KG_NUM_RES; r++) if (has(&got, r) && got.v[r] != 0) nonzero = 1;
+        if (nonzero) {
+            out[*n_out] = got;
+            out_zone[*n_out] = zi;
+            (*n_out)++;
+        }
+        int zero = 1;
+        for (int r = 0; r < KG_NUM_RES; r++) if (has(&req, r) && req.v[r] != 0) zero = 0;
+        if (zero) break;
+    }
+    for (int r = 0; r < KG_NUM_RES; r++)
+        if (((inter >> r) & 1u) && req.v[r] != 0) return -1;
+    return 0;
+}
+
+/* pod requests of PreFilter (PodRequestsAndLimits) */
+static void numa_pod_requests(const kg_cluster_view *v, const kg_pod_spec *pod, kg_resource_list *req) {
+    kg_resource_list lim;
+    pod_requests_and_limits(v, pod, req, &lim);
+}
+
+static int numa_skip(const kg_resource_list *req) {
+    for (int r = 0; r < KG_NUM_RES; r++)
+        if (has(req, r) && req->v[r] != 0) return 0;
+    return 1;
+}
+
+/* Filter + Score of NodeNUMAResource for one pair (no cpuset binding).  `numa` may be NULL (no
+ * topology options).  Returns feasibility; *score the plugin score; the best hint in *hint. */
+static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n,
+                     const kg_numa_spec *numa, int64_t *score, numa_hint *hint) {
+    kg_resource_list preq;
+    numa_pod_requests(v, pod, &preq);
+    *score = 0;
+    hint->nil = 1;
+    hint->mask = 0;
+    hint->pref = 1;
+    hint->score = 0;
+    if (numa_skip(&preq)) return 1;
+    int policy = numa ? numa->policy : KG_NUMA_NONE;
+    /* filterAmplifiedCPUs (plugin.go:340-373) without cpuset allocations */
+    double ratio = numa ? numa->cpu_amplification_ratio : 0.0;
+    int64_t pcpu = get(&preq, KG_RES_CPU);
+    if (pcpu != 0 && ratio > 1.0 && pcpu > get(&n->allocatable, KG_RES_CPU) - get(&n->requested, KG_RES_CPU)) return 0;
+    numa_zones z;
+    if (policy != KG_NUMA_NONE) {
+        if (!numa || numa->n_zones == 0) return 0; /* node(s) missing NUMA resources */
+        numa_zones_of(numa, &z);
+        if (!numa_admit(c, &z, policy, &preq, hint)) return 0;
+        kg_resource_list got[KG_MAX_ZONES];
+        int ng, gz[KG_MAX_ZONES];
+        if (numa_allocate(&z, hint, &preq, got, &ng, gz) != 0) return 0;
+        if (ng > 0) {
+            /* calculateAllocatableAndRequested (scoring.go:118-164) over the allocated zones */
+            kg_resource_list alloc, req;
+            memset(&alloc, 0, sizeof(alloc));
+            memset(&req, 0, sizeof(req));
+            for (int i = 0; i < ng; i++) {
+                int zi = gz[i];
+                if (z.has_alloc[zi]) {
+                    kg_resource_list none, a;
+                    memset(&none, 0, sizeof(none));
+                    rl_sub_nonneg(&z.allocated[zi], &none, &a);
+                    rl_add(&req, &a);
+                }
+                rl_add(&alloc, &z.total[zi]);
+            }
+            *score = numa_scorer(c, c->numa_strategy, &req, &alloc, &preq);
+            return 1;
+        }
+    }
+    *score = numa_scorer(c, c->numa_strategy, &n->requested, &n->allocatable, &preq);
+    return 1;
+}
+
+/* Reserve (plugin.go:375-419 → resourceManager.Update): zone allocations of the chosen node */
+static void numa_reserve(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, kg_numa_spec *numa) {
+    if (!numa || numa->policy == KG_NUMA_NONE || !numa->cpu_topology_valid) return;
+    kg_resource_list preq;
+    numa_pod_requests(v, pod, &preq);
+    if (numa_skip(&preq)) return;
+    numa_zones z;
+    numa_zones_of(numa, &z);
+    numa_hint hint;
+    if (!numa_admit(c, &z, numa->policy, &preq, &hint)) return;
+    kg_resource_list got[KG_MAX_ZONES];
+    int ng, gz[KG_MAX_ZONES];
+    if (numa_allocate(&z, &hint, &preq, got, &ng, gz) != 0) return;
+    for (int i = 0; i < ng; i++) rl_add(&numa->zone_allocated[gz[i]], &got[i]);
+}
+
+int kgo_numa_eval(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n,
+                  int64_t *score) {
+    numa_hint h;
+    const kg_numa_spec *numa = n->numa >= 0 ? &v->numa[n->numa] : NULL;
+    return numa_pair(c, v, pod, n, numa, score, &h);
+}
+
+/* ---------------------------------------------------------------- */
 /* combined per-pair evaluation and the sequential reference cycle    */
 /* ---------------------------------------------------------------- */
 typedef struct {
     kg_node_spec spec;        /* mutable NodeInfo copy */
     assigned_ref *assigned;   /* podAssignCache items of this node */
     int n_assigned, cap_assigned;
+    kg_numa_spec numa;        /* mutable NodeNUMAResource allocation state */
+    int has_numa;
 } node_state;
 
 static int pair_feasible(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n,
                          int64_t now_ns) {
     if ((c->enabled_plugins & KG_PLUGIN_FIT) && kgo_fit_filter(v, pod, n) != KG_CODE_SUCCESS) return 0;
     if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && kgo_loadaware_filter(c, v, pod, n, now_ns) != KG_CODE_SUCCESS) return 0;
+    if (c->enabled_plugins & KG_PLUGIN_NUMA) {
+        int64_t s;
+        if (!kgo_numa_eval(c, v, pod, n, &s)) return 0;
+    }
     return 1;
 }
 
 /* Matrix mode oracle: feasibility + per-plugin scores of every pair.
  * mask[p*N+n] ∈ {0,1}; fit/la [p*N+n] (0 where the plugin is disabled). */
-int kgo_eval_matrix_range(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P,
-                          int32_t node_begin, int32_t node_end, int64_t now_ns, uint8_t *mask, uint8_t *fit,
-                          uint8_t *la) {
+int kgo_eval_matrix3(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P,
+                     int32_t node_begin, int32_t node_end, int64_t now_ns, uint8_t *mask, uint8_t *fit,
+                     uint8_t *la, uint8_t *numa) {
     const int32_t W = node_end - node_begin;
     for (int32_t p = 0; p < P; p++) {
         const kg_pod_spec *pod = &v->pods[pod_index[p]];
@@ -587,9 +1010,20 @@ int kgo_eval_matrix_range(const kg_config *c, const kg_cluster_view *v, const in
             mask[o] = (uint8_t)pair_feasible(c, v, pod, n, now_ns);
             fit[o] = (c->enabled_plugins & KG_PLUGIN_FIT) ? (uint8_t)kgo_fit_score(c, v, pod, n) : 0;
             la[o] = (c->enabled_plugins & KG_PLUGIN_LOADAWARE) ? (uint8_t)kgo_loadaware_score(c, v, pod, n, now_ns) : 0;
+            if (numa) {
+                int64_t s = 0;
+                if (c->enabled_plugins & KG_PLUGIN_NUMA) kgo_numa_eval(c, v, pod, n, &s);
+                numa[o] = (uint8_t)s;
+            }
         }
     }
     return 0;
+}
+
+int kgo_eval_matrix_range(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P,
+                          int32_t node_begin, int32_t node_end, int64_t now_ns, uint8_t *mask, uint8_t *fit,
+                          uint8_t *la) {
+    return kgo_eval_matrix3(c, v, pod_index, P, node_begin, node_end, now_ns, mask, fit, la, NULL);
 }
 
 int kgo_eval_matrix(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P,
@@ -609,6 +1043,8 @@ int kgo_schedule(const kg_config *c, const kg_cluster_view *v, const int32_t *po
         st[j].cap_assigned = v->nodes[j].n_assigned + 4;
         st[j].assigned = (assigned_ref *)malloc(sizeof(assigned_ref) * (size_t)st[j].cap_assigned);
         st[j].n_assigned = gather_assigned(v, &v->nodes[j], st[j].assigned);
+        st[j].has_numa = v->nodes[j].numa >= 0;
+        if (st[j].has_numa) st[j].numa = v->numa[v->nodes[j].numa];
     }
     for (int32_t p = 0; p < P; p++) {
         const kg_pod_spec *pod = &v->pods[pod_index[p]];
@@ -616,12 +1052,20 @@ int kgo_schedule(const kg_config *c, const kg_cluster_view *v, const int32_t *po
         int32_t best_n = -1;
         for (int32_t j = 0; j < N; j++) {
             const kg_node_spec *n = &st[j].spec;
-            if (!pair_feasible(c, &vv, pod, n, now_ns)) continue;
+            int64_t numa_score = 0;
+            if (c->enabled_plugins & KG_PLUGIN_NUMA) {
+                numa_hint h;
+                if (!numa_pair(c, &vv, pod, n, st[j].has_numa ? &st[j].numa : NULL, &numa_score, &h)) continue;
+            }
+            if ((c->enabled_plugins & KG_PLUGIN_FIT) && kgo_fit_filter(&vv, pod, n) != KG_CODE_SUCCESS) continue;
+            if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && kgo_loadaware_filter(c, &vv, pod, n, now_ns) != KG_CODE_SUCCESS)
+                continue;
             int64_t total = 0;
             if (c->enabled_plugins & KG_PLUGIN_FIT) total += c->weight_fit * kgo_fit_score(c, &vv, pod, n);
             if (c->enabled_plugins & KG_PLUGIN_LOADAWARE)
                 total += c->weight_loadaware *
                          loadaware_score_impl(c, &vv, pod, n, st[j].assigned, st[j].n_assigned, now_ns);
+            if (c->enabled_plugins & KG_PLUGIN_NUMA) total += c->weight_numa * numa_score;
             if (total > best) { best = total; best_n = j; }
         }
         out_node[p] = best_n;
@@ -650,6 +1094,9 @@ int kgo_schedule(const kg_config *c, const kg_cluster_view *v, const int32_t *po
             s->spec.nonzero_requested[r] += nz;
         }
         s->spec.pod_count += 1;
+        /* NodeNUMAResource.Reserve → resourceManager.Update: zone allocations of the stored hint (the
+         * zone state is the one the pod was filtered on, so re-admitting reproduces that hint) */
+        if ((c->enabled_plugins & KG_PLUGIN_NUMA) && s->has_numa) numa_reserve(c, &vv, pod, &s->numa);
         /* LoadAware.Reserve → podAssignCache.assign(nodeName, pod) with timestamp now */
         if (!pod->is_terminated) {
             if (s->n_assigned == s->cap_assigned) {
@@ -700,6 +1147,11 @@ static void *par_worker(void *arg) {
             const kg_node_spec *nd = &j->v->nodes[k];
             if (!pair_feasible(j->c, j->v, j->pod, nd, j->now_ns)) continue;
             int64_t total = 0;
+            if (j->c->enabled_plugins & KG_PLUGIN_NUMA) {
+                int64_t ns_;
+                kgo_numa_eval(j->c, j->v, j->pod, nd, &ns_);
+                total += j->c->weight_numa * ns_;
+            }
             if (j->c->enabled_plugins & KG_PLUGIN_FIT) total += j->c->weight_fit * kgo_fit_score(j->c, j->v, j->pod, nd);
             if (j->c->enabled_plugins & KG_PLUGIN_LOADAWARE)
                 total += j->c->weight_loadaware * kgo_loadaware_score(j->c, j->v, j->pod, nd, j->now_ns);

@@ -32,6 +32,12 @@ def lib():
         L.kgo_schedule.argtypes = [vp, vp, vp, i32, i64, vp, vp]
         L.kgo_priority_class.restype = ctypes.c_int
         L.kgo_priority_class.argtypes = [vp, vp]
+        L.kgo_numa_eval.restype = ctypes.c_int
+        L.kgo_numa_eval.argtypes = [vp, vp, vp, vp, vp]
+        L.kgo_numa_merge.restype = ctypes.c_int
+        L.kgo_numa_merge.argtypes = [ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.kgo_eval_matrix3.restype = ctypes.c_int
+        L.kgo_eval_matrix3.argtypes = [vp, vp, vp, i32, i32, i32, i64, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -111,3 +117,52 @@ def eval_parallel(cfg, view, pod_index, now_ns, workers=16):
     L.kgo_eval_parallel(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, len(idx), now_ns, workers,
                         top.ctypes.data)
     return top
+
+
+def numa_eval(cfg, view, pod_i, node_j):
+    """NodeNUMAResource Filter + Score of one pair → (feasible, score)."""
+    sc = ctypes.c_int64(0)
+    ok = lib().kgo_numa_eval(_cfg(cfg), ctypes.byref(view.c_view), _pod(view, pod_i), _node(view, node_j),
+                             ctypes.byref(sc))
+    return bool(ok), int(sc.value)
+
+
+def numa_merge(policy, numa_nodes, lists):
+    """Topology-manager Merge over provider lists: each list is None (nil list), [] (empty) or
+    [(mask_bits | None, preferred[, score]), ...]. Returns (admit, mask_bits | None, preferred)."""
+    nodes = np.ascontiguousarray(numa_nodes, dtype=np.int32)
+    lens, masks, nils, prefs, scores = [], [], [], [], []
+    for l in lists:
+        if l is None:
+            lens.append(-1)
+            continue
+        lens.append(len(l))
+        for h in l:
+            bits, pref = h[0], h[1]
+            masks.append(0 if bits is None else sum(1 << b for b in bits))
+            nils.append(1 if bits is None else 0)
+            prefs.append(int(pref))
+            scores.append(int(h[2]) if len(h) > 2 else 0)
+    arr = lambda x, t: np.ascontiguousarray(x if x else [0], dtype=t)
+    lens_a, masks_a, nils_a = arr(lens, np.int32), arr(masks, np.uint64), arr(nils, np.int32)
+    prefs_a, scores_a = arr(prefs, np.int32), arr(scores, np.int64)
+    om, on, op = ctypes.c_uint64(0), ctypes.c_int32(0), ctypes.c_int32(0)
+    admit = lib().kgo_numa_merge(int(policy), nodes.ctypes.data, len(nodes), len(lens), lens_a.ctypes.data,
+                                 masks_a.ctypes.data, nils_a.ctypes.data, prefs_a.ctypes.data, scores_a.ctypes.data,
+                                 ctypes.byref(om), ctypes.byref(on), ctypes.byref(op))
+    bits = None if on.value else [b for b in range(64) if (om.value >> b) & 1]
+    return bool(admit), bits, bool(op.value)
+
+
+def eval_matrix3(cfg, view, pod_index, now_ns, node_begin=0, node_end=None):
+    """mask, fit, loadaware, numa planes of every pair."""
+    idx = np.ascontiguousarray(pod_index, dtype=np.int32)
+    node_end = len(view.nodes) if node_end is None else node_end
+    P, W = len(idx), node_end - node_begin
+    mask = np.zeros((P, W), np.uint8)
+    fit = np.zeros((P, W), np.uint8)
+    la = np.zeros((P, W), np.uint8)
+    numa = np.zeros((P, W), np.uint8)
+    lib().kgo_eval_matrix3(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, P, node_begin, node_end, now_ns,
+                           mask.ctypes.data, fit.ctypes.data, la.ctypes.data, numa.ctypes.data)
+    return mask.astype(bool), fit, la, numa
