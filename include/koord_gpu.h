@@ -385,8 +385,15 @@ kg_status kg_build_pod_rows(const kg_config *cfg, const kg_cluster_view *view,
                             const int32_t *pod_index, int32_t n, kg_pod_row *out);
 kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view,
                              const int32_t *node_index, int32_t n, kg_node_row *out);
-/* Reserve delta (AssumePod + LoadAware.Reserve) applied to a host-side row. */
+/* Reserve delta (AssumePod + LoadAware.Reserve + NodeNUMAResource.Reserve zone allocations) applied
+ * to a host-side row. */
 kg_status kg_row_commit(const kg_config *cfg, kg_node_row *node, const kg_pod_row *pod);
+/* Filter + Score of one (pod, node) pair on host rows, through the same per-pair code the kernels
+ * run: the single-node checks of a scheduling cycle (RunFilterPluginsWithNominatedPods for one
+ * node, preemption's SelectVictimsOnNode, framework_extender.go:354-372) without a device.
+ * Scores are the plugin scores (0..100) of the enabled plugins, 0 otherwise. */
+kg_status kg_row_eval(const kg_config *cfg, const kg_node_row *node, const kg_pod_row *pod, int64_t now_ns,
+                      int32_t *feasible, int32_t *fit_score, int32_t *la_score, int32_t *numa_score);
 
 /* Engine lifecycle. */
 kg_status kg_engine_create(const kg_config *cfg, kg_engine **out);

@@ -146,7 +146,7 @@ def make_view(pods, containers, nodes, aggregated, pod_metrics, assigned, numa=N
 
 EXPORTED = [
     "kg_abi_version", "kg_struct_size", "kg_config_default", "kg_config_shipped_profile", "kg_config_validate",
-    "kg_build_pod_rows", "kg_build_node_rows", "kg_row_commit", "kg_engine_create", "kg_engine_destroy",
+    "kg_build_pod_rows", "kg_build_node_rows", "kg_row_commit", "kg_row_eval", "kg_engine_create", "kg_engine_destroy",
     "kg_last_error", "kg_set_stream", "kg_sync", "kg_snapshot_reset", "kg_snapshot_upsert", "kg_snapshot_remove",
     "kg_snapshot_download", "kg_set_shard", "kg_pods_set", "kg_eval", "kg_place", "kg_num_tiles",
     "kg_place_chunk_eval", "kg_place_chunk_resolve", "kg_commit", "kg_set_profiling", "kg_eval_kernel_times",
@@ -171,6 +171,7 @@ def lib() -> ctypes.CDLL:
         "kg_config_validate": (i32, [vp, ctypes.c_char_p, i32]),
         "kg_build_pod_rows": (i32, [vp, vp, vp, i32, vp]), "kg_build_node_rows": (i32, [vp, vp, vp, i32, vp]),
         "kg_row_commit": (i32, [vp, vp, vp]),
+        "kg_row_eval": (i32, [vp, vp, vp, i64, vp, vp, vp, vp]),
         "kg_engine_create": (i32, [vp, ctypes.POINTER(vp)]), "kg_engine_destroy": (None, [vp]),
         "kg_last_error": (ctypes.c_char_p, [vp]), "kg_set_stream": (i32, [vp, vp]), "kg_sync": (i32, [vp]),
         "kg_snapshot_reset": (i32, [vp, i32]), "kg_snapshot_upsert": (i32, [vp, vp, vp, i32]),

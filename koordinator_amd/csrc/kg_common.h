@@ -64,6 +64,9 @@ struct kg_pod_dev {
     uint32_t _pad;
     int64_t nonzero[2];
     int64_t la_est_i[2];
+    int64_t numa_req[KG_NUM_RES];// NodeNUMAResource PreFilter requests (PodRequestsAndLimits)
+    uint32_t numa_present;       // their key set
+    uint32_t _pad2;
 };
 
 // config-derived constants passed by value to every kernel
@@ -80,6 +83,10 @@ struct kg_consts {
     int32_t la_shift;            // log2 Σ la_w when a power of two, else 0xFF
     float la_rcp;                // 1 / Σ la_w
     int64_t la_exp_ns;
+    int32_t weight_numa;
+    int32_t numa_most;           // ScoringStrategy MostAllocated
+    int32_t numa_hint_most;      // NUMAScoringStrategy MostAllocated
+    int32_t numa_w[KG_NUM_RES];  // ScoringStrategy.Resources weights
 };
 
 #define KG_NEUTRAL_REQ INT64_MIN  // request that passes every Fit compare
@@ -251,6 +258,334 @@ KG_HD bool kg_la_pass(const kg_consts &c, uint32_t df, bool expired, int variant
 }
 KG_HD bool kg_la_valid(const kg_consts &c, uint32_t df, bool expired) {
     return (df & KGD_HAS_METRIC) && !(c.la_has_exp && expired);
+}
+
+
+// ---- NodeNUMAResource (no cpuset binding) on engine rows -----------------------------------
+// Restates nodenumaresource/{plugin.go:264-373, scoring.go:55-226, resource_manager.go:195-250,
+// 418-532} and topologymanager/{policy.go:94-185, policy_*.go} (the oracle's numa_pair) for zones
+// holding cpu and memory.  Zones are handled in index space (bit i = zone i of the row, i < 8);
+// hint masks become affinity-id masks only where the merge compares them.
+//
+// A hint list exists per requested resource in sorted-name order (cpu, ephemeral-storage,
+// example.com/gpu, batch-cpu, batch-memory, mid-cpu, mid-memory, memory — the reference walks a Go
+// map).  Zone sums are non-negative, so "total ≥ request" and "available ≥ request" are
+// monotone in the mask: the list's minimum affinity size is the first prefix of the descending
+// zone totals that covers the request, and the list is non-empty iff the whole-node mask fits.
+// A preferred merged hint always beats a non-preferred one (policy.go:158-169), so the merge folds
+// only preferred × preferred permutations when one exists; the full fold over every permutation is
+// needed only for a BestEffort node without any.  kg_pods_set bounds a pod to 2 hint lists.
+#define KG_NUMA_MAX_LISTS 2
+
+struct kg_numa_out {
+    bool feasible;
+    uint32_t score;
+    int32_t n_alloc;                  // zones with a non-zero allocation (Reserve)
+    int32_t zone[KG_MAX_ZONES];       // their row zone index
+    int64_t alloc[KG_MAX_ZONES][2];   // allocated cpu, memory
+};
+
+KG_HD int64_t kg_lr_i(int64_t req, int64_t cap) { return (cap == 0 || req > cap) ? 0 : ((cap - req) * 100) / cap; }
+KG_HD int64_t kg_mr_i(int64_t req, int64_t cap) { return cap == 0 ? 0 : ((req > cap ? cap : req) * 100) / cap; }
+
+// resourceAllocationScorer.score (scoring.go:187-226) where only cpu / memory can be allocatable
+// (zone sums): every other resource is either native with allocatable 0 or a missing scalar key.
+KG_HD uint32_t kg_numa_score_zones(const kg_consts &c, bool most, const int64_t used[2], const int64_t total[2],
+                                   const kg_pod_dev &p) {
+    int64_t s = 0, w = 0;
+    for (int r = 0; r < 2; r++) {
+        if (c.numa_w[r] <= 0 || total[r] == 0) continue;
+        const int64_t rq = used[r] + p.numa_req[r];
+        s += (most ? kg_mr_i(rq, total[r]) : kg_lr_i(rq, total[r])) * c.numa_w[r];
+        w += c.numa_w[r];
+    }
+    return w ? (uint32_t)(s / w) : 0u;
+}
+
+// the same over the node's Requested / Allocatable (policy None, or nothing allocated in zones)
+KG_HD uint32_t kg_numa_score_node(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p) {
+    int64_t s = 0, w = 0;
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        if (c.numa_w[r] <= 0) continue;
+        const bool scalar = (KG_SCALAR_RES_MASK >> r) & 1u;
+        const int64_t pr = p.numa_req[r];
+        if (scalar && (pr == 0 || !((row.alloc_present >> r) & 1u))) continue;
+        const int64_t a = row.alloc[r];
+        if (a == 0) continue;
+        const int64_t rq = row.requested[r] + pr;
+        s += (c.numa_most ? kg_mr_i(rq, a) : kg_lr_i(rq, a)) * c.numa_w[r];
+        w += c.numa_w[r];
+    }
+    return w ? (uint32_t)(s / w) : 0u;
+}
+
+// zone total / available of resource r ∈ {cpu, memory} for zone i (available = max(total − allocated, 0))
+KG_HD int64_t kg_zone_total(const kg_node_row &row, int i, int r) {
+    return ((row.zone_keys >> (2 * i + r)) & 1u) ? row.zone_total[i][r] : 0;
+}
+KG_HD int64_t kg_zone_avail(const kg_node_row &row, int i, int r) {
+    const int64_t a = kg_zone_total(row, i, r) - row.zone_allocated[i][r];
+    return a > 0 ? a : 0;
+}
+
+KG_HD void kg_mask_sums(const kg_node_row &row, uint32_t m, int64_t tot[2], int64_t av[2]) {
+    tot[0] = tot[1] = av[0] = av[1] = 0;
+    for (int i = 0; i < KG_MAX_ZONES; i++) {
+        if (!((m >> i) & 1u)) continue;
+        for (int r = 0; r < 2; r++) {
+            tot[r] += kg_zone_total(row, i, r);
+            av[r] += kg_zone_avail(row, i, r);
+        }
+    }
+}
+
+KG_HD uint64_t kg_id_mask(const kg_node_row &row, uint32_t m) {
+    uint64_t out = 0;
+    for (int i = 0; i < KG_MAX_ZONES; i++)
+        if ((m >> i) & 1u) out |= 1ull << row.zone_id[i];
+    return out;
+}
+
+// lexicographic successor of a k-combination of {0..Z-1} held as an index bitmask (0 when done):
+// bitmask.IterateBitMasks order within one size
+KG_HD uint32_t kg_combo_next(uint32_t m, int Z) {
+    int cnt = 0, t = Z - 1;
+    while (t >= 0 && ((m >> t) & 1u)) { cnt++; t--; }
+    int b = t;
+    while (b >= 0 && !((m >> b) & 1u)) b--;
+    if (b < 0) return 0;
+    return (m & ((1u << b) - 1u)) | (((1u << (cnt + 1)) - 1u) << (b + 1));
+}
+
+struct kg_numa_list {
+    int32_t res;       // resource id; zone resources are cpu (0) and memory (1)
+    int32_t k;         // minimum affinity size: hints of this size are preferred
+    bool any;          // the list holds at least one hint
+    int64_t req;
+};
+
+KG_HD bool kg_list_fits(const kg_node_row &row, const kg_numa_list &l, uint32_t m) {
+    if (l.req == 0) return true;
+    if (l.res > 1) return false;
+    int64_t tot[2], av[2];
+    kg_mask_sums(row, m, tot, av);
+    return tot[l.res] >= l.req && av[l.res] >= l.req;
+}
+
+struct kg_numa_best {
+    uint64_t mask;     // affinity-id mask
+    bool pref;
+    uint32_t score;
+};
+
+// mergeFilteredHints: one permutation's merged hint against the running best (policy.go:140-182)
+KG_HD void kg_numa_fold(kg_numa_best &b, uint64_t m, bool pref, uint32_t score) {
+    if (pref && !b.pref) { b = kg_numa_best{m, pref, score}; return; }
+    if (!pref && b.pref) return;
+    const int cm = __builtin_popcountll(m), cb = __builtin_popcountll(b.mask);
+    const bool narrower = cm == cb ? m < b.mask : cm < cb;
+    if (narrower || (cm == cb && score > b.score)) b = kg_numa_best{m, pref, score};
+}
+
+// score of a hint mask (generateResourceHints: the NUMA scorer over requested = total − available)
+KG_HD uint32_t kg_hint_score(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, uint32_t m) {
+    int64_t tot[2], av[2];
+    kg_mask_sums(row, m, tot, av);
+    const int64_t used[2] = {tot[0] - av[0], tot[1] - av[1]};
+    return kg_numa_score_zones(c, c.numa_hint_most != 0, used, tot, p);
+}
+
+// one permutation (masks a, b in index space; `full` stands for a nil hint of an empty list)
+KG_HD void kg_numa_visit(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_best &best,
+                         uint32_t a, bool a_hint, uint32_t b, bool b_hint, bool pref) {
+    const uint32_t m = a & b;
+    if (m == 0) return;
+    const bool member = (a_hint && a == m) || (b_hint && b == m);
+    kg_numa_fold(best, kg_id_mask(row, m), pref, member ? kg_hint_score(c, row, p, m) : 0u);
+}
+
+// Filter + Score of NodeNUMAResource for one pair; o.zone / o.alloc are what Reserve records.
+KG_HD void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o) {
+    o.feasible = true;
+    o.score = 0;
+    o.n_alloc = 0;
+    if (p.flags & KG_POD_NUMA_SKIP) return;
+    const bool opts = (row.flags & KG_NODE_NUMA_OPTIONS) != 0;
+    const int policy = opts ? row.numa_policy : KG_NUMA_NONE;
+    // filterAmplifiedCPUs without cpuset allocations (plugin.go:340-373)
+    const double ratio = opts ? row.cpu_amplification_ratio : 0.0;
+    const int64_t pcpu = p.numa_req[KG_RES_CPU];
+    if (pcpu != 0 && ratio > 1.0 && pcpu > row.alloc[KG_RES_CPU] - row.requested[KG_RES_CPU]) {
+        o.feasible = false;
+        return;
+    }
+    if (policy == KG_NUMA_NONE) {
+        o.score = kg_numa_score_node(c, row, p);
+        return;
+    }
+    const int Z = row.n_zones;
+    if (Z <= 0) {
+        o.feasible = false;
+        return;
+    }
+    const uint32_t full = (1u << Z) - 1u;
+    // hint lists (generateResourceHints) in sorted resource-name order
+    const int sorted[KG_NUM_RES] = {KG_RES_CPU, KG_RES_EPHEMERAL_STORAGE, KG_RES_EXTENDED, KG_RES_BATCH_CPU,
+                                    KG_RES_BATCH_MEMORY, KG_RES_MID_CPU, KG_RES_MID_MEMORY, KG_RES_MEMORY};
+    kg_numa_list L[KG_NUMA_MAX_LISTS];
+    int nl = 0;
+    for (int j = 0; j < KG_NUM_RES; j++) {
+        const int r = sorted[j];
+        if (!((p.numa_present >> r) & 1u)) continue;
+        const int64_t q = p.numa_req[r];
+        kg_numa_list l{r, Z, false, q};
+        bool keyed = false;   // some zone's total has the resource (totalResourceNames)
+        if (r <= KG_RES_MEMORY) {
+            int64_t t[KG_MAX_ZONES];
+            int64_t tot_all = 0, av_all = 0;
+            for (int i = 0; i < Z; i++) {
+                t[i] = kg_zone_total(row, i, r);
+                tot_all += t[i];
+                av_all += kg_zone_avail(row, i, r);
+                if ((row.zone_keys >> (2 * i + r)) & 1u) keyed = true;
+            }
+            // minimum affinity: fewest zones whose largest totals cover the request
+            int64_t acc = 0;
+            for (int k = 1; k <= Z; k++) {
+                int best_i = 0;
+                for (int i = 1; i < Z; i++)
+                    if (t[i] > t[best_i]) best_i = i;
+                acc += t[best_i];
+                t[best_i] = -1;
+                if (acc >= q) { l.k = k; break; }
+            }
+            l.any = tot_all >= q && av_all >= q;
+        } else if (q == 0) {
+            l.k = 1;       // a zero request fits every mask
+            l.any = true;
+        }
+        if (!l.any && !keyed) continue;   // no list for the resource
+        if (nl == KG_NUMA_MAX_LISTS) {    // excluded by kg_pods_set
+            o.feasible = false;
+            return;
+        }
+        L[nl++] = l;
+    }
+    const bool single = policy == KG_NUMA_SINGLE_NUMA_NODE;
+    const uint64_t dflt = kg_id_mask(row, full);
+    kg_numa_best best{dflt, false, 0u};
+    if (nl == 0) {
+        best = kg_numa_best{dflt, true, 0u};   // no provider hints: any affinity, preferred
+    } else {
+        bool can_pref = true;
+        for (int i = 0; i < nl; i++)
+            if (!L[i].any || (single && L[i].k != 1)) can_pref = false;
+        if (can_pref) {
+            for (uint32_t a = (1u << L[0].k) - 1u; a; a = kg_combo_next(a, Z)) {
+                if (!kg_list_fits(row, L[0], a)) continue;
+                if (nl == 1) {
+                    kg_numa_visit(c, row, p, best, a, true, full, false, true);
+                    continue;
+                }
+                for (uint32_t b = (1u << L[1].k) - 1u; b; b = kg_combo_next(b, Z))
+                    if (kg_list_fits(row, L[1], b)) kg_numa_visit(c, row, p, best, a, true, b, true, true);
+            }
+        }
+        if (!best.pref && policy == KG_NUMA_BEST_EFFORT) {
+            // no preferred permutation: the full fold, hints of every size in IterateBitMasks order
+            const int ka0 = L[0].any ? 1 : 0, ka1 = L[0].any ? Z : 0;
+            for (int ka = ka0; ka <= ka1; ka++) {
+                for (uint32_t a = ka ? (1u << ka) - 1u : full; a; a = ka ? kg_combo_next(a, Z) : 0u) {
+                    if (ka && !kg_list_fits(row, L[0], a)) continue;
+                    const bool pa = ka == L[0].k;
+                    if (nl == 1) {
+                        kg_numa_visit(c, row, p, best, a, ka != 0, full, false, pa && ka != 0);
+                        continue;
+                    }
+                    const int kb0 = L[1].any ? 1 : 0, kb1 = L[1].any ? Z : 0;
+                    for (int kb = kb0; kb <= kb1; kb++) {
+                        for (uint32_t b = kb ? (1u << kb) - 1u : full; b; b = kb ? kg_combo_next(b, Z) : 0u) {
+                            if (kb && !kg_list_fits(row, L[1], b)) continue;
+                            const bool pb = kb == L[1].k;
+                            kg_numa_visit(c, row, p, best, a, ka != 0, b, kb != 0, pa && ka != 0 && pb && kb != 0);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    // Admit (manager.go:58-80)
+    if (policy != KG_NUMA_BEST_EFFORT && !best.pref) {
+        o.feasible = false;
+        return;
+    }
+    if (!(single && best.mask == dflt)) {   // SingleNUMANode: the all-zones hint is nil
+        // allocateResourcesByHint: zones of the hint in ascending affinity id, greedily
+        int64_t req[2] = {p.numa_req[0], p.numa_req[1]};
+        bool want[2] = {(p.numa_present & 1u) != 0, ((p.numa_present >> 1) & 1u) != 0};
+        bool inter[2] = {false, false};
+        uint32_t left = 0;
+        for (int i = 0; i < Z; i++)
+            if ((best.mask >> row.zone_id[i]) & 1ull) left |= 1u << i;
+        while (left) {
+            int zi = -1;
+            for (int i = 0; i < Z; i++)
+                if (((left >> i) & 1u) && (zi < 0 || row.zone_id[i] < row.zone_id[zi])) zi = i;
+            left &= ~(1u << zi);
+            int64_t got[2] = {0, 0};
+            for (int r = 0; r < 2; r++) {
+                if (!want[r] || !(((row.zone_keys | row.zone_alloc_keys) >> (2 * zi + r)) & 1u)) continue;
+                inter[r] = true;
+                const int64_t a = kg_zone_avail(row, zi, r);
+                got[r] = a < req[r] ? a : req[r];
+                req[r] -= got[r];
+            }
+            if (got[0] != 0 || got[1] != 0) {
+                o.zone[o.n_alloc] = zi;
+                o.alloc[o.n_alloc][0] = got[0];
+                o.alloc[o.n_alloc][1] = got[1];
+                o.n_alloc++;
+            }
+        }
+        if ((inter[0] && req[0] != 0) || (inter[1] && req[1] != 0)) {
+            o.feasible = false;
+            o.n_alloc = 0;
+            return;
+        }
+    }
+    if (o.n_alloc > 0) {
+        // calculateAllocatableAndRequested (scoring.go:118-164) over the allocated zones
+        int64_t tot[2] = {0, 0}, used[2] = {0, 0};
+        for (int j = 0; j < o.n_alloc; j++) {
+            const int zi = o.zone[j];
+            for (int r = 0; r < 2; r++) {
+                tot[r] += kg_zone_total(row, zi, r);
+                const int64_t u = row.zone_allocated[zi][r];
+                used[r] += u > 0 ? u : 0;
+            }
+        }
+        o.score = kg_numa_score_zones(c, c.numa_most != 0, used, tot, p);
+    } else {
+        o.score = kg_numa_score_node(c, row, p);
+    }
+}
+
+// Reserve of NodeNUMAResource (plugin.go:375-419): record the zone allocations of the chosen node
+KG_HD void kg_numa_commit(const kg_consts &c, kg_node_row &row, const kg_pod_dev &p) {
+    if (!(c.plugins & KG_PLUGIN_NUMA) || !(row.flags & KG_NODE_NUMA_OPTIONS) || row.numa_policy == KG_NUMA_NONE ||
+        !(row.flags & KG_NODE_NUMA_TOPO_VALID))
+        return;
+    kg_numa_out o;
+    kg_numa_pair(c, row, p, o);
+    if (!o.feasible) return;
+    for (int j = 0; j < o.n_alloc; j++) {
+        const int zi = o.zone[j];
+        for (int r = 0; r < 2; r++) {
+            if (o.alloc[j][r] == 0) continue;
+            row.zone_allocated[zi][r] += o.alloc[j][r];
+            row.zone_alloc_keys |= 1u << (2 * zi + r);
+        }
+    }
 }
 
 // Exact int64 evaluation of one (pod, node) pair straight from the canonical row (slow path).

@@ -207,8 +207,8 @@ __device__ __forceinline__ bool eval_pair(const kg_consts &c, const kg_planes &p
     return eval_fast(c, p, n, fit, la);
 }
 
-__device__ __forceinline__ uint32_t total_of(const kg_consts &c, uint32_t fit, uint32_t la) {
-    return (uint32_t)c.weight_fit * fit + (uint32_t)c.weight_la * la;
+__device__ __forceinline__ uint32_t total_of(const kg_consts &c, uint32_t fit, uint32_t la, uint32_t numa = 0u) {
+    return (uint32_t)c.weight_fit * fit + (uint32_t)c.weight_la * la + (uint32_t)c.weight_numa * numa;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -780,6 +780,60 @@ __global__ void k_fix_slow(kg_consts c, kg_planes pl, const kg_pod_dev *__restri
     }
 }
 
+// NodeNUMAResource enabled (config 3): Fit + LoadAware as in k_eval2 (fast planes, exact row for
+// slow nodes) plus kg_numa_pair on the canonical row, all in one pass.  A 256-thread workgroup
+// covers one 1024-node tile in four 256-node passes and KG_NUMA_PODS pods; per-(pod, tile) keys
+// are reduced in LDS.  The hint merge is branchy per-lane integer work over the row's zones (the
+// rows stay L2-resident across the workgroup's pods), so this path is latency-, not HBM-bound.
+#define KG_NUMA_PODS 16
+__global__ __launch_bounds__(256) void k_eval_numa(kg_consts c, kg_planes pl, HotArgs a,
+                                                   const kg_pod_dev *__restrict__ pods,
+                                                   unsigned long long *__restrict__ mask, uint16_t *__restrict__ scores,
+                                                   uint8_t *__restrict__ numa_scores, uint32_t *__restrict__ partials) {
+    __shared__ uint32_t keys[KG_NUMA_PODS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int64_t tile = (int64_t)a.tile_begin + blockIdx.x;
+    const int p0 = blockIdx.y * KG_NUMA_PODS;
+    const int np = min(KG_NUMA_PODS, a.n_pods - p0);
+    if (tid < KG_NUMA_PODS) keys[tid] = 0u;
+    __syncthreads();
+    const BatchMasks bm{0xFFu, 0xFFu};
+    for (int k = 0; k < KG_TILE / 256; k++) {
+        const int local = k * 256 + tid;
+        const int64_t node = tile * KG_TILE + local;
+        const bool in_range = node < a.node_end;
+        const int64_t col = node - a.col_begin;
+        NodeRegs n;
+        load_node(c, pl, node, in_range, bm, a.now_ns, n);
+        for (int j = 0; j < np; j++) {
+            const kg_pod_dev &pd = pods[p0 + j];
+            uint32_t fit = 0, la = 0;
+            kg_numa_out o;
+            o.feasible = false;
+            o.score = 0;
+            bool ok = false;
+            if (in_range) {
+                ok = eval_pair(c, pl, pd, n, node, a.now_ns, fit, la);
+                kg_numa_pair(c, pl.rows[node], pd, o);
+                ok = ok && o.feasible;
+            }
+            const unsigned long long bits = __ballot(ok);
+            const int64_t prow = (int64_t)(p0 + j);
+            if (mask && lane == 0 && col < a.node_end - a.col_begin)
+                mask[prow * a.mask_words + (col >> 6)] = bits;
+            if (in_range) {
+                if (scores) scores[prow * a.score_stride + col] = (uint16_t)(fit | (la << 8));
+                if (numa_scores) numa_scores[prow * a.score_stride + col] = (uint8_t)o.score;
+            }
+            uint32_t key = ok ? ((total_of(c, fit, la, o.score) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local) : 0u;
+            key = wave_max_u32(key);
+            if (lane == 0 && key) atomicMax(&keys[j], key);
+        }
+    }
+    __syncthreads();
+    if (tid < np) partials[(int64_t)(p0 + tid) * a.tiles_total + tile] = keys[tid];
+}
+
 __device__ __forceinline__ unsigned long long decode_partial(uint32_t k, int tile) {
     if (k == 0) return 0ull;
     const uint32_t node = (uint32_t)tile * KG_TILE + (KG_TILE - 1) - (k & (KG_TILE - 1));
@@ -807,9 +861,15 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
     NodeRegs n;
     BatchMasks bm{0xFFu, 0xFFu};
     load_node(c, pl, node, true, bm, now_ns, n);
-    uint32_t fit, la;
+    uint32_t fit, la, numa = 0;
     if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
-    return ((unsigned long long)(total_of(c, fit, la) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
+    if (c.plugins & KG_PLUGIN_NUMA) {
+        kg_numa_out o;
+        kg_numa_pair(c, pl.rows[node], p, o);
+        if (!o.feasible) return 0ull;
+        numa = o.score;
+    }
+    return ((unsigned long long)(total_of(c, fit, la, numa) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
 }
 
 // Sequential commit of pods [pod_begin, pod_begin + n) given their per-tile partial keys.
@@ -858,6 +918,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             for (int q = 0; q < KG_RESOLVE_THREADS / 64; q++) w = w > red[q] ? w : red[q];
             if (w) {
                 const int32_t node = (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull));
+                kg_numa_commit(c, pl.rows[node], pd);
                 kg_apply_commit(pl.rows[node], pd);
                 kg_finalize_node(c, pl, node);
                 bool seen = false;
@@ -875,6 +936,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
 }
 
 __global__ void k_commit_one(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t pod, int32_t node) {
+    kg_numa_commit(c, pl.rows[node], pods[pod]);
     kg_apply_commit(pl.rows[node], pods[pod]);
     kg_finalize_node(c, pl, node);
 }
@@ -1189,7 +1251,7 @@ void launch_cls(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint1
 
 // mask and scores are both produced or both omitted (the host path provides scratch for a missing one)
 kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
-                      uint32_t *partials, bool use_cls = false) {
+                      uint32_t *partials, bool use_cls = false, uint8_t *numa_scores = nullptr) {
     if (n <= 0) return KG_OK;
     if ((mask == nullptr) != (scores == nullptr)) return set_err(e, KG_ERR_INVALID_ARG, "mask and scores go together");
     const int64_t shard_tiles = (e->shard_end - e->shard_begin + KG_TILE - 1) / KG_TILE;
@@ -1206,6 +1268,18 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     a.fit_cap = e->consts.fit_most ? 100u : 0xFFFFFFFFu;
     for (int s = 0; s < 8; s++) a.slot_res[s] = s < e->nslot ? e->slot_res[s] : -1;
     a.now_ns = now_ns;
+    if (e->consts.plugins & KG_PLUGIN_NUMA) {
+        dim3 grid((unsigned)shard_tiles, (unsigned)((n + KG_NUMA_PODS - 1) / KG_NUMA_PODS));
+        if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
+        hipLaunchKernelGGL(k_eval_numa, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
+                           (unsigned long long *)mask, scores, numa_scores, partials);
+        HIP_TRY(e, hipGetLastError());
+        if (e->profiling) {
+            HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
+            e->ev_count++;
+        }
+        return KG_OK;
+    }
     use_cls = use_cls && e->cls_ok && pod_begin == 0 && n == e->n_pods;
     if (use_cls) {
         kg_status st = cls_layout(e, e->shard_end - e->shard_begin, shard_tiles);
@@ -1419,6 +1493,12 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     uint32_t need = 0;
     for (int32_t i = 0; i < n; i++) {
         if (!kg_pod_row_in_bounds(rows[i])) return set_err(e, KG_ERR_RANGE, "pod %d: request outside the engine bounds", i);
+        if ((e->cfg.enabled_plugins & KG_PLUGIN_NUMA) && !(rows[i].flags & KG_POD_NUMA_SKIP)) {
+            if (rows[i].flags & KG_POD_NUMA_CPU_BIND)
+                return set_err(e, KG_ERR_UNSUPPORTED, "pod %d: NodeNUMAResource cpuset binding is not on the engine path", i);
+            if (kg_numa_list_count(rows[i]) > KG_NUMA_MAX_LISTS)
+                return set_err(e, KG_ERR_UNSUPPORTED, "pod %d: more than %d NUMA hint lists", i, KG_NUMA_MAX_LISTS);
+        }
         kg_pod_dev_from_row(e->cfg, rows[i], dev[i]);
         bm.cmp |= dev[i].cmp_mask;
         bm.fit |= dev[i].fit_mask;
@@ -1493,7 +1573,11 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     const bool planes = out->mask || out->scores;
     const bool stage_mask = planes && (!dev || !out->mask);
     const bool stage_scores = planes && (!dev || !out->scores);
-    size_t need = up(part_b) + up(top_b) + (stage_mask ? up(mask_b) : 0) + (stage_scores ? up(score_b) : 0);
+    const size_t numa_b = (size_t)P * (size_t)((width + 63) / 64 * 64);
+    const bool numa_on = (e->consts.plugins & KG_PLUGIN_NUMA) != 0;
+    const bool stage_numa = out->numa_scores && !dev;
+    size_t need = up(part_b) + up(top_b) + (stage_mask ? up(mask_b) : 0) + (stage_scores ? up(score_b) : 0) +
+                  (stage_numa ? up(numa_b) : 0);
     st = ensure_scratch(e, need + 256);
     if (st) return st;
     char *s = (char *)e->scratch;
@@ -1508,8 +1592,14 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
         if (stage_scores) { scores = (uint16_t *)q; q += up(score_b); }
         else scores = (uint16_t *)out->scores;
     }
+    uint8_t *numa = nullptr;
+    if (out->numa_scores) {
+        if (stage_numa) { numa = (uint8_t *)q; q += up(numa_b); }
+        else numa = out->numa_scores;
+        if (!numa_on && numa_b) HIP_TRY(e, hipMemsetAsync(numa, 0, numa_b, e->stream));
+    }
     HIP_TRY(e, hipMemsetAsync(part, 0, part_b, e->stream));
-    st = launch_eval(e, now_ns, 0, P, mask, scores, part, true);
+    st = launch_eval(e, now_ns, 0, P, mask, scores, part, true, numa_on ? numa : nullptr);
     if (st) return st;
     if (out->top1) {
         unsigned long long *dst = dev ? (unsigned long long *)out->top1 : top;
@@ -1522,6 +1612,7 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     if (!dev) {
         if (out->mask && P > 0) HIP_TRY(e, hipMemcpyAsync(out->mask, mask, mask_b, hipMemcpyDeviceToHost, e->stream));
         if (out->scores && P > 0) HIP_TRY(e, hipMemcpyAsync(out->scores, scores, score_b, hipMemcpyDeviceToHost, e->stream));
+        if (out->numa_scores && P > 0) HIP_TRY(e, hipMemcpyAsync(out->numa_scores, numa, numa_b, hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(e, hipStreamSynchronize(e->stream));
     }
     return KG_OK;

@@ -568,7 +568,40 @@ kg_status kg_row_commit(const kg_config *cfg, kg_node_row *node, const kg_pod_ro
     if (!cfg || !node || !pod) return KG_ERR_INVALID_ARG;
     kg_pod_dev pd;
     kg_pod_dev_from_row(*cfg, *pod, pd);
+    kg_consts k;
+    kg_consts_from_config(*cfg, k);
+    kg_numa_commit(k, *node, pd);   // zone allocations first: they see the pre-Reserve node
     kg_apply_commit(*node, pd);
+    return KG_OK;
+}
+
+kg_status kg_row_eval(const kg_config *cfg, const kg_node_row *node, const kg_pod_row *pod, int64_t now_ns,
+                      int32_t *feasible, int32_t *fit_score, int32_t *la_score, int32_t *numa_score) {
+    if (!cfg || !node || !pod || !feasible) return KG_ERR_INVALID_ARG;
+    kg_consts k;
+    kg_consts_from_config(*cfg, k);
+    kg_pod_dev pd;
+    kg_pod_dev_from_row(*cfg, *pod, pd);
+    // one-node planes, only for the derived flags
+    kg_node_row row = *node;
+    int64_t free_[KG_NUM_RES], metric_ns;
+    double fit_R[KG_NUM_RES], fit_F[KG_NUM_RES], la_R[2], la_F[4];
+    uint32_t dflags, fmask;
+    kg_planes pl{&row, free_, fit_R, fit_F, la_R, la_F, &metric_ns, &dflags, &fmask, 1};
+    kg_finalize_node(k, pl, 0);
+    bool ok;
+    uint32_t fit, la, numa = 0;
+    kg_pair_exact(k, row, dflags, pd, now_ns, ok, fit, la);
+    if (k.plugins & KG_PLUGIN_NUMA) {
+        kg_numa_out o;
+        kg_numa_pair(k, row, pd, o);
+        ok = ok && o.feasible;
+        numa = o.score;
+    }
+    *feasible = ok ? 1 : 0;
+    if (fit_score) *fit_score = (int32_t)fit;
+    if (la_score) *la_score = (int32_t)la;
+    if (numa_score) *numa_score = (int32_t)numa;
     return KG_OK;
 }
 
@@ -593,6 +626,10 @@ void kg_consts_from_config(const kg_config &c, kg_consts &k) {
     k.la_filter_expired = c.la_filter_expired_node_metrics;
     k.la_has_exp = c.la_has_expiration;
     k.la_exp_ns = c.la_has_expiration ? c.la_expiration_seconds * 1000000000LL : 0;
+    k.weight_numa = c.weight_numa;
+    k.numa_most = c.numa_strategy == KG_STRATEGY_MOST_ALLOCATED;
+    k.numa_hint_most = c.numa_hint_strategy == KG_STRATEGY_MOST_ALLOCATED;
+    for (int r = 0; r < KG_NUM_RES; r++) k.numa_w[r] = (int32_t)c.numa_resource_weight[r];
 }
 
 void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &d) {
@@ -628,6 +665,16 @@ void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &
     d.nonzero[1] = row.nonzero_request[1];
     d.la_est_i[0] = row.la_estimate[0];
     d.la_est_i[1] = row.la_estimate[1];
+    for (int r = 0; r < KG_NUM_RES; r++) d.numa_req[r] = row.numa_request[r];
+    d.numa_present = row.numa_request_present;
+}
+
+int kg_numa_list_count(const kg_pod_row &row) {
+    // hint lists a pod can produce: cpu / memory (zone resources) and every zero-valued request key
+    int n = 0;
+    for (int r = 0; r < KG_NUM_RES; r++)
+        if (((row.numa_request_present >> r) & 1u) && (r <= KG_RES_MEMORY || row.numa_request[r] == 0)) n++;
+    return n;
 }
 
 template <int S>
@@ -684,7 +731,7 @@ template uint32_t kg_pod_hot_from_row<8>(const kg_config &, const kg_pod_row &, 
 bool kg_pod_row_in_bounds(const kg_pod_row &row) {
     for (int r = 0; r < KG_NUM_RES; r++)
         if (row.request[r] < 0 || row.request[r] >= KG_VAL_LIMIT || row.fit_score_request[r] < 0 ||
-            row.fit_score_request[r] >= KG_VAL_LIMIT)
+            row.fit_score_request[r] >= KG_VAL_LIMIT || row.numa_request[r] < 0 || row.numa_request[r] >= KG_VAL_LIMIT)
             return false;
     return row.la_estimate[0] >= 0 && row.la_estimate[0] < KG_VAL_LIMIT && row.la_estimate[1] >= 0 &&
            row.la_estimate[1] < KG_VAL_LIMIT;

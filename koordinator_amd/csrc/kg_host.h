@@ -5,6 +5,7 @@
 void kg_consts_from_config(const kg_config &c, kg_consts &k);
 void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &d);
 bool kg_pod_row_in_bounds(const kg_pod_row &row);
+int kg_numa_list_count(const kg_pod_row &row);   // NodeNUMAResource hint lists the pod can produce
 // Fills the S-slot hot row (slot s ↔ resource slot_res[s]) and returns the pod's resources that
 // need a slot (compared or scored), so the caller can check the profile covers them.
 template <int S>

@@ -40,6 +40,14 @@ def row_commit(cfg: np.ndarray, node_row: np.ndarray, pod_row: np.ndarray) -> No
     _check(nat.lib().kg_row_commit(nat.ptr(cfg), nat.ptr(node_row), nat.ptr(pod_row)), what="kg_row_commit")
 
 
+def row_eval(cfg: np.ndarray, node_row: np.ndarray, pod_row: np.ndarray, now_ns: int):
+    """(feasible, fit, la, numa) of one pair on host rows (the kernels' per-pair code, run on the CPU)."""
+    f, a, b, c = (ctypes.c_int32() for _ in range(4))
+    _check(nat.lib().kg_row_eval(nat.ptr(cfg), nat.ptr(node_row), nat.ptr(pod_row), int(now_ns), ctypes.byref(f),
+                                 ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), what="kg_row_eval")
+    return bool(f.value), a.value, b.value, c.value
+
+
 class Engine:
     """One engine = one GPU, one HIP stream, one HBM-resident node snapshot."""
 
@@ -130,8 +138,10 @@ class Engine:
     def score_stride(self) -> int:
         return self.mask_words * 64
 
-    def eval(self, now_ns: int, mask: bool = True, scores: bool = True, top1: bool = True) -> dict:
-        """Matrix mode into host arrays: mask [P][words] u64, scores [P][stride][2] u8, top1 [P] u64."""
+    def eval(self, now_ns: int, mask: bool = True, scores: bool = True, top1: bool = True,
+             numa_scores: Optional[bool] = None) -> dict:
+        """Matrix mode into host arrays: mask [P][words] u64, scores [P][stride][2] u8, top1 [P] u64,
+        numa_scores [P][stride] u8 (by default when NodeNUMAResource is enabled)."""
         P = self.n_pods
         res = {}
         out = nat.EvalOut()
@@ -144,13 +154,20 @@ class Engine:
         if top1:
             res["top1"] = np.zeros(P, dtype=np.uint64)
             out.top1 = res["top1"].ctypes.data
+        if numa_scores is None:
+            numa_scores = bool(int(self.cfg["enabled_plugins"]) & nat.PLUGIN_NUMA)
+        if numa_scores:
+            res["numa_scores"] = np.zeros((P, self.score_stride), dtype=np.uint8)
+            out.numa_scores = res["numa_scores"].ctypes.data
         out.out_on_device = 0
         _check(nat.lib().kg_eval(self._h, int(now_ns), ctypes.byref(out)), self, "kg_eval")
         return res
 
-    def eval_device(self, now_ns: int, mask_ptr: int = 0, scores_ptr: int = 0, top1_ptr: int = 0) -> None:
+    def eval_device(self, now_ns: int, mask_ptr: int = 0, scores_ptr: int = 0, top1_ptr: int = 0,
+                    numa_ptr: int = 0) -> None:
         out = nat.EvalOut()
         out.mask, out.scores, out.top1, out.out_on_device = mask_ptr or None, scores_ptr or None, top1_ptr or None, 1
+        out.numa_scores = numa_ptr or None
         _check(nat.lib().kg_eval(self._h, int(now_ns), ctypes.byref(out)), self, "kg_eval")
 
     def place(self, now_ns: int):

@@ -1,0 +1,134 @@
+"""NodeNUMAResource (BASELINE config 3) on the HIP engine against the oracle restatement.
+
+Matrix mode (k_eval_numa: feasibility, Fit / LoadAware / NUMA score planes, top-1 keys), placement
+(k_resolve with zone-allocation Reserve), node shards, and the host-side rejections of pods the
+engine path does not cover (cpuset binding, more than two hint lists).
+"""
+import numpy as np
+import pytest
+
+from kat import load
+from numa_cases import make_numa_edge_cluster, numa_config
+from numa_kat import numa_score_cluster
+from koordinator_amd import _native as nat
+from koordinator_amd import engine, synth
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+SCORE = load("numa_score_kat.json")
+
+
+def _engine_for(cfg, view, pod_index):
+    eng = engine.Engine(cfg)
+    eng.load_snapshot(engine.build_node_rows(cfg, view))
+    eng.set_pods(engine.build_pod_rows(cfg, view, pod_index))
+    return eng
+
+
+def _weights(cfg):
+    return int(cfg["weight_fit"]), int(cfg["weight_loadaware"]), int(cfg["weight_numa"])
+
+
+def _check_matrix3(cfg, cl, P, begin=0, end=None):
+    N = len(cl.nodes)
+    end = N if end is None else end
+    idx = np.arange(P)
+    with _engine_for(cfg, cl, idx) as eng:
+        if (begin, end) != (0, N):
+            eng.set_shard(begin, end)
+        res = eng.eval(cl.now_ns)
+    W = end - begin
+    m, f, l, n = oracle.eval_matrix3(cfg, cl, idx, cl.now_ns, begin, end)
+    np.testing.assert_array_equal(engine.unpack_mask(res["mask"], W), m)
+    np.testing.assert_array_equal(res["scores"][:, :W, 0], f)
+    np.testing.assert_array_equal(res["scores"][:, :W, 1], l)
+    np.testing.assert_array_equal(res["numa_scores"][:, :W], n)
+    wf, wl, wn = _weights(cfg)
+    tot = np.where(m, wf * f.astype(np.int64) + wl * l.astype(np.int64) + wn * n.astype(np.int64), -1)
+    node, best = engine.decode_top1(res["top1"])
+    np.testing.assert_array_equal(node, np.where(tot.max(axis=1) >= 0, tot.argmax(axis=1) + begin, -1))
+    np.testing.assert_array_equal(best, tot.max(axis=1))
+    return m
+
+
+def test_matrix_config3_mix():
+    cl = synth.make_numa_cluster(3_000, 48, seed=3)
+    m = _check_matrix3(numa_config(), cl, 48)
+    assert 0.2 < m.mean() < 0.95
+
+
+@pytest.mark.parametrize("seed,kw", [(11, {}), (12, dict(numa_strategy="MostAllocated", weight_numa=3,
+                                                           numa_hint_strategy="MostAllocated"))])
+def test_matrix_numa_edge_cases(seed, kw):
+    cl = make_numa_edge_cluster(2_100, 64, seed=seed)
+    _check_matrix3(numa_config(**kw), cl, 64)
+
+
+def test_matrix_numa_shard():
+    cl = make_numa_edge_cluster(2_500, 40, seed=13)
+    _check_matrix3(numa_config(), cl, 40, begin=1024, end=2500)
+
+
+@pytest.mark.parametrize("case", SCORE["cases"], ids=lambda c: c["name"])
+def test_kat_numa_node_score(case):
+    """TestNUMANodeScore (nodenumaresource/scoring_test.go) through kg_eval."""
+    cfg, view, pi, cl = numa_score_cluster(case)
+    with _engine_for(cfg, view, [pi]) as eng:
+        res = eng.eval(0)
+    k = len(case["nodes"])
+    assert list(res["numa_scores"][0, :k]) == case["want"]
+    assert engine.unpack_mask(res["mask"], k).all()
+
+
+@pytest.mark.parametrize("chunk", [1, 16, 64])
+def test_placement_numa_matches_sequential_cycle(chunk):
+    cl = make_numa_edge_cluster(700, 200, seed=21)
+    cfg = numa_config(weight_numa=2, place_chunk=chunk)
+    idx = np.arange(200)
+    with _engine_for(cfg, cl, idx) as eng:
+        nodes, scores = eng.place(cl.now_ns)
+        after = eng.download()
+    ref_n, ref_s = oracle.schedule(cfg, cl, idx, cl.now_ns)
+    np.testing.assert_array_equal(nodes, ref_n)
+    np.testing.assert_array_equal(scores, ref_s)
+    rows = engine.build_node_rows(cfg, cl)
+    prow = engine.build_pod_rows(cfg, cl, idx)
+    for p, n in enumerate(nodes):
+        if n >= 0:
+            engine.row_commit(cfg, rows[n:n + 1], prow[p:p + 1])
+    np.testing.assert_array_equal(after, rows)
+    assert (after["zone_allocated"] != engine.build_node_rows(cfg, cl)["zone_allocated"]).any()
+
+
+def test_placement_numa_tight_cluster():
+    """Few NUMA nodes: zones fill up, SingleNUMANode / Restricted start rejecting, pods go unplaced."""
+    cl = make_numa_edge_cluster(12, 400, seed=31)
+    cfg = numa_config(place_chunk=32)
+    idx = np.arange(400)
+    with _engine_for(cfg, cl, idx) as eng:
+        nodes, scores = eng.place(cl.now_ns)
+    ref_n, ref_s = oracle.schedule(cfg, cl, idx, cl.now_ns)
+    assert (ref_n == -1).any()
+    np.testing.assert_array_equal(nodes, ref_n)
+    np.testing.assert_array_equal(scores, ref_s)
+
+
+def test_pods_set_rejects_numa_shapes_off_the_engine_path():
+    cl = synth.make_numa_cluster(100, 4, seed=5)
+    cfg = numa_config()
+    rows = engine.build_pod_rows(cfg, cl, np.arange(4))
+    with engine.Engine(cfg) as eng:
+        eng.load_snapshot(engine.build_node_rows(cfg, cl))
+        bad = rows.copy()
+        bad["flags"][1] |= nat.POD_NUMA_CPU_BIND
+        bad["flags"][1] &= ~np.uint32(nat.POD_NUMA_SKIP)
+        with pytest.raises(engine.EngineError, match="cpuset"):
+            eng.set_pods(bad)
+        bad = rows.copy()
+        bad["flags"][2] &= ~np.uint32(nat.POD_NUMA_SKIP)
+        bad["numa_request_present"][2] = 0b111   # cpu, memory and a zero-valued ephemeral-storage key
+        bad["numa_request"][2, 2] = 0
+        with pytest.raises(engine.EngineError, match="hint lists"):
+            eng.set_pods(bad)
+        eng.set_pods(rows)   # the batch itself is fine
