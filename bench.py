@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--no-placement", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--c3-pods", type=int, default=1_000, help="config-3 (NodeNUMAResource) pods; 0 skips it")
     return ap.parse_args()
 
 
@@ -69,6 +70,56 @@ def cpu_model() -> str:
     except OSError:
         pass
     return platform.processor()
+
+
+def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
+    """BASELINE config 3: the shipped profile with NodeNUMAResource (weight 1) over 100k nodes with
+    4/6/8 NUMA zones (synth.make_numa_cluster, seed 3).  Matrix mode: feasibility + Fit / LoadAware /
+    NUMA score planes + top-1 (k_eval_numa); placement: sequential cycle with zone Reserve."""
+    import torch
+
+    from koordinator_amd import _native as nat
+
+    P, N = args.c3_pods, args.nodes
+    cl = synth.make_numa_cluster(N, P, seed=3)
+    cfg = shipped_profile()
+    cfg["enabled_plugins"] |= nat.PLUGIN_NUMA
+    rows = engine.build_node_rows(cfg, cl)
+    pods = engine.build_pod_rows(cfg, cl, np.arange(P))
+    eng = engine.Engine(cfg)
+    eng.set_stream(stream.cuda_stream)
+    eng.load_snapshot(rows)
+    eng.set_pods(pods)
+    W = eng.mask_words
+    mask = torch.empty((P, W), dtype=torch.int64, device=dev)
+    scores = torch.empty((P, W * 64, 2), dtype=torch.uint8, device=dev)
+    numa = torch.empty((P, W * 64), dtype=torch.uint8, device=dev)
+    top1 = torch.zeros(P, dtype=torch.int64, device=dev)
+    step = lambda: eng.eval_device(cl.now_ns, mask.data_ptr(), scores.data_ptr(), top1.data_ptr(), numa.data_ptr())
+    step()
+    torch.cuda.synchronize(dev)
+    steps = 3
+    eng.set_profiling(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    k_ms = float(np.mean(eng.eval_kernel_times(steps)))
+    eng.set_profiling(False)
+    feasible = float(engine.unpack_mask(mask[: min(P, 64)].cpu().numpy().view(np.uint64), N).mean())
+    eng.load_snapshot(rows)
+    torch.cuda.synchronize(dev)
+    tp0 = time.perf_counter()
+    nodes, _ = eng.place(cl.now_ns)
+    tp1 = time.perf_counter()
+    eng.close()
+    return {"workload": f"config3: {P} pods x {N} nodes, 4/6/8 NUMA zones, policy mix 40% SingleNUMANode / 30% "
+                        "Restricted / 30% None, 60% LS / 40% batch pods, shipped profile + NodeNUMAResource",
+            "evals_per_s": round(P * N / ((t1 - t0) / steps), 1), "ms_per_step": round((t1 - t0) / steps * 1e3, 3),
+            "kernel": "k_eval_numa", "kernel_ms": round(k_ms, 3), "feasible_frac_sample": round(feasible, 4),
+            "placement": {"pods": P, "seconds": round(tp1 - tp0, 4), "pods_placed_per_s": round(P / (tp1 - tp0), 1),
+                          "placed": int((nodes >= 0).sum())}}
 
 
 def main():
@@ -194,6 +245,10 @@ def main():
                                   f"Parallelizer-faithful {workers}-thread node fan-out (oracle/koord_oracle.c "
                                   f"kgo_eval_parallel), {tc:.1f}s on {cpu_model()}"}
 
+    config3 = None
+    if args.c3_pods > 0 and world == 1:
+        config3 = bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model)
+
     traffic, traffic_src = pmc_traffic()
     if rank == 0:
         line = {
@@ -220,6 +275,7 @@ def main():
                          "algorithmic_bytes_per_launch": int(algo_bytes)},
             "cpu_baseline": cpu_baseline,
             "placement": placement,
+            "config3": config3,
             "pods_with_feasible_node": feasible_pods,
         }
         print(json.dumps(line), flush=True)
