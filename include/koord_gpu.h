@@ -27,6 +27,12 @@
  *                           Reserve) for a queue of pods, with Reserve deltas of LoadAware.Reserve
  *                           (load_aware.go:260-267) and NodeInfo.AddPod (mirror reservation/transformer.go:293-306)
  *   kg_commit               one Reserve (AssumePod + LoadAware.Reserve) of a pod on a node
+ *   kg_rsv_set              reservation cache feed (reservation/cache.go:249-269 forEachAvailableReservationOnNode,
+ *                           frameworkext/reservation_info.go:200-300): per-node reservation slots for the
+ *                           Reservation plugin's restore / Filter / Score / Reserve (reservation/transformer.go:49-291,
+ *                           plugin.go:311-476, scoring.go:42-203, nominator.go:76-135)
+ *   kg_quota_set            ElasticQuota group state for its PreFilter / Reserve (elasticquota/plugin.go:210-255,
+ *                           :323-337; core/group_quota_manager.go:613-650, :791-797)
  *
  * Units follow k8s Quantity conversions used by the plugins: cpu-like resources
  * (KG_RES_CPU) in milli-units (Quantity.MilliValue), every other resource in
@@ -47,7 +53,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 2
+#define KG_ABI_VERSION 3
 
 /* ------------------------------------------------------------------ */
 /* status codes                                                          */
@@ -133,6 +139,8 @@ enum kg_scoring_strategy {
 #define KG_PLUGIN_FIT 0x1u       /* NodeResourcesFit       */
 #define KG_PLUGIN_LOADAWARE 0x2u /* LoadAwareScheduling    */
 #define KG_PLUGIN_NUMA 0x4u      /* NodeNUMAResource (zone fit + score; no cpuset binding) */
+#define KG_PLUGIN_RESERVATION 0x8u  /* Reservation (restore, Filter, Score + NormalizeScore, Reserve) */
+#define KG_PLUGIN_ELASTICQUOTA 0x10u /* ElasticQuota (PreFilter quota gate, Reserve used accounting) */
 
 /* NUMA topology policies (apis/extension/numa_aware.go; node label node.koordinator.sh/numa-topology-policy
  * or the NodeResourceTopology kubelet policy, pkg/scheduler/plugins/nodenumaresource/util.go:52-58) */
@@ -185,6 +193,11 @@ typedef struct kg_config {
     /* engine knobs */
     int32_t device;            /* HIP device ordinal */
     int32_t place_chunk;       /* pods per refresh in kg_place (0 ⇒ default 64) */
+
+    /* Reservation (profile weight, config/manager/scheduler-config.yaml:82-91 ships 5000) */
+    int32_t weight_reservation;
+    /* ElasticQuotaArgs.EnableCheckParentQuota (must be 0: parent recursion is not modelled) */
+    int32_t eq_check_parent_quota;
 } kg_config;
 
 /* ------------------------------------------------------------------ */
@@ -208,6 +221,15 @@ typedef struct kg_pod_spec {
     int32_t is_terminated;                      /* util.IsPodTerminated */
     int32_t _pad;
     int64_t name_id;                            /* identity of namespace/name */
+    /* Reservation: the pod's owner class (reservation.Match(pod) ⇔ bit owner_class of the reservation's
+     * owner_classes; −1 ⇔ matches none) and its required reservation affinity class (−1 ⇔ no
+     * scheduling.koordinator.sh/reservation-affinity; else the reservation must have bit affinity_class
+     * in affinity_classes: reservationAffinity.Match(fakeNode), transformer.go:348-372) */
+    int32_t rsv_owner_class;
+    int32_t rsv_affinity_class;
+    /* ElasticQuota: index into kg_cluster_view.quotas (−1 ⇔ no quota: PreFilter skips) */
+    int32_t quota;
+    int32_t non_preemptible;                    /* extension.IsPodNonPreemptible */
 } kg_pod_spec;
 
 typedef struct kg_aggregated_usage { /* slov1alpha1.AggregatedUsage */
@@ -274,6 +296,35 @@ typedef struct kg_numa_spec {
     int32_t _pad;
 } kg_numa_spec;
 
+/* One reservation as the reservation cache holds it (frameworkext.ReservationInfo). */
+enum kg_rsv_policy { /* schedulingv1alpha1.ReservationAllocatePolicy */
+    KG_RSV_POLICY_DEFAULT = 0,   /* "" */
+    KG_RSV_POLICY_ALIGNED = 1,
+    KG_RSV_POLICY_RESTRICTED = 2
+};
+#define KG_RSV_AVAILABLE 0x1u      /* IsAvailable() && ParseError == nil */
+#define KG_RSV_UNSCHEDULABLE 0x2u  /* Spec.Unschedulable || terminating */
+#define KG_RSV_ALLOCATE_ONCE 0x4u  /* IsAllocateOnce() */
+typedef struct kg_reservation {
+    int32_t node;                  /* node index (reservationsOnNode key) */
+    uint32_t flags;                /* KG_RSV_* */
+    int32_t policy;                /* kg_rsv_policy */
+    int32_t n_assigned;            /* len(AssignedPods) */
+    uint32_t owner_classes;        /* bit c ⇔ Match(pod) for pods of owner class c */
+    uint32_t affinity_classes;     /* bit a ⇔ a reservation-affinity class a selects this reservation */
+    int64_t order;                 /* label scheduling.koordinator.sh/reservation-order (0 ⇔ absent / unparsable) */
+    kg_resource_list allocatable;  /* Allocatable; present = ResourceNames */
+    kg_resource_list allocated;    /* Allocated */
+} kg_reservation;
+
+/* One ElasticQuota group (core.QuotaInfo) as its PreFilter reads it. */
+typedef struct kg_quota {
+    kg_resource_list used_limit;           /* getQuotaInfoUsedLimit: runtime (EnableRuntimeQuota) or max */
+    kg_resource_list used;                 /* Used */
+    kg_resource_list min;                  /* CalculateInfo.Min (non-preemptible gate) */
+    kg_resource_list non_preemptible_used; /* NonPreemptibleUsed */
+} kg_quota;
+
 typedef struct kg_cluster_view {
     const kg_pod_spec *pods;                 int32_t n_pods;       int32_t _p0;
     const kg_container *containers;          int32_t n_containers; int32_t _p1;
@@ -282,6 +333,8 @@ typedef struct kg_cluster_view {
     const kg_pod_metric *pod_metrics;        int32_t n_pod_metrics; int32_t _p4;
     const kg_assigned_pod *assigned;         int32_t n_assigned;   int32_t _p5;
     const kg_numa_spec *numa;                int32_t n_numa;       int32_t _p6;
+    const kg_reservation *reservations;      int32_t n_reservations; int32_t _p7;
+    const kg_quota *quotas;                  int32_t n_quotas;     int32_t _p8;
 } kg_cluster_view;
 
 /* ------------------------------------------------------------------ */
@@ -293,6 +346,7 @@ typedef struct kg_cluster_view {
 #define KG_POD_LA_PROD_SCORE 0x8u  /* prodPod && ScoreAccordingProdUsage (load_aware.go:291) */
 #define KG_POD_NUMA_SKIP 0x10u     /* NodeNUMAResource PreFilter skip: all requests zero (plugin.go:225-231) */
 #define KG_POD_NUMA_CPU_BIND 0x20u /* the pod asks for cpuset binding (LSE/LSR prod, plugin.go:232-262): unsupported */
+#define KG_POD_NON_PREEMPTIBLE 0x40u /* ElasticQuota: extension.IsPodNonPreemptible (min gate) */
 #define KG_POD_VALID 0x80000000u
 
 typedef struct kg_pod_row {
@@ -302,9 +356,14 @@ typedef struct kg_pod_row {
     int64_t la_estimate[2];             /* EstimatePod(pod)[cpu], [memory] */
     uint32_t request_present;           /* ScalarResources key set of the Fit request */
     uint32_t flags;                     /* KG_POD_* */
-    int64_t numa_request[KG_NUM_RES];   /* PodRequestsAndLimits requests (NodeNUMAResource PreFilter) */
+    int64_t numa_request[KG_NUM_RES];   /* PodRequestsAndLimits requests (NodeNUMAResource PreFilter,
+                                           Reservation podRequests, ElasticQuota podRequest) */
     uint32_t numa_request_present;      /* key set of those requests */
     uint32_t _pad;
+    int32_t rsv_owner_class;            /* kg_pod_spec.rsv_owner_class */
+    int32_t rsv_affinity_class;         /* kg_pod_spec.rsv_affinity_class */
+    int32_t quota;                      /* kg_pod_spec.quota */
+    int32_t _pad2;
 } kg_pod_row;
 
 #define KG_NODE_VALID 0x1u
@@ -362,6 +421,7 @@ typedef struct kg_eval_out {
     int32_t out_on_device;
     int32_t _pad;
     uint8_t *numa_scores;    /* [P][64·W] NodeNUMAResource score (KG_PLUGIN_NUMA only; may be NULL) */
+    uint8_t *rsv_scores;     /* [P][64·W] Reservation score after NormalizeScore (KG_PLUGIN_RESERVATION; may be NULL) */
 } kg_eval_out;
 
 int32_t kg_abi_version(void);
@@ -369,7 +429,8 @@ int32_t kg_abi_version(void);
 enum kg_struct_id {
     KG_SID_RESOURCE_LIST = 0, KG_SID_CONFIG, KG_SID_CONTAINER, KG_SID_POD_SPEC,
     KG_SID_AGGREGATED_USAGE, KG_SID_POD_METRIC, KG_SID_ASSIGNED_POD, KG_SID_NODE_SPEC,
-    KG_SID_CLUSTER_VIEW, KG_SID_POD_ROW, KG_SID_NODE_ROW, KG_SID_EVAL_OUT, KG_SID_NUMA_SPEC, KG_SID_COUNT
+    KG_SID_CLUSTER_VIEW, KG_SID_POD_ROW, KG_SID_NODE_ROW, KG_SID_EVAL_OUT, KG_SID_NUMA_SPEC,
+    KG_SID_RESERVATION, KG_SID_QUOTA, KG_SID_COUNT
 };
 int64_t kg_struct_size(int32_t sid);
 
@@ -394,6 +455,16 @@ kg_status kg_row_commit(const kg_config *cfg, kg_node_row *node, const kg_pod_ro
  * Scores are the plugin scores (0..100) of the enabled plugins, 0 otherwise. */
 kg_status kg_row_eval(const kg_config *cfg, const kg_node_row *node, const kg_pod_row *pod, int64_t now_ns,
                       int32_t *feasible, int32_t *fit_score, int32_t *la_score, int32_t *numa_score);
+
+/* Reservation-aware Filter + Score of one (pod, node) pair on host rows through the kernels' per-pair
+ * code (kg_rsv_pair): the node's reservation slots `rsv` (≤ KG_MAX_RSV_PER_NODE, in cache order) are
+ * restored for the pod (transformer.go:49-291), Fit / LoadAware / Reservation.Filter run on the
+ * restored NodeInfo, and *rsv_raw / *order / *nominated are the pod's PreScore inputs for this node
+ * (scoreReservation of the nominated reservation, its order label, its slot; −1 none).  The
+ * preferred-node override and NormalizeScore are per-pod reductions over nodes (not per pair). */
+kg_status kg_row_eval_rsv(const kg_config *cfg, const kg_node_row *node, const kg_reservation *rsv, int32_t n_rsv,
+                          const kg_pod_row *pod, int64_t now_ns, int32_t *feasible, int32_t *fit_score,
+                          int32_t *la_score, int32_t *rsv_raw, int64_t *order, int32_t *nominated);
 
 /* Engine lifecycle. */
 kg_status kg_engine_create(const kg_config *cfg, kg_engine **out);
@@ -431,6 +502,17 @@ int32_t kg_num_tiles(const kg_engine *eng);
 kg_status kg_place_chunk_eval(kg_engine *eng, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev);
 kg_status kg_place_chunk_resolve(kg_engine *eng, int64_t now_ns, int32_t pod_begin, int32_t n,
                                  const uint32_t *partial_dev, int32_t *out_node_dev, int64_t *out_score_dev);
+
+/* Reservation cache (KG_PLUGIN_RESERVATION): replaces every reservation slot; a node holds at most
+ * KG_MAX_RSV_PER_NODE.  Nodes carrying slots are evaluated on the exact per-pair path with the
+ * restore of transformer.go:49-291.  Matrix mode with reservations needs the unsharded engine.
+ * kg_rsv_download returns the slots (allocated / n_assigned after placements) in kg_rsv_set order. */
+#define KG_MAX_RSV_PER_NODE 4
+kg_status kg_rsv_set(kg_engine *eng, const kg_reservation *rsv, int32_t n);
+kg_status kg_rsv_download(kg_engine *eng, kg_reservation *out, int32_t n);
+/* ElasticQuota groups (KG_PLUGIN_ELASTICQUOTA); kg_pod_row.quota indexes them. */
+kg_status kg_quota_set(kg_engine *eng, const kg_quota *q, int32_t n);
+kg_status kg_quota_download(kg_engine *eng, kg_quota *out, int32_t n);
 
 /* Single Reserve on the device snapshot (pod = index in the uploaded batch). */
 kg_status kg_commit(kg_engine *eng, int32_t pod, int32_t node);

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 NUM_RES = 8
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
  RES_EXTENDED) = range(8)
@@ -25,12 +25,15 @@ KUBE_QOS_UNSET, KUBE_QOS_GUARANTEED, KUBE_QOS_BURSTABLE, KUBE_QOS_BESTEFFORT = r
 AGG_UNSET, AGG_AVG, AGG_P50, AGG_P90, AGG_P95, AGG_P99 = range(6)
 NUM_AGG_TYPES = 6
 STRATEGY_LEAST_ALLOCATED, STRATEGY_MOST_ALLOCATED = 0, 1
-PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA = 0x1, 0x2, 0x4
+PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_RESERVATION, PLUGIN_ELASTICQUOTA = 0x1, 0x2, 0x4, 0x8, 0x10
+RSV_POLICY_DEFAULT, RSV_POLICY_ALIGNED, RSV_POLICY_RESTRICTED = range(3)
+RSV_AVAILABLE, RSV_UNSCHEDULABLE, RSV_ALLOCATE_ONCE = 0x1, 0x2, 0x4
+MAX_RSV_PER_NODE = 4
 NUMA_NONE, NUMA_BEST_EFFORT, NUMA_RESTRICTED, NUMA_SINGLE_NUMA_NODE = range(4)
 MAX_ZONES = 8
 
 POD_HAS_REQUEST, POD_DAEMONSET, POD_PROD, POD_LA_PROD_SCORE, POD_VALID = 0x1, 0x2, 0x4, 0x8, 0x80000000
-POD_NUMA_SKIP, POD_NUMA_CPU_BIND = 0x10, 0x20
+POD_NUMA_SKIP, POD_NUMA_CPU_BIND, POD_NON_PREEMPTIBLE = 0x10, 0x20, 0x40
 NODE_VALID, NODE_HAS_METRIC, NODE_HAS_UPDATE_TIME, NODE_LA_PASS_NONPROD, NODE_LA_PASS_PROD = 0x1, 0x2, 0x4, 0x8, 0x10
 NODE_NUMA_OPTIONS, NODE_NUMA_TOPO_VALID = 0x40, 0x80
 
@@ -51,6 +54,7 @@ CONFIG = np.dtype([
     ("weight_numa", "<i4"), ("numa_strategy", "<i4"), ("numa_hint_strategy", "<i4"), ("_pad1", "<i4"),
     ("numa_resource_weight", "<i8", (NUM_RES,)),
     ("device", "<i4"), ("place_chunk", "<i4"),
+    ("weight_reservation", "<i4"), ("eq_check_parent_quota", "<i4"),
 ], align=True)
 
 CONTAINER = np.dtype([("requests", RESOURCE_LIST), ("limits", RESOURCE_LIST)], align=True)
@@ -60,6 +64,7 @@ POD_SPEC = np.dtype([
     ("overhead", RESOURCE_LIST), ("has_priority", "<i4"), ("priority", "<i4"), ("label_priority_class", "<i4"),
     ("label_qos", "<i4"), ("status_qos", "<i4"), ("is_daemonset", "<i4"), ("is_terminated", "<i4"), ("_pad", "<i4"),
     ("name_id", "<i8"),
+    ("rsv_owner_class", "<i4"), ("rsv_affinity_class", "<i4"), ("quota", "<i4"), ("non_preemptible", "<i4"),
 ], align=True)
 
 AGGREGATED_USAGE = np.dtype([("duration_ns", "<i8"), ("usage", RESOURCE_LIST, (NUM_AGG_TYPES,))], align=True)
@@ -89,6 +94,7 @@ POD_ROW = np.dtype([
     ("request", "<i8", (NUM_RES,)), ("fit_score_request", "<i8", (NUM_RES,)), ("nonzero_request", "<i8", (2,)),
     ("la_estimate", "<i8", (2,)), ("request_present", "<u4"), ("flags", "<u4"),
     ("numa_request", "<i8", (NUM_RES,)), ("numa_request_present", "<u4"), ("_pad", "<u4"),
+    ("rsv_owner_class", "<i4"), ("rsv_affinity_class", "<i4"), ("quota", "<i4"), ("_pad2", "<i4"),
 ], align=True)
 
 NODE_ROW = np.dtype([
@@ -100,8 +106,18 @@ NODE_ROW = np.dtype([
     ("zone_keys", "<u4"), ("zone_alloc_keys", "<u4"), ("cpu_amplification_ratio", "<f8"),
 ], align=True)
 
+RESERVATION = np.dtype([
+    ("node", "<i4"), ("flags", "<u4"), ("policy", "<i4"), ("n_assigned", "<i4"), ("owner_classes", "<u4"),
+    ("affinity_classes", "<u4"), ("order", "<i8"), ("allocatable", RESOURCE_LIST), ("allocated", RESOURCE_LIST),
+], align=True)
+
+QUOTA = np.dtype([
+    ("used_limit", RESOURCE_LIST), ("used", RESOURCE_LIST), ("min", RESOURCE_LIST),
+    ("non_preemptible_used", RESOURCE_LIST),
+], align=True)
+
 STRUCT_IDS = [RESOURCE_LIST, CONFIG, CONTAINER, POD_SPEC, AGGREGATED_USAGE, POD_METRIC, ASSIGNED_POD, NODE_SPEC,
-              None, POD_ROW, NODE_ROW, None, NUMA_SPEC]
+              None, POD_ROW, NODE_ROW, None, NUMA_SPEC, RESERVATION, QUOTA]
 
 
 class ClusterView(ctypes.Structure):
@@ -113,12 +129,15 @@ class ClusterView(ctypes.Structure):
         ("pod_metrics", ctypes.c_void_p), ("n_pod_metrics", ctypes.c_int32), ("_p4", ctypes.c_int32),
         ("assigned", ctypes.c_void_p), ("n_assigned", ctypes.c_int32), ("_p5", ctypes.c_int32),
         ("numa", ctypes.c_void_p), ("n_numa", ctypes.c_int32), ("_p6", ctypes.c_int32),
+        ("reservations", ctypes.c_void_p), ("n_reservations", ctypes.c_int32), ("_p7", ctypes.c_int32),
+        ("quotas", ctypes.c_void_p), ("n_quotas", ctypes.c_int32), ("_p8", ctypes.c_int32),
     ]
 
 
 class EvalOut(ctypes.Structure):
     _fields_ = [("mask", ctypes.c_void_p), ("scores", ctypes.c_void_p), ("top1", ctypes.c_void_p),
-                ("out_on_device", ctypes.c_int32), ("_pad", ctypes.c_int32), ("numa_scores", ctypes.c_void_p)]
+                ("out_on_device", ctypes.c_int32), ("_pad", ctypes.c_int32), ("numa_scores", ctypes.c_void_p),
+                ("rsv_scores", ctypes.c_void_p)]
 
 
 def ptr(a) -> ctypes.c_void_p:
@@ -129,18 +148,24 @@ def ptr(a) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
 
 
-def make_view(pods, containers, nodes, aggregated, pod_metrics, assigned, numa=None) -> ClusterView:
+def make_view(pods, containers, nodes, aggregated, pod_metrics, assigned, numa=None, reservations=None,
+              quotas=None) -> ClusterView:
     if numa is None:
         numa = np.zeros(0, dtype=NUMA_SPEC)
+    if reservations is None:
+        reservations = np.zeros(0, dtype=RESERVATION)
+    if quotas is None:
+        quotas = np.zeros(0, dtype=QUOTA)
     v = ClusterView()
     for name, arr in (("pods", pods), ("containers", containers), ("nodes", nodes), ("aggregated", aggregated),
-                      ("pod_metrics", pod_metrics), ("assigned", assigned), ("numa", numa)):
+                      ("pod_metrics", pod_metrics), ("assigned", assigned), ("numa", numa),
+                      ("reservations", reservations), ("quotas", quotas)):
         assert arr.flags["C_CONTIGUOUS"]
         setattr(v, name, arr.ctypes.data if len(arr) else 0)
     v.n_pods, v.n_containers, v.n_nodes = len(pods), len(containers), len(nodes)
     v.n_aggregated, v.n_pod_metrics, v.n_assigned = len(aggregated), len(pod_metrics), len(assigned)
-    v.n_numa = len(numa)
-    v._keep = (pods, containers, nodes, aggregated, pod_metrics, assigned, numa)
+    v.n_numa, v.n_reservations, v.n_quotas = len(numa), len(reservations), len(quotas)
+    v._keep = (pods, containers, nodes, aggregated, pod_metrics, assigned, numa, reservations, quotas)
     return v
 
 
@@ -150,6 +175,7 @@ EXPORTED = [
     "kg_last_error", "kg_set_stream", "kg_sync", "kg_snapshot_reset", "kg_snapshot_upsert", "kg_snapshot_remove",
     "kg_snapshot_download", "kg_set_shard", "kg_pods_set", "kg_eval", "kg_place", "kg_num_tiles",
     "kg_place_chunk_eval", "kg_place_chunk_resolve", "kg_commit", "kg_set_profiling", "kg_eval_kernel_times",
+    "kg_rsv_set", "kg_rsv_download", "kg_quota_set", "kg_quota_download", "kg_row_eval_rsv",
 ]
 
 _lib = None
@@ -182,6 +208,9 @@ def lib() -> ctypes.CDLL:
         "kg_place_chunk_resolve": (i32, [vp, i64, i32, i32, vp, vp, vp]),
         "kg_commit": (i32, [vp, i32, i32]),
         "kg_set_profiling": (i32, [vp, i32]), "kg_eval_kernel_times": (i32, [vp, vp, i32]),
+        "kg_rsv_set": (i32, [vp, vp, i32]), "kg_rsv_download": (i32, [vp, vp, i32]),
+        "kg_quota_set": (i32, [vp, vp, i32]), "kg_quota_download": (i32, [vp, vp, i32]),
+        "kg_row_eval_rsv": (i32, [vp, vp, vp, i32, vp, i64, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

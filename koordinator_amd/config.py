@@ -40,13 +40,14 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
                 aggregated: Optional[dict] = None,
                 weight_numa: int = 1, numa_strategy: str = "LeastAllocated",
                 numa_hint_strategy: str = "LeastAllocated", numa_resources: Optional[Dict[str, int]] = None,
-                device: int = 0, place_chunk: int = 64) -> np.ndarray:
+                weight_reservation: int = 1, device: int = 0, place_chunk: int = 64) -> np.ndarray:
     c = np.zeros((), dtype=nat.CONFIG)
     c["abi_version"] = nat.ABI_VERSION
     bits = 0
     for p in plugins:
         bits |= {"NodeResourcesFit": nat.PLUGIN_FIT, "LoadAwareScheduling": nat.PLUGIN_LOADAWARE,
-                 "NodeNUMAResource": nat.PLUGIN_NUMA}[p]
+                 "NodeNUMAResource": nat.PLUGIN_NUMA, "Reservation": nat.PLUGIN_RESERVATION,
+                 "ElasticQuota": nat.PLUGIN_ELASTICQUOTA}[p]
     c["enabled_plugins"] = bits
     c["weight_fit"] = weight_fit
     c["weight_loadaware"] = weight_loadaware
@@ -82,6 +83,7 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
     c["numa_hint_strategy"] = strategies[numa_hint_strategy]
     for k, w in (numa_resources or {"cpu": 1, "memory": 1}).items():
         c["numa_resource_weight"][RES[k]] = w
+    c["weight_reservation"] = weight_reservation  # profile weight (the shipped profile: 5000)
     c["device"] = device
     c["place_chunk"] = place_chunk
     return c
@@ -90,6 +92,6 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
 def shipped_profile(**kw) -> np.ndarray:
     """config/manager/scheduler-config.yaml:17-45 (Fit scores batch resources too)."""
     base = dict(fit_resources={"cpu": 1, "memory": 1, "kubernetes.io/batch-cpu": 1, "kubernetes.io/batch-memory": 1},
-                filter_expired_node_metrics=False, node_metric_expiration_seconds=300)
+                filter_expired_node_metrics=False, node_metric_expiration_seconds=300, weight_reservation=5000)
     base.update(kw)
     return make_config(**base)

@@ -47,6 +47,11 @@
 #define KGD_HAS_UPDATE 0x80u
 #define KGD_LA_PASS_NP 0x100u
 #define KGD_LA_PASS_P 0x200u
+#define KGD_RSV 0x400u              // carries reservation slots: only the exact Reservation path evaluates it
+
+// engine-internal pod flag: Reservation is enabled and the pod has a required reservation affinity,
+// so every node without a matching reservation fails Reservation.Filter (plugin.go:354-357)
+#define KGP_RSV_REQUIRED 0x40000000u
 
 // per-pod derived data the kernels read (uniform → scalar loads)
 struct kg_pod_dev {
@@ -66,6 +71,9 @@ struct kg_pod_dev {
     int64_t la_est_i[2];
     int64_t numa_req[KG_NUM_RES];// NodeNUMAResource PreFilter requests (PodRequestsAndLimits)
     uint32_t numa_present;       // their key set
+    int32_t rsv_owner;           // Reservation owner class (−1 none)
+    int32_t rsv_aff;             // required reservation-affinity class (−1 none)
+    int32_t quota;               // ElasticQuota group (−1 none)
     uint32_t _pad2;
 };
 
@@ -87,6 +95,8 @@ struct kg_consts {
     int32_t numa_most;           // ScoringStrategy MostAllocated
     int32_t numa_hint_most;      // NUMAScoringStrategy MostAllocated
     int32_t numa_w[KG_NUM_RES];  // ScoringStrategy.Resources weights
+    int32_t weight_rsv;          // Reservation profile weight
+    int32_t _pad;
 };
 
 #define KG_NEUTRAL_REQ INT64_MIN  // request that passes every Fit compare
@@ -159,6 +169,7 @@ struct kg_planes {
     uint32_t *dflags;    // [cap]
     uint32_t *fit_mask;  // [cap] resources the node contributes to the Fit score
     int64_t cap;
+    int32_t *rsv_of;     // [cap] index of the node in the reservation node list, −1 none (nullptr: no list)
 };
 
 KG_HD int64_t kg_abs64(int64_t x) { return x < 0 ? -x : x; }
@@ -220,6 +231,7 @@ KG_HD void kg_finalize_node(const kg_consts &c, const kg_planes &pl, int64_t i) 
         pl.la_F[(1 * 2 + r) * cap + i] = F1;
     }
     if (slow) df |= KGD_SLOW;
+    if (pl.rsv_of && pl.rsv_of[i] >= 0) df = (df & ~(KGD_VALID | KGD_SLOW)) | KGD_RSV;  // kg_rsv_pair owns it
     if (row.flags & KG_NODE_HAS_METRIC) df |= KGD_HAS_METRIC;
     if (row.flags & KG_NODE_HAS_UPDATE_TIME) df |= KGD_HAS_UPDATE;
     if (row.flags & KG_NODE_LA_PASS_NONPROD) df |= KGD_LA_PASS_NP;
@@ -588,17 +600,19 @@ KG_HD void kg_numa_commit(const kg_consts &c, kg_node_row &row, const kg_pod_dev
     }
 }
 
-// Exact int64 evaluation of one (pod, node) pair straight from the canonical row (slow path).
-KG_HD void kg_pair_exact(const kg_consts &c, const kg_node_row &row, uint32_t df, const kg_pod_dev &p,
-                         int64_t now_ns, bool &feasible, uint32_t &fit, uint32_t &la) {
+// Exact int64 evaluation of one (pod, node) pair from the canonical row with NodeInfo's Requested /
+// NonZeroRequested / pod count given separately (the row's own, or the Reservation restore's view).
+KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_t *requested, const int64_t *nonzero,
+                        int64_t pod_count, uint32_t df, const kg_pod_dev &p, int64_t now_ns, bool &feasible,
+                        uint32_t &fit, uint32_t &la) {
     bool expired = kg_metric_expired(c, df, row.metric_update_ns, now_ns);
-    bool ok = (df & KGD_VALID) != 0;
+    bool ok = (row.flags & KG_NODE_VALID) != 0;
     if (c.plugins & KG_PLUGIN_FIT) {
-        if (df & KGD_PODS_FULL) ok = false;
+        if (pod_count + 1 > (int64_t)row.allowed_pods) ok = false;
         if (p.flags & KG_POD_HAS_REQUEST) {
             for (int r = 0; r < KG_NUM_RES; r++) {
                 bool chk = r < 3 || ((p.request_present >> r) & 1u);
-                if (chk && p.req[r] > row.alloc[r] - row.requested[r]) ok = false;
+                if (chk && p.req[r] > row.alloc[r] - requested[r]) ok = false;
             }
         }
     }
@@ -615,7 +629,7 @@ KG_HD void kg_pair_exact(const kg_consts &c, const kg_node_row &row, uint32_t df
             bool present = r < 3 || ((row.alloc_present >> r) & 1u);
             int64_t a = row.alloc[r];
             if (!present || a == 0) continue;
-            int64_t base = r < 2 ? row.nonzero_requested[r] : row.requested[r];
+            int64_t base = r < 2 ? nonzero[r] : requested[r];
             int64_t req = base + p.fit_pr_i[r];
             int64_t q;
             if (c.fit_most) q = (req > a ? a : req) * 100 / a;
@@ -637,4 +651,241 @@ KG_HD void kg_pair_exact(const kg_consts &c, const kg_node_row &row, uint32_t df
         }
         la = c.la_wsum ? (uint32_t)(s / c.la_wsum) : 0;
     }
+}
+
+// Exact int64 evaluation of one (pod, node) pair straight from the canonical row (slow path).
+KG_HD void kg_pair_exact(const kg_consts &c, const kg_node_row &row, uint32_t df, const kg_pod_dev &p,
+                         int64_t now_ns, bool &feasible, uint32_t &fit, uint32_t &la) {
+    kg_pair_view(c, row, row.requested, row.nonzero_requested, row.pod_count, df, p, now_ns, feasible, fit, la);
+}
+
+// ---- Reservation on engine rows ------------------------------------------------------------
+// Restates reservation/{transformer.go:49-346 (restore), plugin.go:311-476 (Filter, fitsNode),
+// scoring.go:42-203 (PreScore order preference, scoreReservation), nominator.go:76-135} and
+// ReservationInfo.AddAssignedPod (reservation_info.go:379-388) per (pod, node) — the oracle's
+// rsv_* functions.  A node's slots are walked in kg_rsv_set order (the reservation cache walks a Go
+// map, cache.go:256).  Pod requests are PodRequestsAndLimits (kg_pod_dev.numa_req / numa_present).
+#define KG_MIB200 (200LL * 1024 * 1024)
+
+KG_HD int64_t kg_rl_get(const kg_resource_list &l, int r) { return ((l.present >> r) & 1u) ? l.v[r] : 0; }
+
+struct kg_rsv_view {
+    bool has_state;                        // nodeReservationStates[node] exists
+    int32_t n_matched;
+    int32_t matched[KG_MAX_RSV_PER_NODE];  // slot indices of the node
+    int64_t requested[KG_NUM_RES];         // NodeInfo.Requested after the restore
+    int64_t nonzero[2];                    // NodeInfo.NonZeroRequested after the restore
+    int64_t pod_count;                     // len(NodeInfo.Pods) after the restore
+    int64_t pod_requested[KG_NUM_RES];     // nodeRState.podRequested
+    int64_t r_allocated[KG_NUM_RES];       // nodeRState.rAllocated
+};
+
+// updateNodeInfoRequested / NodeInfo.RemovePod of a pod requesting `l` (calculateResource with
+// GetNonzeroRequests' 100m / 200Mi defaults for absent cpu / memory keys)
+KG_HD void kg_rsv_update(kg_rsv_view &v, const kg_resource_list &l, int64_t sign) {
+    for (int r = 0; r < KG_NUM_RES; r++) v.requested[r] += sign * kg_rl_get(l, r);
+    v.nonzero[0] += sign * ((l.present & 1u) ? l.v[0] : 100);
+    v.nonzero[1] += sign * ((l.present & 2u) ? l.v[1] : KG_MIB200);
+}
+KG_HD bool kg_rsv_usable(const kg_reservation &r) {
+    return (r.flags & KG_RSV_AVAILABLE) && !((r.flags & KG_RSV_ALLOCATE_ONCE) && r.n_assigned > 0);
+}
+KG_HD bool kg_rsv_match(const kg_pod_dev &p, const kg_reservation &r) {
+    if (p.rsv_owner < 0 || p.rsv_owner > 31 || !((r.owner_classes >> p.rsv_owner) & 1u)) return false;
+    if (p.rsv_aff >= 0 && (p.rsv_aff > 31 || !((r.affinity_classes >> p.rsv_aff) & 1u))) return false;
+    return true;
+}
+// quotav1.SubtractWithNonNegativeResult(a, b)[q]
+KG_HD int64_t kg_rsv_remained(const kg_reservation &r, int q) {
+    int64_t x = kg_rl_get(r.allocatable, q) - kg_rl_get(r.allocated, q);
+    return x > 0 ? x : 0;
+}
+
+KG_HD void kg_rsv_restore(const kg_node_row &row, const kg_reservation *rs, int nr, const kg_pod_dev &p, kg_rsv_view &v) {
+    v.has_state = false;
+    v.n_matched = 0;
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        v.requested[r] = row.requested[r];
+        v.pod_requested[r] = row.requested[r];
+        v.r_allocated[r] = 0;
+    }
+    v.nonzero[0] = row.nonzero_requested[0];
+    v.nonzero[1] = row.nonzero_requested[1];
+    v.pod_count = row.pod_count;
+    int32_t unm[KG_MAX_RSV_PER_NODE];
+    int nu = 0;
+    for (int i = 0; i < nr; i++) {
+        const kg_reservation &r = rs[i];
+        if (!kg_rsv_usable(r)) continue;
+        if (!(r.flags & KG_RSV_UNSCHEDULABLE) && kg_rsv_match(p, r)) v.matched[v.n_matched++] = i;
+        else if (r.n_assigned > 0) unm[nu++] = i;
+    }
+    if (v.n_matched == 0 && nu == 0) return;
+    if (p.rsv_aff >= 0 && v.n_matched == 0) return;  // the affinity needs a match: node left alone
+    v.has_state = true;
+    for (int k = 0; k < nu; k++) {  // restoreUnmatchedReservations
+        const kg_reservation &r = rs[unm[k]];
+        kg_rsv_update(v, r.allocatable, -1);
+        kg_resource_list rem;
+        rem.present = r.allocatable.present | r.allocated.present;
+        rem._pad = 0;
+        bool zero = true;
+        for (int q = 0; q < KG_NUM_RES; q++) {
+            rem.v[q] = ((rem.present >> q) & 1u) ? kg_rsv_remained(r, q) : 0;
+            if (rem.v[q] != 0) zero = false;
+        }
+        if (!zero) kg_rsv_update(v, rem, +1);
+    }
+    for (int q = 0; q < KG_NUM_RES; q++) v.pod_requested[q] = v.requested[q];
+    for (int k = 0; k < v.n_matched; k++) {  // restoreMatchedReservation → RemovePod(reserve pod)
+        const kg_reservation &r = rs[v.matched[k]];
+        kg_rsv_update(v, r.allocatable, -1);
+        v.pod_count -= 1;
+        for (int q = 0; q < KG_NUM_RES; q++) v.r_allocated[q] += kg_rl_get(r.allocated, q);
+    }
+}
+
+// fitsNode(podRequests, nodeInfo, nodeRState, rInfo, preemptible = nil) (plugin.go:427-476)
+KG_HD bool kg_rsv_fits_node(const kg_node_row &row, const kg_rsv_view &v, const kg_reservation &r, const kg_pod_dev &p) {
+    if (v.pod_count - v.n_matched + 1 > (int64_t)row.allowed_pods) return false;
+    const uint32_t scal = p.numa_present & KG_SCALAR_RES_MASK;
+    if (p.numa_req[0] == 0 && p.numa_req[1] == 0 && p.numa_req[2] == 0 && scal == 0) return true;
+    for (int q = 0; q < KG_NUM_RES; q++) {
+        if (q >= 3 && !((scal >> q) & 1u)) continue;
+        const int64_t free_q = row.alloc[q] - (v.pod_requested[q] - kg_rsv_remained(r, q) - v.r_allocated[q]);
+        if (p.numa_req[q] > free_q) return false;
+    }
+    return true;
+}
+
+// filterWithReservations over the slots `list` (plugin.go:377-425)
+KG_HD bool kg_rsv_filter_with(const kg_node_row &row, const kg_rsv_view &v, const kg_reservation *rs,
+                              const int32_t *list, int nl, bool required, const kg_pod_dev &p) {
+    bool ok = false;
+    for (int k = 0; k < nl && !ok; k++) {
+        const kg_reservation &r = rs[list[k]];
+        if ((r.allocatable.present & p.numa_present) == 0) continue;
+        const bool node_fits = kg_rsv_fits_node(row, v, r, p);
+        if (r.policy == KG_RSV_POLICY_DEFAULT || r.policy == KG_RSV_POLICY_ALIGNED) {
+            ok = node_fits;
+        } else if (r.policy == KG_RSV_POLICY_RESTRICTED) {
+            bool fits = true;  // Mask(podRequests, names) ≤ Allocatable − Mask(Allocated, names)
+            for (int q = 0; q < KG_NUM_RES; q++) {
+                if (!((r.allocatable.present >> q) & 1u) || !((p.numa_present >> q) & 1u)) continue;
+                const int64_t rem = r.allocatable.v[q] - kg_rl_get(r.allocated, q);
+                if (p.numa_req[q] > (rem > 0 ? rem : 0)) fits = false;
+            }
+            ok = fits && node_fits;
+        }
+    }
+    return ok || !required;
+}
+
+// findMostPreferredReservationByOrder (scoring.go:162-181): position in `list` or −1; *order
+KG_HD int kg_rsv_most_preferred(const kg_reservation *rs, const int32_t *list, int nl, int64_t &order) {
+    order = INT64_MAX;
+    int hi = -1;
+    for (int k = 0; k < nl; k++) {
+        const int64_t o = rs[list[k]].order;
+        if (o != 0 && order > o) {
+            order = o;
+            hi = k;
+        }
+    }
+    return hi;
+}
+
+// scoreReservation (scoring.go:183-203): MostAllocated over RemoveZeros(Allocatable) in MilliValue
+KG_HD uint32_t kg_rsv_score(const kg_reservation &r, const kg_pod_dev &p) {
+    int64_t w = 0, s = 0;
+    for (int q = 0; q < KG_NUM_RES; q++) {
+        if (!((r.allocatable.present >> q) & 1u) || r.allocatable.v[q] == 0) continue;
+        w++;
+        const int64_t cap = r.allocatable.v[q];
+        const int64_t req = (((p.numa_present >> q) & 1u) ? p.numa_req[q] : 0) + kg_rl_get(r.allocated, q);
+        const int64_t m = q == KG_RES_CPU ? 1 : 1000;  // Quantity.MilliValue of the stored unit
+        if (req <= cap) s += 100 * (req * m) / (cap * m);
+    }
+    return w <= 0 ? 0u : (uint32_t)(s / w);
+}
+
+// NominateReservation (nominator.go:76-135): slot index or −1
+KG_HD int kg_rsv_nominate(const kg_node_row &row, const kg_rsv_view &v, const kg_reservation *rs, const kg_pod_dev &p) {
+    int32_t cand[KG_MAX_RSV_PER_NODE];
+    int nc = 0;
+    for (int k = 0; k < v.n_matched; k++)
+        if (kg_rsv_filter_with(row, v, rs, &v.matched[k], 1, true, p)) cand[nc++] = v.matched[k];
+    if (nc == 0) return -1;
+    int64_t order;
+    const int hi = kg_rsv_most_preferred(rs, cand, nc, order);
+    if (hi >= 0) return cand[hi];
+    int best = cand[0];  // sort.Slice by score descending: insertion sort (≤ 12 items) keeps the first
+    uint32_t bs = kg_rsv_score(rs[cand[0]], p);
+    for (int k = 1; k < nc; k++) {
+        const uint32_t sc = kg_rsv_score(rs[cand[k]], p);
+        if (sc > bs) {
+            bs = sc;
+            best = cand[k];
+        }
+    }
+    return best;
+}
+
+struct kg_rsv_out {
+    bool feasible;
+    uint32_t fit, la;       // plugin scores on the restored NodeInfo
+    uint32_t raw;           // Reservation.Score before the preferred-node override and NormalizeScore
+    int64_t order;          // PreScore node order (INT64_MAX: none)
+    int32_t nominated;      // slot of the nominated reservation, −1 none
+};
+
+// Filter + Score of one (pod, node-with-reservations) pair.
+KG_HD void kg_rsv_pair(const kg_consts &c, const kg_node_row &row, uint32_t df, const kg_reservation *rs, int nr,
+                       const kg_pod_dev &p, int64_t now_ns, kg_rsv_out &o) {
+    kg_rsv_view v;
+    kg_rsv_restore(row, rs, nr, p, v);
+    bool feas;
+    kg_pair_view(c, row, v.requested, v.nonzero, v.pod_count, df, p, now_ns, feas, o.fit, o.la);
+    if (v.n_matched == 0) feas = feas && p.rsv_aff < 0;  // Reservation.Filter (plugin.go:351-369)
+    else feas = feas && kg_rsv_filter_with(row, v, rs, v.matched, v.n_matched, p.rsv_aff >= 0, p);
+    o.feasible = feas;
+    o.raw = 0;
+    o.order = INT64_MAX;
+    o.nominated = -1;
+    if (feas && v.n_matched > 0) {
+        kg_rsv_most_preferred(rs, v.matched, v.n_matched, o.order);
+        o.nominated = kg_rsv_nominate(row, v, rs, p);
+        if (o.nominated >= 0) o.raw = kg_rsv_score(rs[o.nominated], p);
+    }
+}
+
+// Reservation.Reserve → ReservationInfo.AddAssignedPod: Allocated += Mask(requests, ResourceNames)
+KG_HD void kg_rsv_commit(kg_reservation &r, const kg_pod_dev &p) {
+    const uint32_t m = p.numa_present & r.allocatable.present;
+    for (int q = 0; q < KG_NUM_RES; q++)
+        if ((m >> q) & 1u) r.allocated.v[q] = kg_rl_get(r.allocated, q) + p.numa_req[q];
+    r.allocated.present |= m;
+    r.n_assigned += 1;
+}
+
+// ---- ElasticQuota (plugin.go:210-255 PreFilter, :323-337 Reserve) ----------------------------
+KG_HD bool kg_quota_leq(const kg_pod_dev &p, const kg_resource_list &used, const kg_resource_list &limit) {
+    for (int q = 0; q < KG_NUM_RES; q++)
+        if (((limit.present >> q) & 1u) && ((p.numa_present >> q) & 1u) && p.numa_req[q] + kg_rl_get(used, q) > limit.v[q])
+            return false;
+    return true;
+}
+KG_HD bool kg_quota_pass(const kg_quota &q, const kg_pod_dev &p) {
+    if (!kg_quota_leq(p, q.used, q.used_limit)) return false;
+    if ((p.flags & KG_POD_NON_PREEMPTIBLE) && !kg_quota_leq(p, q.non_preemptible_used, q.min)) return false;
+    return true;
+}
+KG_HD void kg_rl_add_pod(kg_resource_list &l, const kg_pod_dev &p) {
+    for (int q = 0; q < KG_NUM_RES; q++)
+        if ((p.numa_present >> q) & 1u) l.v[q] = kg_rl_get(l, q) + p.numa_req[q];
+    l.present |= p.numa_present;
+}
+KG_HD void kg_quota_commit(kg_quota &q, const kg_pod_dev &p) {
+    kg_rl_add_pod(q.used, p);
+    if (p.flags & KG_POD_NON_PREEMPTIBLE) kg_rl_add_pod(q.non_preemptible_used, p);
 }

@@ -26,6 +26,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <string>
 #include <vector>
@@ -872,24 +873,236 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
     return ((unsigned long long)(total_of(c, fit, la, numa) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
 }
 
+// ---------------------------------------------------------------------------------------
+// Reservation + ElasticQuota (BASELINE config 5)
+// ---------------------------------------------------------------------------------------
+// Nodes carrying reservation slots (KGD_RSV) are dropped by every fast path (their derived VALID bit
+// is cleared) and evaluated here, pair by pair, with kg_rsv_pair on the canonical row: the restore of
+// transformer.go:49-291 depends on the pod's owner class, so these pairs have no pod-independent
+// planes.  One entry per (pod, reservation node):
+//   E = feasible ? (base + 1) << 32 | raw << 16 | (nominated + 1) : 0     base = Σ weight·score
+//   O = PreScore order of the node (INT64_MAX: none or infeasible)
+// The per-pod PreScore preferred node, Score override (1000) and DefaultNormalizeScore max
+// are block reductions over the pod's entries (rsv_best_block).
+struct RsvArgs {
+    kg_reservation *rsv;        // slots, grouped by node (nullptr: Reservation off)
+    const int32_t *rfirst;      // [n_rn + 1] first slot of each reservation node
+    const int32_t *rnode;       // [n_rn] node of each reservation node (ascending)
+    int32_t n_rn;
+    int32_t _pad;
+    unsigned long long *E;      // [pods][n_rn]
+    int64_t *O;                 // [pods][n_rn]
+    kg_quota *quota;            // ElasticQuota groups (nullptr: ElasticQuota off)
+};
+
+__device__ __forceinline__ void rsv_entry(const kg_consts &c, const kg_planes &pl, const RsvArgs &ra,
+                                          const kg_pod_dev &p, int32_t k, int64_t now_ns, kg_rsv_out *keep,
+                                          unsigned long long &e, int64_t &o) {
+    const int32_t node = ra.rnode[k];
+    kg_rsv_out r;
+    kg_rsv_pair(c, pl.rows[node], pl.dflags[node], ra.rsv + ra.rfirst[k], ra.rfirst[k + 1] - ra.rfirst[k], p, now_ns, r);
+    const uint32_t base = total_of(c, r.fit, r.la);
+    e = r.feasible ? ((unsigned long long)(base + 1u) << 32) | ((unsigned long long)r.raw << 16) |
+                         (unsigned long long)(uint32_t)(r.nominated + 1)
+                   : 0ull;
+    o = r.feasible ? r.order : INT64_MAX;
+    if (keep) *keep = r;
+}
+
+// PreScore / Score / NormalizeScore of one pod over its reservation-node entries, by a whole
+// workgroup of NT threads; returns the best key (total + 1) << 32 | (0xFFFFFFFF − node) (all threads).
+// `plane` (optional) receives the normalized Reservation score of columns [col_begin, col_end).
+template <int NT>
+__device__ unsigned long long rsv_best_block(const kg_consts &c, const unsigned long long *E, const int64_t *O,
+                                             const int32_t *rnode, int32_t n_rn, uint8_t *plane, int64_t col_begin,
+                                             int64_t col_end, unsigned long long *red, int64_t *redo) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    constexpr int NW = NT / 64;
+    // 1. preferred node: the smallest non-zero order among feasible nodes, lowest node on ties
+    int64_t bo = INT64_MAX;
+    int32_t bk = INT32_MAX;
+    for (int32_t k = tid; k < n_rn; k += NT) {
+        const int64_t o = O[k];
+        if (E[k] && o != 0 && o != INT64_MAX && o < bo) {
+            bo = o;
+            bk = k;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const int64_t o2 = __shfl_xor(bo, off, 64);
+        const int32_t k2 = __shfl_xor(bk, off, 64);
+        if (o2 < bo || (o2 == bo && k2 < bk)) {
+            bo = o2;
+            bk = k2;
+        }
+    }
+    if (lane == 0) {
+        redo[wv] = bo;
+        red[wv] = (unsigned long long)(uint32_t)bk;
+    }
+    __syncthreads();
+    bo = redo[0];
+    bk = (int32_t)(uint32_t)red[0];
+    for (int w = 1; w < NW; w++) {
+        const int32_t k2 = (int32_t)(uint32_t)red[w];
+        if (redo[w] < bo || (redo[w] == bo && k2 < bk)) {
+            bo = redo[w];
+            bk = k2;
+        }
+    }
+    const int32_t pref = bo == INT64_MAX ? -1 : bk;
+    __syncthreads();
+    // 2. DefaultNormalizeScore max over feasible nodes (the preferred node scores 1000)
+    unsigned long long mx = 0;
+    for (int32_t k = tid; k < n_rn; k += NT) {
+        const unsigned long long e = E[k];
+        if (!e) continue;
+        const unsigned long long raw = k == pref ? 1000ull : ((e >> 16) & 0xFFFFull);
+        mx = mx > raw ? mx : raw;
+    }
+    mx = wave_max_u64(mx);
+    if (lane == 0) red[wv] = mx;
+    __syncthreads();
+    mx = 0;
+    for (int w = 0; w < NW; w++) mx = mx > red[w] ? mx : red[w];
+    __syncthreads();
+    // 3. totals and the best key
+    unsigned long long best = 0;
+    for (int32_t k = tid; k < n_rn; k += NT) {
+        const unsigned long long e = E[k];
+        const int64_t node = rnode[k];
+        uint32_t sn = 0;
+        if (e) {
+            const unsigned long long raw = k == pref ? 1000ull : ((e >> 16) & 0xFFFFull);
+            sn = mx ? (uint32_t)(100ull * raw / mx) : 0u;
+            const unsigned long long total = (e >> 32) - 1ull + (unsigned long long)c.weight_rsv * sn;
+            const unsigned long long key = ((total + 1ull) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
+            best = best > key ? best : key;
+        }
+        if (plane && node >= col_begin && node < col_end) plane[node - col_begin] = (uint8_t)sn;
+    }
+    best = wave_max_u64(best);
+    if (lane == 0) red[wv] = best;
+    __syncthreads();
+    best = 0;
+    for (int w = 0; w < NW; w++) best = best > red[w] ? best : red[w];
+    __syncthreads();
+    return best;
+}
+
+// entries of pods [0, P) × every reservation node; matrix mode also writes their planes
+__global__ __launch_bounds__(256) void k_rsv_eval(kg_consts c, kg_planes pl, RsvArgs ra, const kg_pod_dev *pods,
+                                                  int32_t P, int64_t now_ns, unsigned long long *mask,
+                                                  uint16_t *scores, int64_t col_begin, int64_t col_end,
+                                                  int32_t mask_words, int64_t score_stride) {
+    const int32_t k = blockIdx.x * 256 + threadIdx.x;
+    const int32_t p = blockIdx.y;
+    if (k >= ra.n_rn || p >= P) return;
+    kg_rsv_out r;
+    unsigned long long e;
+    int64_t o;
+    rsv_entry(c, pl, ra, pods[p], k, now_ns, &r, e, o);
+    ra.E[(int64_t)p * ra.n_rn + k] = e;
+    ra.O[(int64_t)p * ra.n_rn + k] = o;
+    const int64_t node = ra.rnode[k];
+    if (scores && node >= col_begin && node < col_end) {
+        const int64_t col = node - col_begin;
+        scores[(int64_t)p * score_stride + col] = (uint16_t)(r.fit | (r.la << 8));
+        if (r.feasible) atomicOr(&mask[(int64_t)p * mask_words + (col >> 6)], 1ull << (col & 63));
+    }
+}
+
+// per pod: reservation-node best merged into top1; the normalized Reservation plane
+__global__ __launch_bounds__(256) void k_rsv_reduce(kg_consts c, RsvArgs ra, int32_t P, unsigned long long *top1,
+                                                    uint8_t *plane, int64_t col_begin, int64_t col_end,
+                                                    int64_t plane_stride) {
+    __shared__ unsigned long long red[4];
+    __shared__ int64_t redo[4];
+    const int32_t p = blockIdx.x;
+    if (p >= P) return;
+    const unsigned long long best = rsv_best_block<256>(c, ra.E + (int64_t)p * ra.n_rn, ra.O + (int64_t)p * ra.n_rn,
+                                                        ra.rnode, ra.n_rn, plane ? plane + (int64_t)p * plane_stride : nullptr,
+                                                        col_begin, col_end, red, redo);
+    if (threadIdx.x == 0 && top1 && best > top1[p]) top1[p] = best;
+}
+
+// ElasticQuota PreFilter of pods [0, P) against the current quota state
+// gate[p]: ElasticQuota PreFilter; gate[P + p]: the plain (reservation-less) nodes are open to the pod
+__global__ void k_pod_gate(const kg_quota *__restrict__ quota, const kg_pod_dev *__restrict__ pods, int32_t P,
+                           uint8_t *__restrict__ gate) {
+    const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const bool q = !quota || pods[p].quota < 0 || kg_quota_pass(quota[pods[p].quota], pods[p]);
+    gate[p] = q ? 1 : 0;
+    gate[P + p] = (q && !(pods[p].flags & KGP_RSV_REQUIRED)) ? 1 : 0;
+}
+
+// pods failing the quota gate are infeasible everywhere: clear their mask rows and top1
+__global__ void k_quota_apply(const uint8_t *__restrict__ gate, int32_t P, unsigned long long *mask, int32_t mask_words,
+                              unsigned long long *top1, uint8_t *plane, int64_t plane_stride) {
+    const int32_t p = blockIdx.x;
+    if (p >= P || gate[p]) return;
+    if (mask)
+        for (int32_t w = threadIdx.x; w < mask_words; w += blockDim.x) mask[(int64_t)p * mask_words + w] = 0ull;
+    if (plane)
+        for (int64_t w = threadIdx.x; w < plane_stride; w += blockDim.x) plane[p * plane_stride + w] = 0;
+    if (top1 && threadIdx.x == 0) top1[p] = 0ull;
+}
+
+// Reserve of the Reservation (nominated slot) and ElasticQuota (used) parts on `node`.
+// Reservation.Reserve takes the nomination of PreScore, or runs NominateReservation itself when
+// scheduleOne skipped scoring (plugin.go:525-560): on a feasible node both are kg_rsv_nominate
+// over the same restored state.
+__device__ __forceinline__ void rsv_quota_commit(const kg_planes &pl, const RsvArgs &ra, const kg_pod_dev &p,
+                                                 int32_t node) {
+    if (ra.rsv && pl.rsv_of) {
+        const int32_t k = pl.rsv_of[node];
+        if (k >= 0) {
+            const kg_reservation *rs = ra.rsv + ra.rfirst[k];
+            kg_rsv_view v;
+            kg_rsv_restore(pl.rows[node], rs, ra.rfirst[k + 1] - ra.rfirst[k], p, v);
+            const int nom = kg_rsv_nominate(pl.rows[node], v, rs, p);
+            if (nom >= 0) kg_rsv_commit(ra.rsv[ra.rfirst[k] + nom], p);
+        }
+    }
+    if (ra.quota && p.quota >= 0) kg_quota_commit(ra.quota[p.quota], p);
+}
+
 // Sequential commit of pods [pod_begin, pod_begin + n) given their per-tile partial keys.
 __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_planes pl,
                                                                 const kg_pod_dev *__restrict__ pods, int32_t pod_begin,
                                                                 int32_t n, const uint32_t *partials, int32_t tiles_total,
                                                                 int64_t n_nodes, int64_t now_ns, int32_t *out_node,
-                                                                int64_t *out_score) {
+                                                                int64_t *out_score, RsvArgs ra) {
     __shared__ int32_t touched[KG_MAX_CHUNK];
     __shared__ int32_t rescan[KG_MAX_TILES];
     __shared__ unsigned long long red[KG_RESOLVE_THREADS / 64];
-    __shared__ int32_t n_touched, n_rescan;
+    __shared__ int64_t redo[KG_RESOLVE_THREADS / 64];
+    __shared__ int32_t n_touched, n_rescan, gate_ok;
+    __shared__ unsigned long long wbest;
     const int tid = threadIdx.x;
     if (tid == 0) n_touched = 0;
     for (int j = 0; j < n; j++) {
-        if (tid == 0) n_rescan = 0;
+        if (tid == 0) {
+            n_rescan = 0;
+            const kg_pod_dev &pq = pods[pod_begin + j];
+            // ElasticQuota PreFilter on the quota state after every earlier Reserve
+            gate_ok = !ra.quota || pq.quota < 0 || kg_quota_pass(ra.quota[pq.quota], pq);
+        }
         __syncthreads();
+        if (!gate_ok) {
+            if (tid == 0) {
+                out_node[j] = -1;
+                out_score[j] = -1;
+            }
+            __syncthreads();
+            continue;
+        }
         const kg_pod_dev &pd = pods[pod_begin + j];
         unsigned long long best = 0;
         const int nt = n_touched;
+        // a pod that requires a reservation can only land on reservation nodes (rsv part below)
+        const bool plain_ok = !(pd.flags & KGP_RSV_REQUIRED);
         for (int t = tid; t < tiles_total; t += KG_RESOLVE_THREADS) {
             const unsigned long long k = decode_partial(partials[(int64_t)j * tiles_total + t], t);
             if (!k) continue;
@@ -899,12 +1112,13 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             if (hit) rescan[atomicAdd(&n_rescan, 1)] = t;
             else best = best > k ? best : k;
         }
-        for (int q = tid; q < nt; q += KG_RESOLVE_THREADS) {
+        if (!plain_ok) best = 0;
+        for (int q = tid; q < nt && plain_ok; q += KG_RESOLVE_THREADS) {
             const unsigned long long k = pair_key(c, pl, pd, touched[q], n_nodes, now_ns);
             best = best > k ? best : k;
         }
         __syncthreads();
-        const int nr = n_rescan;
+        const int nr = plain_ok ? n_rescan : 0;
         for (int q = tid; q < nr * KG_TILE; q += KG_RESOLVE_THREADS) {
             const int64_t node = (int64_t)rescan[q / KG_TILE] * KG_TILE + (q % KG_TILE);
             const unsigned long long k = pair_key(c, pl, pd, node, n_nodes, now_ns);
@@ -916,8 +1130,29 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         if (tid == 0) {
             unsigned long long w = 0;
             for (int q = 0; q < KG_RESOLVE_THREADS / 64; q++) w = w > red[q] ? w : red[q];
+            wbest = w;
+        }
+        __syncthreads();
+        if (ra.rsv && ra.n_rn > 0) {
+            // nodes with reservations: refresh this pod's entries of the nodes earlier pods touched,
+            // then PreScore / Score / NormalizeScore over every reservation node
+            unsigned long long *E = ra.E + (int64_t)j * ra.n_rn;
+            int64_t *O = ra.O + (int64_t)j * ra.n_rn;
+            for (int q = tid; q < nt; q += KG_RESOLVE_THREADS) {
+                const int32_t k = pl.rsv_of[touched[q]];
+                if (k >= 0) rsv_entry(c, pl, ra, pd, k, now_ns, nullptr, E[k], O[k]);
+            }
+            __syncthreads();
+            const unsigned long long rk =
+                rsv_best_block<KG_RESOLVE_THREADS>(c, E, O, ra.rnode, ra.n_rn, nullptr, 0, 0, red, redo);
+            if (tid == 0 && rk > wbest) wbest = rk;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long w = wbest;
             if (w) {
                 const int32_t node = (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull));
+                rsv_quota_commit(pl, ra, pd, node);
                 kg_numa_commit(c, pl.rows[node], pd);
                 kg_apply_commit(pl.rows[node], pd);
                 kg_finalize_node(c, pl, node);
@@ -935,7 +1170,9 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     }
 }
 
-__global__ void k_commit_one(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t pod, int32_t node) {
+__global__ void k_commit_one(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t pod, int32_t node,
+                             RsvArgs ra) {
+    rsv_quota_commit(pl, ra, pods[pod], node);
     kg_numa_commit(c, pl.rows[node], pods[pod]);
     kg_apply_commit(pl.rows[node], pods[pod]);
     kg_finalize_node(c, pl, node);
@@ -980,6 +1217,19 @@ struct kg_engine {
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
     bool profiling = false;
+    // Reservation / ElasticQuota (config 5)
+    void *rsv_mem = nullptr;            // slots | rfirst | rnode | E | O
+    kg_reservation *rsv = nullptr;      // slots grouped by node (stable)
+    std::vector<int32_t> rsv_perm;      // device slot → caller index
+    int32_t n_rsv = 0;
+    int32_t *rfirst = nullptr, *rnode = nullptr;
+    int32_t n_rn = 0;
+    unsigned long long *rsv_e = nullptr;
+    int64_t *rsv_o = nullptr;
+    kg_quota *quota = nullptr;
+    int32_t n_quota = 0;
+    int32_t max_pod_quota = -1;         // largest quota index of the batch
+    uint8_t *gate = nullptr;            // [pods] ElasticQuota PreFilter outcome (matrix mode)
     static constexpr int kRing = 256;   // event pairs: one per profiled k_eval launch
     hipEvent_t ev0[kRing] = {}, ev1[kRing] = {};
     int64_t ev_count = 0;               // launches recorded since kg_set_profiling
@@ -1308,6 +1558,42 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     return KG_OK;
 }
 
+#define KG_RSV_POD_CHUNK 1024   // pods per reservation-entry pass (E/O hold [chunk][n_rn])
+
+RsvArgs rsv_args(const kg_engine *e) {
+    RsvArgs ra{};
+    if ((e->consts.plugins & KG_PLUGIN_RESERVATION) && e->n_rn > 0) {
+        ra.rsv = e->rsv;
+        ra.rfirst = e->rfirst;
+        ra.rnode = e->rnode;
+        ra.n_rn = e->n_rn;
+        ra.E = e->rsv_e;
+        ra.O = e->rsv_o;
+    }
+    if (e->consts.plugins & KG_PLUGIN_ELASTICQUOTA) ra.quota = e->quota;
+    return ra;
+}
+
+kg_status quota_ready(kg_engine *e) {
+    if (!(e->consts.plugins & KG_PLUGIN_ELASTICQUOTA)) return KG_OK;
+    if (e->max_pod_quota >= e->n_quota)
+        return set_err(e, KG_ERR_STATE, "pod quota index %d without a kg_quota_set group (have %d)", e->max_pod_quota,
+                       e->n_quota);
+    return KG_OK;
+}
+
+// entries of pods [pod_begin, pod_begin + n) (n ≤ KG_RSV_POD_CHUNK) for every reservation node
+kg_status rsv_eval_chunk(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
+                         int32_t mask_words, int64_t score_stride) {
+    const RsvArgs ra = rsv_args(e);
+    if (!ra.rsv || n <= 0) return KG_OK;
+    dim3 grid((unsigned)((ra.n_rn + 255) / 256), (unsigned)n);
+    hipLaunchKernelGGL(k_rsv_eval, grid, dim3(256), 0, e->stream, e->consts, e->pl, ra, e->pods + pod_begin, n, now_ns,
+                       (unsigned long long *)mask, scores, e->shard_begin, e->shard_end, mask_words, score_stride);
+    HIP_TRY(e, hipGetLastError());
+    return KG_OK;
+}
+
 kg_status check_engine(kg_engine *e) {
     if (!e) return KG_ERR_INVALID_ARG;
     HIP_TRY(e, hipSetDevice(e->device));
@@ -1355,6 +1641,9 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->hot) (void)hipFree(e->hot);
     if (e->scratch) (void)hipFree(e->scratch);
     if (e->cls_mem) (void)hipFree(e->cls_mem);
+    if (e->rsv_mem) (void)hipFree(e->rsv_mem);
+    if (e->quota) (void)hipFree(e->quota);
+    if (e->gate) (void)hipFree(e->gate);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     for (int k = 0; k < kg_engine::kRing; k++) {
         if (e->ev0[k]) (void)hipEventDestroy(e->ev0[k]);
@@ -1405,7 +1694,7 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
     size_t total = 0;
     const size_t sizes[] = {sizeof(kg_node_row) * (size_t)cap, (size_t)KG_NUM_RES * 8 * cap, (size_t)KG_NUM_RES * 8 * cap,
                             (size_t)KG_NUM_RES * 8 * cap, 2 * 8 * (size_t)cap, 4 * 8 * (size_t)cap, 8 * (size_t)cap,
-                            4 * (size_t)cap, 4 * (size_t)cap, 4 * (size_t)cap, 256};
+                            4 * (size_t)cap, 4 * (size_t)cap, 4 * (size_t)cap, 256, 4 * (size_t)cap};
     for (size_t s : sizes) total += (s + 255) / 256 * 256;
     HIP_TRY(e, hipMalloc(&e->plane_mem, total));
     HIP_TRY(e, hipMemsetAsync(e->plane_mem, 0, total, e->stream));
@@ -1421,6 +1710,16 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
     e->pl.fit_mask = (uint32_t *)carve(sizes[8]);
     e->slow_list = (int32_t *)carve(sizes[9]);
     e->slow_count = (int32_t *)carve(sizes[10]);
+    e->pl.rsv_of = (int32_t *)carve(sizes[11]);
+    HIP_TRY(e, hipMemsetAsync(e->pl.rsv_of, 0xFF, sizes[11], e->stream));  // −1: no reservations
+    if (e->rsv_mem) HIP_TRY(e, hipFree(e->rsv_mem));  // reservations refer to node indices: dropped
+    e->rsv_mem = nullptr;
+    e->rsv = nullptr;
+    e->rfirst = e->rnode = nullptr;
+    e->rsv_e = nullptr;
+    e->rsv_o = nullptr;
+    e->n_rsv = e->n_rn = 0;
+    e->rsv_perm.clear();
     e->pl.cap = cap;
     e->n_nodes = n_nodes;
     e->shard_begin = 0;
@@ -1491,6 +1790,7 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     BatchMasks bm{0, 0};
     bool la_prod = false, pow2 = true;
     uint32_t need = 0;
+    int32_t max_quota = -1;
     for (int32_t i = 0; i < n; i++) {
         if (!kg_pod_row_in_bounds(rows[i])) return set_err(e, KG_ERR_RANGE, "pod %d: request outside the engine bounds", i);
         if ((e->cfg.enabled_plugins & KG_PLUGIN_NUMA) && !(rows[i].flags & KG_POD_NUMA_SKIP)) {
@@ -1500,6 +1800,7 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
                 return set_err(e, KG_ERR_UNSUPPORTED, "pod %d: more than %d NUMA hint lists", i, KG_NUMA_MAX_LISTS);
         }
         kg_pod_dev_from_row(e->cfg, rows[i], dev[i]);
+        if ((e->cfg.enabled_plugins & KG_PLUGIN_ELASTICQUOTA) && rows[i].quota > max_quota) max_quota = rows[i].quota;
         bm.cmp |= dev[i].cmp_mask;
         bm.fit |= dev[i].fit_mask;
         la_prod |= (rows[i].flags & KG_POD_LA_PROD_SCORE) != 0;
@@ -1530,12 +1831,15 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     if (n > e->pods_cap || hot.size() > e->hot_bytes) {
         if (e->pods) HIP_TRY(e, hipFree(e->pods));
         if (e->hot) HIP_TRY(e, hipFree(e->hot));
+        if (e->gate) HIP_TRY(e, hipFree(e->gate));
         e->pods = nullptr;
         e->hot = nullptr;
+        e->gate = nullptr;
         e->pods_cap = 0;
         e->hot_bytes = 0;
         HIP_TRY(e, hipMalloc(&e->pods, sizeof(kg_pod_dev) * (size_t)(n > 0 ? n : 1)));
         HIP_TRY(e, hipMalloc(&e->hot, sizeof(kg_pod_hot_t<8>) * (size_t)(n > 0 ? n : 1)));
+        HIP_TRY(e, hipMalloc(&e->gate, 2 * (size_t)(n > 0 ? n : 1)));
         e->pods_cap = n;
         e->hot_bytes = sizeof(kg_pod_hot_t<8>) * (size_t)(n > 0 ? n : 1);
     }
@@ -1547,6 +1851,7 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     e->nslot = nslot;
     for (int s = 0; s < 8; s++) e->slot_res[s] = slot_res[s];
     e->n_pods = n;
+    e->max_pod_quota = max_quota;
     e->bm = bm;
     e->la_prod = la_prod;
     e->pow2 = pow2;
@@ -1576,8 +1881,9 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     const size_t numa_b = (size_t)P * (size_t)((width + 63) / 64 * 64);
     const bool numa_on = (e->consts.plugins & KG_PLUGIN_NUMA) != 0;
     const bool stage_numa = out->numa_scores && !dev;
+    const bool stage_rsv = out->rsv_scores && !dev;
     size_t need = up(part_b) + up(top_b) + (stage_mask ? up(mask_b) : 0) + (stage_scores ? up(score_b) : 0) +
-                  (stage_numa ? up(numa_b) : 0);
+                  (stage_numa ? up(numa_b) : 0) + (stage_rsv ? up(numa_b) : 0);
     st = ensure_scratch(e, need + 256);
     if (st) return st;
     char *s = (char *)e->scratch;
@@ -1598,21 +1904,61 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
         else numa = out->numa_scores;
         if (!numa_on && numa_b) HIP_TRY(e, hipMemsetAsync(numa, 0, numa_b, e->stream));
     }
+    uint8_t *rsvp = nullptr;
+    if (out->rsv_scores) {
+        if (stage_rsv) { rsvp = (uint8_t *)q; q += up(numa_b); }
+        else rsvp = out->rsv_scores;
+        if (numa_b) HIP_TRY(e, hipMemsetAsync(rsvp, 0, numa_b, e->stream));
+    }
+    const RsvArgs ra = rsv_args(e);
+    if (ra.rsv && (e->shard_begin != 0 || e->shard_end != e->n_nodes))
+        return set_err(e, KG_ERR_UNSUPPORTED, "Reservation matrix mode needs the whole snapshot (no shard)");
+    st = quota_ready(e);
+    if (st) return st;
+    const bool gated = (ra.quota || ra.rsv) && P > 0;
+    if (gated) {
+        hipLaunchKernelGGL(k_pod_gate, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, e->stream, ra.quota, e->pods, P,
+                           e->gate);
+        HIP_TRY(e, hipGetLastError());
+    }
     HIP_TRY(e, hipMemsetAsync(part, 0, part_b, e->stream));
     st = launch_eval(e, now_ns, 0, P, mask, scores, part, true, numa_on ? numa : nullptr);
     if (st) return st;
-    if (out->top1) {
-        unsigned long long *dst = dev ? (unsigned long long *)out->top1 : top;
-        if (P > 0) {
-            hipLaunchKernelGGL(k_top1, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, e->stream, part, (int32_t)T, P, dst);
+    unsigned long long *tdst = out->top1 ? (dev ? (unsigned long long *)out->top1 : top) : nullptr;
+    if (tdst && P > 0) {
+        hipLaunchKernelGGL(k_top1, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, e->stream, part, (int32_t)T, P, tdst);
+        HIP_TRY(e, hipGetLastError());
+    }
+    const int32_t mask_words = (int32_t)((width + 63) / 64);
+    const int64_t stride = (width + 63) / 64 * 64;
+    if (gated) {  // plain nodes closed to pods failing the quota or requiring a reservation
+        hipLaunchKernelGGL(k_quota_apply, dim3((unsigned)P), dim3(256), 0, e->stream, e->gate + P, P,
+                           (unsigned long long *)mask, mask_words, tdst, (uint8_t *)nullptr, stride);
+        HIP_TRY(e, hipGetLastError());
+    }
+    if (ra.rsv) {
+        for (int32_t b = 0; b < P; b += KG_RSV_POD_CHUNK) {
+            const int32_t n = P - b < KG_RSV_POD_CHUNK ? P - b : KG_RSV_POD_CHUNK;
+            st = rsv_eval_chunk(e, now_ns, b, n, mask ? mask + (int64_t)b * mask_words : nullptr,
+                                scores ? scores + (int64_t)b * stride : nullptr, mask_words, stride);
+            if (st) return st;
+            hipLaunchKernelGGL(k_rsv_reduce, dim3((unsigned)n), dim3(256), 0, e->stream, e->consts, ra, n,
+                               tdst ? tdst + b : nullptr, rsvp ? rsvp + (int64_t)b * stride : nullptr, e->shard_begin,
+                               e->shard_end, stride);
             HIP_TRY(e, hipGetLastError());
         }
-        if (!dev && P > 0) HIP_TRY(e, hipMemcpyAsync(out->top1, top, top_b, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (ra.quota && P > 0) {
+        hipLaunchKernelGGL(k_quota_apply, dim3((unsigned)P), dim3(256), 0, e->stream, e->gate, P,
+                           (unsigned long long *)mask, mask_words, tdst, rsvp, stride);
+        HIP_TRY(e, hipGetLastError());
     }
     if (!dev) {
+        if (out->top1 && P > 0) HIP_TRY(e, hipMemcpyAsync(out->top1, top, top_b, hipMemcpyDeviceToHost, e->stream));
         if (out->mask && P > 0) HIP_TRY(e, hipMemcpyAsync(out->mask, mask, mask_b, hipMemcpyDeviceToHost, e->stream));
         if (out->scores && P > 0) HIP_TRY(e, hipMemcpyAsync(out->scores, scores, score_b, hipMemcpyDeviceToHost, e->stream));
         if (out->numa_scores && P > 0) HIP_TRY(e, hipMemcpyAsync(out->numa_scores, numa, numa_b, hipMemcpyDeviceToHost, e->stream));
+        if (out->rsv_scores && P > 0) HIP_TRY(e, hipMemcpyAsync(out->rsv_scores, rsvp, numa_b, hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(e, hipStreamSynchronize(e->stream));
     }
     return KG_OK;
@@ -1624,7 +1970,15 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
     if (pod_begin < 0 || n < 0 || pod_begin + (int64_t)n > e->n_pods || (n > 0 && !partial_dev))
         return set_err(e, KG_ERR_RANGE, "bad chunk");
     HIP_TRY(e, hipMemsetAsync(partial_dev, 0, (size_t)n * (size_t)tiles_total(e) * 4, e->stream));
-    return launch_eval(e, now_ns, pod_begin, n, nullptr, nullptr, partial_dev);
+    st = launch_eval(e, now_ns, pod_begin, n, nullptr, nullptr, partial_dev);
+    if (st) return st;
+    // reservation nodes: entries of every reservation node (the snapshot is replicated across
+    // ranks in the multi-GPU placement, so each rank holds all of them), rows 0..n of E / O
+    if (rsv_args(e).rsv) {
+        if (n > KG_RSV_POD_CHUNK) return set_err(e, KG_ERR_RANGE, "chunk larger than the reservation entry buffer");
+        return rsv_eval_chunk(e, now_ns, pod_begin, n, nullptr, nullptr, 0, 0);
+    }
+    return KG_OK;
 }
 
 kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, const uint32_t *partial_dev,
@@ -1634,8 +1988,14 @@ kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin
     if (pod_begin < 0 || n < 0 || n > KG_MAX_CHUNK || pod_begin + (int64_t)n > e->n_pods)
         return set_err(e, KG_ERR_RANGE, "bad chunk");
     if (n == 0) return KG_OK;
+    st = quota_ready(e);
+    if (st) return st;
+    RsvArgs ra = rsv_args(e);
+    if (ra.rsv) {  // this chunk's entries were written by kg_place_chunk_eval from row 0
+        if (n > KG_RSV_POD_CHUNK) return set_err(e, KG_ERR_RANGE, "chunk larger than the reservation entry buffer");
+    }
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream, e->consts, e->pl, e->pods, pod_begin, n,
-                       partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev);
+                       partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev, ra);
     HIP_TRY(e, hipGetLastError());
     return KG_OK;
 }
@@ -1699,11 +2059,109 @@ int32_t kg_eval_kernel_times(kg_engine *e, float *ms, int32_t n) {
     return k;
 }
 
+kg_status kg_rsv_set(kg_engine *e, const kg_reservation *rsv, int32_t n) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (!(e->consts.plugins & KG_PLUGIN_RESERVATION)) return set_err(e, KG_ERR_STATE, "Reservation plugin not enabled");
+    if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised");
+    if (n < 0 || (n > 0 && !rsv)) return set_err(e, KG_ERR_INVALID_ARG, "bad reservation list");
+    std::vector<int32_t> order((size_t)n);
+    std::vector<int32_t> per_node_count;
+    std::map<int32_t, int32_t> count;
+    for (int32_t i = 0; i < n; i++) {
+        if (rsv[i].node < 0 || rsv[i].node >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "reservation %d: bad node", i);
+        if (++count[rsv[i].node] > KG_MAX_RSV_PER_NODE)
+            return set_err(e, KG_ERR_UNSUPPORTED, "node %d: more than %d reservations", rsv[i].node, KG_MAX_RSV_PER_NODE);
+        if (rsv[i].policy < KG_RSV_POLICY_DEFAULT || rsv[i].policy > KG_RSV_POLICY_RESTRICTED)
+            return set_err(e, KG_ERR_INVALID_ARG, "reservation %d: bad allocate policy", i);
+        order[(size_t)i] = i;
+    }
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return rsv[a].node < rsv[b].node; });
+    std::vector<kg_reservation> slots((size_t)n);
+    std::vector<int32_t> rfirst, rnode;
+    std::vector<int32_t> rsv_of((size_t)e->pl.cap, -1);
+    for (int32_t k = 0; k < n; k++) {
+        slots[(size_t)k] = rsv[order[(size_t)k]];
+        const int32_t node = slots[(size_t)k].node;
+        if (rnode.empty() || rnode.back() != node) {
+            rsv_of[(size_t)node] = (int32_t)rnode.size();
+            rnode.push_back(node);
+            rfirst.push_back(k);
+        }
+    }
+    rfirst.push_back(n);
+    const int32_t n_rn = (int32_t)rnode.size();
+    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t sb = up(sizeof(kg_reservation) * (size_t)(n > 0 ? n : 1)), fb = up(4 * rfirst.size()),
+                 nb = up(4 * (size_t)(n_rn > 0 ? n_rn : 1)),
+                 eb = up(8 * (size_t)KG_RSV_POD_CHUNK * (size_t)(n_rn > 0 ? n_rn : 1));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (e->rsv_mem) HIP_TRY(e, hipFree(e->rsv_mem));
+    e->rsv_mem = nullptr;
+    HIP_TRY(e, hipMalloc(&e->rsv_mem, sb + fb + nb + 2 * eb));
+    char *m = (char *)e->rsv_mem;
+    e->rsv = (kg_reservation *)m;
+    e->rfirst = (int32_t *)(m + sb);
+    e->rnode = (int32_t *)(m + sb + fb);
+    e->rsv_e = (unsigned long long *)(m + sb + fb + nb);
+    e->rsv_o = (int64_t *)(m + sb + fb + nb + eb);
+    if (n) HIP_TRY(e, hipMemcpyAsync(e->rsv, slots.data(), sizeof(kg_reservation) * (size_t)n, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(e->rfirst, rfirst.data(), 4 * rfirst.size(), hipMemcpyHostToDevice, e->stream));
+    if (n_rn) HIP_TRY(e, hipMemcpyAsync(e->rnode, rnode.data(), 4 * (size_t)n_rn, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(e->pl.rsv_of, rsv_of.data(), 4 * rsv_of.size(), hipMemcpyHostToDevice, e->stream));
+    e->n_rsv = n;
+    e->n_rn = n_rn;
+    e->rsv_perm = order;
+    // re-derive every node's planes: reservation nodes leave the fast paths, the others rejoin
+    hipLaunchKernelGGL(k_finalize_range, dim3((unsigned)((e->pl.cap + 255) / 256)), dim3(256), 0, e->stream, e->consts,
+                       e->pl, (int64_t)0, e->pl.cap);
+    HIP_TRY(e, hipGetLastError());
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return KG_OK;
+}
+
+kg_status kg_rsv_download(kg_engine *e, kg_reservation *out, int32_t n) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (n != e->n_rsv || (n > 0 && !out)) return set_err(e, KG_ERR_RANGE, "download %d reservations, have %d", n, e->n_rsv);
+    if (n == 0) return KG_OK;
+    std::vector<kg_reservation> slots((size_t)n);
+    HIP_TRY(e, hipMemcpyAsync(slots.data(), e->rsv, sizeof(kg_reservation) * (size_t)n, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    for (int32_t k = 0; k < n; k++) out[e->rsv_perm[(size_t)k]] = slots[(size_t)k];
+    return KG_OK;
+}
+
+kg_status kg_quota_set(kg_engine *e, const kg_quota *q, int32_t n) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (!(e->consts.plugins & KG_PLUGIN_ELASTICQUOTA)) return set_err(e, KG_ERR_STATE, "ElasticQuota plugin not enabled");
+    if (n < 0 || (n > 0 && !q)) return set_err(e, KG_ERR_INVALID_ARG, "bad quota list");
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (e->quota) HIP_TRY(e, hipFree(e->quota));
+    e->quota = nullptr;
+    HIP_TRY(e, hipMalloc(&e->quota, sizeof(kg_quota) * (size_t)(n > 0 ? n : 1)));
+    if (n) HIP_TRY(e, hipMemcpyAsync(e->quota, q, sizeof(kg_quota) * (size_t)n, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->n_quota = n;
+    return KG_OK;
+}
+
+kg_status kg_quota_download(kg_engine *e, kg_quota *out, int32_t n) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (n != e->n_quota || (n > 0 && !out)) return set_err(e, KG_ERR_RANGE, "download %d quotas, have %d", n, e->n_quota);
+    if (n == 0) return KG_OK;
+    HIP_TRY(e, hipMemcpyAsync(out, e->quota, sizeof(kg_quota) * (size_t)n, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return KG_OK;
+}
+
 kg_status kg_commit(kg_engine *e, int32_t pod, int32_t node) {
     kg_status st = check_engine(e);
     if (st) return st;
     if (pod < 0 || pod >= e->n_pods || node < 0 || node >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "bad commit");
-    hipLaunchKernelGGL(k_commit_one, dim3(1), dim3(1), 0, e->stream, e->consts, e->pl, e->pods, pod, node);
+    hipLaunchKernelGGL(k_commit_one, dim3(1), dim3(1), 0, e->stream, e->consts, e->pl, e->pods, pod, node, rsv_args(e));
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     return KG_OK;

@@ -332,6 +332,8 @@ int64_t kg_struct_size(int32_t sid) {
         case KG_SID_NODE_ROW: return sizeof(kg_node_row);
         case KG_SID_EVAL_OUT: return sizeof(kg_eval_out);
         case KG_SID_NUMA_SPEC: return sizeof(kg_numa_spec);
+        case KG_SID_RESERVATION: return sizeof(kg_reservation);
+        case KG_SID_QUOTA: return sizeof(kg_quota);
     }
     return -1;
 }
@@ -371,6 +373,7 @@ void kg_config_shipped_profile(kg_config *c) {
     c->la_filter_expired_node_metrics = 0;
     c->la_has_expiration = 1;
     c->la_expiration_seconds = 300;
+    c->weight_reservation = 5000;  // scheduler-config.yaml:82-91
 }
 
 kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
@@ -380,7 +383,12 @@ kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
     };
     if (!c) return fail("null config");
     if (c->abi_version != KG_ABI_VERSION) return fail("abi_version mismatch");
-    if (c->enabled_plugins & ~(KG_PLUGIN_FIT | KG_PLUGIN_LOADAWARE | KG_PLUGIN_NUMA)) return fail("unsupported plugin bit");
+    if (c->enabled_plugins &
+        ~(KG_PLUGIN_FIT | KG_PLUGIN_LOADAWARE | KG_PLUGIN_NUMA | KG_PLUGIN_RESERVATION | KG_PLUGIN_ELASTICQUOTA))
+        return fail("unsupported plugin bit");
+    if ((c->enabled_plugins & KG_PLUGIN_RESERVATION) && (c->enabled_plugins & KG_PLUGIN_NUMA))
+        return fail("Reservation together with NodeNUMAResource is not supported by the engine");
+    if (c->eq_check_parent_quota) return fail("ElasticQuota EnableCheckParentQuota is not supported by the engine");
     int64_t fw = 0, lw = 0, nw = 0;
     for (int r = 0; r < KG_NUM_RES; r++) {
         if (c->fit_resource_weight[r] < 0 || c->la_resource_weight[r] < 0 || c->numa_resource_weight[r] < 0)
@@ -399,8 +407,10 @@ kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
         return fail("unsupported NodeNUMAResource NUMA scoring strategy");
     if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && lw == 0) return fail("LoadAwareScheduling needs resourceWeights");
     // totals are packed as ((total + 1) << 10) | node into 32-bit per-tile keys: 100·Σweights < 2^22
-    if (c->weight_fit < 0 || c->weight_loadaware < 0 || c->weight_numa < 0 ||
-        (int64_t)c->weight_fit + c->weight_loadaware + ((c->enabled_plugins & KG_PLUGIN_NUMA) ? c->weight_numa : 0) > 40000)
+    if (c->weight_fit < 0 || c->weight_loadaware < 0 || c->weight_numa < 0 || c->weight_reservation < 0 ||
+        (int64_t)c->weight_fit + c->weight_loadaware + ((c->enabled_plugins & KG_PLUGIN_NUMA) ? c->weight_numa : 0) +
+                ((c->enabled_plugins & KG_PLUGIN_RESERVATION) ? c->weight_reservation : 0) >
+            40000)
         return fail("plugin weight out of range (each >= 0, sum <= 40000)");
     if (c->fit_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->fit_strategy != KG_STRATEGY_MOST_ALLOCATED)
         return fail("unsupported NodeResourcesFit scoring strategy");
@@ -471,6 +481,10 @@ kg_status kg_build_pod_rows(const kg_config *cfg, const kg_cluster_view *view, c
         if (pc == KG_PRIO_PROD) row.flags |= KG_POD_PROD;
         if (pc == KG_PRIO_PROD && cfg->la_score_according_prod_usage) row.flags |= KG_POD_LA_PROD_SCORE;
         if (pv.p.is_daemonset) row.flags |= KG_POD_DAEMONSET;
+        if (pv.p.non_preemptible) row.flags |= KG_POD_NON_PREEMPTIBLE;
+        row.rsv_owner_class = pv.p.rsv_owner_class;
+        row.rsv_affinity_class = pv.p.rsv_affinity_class;
+        row.quota = pv.p.quota;
         row.flags |= KG_POD_VALID;
     }
     return KG_OK;
@@ -592,6 +606,7 @@ kg_status kg_row_eval(const kg_config *cfg, const kg_node_row *node, const kg_po
     bool ok;
     uint32_t fit, la, numa = 0;
     kg_pair_exact(k, row, dflags, pd, now_ns, ok, fit, la);
+    if (pd.flags & KGP_RSV_REQUIRED) ok = false;  // no reservation on this node can match
     if (k.plugins & KG_PLUGIN_NUMA) {
         kg_numa_out o;
         kg_numa_pair(k, row, pd, o);
@@ -602,6 +617,32 @@ kg_status kg_row_eval(const kg_config *cfg, const kg_node_row *node, const kg_po
     if (fit_score) *fit_score = (int32_t)fit;
     if (la_score) *la_score = (int32_t)la;
     if (numa_score) *numa_score = (int32_t)numa;
+    return KG_OK;
+}
+
+kg_status kg_row_eval_rsv(const kg_config *cfg, const kg_node_row *node, const kg_reservation *rsv, int32_t n_rsv,
+                          const kg_pod_row *pod, int64_t now_ns, int32_t *feasible, int32_t *fit_score,
+                          int32_t *la_score, int32_t *rsv_raw, int64_t *order, int32_t *nominated) {
+    if (!cfg || !node || !pod || !feasible || n_rsv < 0 || n_rsv > KG_MAX_RSV_PER_NODE || (n_rsv > 0 && !rsv))
+        return KG_ERR_INVALID_ARG;
+    kg_consts k;
+    kg_consts_from_config(*cfg, k);
+    kg_pod_dev pd;
+    kg_pod_dev_from_row(*cfg, *pod, pd);
+    kg_node_row row = *node;
+    int64_t free_[KG_NUM_RES], metric_ns;
+    double fit_R[KG_NUM_RES], fit_F[KG_NUM_RES], la_R[2], la_F[4];
+    uint32_t dflags, fmask;
+    kg_planes pl{&row, free_, fit_R, fit_F, la_R, la_F, &metric_ns, &dflags, &fmask, 1};
+    kg_finalize_node(k, pl, 0);
+    kg_rsv_out o;
+    kg_rsv_pair(k, row, dflags, rsv, n_rsv, pd, now_ns, o);
+    *feasible = o.feasible ? 1 : 0;
+    if (fit_score) *fit_score = (int32_t)o.fit;
+    if (la_score) *la_score = (int32_t)o.la;
+    if (rsv_raw) *rsv_raw = (int32_t)o.raw;
+    if (order) *order = o.order;
+    if (nominated) *nominated = o.nominated;
     return KG_OK;
 }
 
@@ -630,6 +671,7 @@ void kg_consts_from_config(const kg_config &c, kg_consts &k) {
     k.numa_most = c.numa_strategy == KG_STRATEGY_MOST_ALLOCATED;
     k.numa_hint_most = c.numa_hint_strategy == KG_STRATEGY_MOST_ALLOCATED;
     for (int r = 0; r < KG_NUM_RES; r++) k.numa_w[r] = (int32_t)c.numa_resource_weight[r];
+    k.weight_rsv = (c.enabled_plugins & KG_PLUGIN_RESERVATION) ? c.weight_reservation : 0;
 }
 
 void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &d) {
@@ -667,6 +709,10 @@ void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &
     d.la_est_i[1] = row.la_estimate[1];
     for (int r = 0; r < KG_NUM_RES; r++) d.numa_req[r] = row.numa_request[r];
     d.numa_present = row.numa_request_present;
+    d.rsv_owner = row.rsv_owner_class;
+    d.rsv_aff = row.rsv_affinity_class;
+    d.quota = (c.enabled_plugins & KG_PLUGIN_ELASTICQUOTA) ? row.quota : -1;
+    if ((c.enabled_plugins & KG_PLUGIN_RESERVATION) && row.rsv_affinity_class >= 0) d.flags |= KGP_RSV_REQUIRED;
 }
 
 int kg_numa_list_count(const kg_pod_row &row) {

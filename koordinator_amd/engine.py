@@ -48,6 +48,17 @@ def row_eval(cfg: np.ndarray, node_row: np.ndarray, pod_row: np.ndarray, now_ns:
     return bool(f.value), a.value, b.value, c.value
 
 
+def row_eval_rsv(cfg: np.ndarray, node_row: np.ndarray, rsv: np.ndarray, pod_row: np.ndarray, now_ns: int):
+    """(feasible, fit, la, raw, order, nominated) of one pair with the node's reservation slots (host rows)."""
+    rsv = np.ascontiguousarray(rsv, dtype=nat.RESERVATION)
+    f, a, b, r, nm = (ctypes.c_int32() for _ in range(5))
+    o = ctypes.c_int64()
+    _check(nat.lib().kg_row_eval_rsv(nat.ptr(cfg), nat.ptr(node_row), nat.ptr(rsv) if len(rsv) else None, len(rsv),
+                                     nat.ptr(pod_row), int(now_ns), ctypes.byref(f), ctypes.byref(a), ctypes.byref(b),
+                                     ctypes.byref(r), ctypes.byref(o), ctypes.byref(nm)), what="kg_row_eval_rsv")
+    return bool(f.value), a.value, b.value, r.value, o.value, nm.value
+
+
 class Engine:
     """One engine = one GPU, one HIP stream, one HBM-resident node snapshot."""
 
@@ -139,9 +150,10 @@ class Engine:
         return self.mask_words * 64
 
     def eval(self, now_ns: int, mask: bool = True, scores: bool = True, top1: bool = True,
-             numa_scores: Optional[bool] = None) -> dict:
+             numa_scores: Optional[bool] = None, rsv_scores: Optional[bool] = None) -> dict:
         """Matrix mode into host arrays: mask [P][words] u64, scores [P][stride][2] u8, top1 [P] u64,
-        numa_scores [P][stride] u8 (by default when NodeNUMAResource is enabled)."""
+        numa_scores [P][stride] u8 (by default when NodeNUMAResource is enabled), rsv_scores [P][stride]
+        u8 (normalized Reservation score, by default when Reservation is enabled)."""
         P = self.n_pods
         res = {}
         out = nat.EvalOut()
@@ -159,6 +171,11 @@ class Engine:
         if numa_scores:
             res["numa_scores"] = np.zeros((P, self.score_stride), dtype=np.uint8)
             out.numa_scores = res["numa_scores"].ctypes.data
+        if rsv_scores is None:
+            rsv_scores = bool(int(self.cfg["enabled_plugins"]) & nat.PLUGIN_RESERVATION)
+        if rsv_scores:
+            res["rsv_scores"] = np.zeros((P, self.score_stride), dtype=np.uint8)
+            out.rsv_scores = res["rsv_scores"].ctypes.data
         out.out_on_device = 0
         _check(nat.lib().kg_eval(self._h, int(now_ns), ctypes.byref(out)), self, "kg_eval")
         return res
@@ -189,6 +206,27 @@ class Engine:
 
     def commit(self, pod: int, node: int) -> None:
         _check(nat.lib().kg_commit(self._h, pod, node), self, "kg_commit")
+
+    # Reservation / ElasticQuota -----------------------------------------------------------
+    def set_reservations(self, rsv: np.ndarray) -> None:
+        rsv = np.ascontiguousarray(rsv, dtype=nat.RESERVATION)
+        _check(nat.lib().kg_rsv_set(self._h, nat.ptr(rsv), len(rsv)), self, "kg_rsv_set")
+        self.n_rsv = len(rsv)
+
+    def download_reservations(self) -> np.ndarray:
+        out = np.zeros(getattr(self, "n_rsv", 0), dtype=nat.RESERVATION)
+        _check(nat.lib().kg_rsv_download(self._h, nat.ptr(out), len(out)), self, "kg_rsv_download")
+        return out
+
+    def set_quotas(self, q: np.ndarray) -> None:
+        q = np.ascontiguousarray(q, dtype=nat.QUOTA)
+        _check(nat.lib().kg_quota_set(self._h, nat.ptr(q), len(q)), self, "kg_quota_set")
+        self.n_quota = len(q)
+
+    def download_quotas(self) -> np.ndarray:
+        out = np.zeros(getattr(self, "n_quota", 0), dtype=nat.QUOTA)
+        _check(nat.lib().kg_quota_download(self._h, nat.ptr(out), len(out)), self, "kg_quota_download")
+        return out
 
 
 def decode_top1(keys: np.ndarray):

@@ -324,6 +324,10 @@ def pod_spec_record(p: Pod, containers: list, name_id: int) -> np.ndarray:
     rec["is_daemonset"] = int(p.daemonset)
     rec["is_terminated"] = int(p.terminated)
     rec["name_id"] = name_id
+    rec["rsv_owner_class"] = getattr(p, "rsv_owner_class", -1)
+    rec["rsv_affinity_class"] = getattr(p, "rsv_affinity_class", -1)
+    rec["quota"] = getattr(p, "quota", -1)
+    rec["non_preemptible"] = int(getattr(p, "non_preemptible", False))
     return rec
 
 

@@ -30,7 +30,7 @@ MI = 1 << 20
 class SynthView:
     """Same attribute surface as objects.FlatView (pods, containers, nodes, c_view …)."""
 
-    def __init__(self, pods, containers, nodes, now_ns, numa=None):
+    def __init__(self, pods, containers, nodes, now_ns, numa=None, reservations=None, quotas=None):
         self.pods = pods
         self.containers = containers
         self.nodes = nodes
@@ -38,9 +38,11 @@ class SynthView:
         self.pod_metrics_arr = np.zeros(0, dtype=nat.POD_METRIC)
         self.assigned_arr = np.zeros(0, dtype=nat.ASSIGNED_POD)
         self.numa_arr = np.zeros(0, dtype=nat.NUMA_SPEC) if numa is None else numa
+        self.rsv_arr = np.zeros(0, dtype=nat.RESERVATION) if reservations is None else reservations
+        self.quota_arr = np.zeros(0, dtype=nat.QUOTA) if quotas is None else quotas
         self.now_ns = now_ns
         self.c_view = nat.make_view(self.pods, self.containers, self.nodes, self.aggregated_arr, self.pod_metrics_arr,
-                                    self.assigned_arr, self.numa_arr)
+                                    self.assigned_arr, self.numa_arr, self.rsv_arr, self.quota_arr)
 
     def subset_nodes(self, begin: int, end: int) -> "SynthView":
         nodes = np.ascontiguousarray(self.nodes[begin:end])
@@ -124,6 +126,9 @@ def make_pods(p: int, seed: int):
     pods["label_priority_class"] = -1
     pods["label_qos"] = -1
     pods["name_id"] = np.arange(p) + 10_000_000
+    pods["rsv_owner_class"] = -1
+    pods["rsv_affinity_class"] = -1
+    pods["quota"] = -1
     return pods, cont
 
 
@@ -191,6 +196,90 @@ def make_numa_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS
     _rl_fill(lm, nat.RES_BATCH_CPU, cpu_r, batch)
     _rl_fill(lm, nat.RES_BATCH_MEMORY, mem_r, batch)
     return SynthView(pods, cont, nodes, now_ns, numa)
+
+
+def make_rsv_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, rsv_node_frac: float = 0.10,
+                     owner_classes: int = 16, n_quotas: int = 64, quota_ratio: float = 0.8,
+                     owned_frac: float = 0.8, affinity_frac: float = 0.1, non_preemptible_frac: float = 0.1) -> SynthView:
+    """BASELINE config 5: colocation burst of batch pods (batch-cpu / batch-memory
+    requests) with Reservations and ElasticQuota.  `rsv_node_frac` of the nodes carry 1–2
+    reservations of batch resources (10–30 % of the node's batch allocatable; 95 % available, 5 %
+    unschedulable, 20 % allocate-once; policy 70 % Default / 20 % Aligned / 10 % Restricted; owner
+    classes: one or two of `owner_classes`; an order label on 30 %; 0–3 assigned pods holding 0–100 %
+    of it).  The reserve pods and their assigned pods are pods of the node (Requested, pod count).
+    Pods: `owned_frac` belong to an owner class, `affinity_frac` of those require a matching
+    reservation; each pod is in one of `n_quotas` quota groups whose runtime is `quota_ratio` of the
+    group's total demand (min = half of it); `non_preemptible_frac` are non-preemptible."""
+    rng = np.random.default_rng(seed + 555)
+    nodes = make_nodes(n_nodes, seed, now_ns)
+    rn = np.sort(rng.choice(n_nodes, int(round(rsv_node_frac * n_nodes)), replace=False))
+    node_of = np.repeat(rn, rng.integers(1, 3, len(rn)))
+    R = len(node_of)
+    rsv = np.zeros(R, dtype=nat.RESERVATION)
+    rsv["node"] = node_of
+    flags = np.where(rng.random(R) < 0.95, nat.RSV_AVAILABLE, 0)
+    flags |= np.where(rng.random(R) < 0.05, nat.RSV_UNSCHEDULABLE, 0)
+    flags |= np.where(rng.random(R) < 0.2, nat.RSV_ALLOCATE_ONCE, 0)
+    rsv["flags"] = flags
+    pu = rng.random(R)
+    rsv["policy"] = np.where(pu < 0.7, nat.RSV_POLICY_DEFAULT, np.where(pu < 0.9, nat.RSV_POLICY_ALIGNED,
+                                                                       nat.RSV_POLICY_RESTRICTED))
+    o1 = rng.integers(0, owner_classes, R)
+    o2 = rng.integers(0, owner_classes, R)
+    owners = (np.uint32(1) << o1.astype(np.uint32)) | np.where(rng.random(R) < 0.3,
+                                                               np.uint32(1) << o2.astype(np.uint32), np.uint32(0))
+    rsv["owner_classes"] = owners
+    rsv["affinity_classes"] = owners
+    rsv["order"] = np.where(rng.random(R) < 0.3, rng.integers(1, 101, R), 0)
+    bcpu = nodes["allocatable"]["v"][node_of, nat.RES_BATCH_CPU]
+    bmem = nodes["allocatable"]["v"][node_of, nat.RES_BATCH_MEMORY]
+    ac = bcpu * rng.integers(10, 31, R) // 100
+    am = (bmem // 100) * rng.integers(10, 31, R)
+    _rl_fill(rsv["allocatable"], nat.RES_BATCH_CPU, ac)
+    _rl_fill(rsv["allocatable"], nat.RES_BATCH_MEMORY, am)
+    assigned = rng.integers(0, 4, R)
+    fill = np.where(assigned > 0, rng.integers(0, 101, R), 0)
+    xc = ac * fill // 100
+    xm = (am // 100) * fill
+    has = assigned > 0
+    _rl_fill(rsv["allocated"], nat.RES_BATCH_CPU, xc, has)
+    _rl_fill(rsv["allocated"], nat.RES_BATCH_MEMORY, xm, has)
+    rsv["n_assigned"] = assigned
+    rv = nodes["requested"]["v"]
+    np.add.at(rv[:, nat.RES_BATCH_CPU], node_of, ac + xc)
+    np.add.at(rv[:, nat.RES_BATCH_MEMORY], node_of, am + xm)
+    np.add.at(nodes["nonzero_requested"][:, 0], node_of, 100 * (1 + assigned))
+    np.add.at(nodes["nonzero_requested"][:, 1], node_of, 200 * MI * (1 + assigned))
+    np.add.at(nodes["pod_count"], node_of, 1 + assigned)
+
+    pods, cont = make_pods(n_pods, seed)
+    rq, lm = cont["requests"], cont["limits"]
+    cpu_r = np.where(rq["present"] & (1 << nat.RES_CPU), rq["v"][:, nat.RES_CPU], rq["v"][:, nat.RES_BATCH_CPU])
+    mem_r = np.where(rq["present"] & (1 << nat.RES_MEMORY), rq["v"][:, nat.RES_MEMORY], rq["v"][:, nat.RES_BATCH_MEMORY])
+    for arr in (rq, lm):
+        arr["v"][:] = 0
+        arr["present"][:] = 0
+    for arr in (rq, lm):
+        _rl_fill(arr, nat.RES_BATCH_CPU, cpu_r)
+        _rl_fill(arr, nat.RES_BATCH_MEMORY, mem_r)
+    prng = np.random.default_rng(seed + 4242)
+    owned = prng.random(n_pods) < owned_frac
+    owner = prng.integers(0, owner_classes, n_pods)
+    pods["rsv_owner_class"] = np.where(owned, owner, -1)
+    pods["rsv_affinity_class"] = np.where(owned & (prng.random(n_pods) < affinity_frac), owner, -1)
+    q = prng.integers(0, n_quotas, n_pods)
+    pods["quota"] = q
+    pods["non_preemptible"] = prng.random(n_pods) < non_preemptible_frac
+    quotas = np.zeros(n_quotas, dtype=nat.QUOTA)
+    dc = np.bincount(q, weights=cpu_r, minlength=n_quotas).astype(np.int64)
+    dm = np.bincount(q, weights=mem_r, minlength=n_quotas).astype(np.int64)
+    lim_c = (dc * int(quota_ratio * 100)) // 100
+    lim_m = (dm // 100) * int(quota_ratio * 100)
+    _rl_fill(quotas["used_limit"], nat.RES_BATCH_CPU, lim_c)
+    _rl_fill(quotas["used_limit"], nat.RES_BATCH_MEMORY, lim_m)
+    _rl_fill(quotas["min"], nat.RES_BATCH_CPU, lim_c // 2)
+    _rl_fill(quotas["min"], nat.RES_BATCH_MEMORY, lim_m // 2)
+    return SynthView(pods, cont, nodes, now_ns, reservations=rsv, quotas=quotas)
 
 
 # BASELINE.json configs (single-GPU bench uses config 2)

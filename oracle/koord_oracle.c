@@ -975,6 +975,214 @@ int kgo_numa_eval(const kg_config *c, const kg_cluster_view *v, const kg_pod_spe
 }
 
 /* ---------------------------------------------------------------- */
+/* Reservation (restore, Filter, Score + NormalizeScore, Reserve)      */
+/* pkg/scheduler/plugins/reservation/{transformer.go:49-346,          */
+/* plugin.go:311-476, 497-560, scoring.go:42-203, nominator.go:76-135},*/
+/* frameworkext/reservation_info.go:215-300,379-388.                  */
+/* The reservation cache walks reservationsOnNode as a Go map          */
+/* (cache.go:256, random order); this restatement fixes it to the     */
+/* order of kg_cluster_view.reservations.  Reservation    */
+/* owner / affinity matchers are given as class bitmasks.  No          */
+/* preemption (preemptible maps stay empty), no reserve pods.          */
+/* ---------------------------------------------------------------- */
+typedef struct {
+    kg_reservation r;        /* mutable copy (allocated, n_assigned) */
+} rsv_state;
+
+/* framework.Resource of calculateResource(pod with one container requesting `l`) and its
+ * non-zero cpu / memory (transformer.go:316-346; schedutil.GetNonzeroRequests) */
+static void rsv_calc_resource(const kg_resource_list *l, int64_t res[KG_NUM_RES], int64_t *nz_cpu, int64_t *nz_mem) {
+    for (int r = 0; r < KG_NUM_RES; r++) res[r] = get(l, r);
+    *nz_cpu = has(l, KG_RES_CPU) ? l->v[KG_RES_CPU] : 100;
+    *nz_mem = has(l, KG_RES_MEMORY) ? l->v[KG_RES_MEMORY] : 200LL * 1024 * 1024;
+}
+
+/* updateNodeInfoRequested (transformer.go:293-306) / NodeInfo.RemovePod resource part */
+static void rsv_update_requested(kg_node_spec *n, const kg_resource_list *l, int64_t sign) {
+    int64_t res[KG_NUM_RES], nzc, nzm;
+    rsv_calc_resource(l, res, &nzc, &nzm);
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        if (r >= 3 && !has(l, r)) continue;
+        n->requested.v[r] = get(&n->requested, r) + sign * res[r];
+        n->requested.present |= 1u << r;
+    }
+    n->nonzero_requested[0] += sign * nzc;
+    n->nonzero_requested[1] += sign * nzm;
+}
+
+static int rl_is_zero(const kg_resource_list *l) { /* quotav1.IsZero */
+    for (int r = 0; r < KG_NUM_RES; r++)
+        if (has(l, r) && l->v[r] != 0) return 0;
+    return 1;
+}
+
+static int rsv_usable(const kg_reservation *r) { /* transformer.go:116-124 */
+    if (!(r->flags & KG_RSV_AVAILABLE)) return 0;
+    if ((r->flags & KG_RSV_ALLOCATE_ONCE) && r->n_assigned > 0) return 0;
+    return 1;
+}
+static int rsv_match(const kg_pod_spec *pod, const kg_reservation *r) { /* matchReservation :348-372 */
+    if (pod->rsv_owner_class < 0 || !((r->owner_classes >> pod->rsv_owner_class) & 1u)) return 0;
+    if (pod->rsv_affinity_class >= 0 && !((r->affinity_classes >> pod->rsv_affinity_class) & 1u)) return 0;
+    return 1;
+}
+
+typedef struct {
+    int has_state;                       /* nodeReservationStates[node] exists */
+    int n_matched;
+    int matched[KG_MAX_RSV_PER_NODE];    /* indices into the node's reservation list */
+    int64_t pod_requested[KG_NUM_RES];   /* nodeRState.podRequested */
+    int64_t r_allocated[KG_NUM_RES];     /* nodeRState.rAllocated */
+} rsv_node_state;
+
+/* prepareMatchReservationState for one node (transformer.go:100-188): restores `n` in place. */
+static void rsv_restore(const kg_pod_spec *pod, rsv_state *const *rs, int nr, kg_node_spec *n, rsv_node_state *out) {
+    memset(out, 0, sizeof(*out));
+    int unmatched[KG_MAX_RSV_PER_NODE], nu = 0;
+    for (int i = 0; i < nr; i++) {
+        const kg_reservation *r = &rs[i]->r;
+        if (!rsv_usable(r)) continue;
+        if (!(r->flags & KG_RSV_UNSCHEDULABLE) && rsv_match(pod, r)) out->matched[out->n_matched++] = i;
+        else if (r->n_assigned > 0) unmatched[nu++] = i;
+    }
+    if (out->n_matched == 0 && nu == 0) { out->n_matched = 0; return; }
+    if (pod->rsv_affinity_class >= 0 && out->n_matched == 0) { out->n_matched = 0; return; }
+    out->has_state = 1;
+    for (int k = 0; k < nu; k++) { /* restoreUnmatchedReservations :265-291 */
+        const kg_reservation *r = &rs[unmatched[k]]->r;
+        rsv_update_requested(n, &r->allocatable, -1);
+        kg_resource_list remained;
+        rl_sub_nonneg(&r->allocatable, &r->allocated, &remained);
+        if (!rl_is_zero(&remained)) rsv_update_requested(n, &remained, +1);
+    }
+    for (int q = 0; q < KG_NUM_RES; q++) out->pod_requested[q] = get(&n->requested, q);
+    for (int k = 0; k < out->n_matched; k++) { /* restoreMatchedReservation :240-263 → RemovePod */
+        const kg_reservation *r = &rs[out->matched[k]]->r;
+        rsv_update_requested(n, &r->allocatable, -1);
+        n->pod_count -= 1;
+        for (int q = 0; q < KG_NUM_RES; q++) out->r_allocated[q] += get(&r->allocated, q);
+    }
+}
+
+/* fitsNode (plugin.go:427-476) with rInfo != nil and no preemptible */
+static int rsv_fits_node(const kg_resource_list *preq, const kg_node_spec *n, const rsv_node_state *st,
+                         const kg_reservation *r) {
+    if (n->pod_count - st->n_matched + 1 > n->allowed_pods) return 0;
+    uint32_t scal = preq->present & KG_SCALAR_RES_MASK;
+    if (get(preq, 0) == 0 && get(preq, 1) == 0 && get(preq, 2) == 0 && scal == 0) return 1;
+    kg_resource_list remained;
+    rl_sub_nonneg(&r->allocatable, &r->allocated, &remained);
+    for (int q = 0; q < KG_NUM_RES; q++) {
+        if (q >= 3 && !((scal >> q) & 1u)) continue;
+        int64_t free = get(&n->allocatable, q) - (st->pod_requested[q] - get(&remained, q) - st->r_allocated[q]);
+        if (get(preq, q) > free) return 0;
+    }
+    return 1;
+}
+
+/* filterWithReservations (plugin.go:377-425) */
+static int rsv_filter_with(const kg_resource_list *preq, const kg_node_spec *n, const rsv_node_state *st,
+                           rsv_state *const *rs, const int *list, int nl, int required) {
+    int ok = 0;
+    for (int k = 0; k < nl && !ok; k++) {
+        const kg_reservation *r = &rs[list[k]]->r;
+        if ((r->allocatable.present & preq->present) == 0) continue;
+        int node_fits = rsv_fits_node(preq, n, st, r);
+        if (r->policy == KG_RSV_POLICY_DEFAULT || r->policy == KG_RSV_POLICY_ALIGNED) {
+            if (node_fits) ok = 1;
+        } else if (r->policy == KG_RSV_POLICY_RESTRICTED) {
+            kg_resource_list alloc_m = r->allocated, remained;
+            alloc_m.present &= r->allocatable.present; /* quotav1.Mask(allocated, ResourceNames) */
+            rl_sub_nonneg(&r->allocatable, &alloc_m, &remained);
+            int fits = 1; /* LessThanOrEqual(Mask(podRequests, names), rRemained) */
+            for (int q = 0; q < KG_NUM_RES; q++)
+                if (has(&remained, q) && has(preq, q) && has(&r->allocatable, q) && preq->v[q] > remained.v[q]) fits = 0;
+            if (fits && node_fits) ok = 1;
+        }
+    }
+    if (!ok && required) return 0;
+    return 1;
+}
+
+/* Reservation.Filter for a non-reserve pod (plugin.go:351-369) */
+static int rsv_filter(const kg_pod_spec *pod, const kg_resource_list *preq, const kg_node_spec *n,
+                      const rsv_node_state *st, rsv_state *const *rs) {
+    if (st->n_matched == 0) return pod->rsv_affinity_class < 0;
+    return rsv_filter_with(preq, n, st, rs, st->matched, st->n_matched, pod->rsv_affinity_class >= 0);
+}
+
+/* findMostPreferredReservationByOrder (scoring.go:162-181): index into list or −1, *order */
+static int rsv_most_preferred(rsv_state *const *rs, const int *list, int nl, int64_t *order) {
+    int64_t sel = INT64_MAX;
+    int hi = -1;
+    for (int k = 0; k < nl; k++) {
+        int64_t o = rs[list[k]]->r.order;
+        if (o != 0 && sel > o) { sel = o; hi = k; }
+    }
+    *order = sel;
+    return hi;
+}
+
+/* scoreReservation (scoring.go:183-203): MostAllocated over RemoveZeros(Allocatable), MilliValue */
+static int64_t rsv_score_reservation(const kg_resource_list *preq, const kg_reservation *r) {
+    int64_t w = 0, s = 0;
+    for (int q = 0; q < KG_NUM_RES; q++) {
+        if (!has(&r->allocatable, q) || r->allocatable.v[q] == 0) continue;
+        w++;
+        int64_t cap = r->allocatable.v[q];
+        int64_t req = get(preq, q) + get(&r->allocated, q);
+        if (req <= cap) s += MAX_NODE_SCORE * milli(q, req) / milli(q, cap);
+    }
+    return w <= 0 ? 0 : s / w;
+}
+
+/* NominateReservation (nominator.go:76-135): reservation index on the node or −1 */
+static int rsv_nominate(const kg_resource_list *preq, const kg_node_spec *n, const rsv_node_state *st,
+                        rsv_state *const *rs) {
+    int cand[KG_MAX_RSV_PER_NODE], nc = 0;
+    for (int k = 0; k < st->n_matched; k++) { /* RunReservationFilterPlugins → FilterReservation :497-522 */
+        int one = st->matched[k];
+        if (rsv_filter_with(preq, n, st, rs, &one, 1, 1)) cand[nc++] = one;
+    }
+    if (nc == 0) return -1;
+    int64_t order;
+    int hi = rsv_most_preferred(rs, cand, nc, &order);
+    if (hi >= 0) return cand[hi];
+    /* prioritizeReservations + sort.Slice by score descending (insertion sort for ≤ 12 items is
+     * stable: the first of equal scores wins) */
+    int best = cand[0];
+    int64_t bs = rsv_score_reservation(preq, &rs[cand[0]]->r);
+    for (int k = 1; k < nc; k++) {
+        int64_t s = rsv_score_reservation(preq, &rs[cand[k]]->r);
+        if (s > bs) { bs = s; best = cand[k]; }
+    }
+    return best;
+}
+
+/* ---------------------------------------------------------------- */
+/* ElasticQuota PreFilter gate + Reserve (elasticquota/plugin.go:210-255, 323-337; */
+/* core/group_quota_manager.go:613-650 updatePodUsedNoLock).  Runtime (or max) is   */
+/* an input: it depends on the groups' requests, which pending pods already carry. */
+/* ---------------------------------------------------------------- */
+static int quota_leq(const kg_resource_list *preq, const kg_resource_list *used, const kg_resource_list *limit) {
+    for (int q = 0; q < KG_NUM_RES; q++) /* LessThanOrEqual(Mask(Add(podRequest, used), names(podRequest)), limit) */
+        if (has(limit, q) && has(preq, q) && preq->v[q] + get(used, q) > limit->v[q]) return 0;
+    return 1;
+}
+static int quota_prefilter(const kg_pod_spec *pod, const kg_resource_list *preq, const kg_quota *qs) {
+    if (pod->quota < 0) return 1;
+    const kg_quota *q = &qs[pod->quota];
+    if (!quota_leq(preq, &q->used, &q->used_limit)) return 0;
+    if (pod->non_preemptible && !quota_leq(preq, &q->non_preemptible_used, &q->min)) return 0;
+    return 1;
+}
+static void quota_reserve(const kg_pod_spec *pod, const kg_resource_list *preq, kg_quota *qs) {
+    if (pod->quota < 0) return;
+    rl_add(&qs[pod->quota].used, preq);
+    if (pod->non_preemptible) rl_add(&qs[pod->quota].non_preemptible_used, preq);
+}
+
+/* ---------------------------------------------------------------- */
 /* combined per-pair evaluation and the sequential reference cycle    */
 /* ---------------------------------------------------------------- */
 typedef struct {
@@ -1031,13 +1239,103 @@ int kgo_eval_matrix(const kg_config *c, const kg_cluster_view *v, const int32_t 
     return kgo_eval_matrix_range(c, v, pod_index, P, 0, v->n_nodes, now_ns, mask, fit, la);
 }
 
-/* Sequential reference cycle over pod_index[0..P) in queue order.
- * out_node[p] = chosen node or -1; out_score[p] = weighted total or -1. */
-int kgo_schedule(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
-                 int32_t *out_node, int64_t *out_score) {
-    int32_t N = v->n_nodes;
-    node_state *st = (node_state *)calloc((size_t)N, sizeof(node_state));
-    kg_cluster_view vv = *v;
+/* Per-node reservation lists (pointers into the mutable reservation states, view order). */
+typedef struct {
+    rsv_state *states;
+    rsv_state *(*of)[KG_MAX_RSV_PER_NODE];
+    int *n_of;
+} rsv_index;
+
+static int rsv_index_build(const kg_cluster_view *v, int32_t N, rsv_index *ri) {
+    ri->states = (rsv_state *)calloc((size_t)(v->n_reservations > 0 ? v->n_reservations : 1), sizeof(rsv_state));
+    ri->of = calloc((size_t)(N > 0 ? N : 1), sizeof(*ri->of));
+    ri->n_of = (int *)calloc((size_t)(N > 0 ? N : 1), sizeof(int));
+    for (int32_t i = 0; i < v->n_reservations; i++) {
+        ri->states[i].r = v->reservations[i];
+        int32_t j = v->reservations[i].node;
+        if (j < 0 || j >= N || ri->n_of[j] >= KG_MAX_RSV_PER_NODE) return -1;
+        ri->of[j][ri->n_of[j]++] = &ri->states[i];
+    }
+    return 0;
+}
+static void rsv_index_free(rsv_index *ri) { free(ri->states); free(ri->of); free(ri->n_of); }
+
+/* One scheduling cycle's Filter + Score of `pod` over every node of `st` (nothing is committed):
+ * BeforePreFilter restore (per node, on a copy), PreFilter (ElasticQuota), Filter, PreScore /
+ * Score / NormalizeScore (Reservation), weights.  Optional per-node outputs.  Returns the best
+ * node (lowest index on ties) or −1; *best_total its weighted total, *best_nom the nominated
+ * reservation (index into that node's list) or −1. */
+static int32_t oracle_pod(const kg_config *c, kg_cluster_view *vv, node_state *st, const rsv_index *ri, int32_t N,
+                          const kg_pod_spec *pod, int64_t now_ns, const kg_quota *quotas, uint8_t *mask,
+                          uint8_t *fitp, uint8_t *lap, uint8_t *numap, uint8_t *rsvp, int64_t *best_total,
+                          int *best_nom) {
+    const int rsv_on = (c->enabled_plugins & KG_PLUGIN_RESERVATION) != 0;
+    kg_resource_list preq;
+    numa_pod_requests(vv, pod, &preq);
+    const int gate = !(c->enabled_plugins & KG_PLUGIN_ELASTICQUOTA) || quota_prefilter(pod, &preq, quotas);
+    int64_t *base = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
+    int64_t *raw = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
+    int64_t *ord = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
+    int *nom = (int *)malloc(sizeof(int) * (size_t)(N + 1));
+    uint8_t *feas = (uint8_t *)malloc((size_t)(N + 1));
+    for (int32_t j = 0; j < N; j++) {
+        kg_node_spec n = st[j].spec;
+        rsv_node_state rst;
+        memset(&rst, 0, sizeof(rst));
+        if (rsv_on && ri->n_of[j]) rsv_restore(pod, ri->of[j], ri->n_of[j], &n, &rst);
+        int ok = gate;
+        int64_t numa_score = 0;
+        if (c->enabled_plugins & KG_PLUGIN_NUMA) {
+            numa_hint h;
+            if (!numa_pair(c, vv, pod, &n, st[j].has_numa ? &st[j].numa : NULL, &numa_score, &h)) ok = 0;
+        }
+        if ((c->enabled_plugins & KG_PLUGIN_FIT) && kgo_fit_filter(vv, pod, &n) != KG_CODE_SUCCESS) ok = 0;
+        if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && kgo_loadaware_filter(c, vv, pod, &n, now_ns) != KG_CODE_SUCCESS)
+            ok = 0;
+        if (rsv_on && !rsv_filter(pod, &preq, &n, &rst, ri->of[j])) ok = 0;
+        int64_t fit = (c->enabled_plugins & KG_PLUGIN_FIT) ? kgo_fit_score(c, vv, pod, &n) : 0;
+        int64_t la = (c->enabled_plugins & KG_PLUGIN_LOADAWARE)
+                         ? loadaware_score_impl(c, vv, pod, &n, st[j].assigned, st[j].n_assigned, now_ns) : 0;
+        feas[j] = (uint8_t)ok;
+        base[j] = c->weight_fit * fit + c->weight_loadaware * la + c->weight_numa * numa_score;
+        if (mask) mask[j] = (uint8_t)ok;
+        if (fitp) fitp[j] = (uint8_t)fit;
+        if (lap) lap[j] = (uint8_t)la;
+        if (numap) numap[j] = (uint8_t)numa_score;
+        raw[j] = 0;
+        nom[j] = -1;
+        ord[j] = INT64_MAX;
+        if (rsv_on && ok && rst.n_matched > 0) { /* PreScore (scoring.go:42-101) */
+            rsv_most_preferred(ri->of[j], rst.matched, rst.n_matched, &ord[j]);
+            nom[j] = rsv_nominate(&preq, &n, &rst, ri->of[j]);
+            if (nom[j] >= 0) raw[j] = rsv_score_reservation(&preq, &ri->of[j][nom[j]]->r);
+        }
+    }
+    int32_t pref = -1;
+    int64_t sel = INT64_MAX;
+    for (int32_t j = 0; j < N; j++)
+        if (feas[j] && ord[j] != 0 && sel > ord[j]) { sel = ord[j]; pref = j; }
+    if (pref >= 0) raw[pref] = 1000; /* mostPreferredScore (scoring.go:39,114-116) */
+    int64_t mx = 0;                  /* DefaultNormalizeScore over the feasible nodes */
+    for (int32_t j = 0; j < N; j++)
+        if (feas[j] && raw[j] > mx) mx = raw[j];
+    int64_t best = -1;
+    int32_t best_n = -1;
+    for (int32_t j = 0; j < N; j++) {
+        int64_t s = feas[j] ? (mx > 0 ? MAX_NODE_SCORE * raw[j] / mx : raw[j]) : 0;
+        if (rsvp) rsvp[j] = (uint8_t)s;
+        if (!feas[j]) continue;
+        int64_t total = base[j] + (rsv_on ? c->weight_reservation * s : 0);
+        if (total > best) { best = total; best_n = j; }
+    }
+    *best_total = best;
+    *best_nom = best_n >= 0 ? nom[best_n] : -1;
+    free(base); free(raw); free(ord); free(nom); free(feas);
+    return best_n;
+}
+
+static node_state *states_build(const kg_cluster_view *v, int32_t N) {
+    node_state *st = (node_state *)calloc((size_t)(N > 0 ? N : 1), sizeof(node_state));
     for (int32_t j = 0; j < N; j++) {
         st[j].spec = v->nodes[j];
         st[j].cap_assigned = v->nodes[j].n_assigned + 4;
@@ -1046,30 +1344,79 @@ int kgo_schedule(const kg_config *c, const kg_cluster_view *v, const int32_t *po
         st[j].has_numa = v->nodes[j].numa >= 0;
         if (st[j].has_numa) st[j].numa = v->numa[v->nodes[j].numa];
     }
+    return st;
+}
+static void states_free(node_state *st, int32_t N) {
+    for (int32_t j = 0; j < N; j++) free(st[j].assigned);
+    free(st);
+}
+
+/* Reservation Filter and PreScore inputs of one pair on the view's initial state (KAT checks):
+ * returns Reservation.Filter; *raw = scoreReservation of the nominated reservation (0 none),
+ * *nominated its index in the node's reservation list (−1 none). */
+int kgo_rsv_pair(const kg_config *c, const kg_cluster_view *v, int32_t pod_i, int32_t node_j, int64_t *raw,
+                 int32_t *nominated) {
+    const int32_t N = v->n_nodes;
+    rsv_index ri;
+    if (rsv_index_build(v, N, &ri) != 0) { rsv_index_free(&ri); return -1; }
+    const kg_pod_spec *pod = &v->pods[pod_i];
+    kg_resource_list preq;
+    numa_pod_requests(v, pod, &preq);
+    kg_node_spec n = v->nodes[node_j];
+    rsv_node_state rst;
+    memset(&rst, 0, sizeof(rst));
+    if (ri.n_of[node_j]) rsv_restore(pod, ri.of[node_j], ri.n_of[node_j], &n, &rst);
+    int ok = rsv_filter(pod, &preq, &n, &rst, ri.of[node_j]);
+    *raw = 0;
+    *nominated = -1;
+    if (rst.n_matched > 0) {
+        *nominated = rsv_nominate(&preq, &n, &rst, ri.of[node_j]);
+        if (*nominated >= 0) *raw = rsv_score_reservation(&preq, &ri.of[node_j][*nominated]->r);
+    }
+    (void)c;
+    rsv_index_free(&ri);
+    return ok;
+}
+
+/* Matrix mode with every plugin (mask / per-plugin planes [P][N], top1 [P]); nothing committed. */
+int kgo_eval_matrix5(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
+                     uint8_t *mask, uint8_t *fit, uint8_t *la, uint8_t *numa, uint8_t *rsv, uint64_t *top1) {
+    const int32_t N = v->n_nodes;
+    kg_cluster_view vv = *v;
+    node_state *st = states_build(v, N);
+    rsv_index ri;
+    if (rsv_index_build(v, N, &ri) != 0) { rsv_index_free(&ri); states_free(st, N); return -1; }
+    for (int32_t p = 0; p < P; p++) {
+        int64_t o = (int64_t)p * N, tot;
+        int nm;
+        int32_t b = oracle_pod(c, &vv, st, &ri, N, &v->pods[pod_index[p]], now_ns, v->quotas, mask + o, fit + o, la + o,
+                               numa ? numa + o : NULL, rsv ? rsv + o : NULL, &tot, &nm);
+        if (top1) top1[p] = b < 0 ? 0 : ((uint64_t)(tot + 1) << 32) | (0xFFFFFFFFull - (uint64_t)b);
+    }
+    rsv_index_free(&ri);
+    states_free(st, N);
+    return 0;
+}
+
+/* Sequential reference cycle over pod_index[0..P) in queue order.
+ * out_node[p] = chosen node or -1; out_score[p] = weighted total or -1.  out_rsv / out_quota
+ * (may be NULL) receive the reservation / quota states after the last Reserve. */
+int kgo_schedule2(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
+                  int32_t *out_node, int64_t *out_score, kg_reservation *out_rsv, kg_quota *out_quota) {
+    int32_t N = v->n_nodes;
+    node_state *st = states_build(v, N);
+    kg_cluster_view vv = *v;
+    rsv_index ri;
+    if (rsv_index_build(v, N, &ri) != 0) { rsv_index_free(&ri); states_free(st, N); return -1; }
+    kg_quota *quotas = (kg_quota *)calloc((size_t)(v->n_quotas > 0 ? v->n_quotas : 1), sizeof(kg_quota));
+    if (v->n_quotas > 0) memcpy(quotas, v->quotas, sizeof(kg_quota) * (size_t)v->n_quotas);
     for (int32_t p = 0; p < P; p++) {
         const kg_pod_spec *pod = &v->pods[pod_index[p]];
-        int64_t best = -1;
-        int32_t best_n = -1;
-        for (int32_t j = 0; j < N; j++) {
-            const kg_node_spec *n = &st[j].spec;
-            int64_t numa_score = 0;
-            if (c->enabled_plugins & KG_PLUGIN_NUMA) {
-                numa_hint h;
-                if (!numa_pair(c, &vv, pod, n, st[j].has_numa ? &st[j].numa : NULL, &numa_score, &h)) continue;
-            }
-            if ((c->enabled_plugins & KG_PLUGIN_FIT) && kgo_fit_filter(&vv, pod, n) != KG_CODE_SUCCESS) continue;
-            if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && kgo_loadaware_filter(c, &vv, pod, n, now_ns) != KG_CODE_SUCCESS)
-                continue;
-            int64_t total = 0;
-            if (c->enabled_plugins & KG_PLUGIN_FIT) total += c->weight_fit * kgo_fit_score(c, &vv, pod, n);
-            if (c->enabled_plugins & KG_PLUGIN_LOADAWARE)
-                total += c->weight_loadaware *
-                         loadaware_score_impl(c, &vv, pod, n, st[j].assigned, st[j].n_assigned, now_ns);
-            if (c->enabled_plugins & KG_PLUGIN_NUMA) total += c->weight_numa * numa_score;
-            if (total > best) { best = total; best_n = j; }
-        }
+        int64_t best;
+        int nom;
+        int32_t best_n = oracle_pod(c, &vv, st, &ri, N, pod, now_ns, quotas, NULL, NULL, NULL, NULL, NULL, &best, &nom);
         out_node[p] = best_n;
-        out_score[p] = best;
+        out_score[p] = best_n < 0 ? -1 : best;
         if (best_n < 0) continue;
         /* Reserve: AssumePod → NodeInfo.AddPod (calculateResource) */
         node_state *s = &st[best_n];
@@ -1097,6 +1444,19 @@ int kgo_schedule(const kg_config *c, const kg_cluster_view *v, const int32_t *po
         /* NodeNUMAResource.Reserve → resourceManager.Update: zone allocations of the stored hint (the
          * zone state is the one the pod was filtered on, so re-admitting reproduces that hint) */
         if ((c->enabled_plugins & KG_PLUGIN_NUMA) && s->has_numa) numa_reserve(c, &vv, pod, &s->numa);
+        kg_resource_list preq;
+        numa_pod_requests(&vv, pod, &preq);
+        /* Reservation.Reserve → reservationCache.assumePod → ReservationInfo.AddAssignedPod
+         * (plugin.go:525-560, reservation_info.go:379-388) on the nominated reservation */
+        if ((c->enabled_plugins & KG_PLUGIN_RESERVATION) && nom >= 0) {
+            kg_reservation *r = &ri.of[best_n][nom]->r;
+            kg_resource_list m = preq;
+            m.present &= r->allocatable.present;
+            rl_add(&r->allocated, &m);
+            r->n_assigned += 1;
+        }
+        /* ElasticQuota.Reserve → GroupQuotaManager.ReservePod → used += requests */
+        if (c->enabled_plugins & KG_PLUGIN_ELASTICQUOTA) quota_reserve(pod, &preq, quotas);
         /* LoadAware.Reserve → podAssignCache.assign(nodeName, pod) with timestamp now */
         if (!pod->is_terminated) {
             if (s->n_assigned == s->cap_assigned) {
@@ -1108,9 +1468,18 @@ int kgo_schedule(const kg_config *c, const kg_cluster_view *v, const int32_t *po
             s->n_assigned++;
         }
     }
-    for (int32_t j = 0; j < N; j++) free(st[j].assigned);
-    free(st);
+    if (out_rsv)
+        for (int32_t i = 0; i < v->n_reservations; i++) out_rsv[i] = ri.states[i].r;
+    if (out_quota && v->n_quotas > 0) memcpy(out_quota, quotas, sizeof(kg_quota) * (size_t)v->n_quotas);
+    free(quotas);
+    rsv_index_free(&ri);
+    states_free(st, N);
     return 0;
+}
+
+int kgo_schedule(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
+                 int32_t *out_node, int64_t *out_score) {
+    return kgo_schedule2(c, v, pod_index, P, now_ns, out_node, out_score, NULL, NULL);
 }
 
 int kgo_abi_version(void) { return KG_ABI_VERSION; }

@@ -166,3 +166,54 @@ def eval_matrix3(cfg, view, pod_index, now_ns, node_begin=0, node_end=None):
     lib().kgo_eval_matrix3(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, P, node_begin, node_end, now_ns,
                            mask.ctypes.data, fit.ctypes.data, la.ctypes.data, numa.ctypes.data)
     return mask.astype(bool), fit, la, numa
+
+
+def eval_matrix5(cfg, view, pod_index, now_ns):
+    """Every plugin (incl. Reservation with its per-pod NormalizeScore and the ElasticQuota gate):
+    mask, fit, loadaware, numa, reservation planes [P][N] and top1 keys [P]."""
+    idx = np.ascontiguousarray(pod_index, dtype=np.int32)
+    P, N = len(idx), len(view.nodes)
+    planes = [np.zeros((P, N), np.uint8) for _ in range(5)]
+    top1 = np.zeros(P, np.uint64)
+    L = lib()
+    L.kgo_eval_matrix5.restype = ctypes.c_int
+    L.kgo_eval_matrix5.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32, ctypes.c_int64] + [ctypes.c_void_p] * 6
+    st = L.kgo_eval_matrix5(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, P, now_ns,
+                            *[a.ctypes.data for a in planes], top1.ctypes.data)
+    if st != 0:
+        raise RuntimeError("kgo_eval_matrix5 failed")
+    mask, fit, la, numa, rsv = planes
+    return mask.astype(bool), fit, la, numa, rsv, top1
+
+
+def schedule2(cfg, view, pod_index, now_ns):
+    """Sequential cycle; also returns the reservation and quota states after the last Reserve."""
+    from koordinator_amd import _native as nat
+    idx = np.ascontiguousarray(pod_index, dtype=np.int32)
+    nodes = np.zeros(len(idx), np.int32)
+    scores = np.zeros(len(idx), np.int64)
+    rsv = np.zeros(view.c_view.n_reservations, dtype=nat.RESERVATION)
+    quota = np.zeros(view.c_view.n_quotas, dtype=nat.QUOTA)
+    L = lib()
+    L.kgo_schedule2.restype = ctypes.c_int
+    L.kgo_schedule2.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32, ctypes.c_int64] + [ctypes.c_void_p] * 4
+    st = L.kgo_schedule2(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, len(idx), now_ns, nodes.ctypes.data,
+                         scores.ctypes.data, rsv.ctypes.data if len(rsv) else None,
+                         quota.ctypes.data if len(quota) else None)
+    if st != 0:
+        raise RuntimeError("kgo_schedule2 failed")
+    return nodes, scores, rsv, quota
+
+
+def rsv_pair(cfg, view, pod_i, node_j):
+    """(Reservation.Filter, scoreReservation of the nominated reservation, nominated index) of one pair."""
+    L = lib()
+    L.kgo_rsv_pair.restype = ctypes.c_int
+    L.kgo_rsv_pair.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                               ctypes.c_void_p]
+    raw, nom = ctypes.c_int64(), ctypes.c_int32()
+    ok = L.kgo_rsv_pair(_cfg(cfg), ctypes.byref(view.c_view), int(pod_i), int(node_j), ctypes.byref(raw),
+                        ctypes.byref(nom))
+    if ok < 0:
+        raise RuntimeError("kgo_rsv_pair failed")
+    return bool(ok), raw.value, nom.value

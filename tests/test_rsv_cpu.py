@@ -1,0 +1,54 @@
+"""Reservation / ElasticQuota on the CPU: the oracle and the engine's shared per-pair code
+(kg_row_eval_rsv) against the reference's TestScore known answers, and the host-row mirror of the
+engine's per-pod reduction against the oracle on seeded config-5 clusters."""
+import numpy as np
+import pytest
+
+from koordinator_amd import engine
+from koordinator_amd.config import make_config, shipped_profile
+from oracle import oracle
+from rsv_cases import kat_cluster, kat_doc, rows_matrix5, rsv_cluster
+
+DOC = kat_doc()
+RSV = ("NodeResourcesFit", "LoadAwareScheduling", "Reservation")
+
+
+@pytest.mark.parametrize("case", DOC["cases"], ids=lambda c: c["name"])
+def test_reservation_score_kat(case):
+    cfg = make_config(plugins=("Reservation",))
+    view = kat_cluster(DOC, case)
+    ok, raw, nom = oracle.rsv_pair(cfg, view, 0, 0)
+    assert raw == case["want"]
+    rows = engine.build_node_rows(cfg, view)
+    prow = engine.build_pod_rows(cfg, view, [0])
+    f, _, _, raw2, _, nom2 = engine.row_eval_rsv(cfg, rows[0:1], view.rsv_arr, prow[0:1], view.now_ns)
+    assert (f, raw2, nom2) == (ok, raw, nom)
+
+
+@pytest.mark.parametrize("seed", [51, 52])
+def test_rows_match_oracle_matrix(seed):
+    cl = rsv_cluster(600, 24, seed=seed, rsv_node_frac=0.3)
+    cfg = shipped_profile(plugins=RSV)
+    idx = np.arange(24)
+    got = rows_matrix5(cfg, cl, idx, cl.now_ns)
+    m, fit, la, _, rsv, top1 = oracle.eval_matrix5(cfg, cl, idx, cl.now_ns)
+    for a, b in zip(got, (m, fit, la, rsv, top1)):
+        np.testing.assert_array_equal(a, b)
+    assert rsv.max() == 100 and m.any()
+
+
+def test_oracle_quota_gate_and_reserve():
+    """ElasticQuota: pods beyond the group's runtime are unschedulable; used grows by the placed
+    pods' requests (oracle invariants on a config-5 cluster)."""
+    cl = rsv_cluster(400, 300, seed=53, n_quotas=4, quota_ratio=0.3)
+    cfg = shipped_profile(plugins=RSV + ("ElasticQuota",))
+    nodes, scores, rsv, quota = oracle.schedule2(cfg, cl, np.arange(300), cl.now_ns)
+    assert (nodes == -1).any() and (nodes >= 0).any()
+    req = cl.containers["requests"]["v"]
+    for g in range(4):
+        placed = (nodes >= 0) & (cl.pods["quota"] == g)
+        for r in (3, 4):
+            assert quota["used"]["v"][g, r] == req[placed, r].sum()
+            assert quota["used"]["v"][g, r] <= cl.quota_arr["used_limit"]["v"][g, r]
+    # every placement on a node with a nominated reservation added to that reservation
+    assert (rsv["n_assigned"] >= cl.rsv_arr["n_assigned"]).all()
