@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--c3-pods", type=int, default=1_000, help="config-3 (NodeNUMAResource) pods; 0 skips it")
+    ap.add_argument("--c5-pods", type=int, default=100_000,
+                    help="config-5 (Reservation + ElasticQuota) pods placed in sequence; 0 skips it")
+    ap.add_argument("--c5-matrix-pods", type=int, default=1_000, help="config-5 matrix-mode pods")
     return ap.parse_args()
 
 
@@ -120,6 +123,78 @@ def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
             "kernel": "k_eval_numa", "kernel_ms": round(k_ms, 3), "feasible_frac_sample": round(feasible, 4),
             "placement": {"pods": P, "seconds": round(tp1 - tp0, 4), "pods_placed_per_s": round(P / (tp1 - tp0), 1),
                           "placed": int((nodes >= 0).sum())}}
+
+
+def bench_config5(args, engine, synth, shipped_profile, dev, stream, cpu_model):
+    """BASELINE config 5: colocation burst — batch pods with Reservation (weight 5000) and ElasticQuota
+    over 100k nodes, 10 % of them with 1–2 reservations, 16 owner classes, 64 quota groups at 80 % of
+    demand (synth.make_rsv_cluster, seed 5).  Placement = greedy sequential commit (kg_place); matrix
+    mode on a pod sample; the CPU baseline is the oracle's sequential cycle on a bounded pod prefix."""
+    import torch
+
+    from koordinator_amd import _native as nat
+
+    P, N, PM = args.c5_pods, args.nodes, min(args.c5_matrix_pods, args.c5_pods)
+    cl = synth.make_rsv_cluster(N, P, seed=5)
+    cfg = shipped_profile()
+    cfg["enabled_plugins"] |= nat.PLUGIN_RESERVATION | nat.PLUGIN_ELASTICQUOTA
+    rows = engine.build_node_rows(cfg, cl)
+    pods = engine.build_pod_rows(cfg, cl, np.arange(P))
+    eng = engine.Engine(cfg)
+    eng.set_stream(stream.cuda_stream)
+
+    def reset(pod_rows):
+        eng.load_snapshot(rows)
+        eng.set_reservations(cl.rsv_arr)
+        eng.set_quotas(cl.quota_arr)
+        eng.set_pods(pod_rows)
+
+    # matrix mode on the first PM pods
+    reset(pods[:PM])
+    W = eng.mask_words
+    mask = torch.empty((PM, W), dtype=torch.int64, device=dev)
+    scores = torch.empty((PM, W * 64, 2), dtype=torch.uint8, device=dev)
+    top1 = torch.zeros(PM, dtype=torch.int64, device=dev)
+    step = lambda: eng.eval_device(cl.now_ns, mask.data_ptr(), scores.data_ptr(), top1.data_ptr())
+    step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
+    tm = (time.perf_counter() - t0) / 3
+    # placement of the whole burst
+    reset(pods)
+    torch.cuda.synchronize(dev)
+    tp0 = time.perf_counter()
+    nodes, _ = eng.place(cl.now_ns)
+    tp = time.perf_counter() - tp0
+    rsv_after = eng.download_reservations()
+    eng.close()
+    rnodes = set(cl.rsv_arr["node"].tolist())
+    on_rsv = int(sum(1 for n in nodes[nodes >= 0].tolist() if n in rnodes))
+    out = {"workload": f"config5: {P} batch pods x {N} nodes, {len(rnodes)} nodes with {len(cl.rsv_arr)} reservations "
+                       f"(16 owner classes), {len(cl.quota_arr)} ElasticQuota groups at 80% of demand, shipped profile "
+                       "+ Reservation (weight 5000) + ElasticQuota",
+           "placement": {"pods": P, "seconds": round(tp, 4), "pods_placed_per_s": round(P / tp, 1),
+                         "placed": int((nodes >= 0).sum()), "placed_on_reservation_nodes": on_rsv,
+                         "reservation_assignments": int((rsv_after["n_assigned"] - cl.rsv_arr["n_assigned"]).sum()),
+                         "mode": "kg_place (greedy sequential commit, touched-node re-score)"},
+           "matrix": {"pods": PM, "evals_per_s": round(PM * N / tm, 1), "ms_per_step": round(tm * 1e3, 3)}}
+    if not args.no_cpu_baseline:
+        from oracle import oracle  # CPU restatement of the sequential cycle, timed as the baseline only
+        k, tc = 4, 0.0
+        while True:
+            tc0 = time.perf_counter()
+            oracle.schedule2(cfg, cl, np.arange(k), cl.now_ns)
+            tc = time.perf_counter() - tc0
+            if tc > args.cpu_budget_s / 4 or k >= P:
+                break
+            k = min(P, k * 2)
+        out["cpu_baseline"] = {"value": round(k / tc, 2), "unit": "pods placed/s", "cores": 1, "kind": "port",
+                               "sample": f"first {k} pods of the same burst, sequential cycle over all {N} nodes "
+                                         f"(oracle/koord_oracle.c kgo_schedule2), {tc:.1f}s on {cpu_model()}"}
+    return out
 
 
 def main():
@@ -249,6 +324,10 @@ def main():
     if args.c3_pods > 0 and world == 1:
         config3 = bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model)
 
+    config5 = None
+    if args.c5_pods > 0 and world == 1:
+        config5 = bench_config5(args, engine, synth, shipped_profile, dev, stream, cpu_model)
+
     traffic, traffic_src = pmc_traffic()
     if rank == 0:
         line = {
@@ -276,6 +355,7 @@ def main():
             "cpu_baseline": cpu_baseline,
             "placement": placement,
             "config3": config3,
+            "config5": config5,
             "pods_with_feasible_node": feasible_pods,
         }
         print(json.dumps(line), flush=True)
