@@ -569,12 +569,22 @@ __device__ __forceinline__ kg_pod_cls_t<NC, NF> load_cls_row(const kg_pod_cls_t<
     return u.h;
 }
 
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool FULL>
-__device__ __forceinline__ bool cls_pair(const kg_consts &c, const kg_cls_desc &d, const kg_pod_cls_t<NC, NF> &pd,
-                                         const ClsNode<NC, NF> &n, uint32_t &fit, uint32_t &la) {
-    bool ok = n.ok;
+// Fit compares of one pod against the lane's node as a wave lane mask: each int64 compare writes an
+// SGPR pair and the masks are ANDed on the scalar unit (no per-lane booleans in VGPRs)
+template <int NC, int NF>
+__device__ __forceinline__ unsigned long long cls_ok_mask(const kg_pod_cls_t<NC, NF> &pd, const ClsNode<NC, NF> &n,
+                                                          unsigned long long okm) {
+    unsigned long long m = okm;
 #pragma unroll
-    for (int k = 0; k < NC; k++) ok &= pd.req[k] <= n.fr[k];
+    for (int k = 0; k < NC; k++) m &= __builtin_amdgcn_ballot_w64(pd.req[k] <= n.fr[k]);
+    return m;
+}
+
+// Fit and LoadAware scores of one pair.  UNIT: every Fit / LoadAware resource weight is 1, so the
+// weighted sums are plain sums.
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool FULL, bool UNIT>
+__device__ __forceinline__ void cls_scores(const kg_consts &c, const kg_cls_desc &d, const kg_pod_cls_t<NC, NF> &pd,
+                                           const ClsNode<NC, NF> &n, uint32_t &fit, uint32_t &la) {
     fit = 0;
     if (FIT_ON) {
         uint32_t sum = 0;
@@ -582,7 +592,7 @@ __device__ __forceinline__ bool cls_pair(const kg_consts &c, const kg_cls_desc &
         for (int f = 0; f < NF; f++) {
             uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n.R[f], n.F[f]));
             if (MOST) q = q < 100u ? q : 100u;
-            sum = __umul24(d.fit_w[f], q) + sum;
+            sum = UNIT ? sum + q : __umul24(d.fit_w[f], q) + sum;
         }
         if (FULL) fit = sum >> d.fit_shift;
         else fit = n.w ? sum / n.w : 0u;  // the node lacks a scored resource: its weight drops out
@@ -591,9 +601,15 @@ __device__ __forceinline__ bool cls_pair(const kg_consts &c, const kg_cls_desc &
     if (LA_ON) {
         const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la[0], n.laR[0], n.laF[0]));
         const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la[1], n.laR[1], n.laF[1]));
-        la = (__umul24((uint32_t)c.la_w[0], q0) + __umul24((uint32_t)c.la_w[1], q1)) >> c.la_shift;
+        la = (UNIT ? q0 + q1 : __umul24((uint32_t)c.la_w[0], q0) + __umul24((uint32_t)c.la_w[1], q1)) >> c.la_shift;
     }
-    return ok;
+}
+
+// v_cndmask_b32 with a wave lane mask as the condition: v where the lane's bit is set, else 0
+__device__ __forceinline__ uint32_t sel_lanes(unsigned long long m, uint32_t v) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(m));
+    return r;
 }
 
 // v_writelane_b32 ×4: lane `lane` of mb[0..3] := the wave-uniform words (no exec change; the
@@ -613,18 +629,22 @@ __device__ __forceinline__ void write_lanes(uint32_t (&mb)[4], uint32_t lane, un
 // Pods [p0, p1) of one class against the lane's two nodes; rows come from the LDS chunk buffer.
 // The feasibility ballots of the chunk are collected into lanes (p − p0) of four VGPRs and written
 // once per chunk; EDGE workgroups (the shard's last tile) check that a segment lies in the row.
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1>
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool STAGE>
 __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> &n0,
-                                         const ClsNode<NC, NF> &n1, const char *lrows, int p0, int p1,
-                                         uint16_t *__restrict__ scores, uint32_t scol, bool seg0, bool seg1,
-                                         uint32_t kb0, uint32_t kb1, uint32_t *kbuf, uint32_t (&mb)[4]) {
+                                         const ClsNode<NC, NF> &n1, unsigned long long okm0, unsigned long long okm1,
+                                         const char *lrows, int p0, int p1, uint16_t *__restrict__ scores,
+                                         uint32_t scol, bool seg0, bool seg1, uint32_t kb0, uint32_t kb1,
+                                         uint32_t *kbuf, uint32_t (&mb)[4], uint16_t *sst) {
     const int tid = threadIdx.x;
+    const int lane = tid & 63;
     for (int p = p0; p < p1; p++) {
         const kg_pod_cls_t<NC, NF> pd =
             *reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(lrows + (p - p0) * (int)sizeof(kg_pod_cls_t<NC, NF>));
         uint32_t fit0, la0, fit1, la1;
-        const bool ok0 = cls_pair<NC, NF, MOST, FIT_ON, LA_ON, FULL>(c, d, pd, n0, fit0, la0);
-        const bool ok1 = cls_pair<NC, NF, MOST, FIT_ON, LA_ON, FULL>(c, d, pd, n1, fit1, la1);
+        const unsigned long long m0 = cls_ok_mask<NC, NF>(pd, n0, okm0);
+        const unsigned long long m1 = cls_ok_mask<NC, NF>(pd, n1, okm1);
+        cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n0, fit0, la0);
+        cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n1, fit1, la1);
         uint32_t tot0, tot1;
         if (W1) {
             tot0 = fit0 + la0;
@@ -633,25 +653,33 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
             tot0 = __umul24((uint32_t)c.weight_fit, fit0) + __umul24((uint32_t)c.weight_la, la0);
             tot1 = __umul24((uint32_t)c.weight_fit, fit1) + __umul24((uint32_t)c.weight_la, la1);
         }
-        const uint32_t k0 = ok0 ? (tot0 << KG_TILE_SHIFT) + kb0 : 0u;
-        const uint32_t k1 = ok1 ? (tot1 << KG_TILE_SHIFT) + kb1 : 0u;
+        const uint32_t k0 = sel_lanes(m0, (tot0 << KG_TILE_SHIFT) + kb0);
+        const uint32_t k1 = sel_lanes(m1, (tot1 << KG_TILE_SHIFT) + kb1);
         kbuf[(p - p0) * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
         if (OUT) {
-            write_lanes(mb, (uint32_t)(p - p0), __ballot(ok0), __ballot(ok1));
-            uint16_t *srow = scores + pd.score_off;
-            if (seg0) srow[scol] = (uint16_t)(fit0 | (la0 << 8));
-            if (seg1) srow[scol + 64] = (uint16_t)(fit1 | (la1 << 8));
+            write_lanes(mb, (uint32_t)(p - p0), m0, m1);
+            if (STAGE) {  // the wave's 128-column score segment of this pod, written out per chunk
+                sst[(p - p0) * 128 + lane] = (uint16_t)(fit0 | (la0 << 8));
+                sst[(p - p0) * 128 + 64 + lane] = (uint16_t)(fit1 | (la1 << 8));
+            } else {
+                uint16_t *srow = scores + pd.score_off;
+                if (seg0) srow[scol] = (uint16_t)(fit0 | (la0 << 8));
+                if (seg1) srow[scol + 64] = (uint16_t)(fit1 | (la1 << 8));
+            }
         }
     }
 }
 
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1>
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE>
 __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
                                           const kg_cls_work &w, const char *__restrict__ rows_base,
                                           uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
-                                          uint32_t *__restrict__ partials, uint32_t *kbuf, char *lrows) {
+                                          uint32_t *__restrict__ partials, uint32_t *kbuf, char *lrows,
+                                          uint16_t *sstage) {
     constexpr int RB = (int)sizeof(kg_pod_cls_t<NC, NF>);
-    constexpr int CHUNK_DW = KG_KCHUNK * RB / 4;          // dwords of one chunk of rows (≤ KG_BLOCK)
+    constexpr int CHUNK_DW = CC * RB / 4;                 // dwords of one chunk of rows (≤ KG_BLOCK)
+    constexpr int G = KG_BLOCK / CC;                      // threads reducing one pod's keys
+    static_assert(G == 32 || G == 64, "key reduction groups are half or whole waves");
     static_assert(CHUNK_DW <= KG_BLOCK, "one dword per thread stages a chunk");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -661,6 +689,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     ClsNode<NC, NF> n0, n1;
     load_cls_node<NC, NF, FIT_ON, LA_ON>(c, pl, d, wave_base + lane, a.node_end, a.now_ns, n0);
     load_cls_node<NC, NF, FIT_ON, LA_ON>(c, pl, d, wave_base + 64 + lane, a.node_end, a.now_ns, n1);
+    const unsigned long long okm0 = __builtin_amdgcn_ballot_w64(n0.ok), okm1 = __builtin_amdgcn_ballot_w64(n1.ok);
     const uint32_t W = 1u << d.fit_shift;
     const bool full = !FIT_ON || __all((n0.w == W || wave_base + lane >= a.node_end) &&
                                        (n1.w == W || wave_base + 64 + lane >= a.node_end));
@@ -682,24 +711,41 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     // vector memory (its stores included)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __syncthreads();
-    const int rj = tid >> 5, rg = tid & 31;
+    const int rj = tid / G, rg = tid % G;
+    uint16_t *sst = sstage + wave * (CC * 128);
     int buf = 0;
-    for (int p0 = w.begin; p0 < w.end; p0 += KG_KCHUNK) {
-        const int p1 = min(p0 + KG_KCHUNK, w.end);
+    for (int p0 = w.begin; p0 < w.end; p0 += CC) {
+        const int p1 = min(p0 + CC, w.end);
         uint32_t staged = 0;
         const bool more = p1 < w.end;
         if (more && tid < CHUNK_DW) {
             const int64_t src = (int64_t)p1 * (RB / 4) + tid;
             staged = gsrc[src < last_dw ? src : last_dw];
         }
-        const char *cur = lrows + buf * (KG_KCHUNK * RB);
+        const char *cur = lrows + buf * (CC * RB);
         uint32_t mb[4] = {0u, 0u, 0u, 0u};
         if (full)
-            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, true, W1>(c, d, n0, n1, cur, p0, p1, scores, scol, seg0,
-                                                                       seg1, kb0, kb1, kbuf, mb);
+            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, true, W1, STAGE>(c, d, n0, n1, okm0, okm1, cur, p0, p1, scores,
+                                                                              scol, seg0, seg1, kb0, kb1, kbuf, mb, sst);
         else
-            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, false, W1>(c, d, n0, n1, cur, p0, p1, scores, scol, seg0,
-                                                                        seg1, kb0, kb1, kbuf, mb);
+            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, false, W1, STAGE>(c, d, n0, n1, okm0, okm1, cur, p0, p1, scores,
+                                                                               scol, seg0, seg1, kb0, kb1, kbuf, mb, sst);
+        if (OUT && STAGE) {
+            // 16 lanes × 16 B cover one pod's 128 columns: four pods per wave-wide 1 KiB store.  The
+            // reads see the other lanes' ds_writes: a wave's LDS operations complete in order.
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const int np = p1 - p0, s8 = lane & 15;
+            const bool segs = s8 < 8 ? seg0 : seg1;
+            for (int it = 0; it * 4 < np; it++) {
+                const int pp = it * 4 + (lane >> 4);
+                if (pp < np && segs) {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(sst + pp * 128 + s8 * 8);
+                    const int64_t off = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[pp].score_off;
+                    *reinterpret_cast<uint4 *>(scores + off + col0 + s8 * 8) = v;
+                }
+            }
+        }
         if (OUT && lane < p1 - p0 && seg0) {
             // lane l writes the two feasibility words of pod p0 + l
             const kg_pod_cls_t<NC, NF> &pr = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[lane];
@@ -707,12 +753,12 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
             mw[0] = (uint64_t)mb[0] | ((uint64_t)mb[1] << 32);
             if (seg1) mw[1] = (uint64_t)mb[2] | ((uint64_t)mb[3] << 32);
         }
-        if (more && tid < CHUNK_DW) lbuf[(buf ^ 1) * (KG_KCHUNK * RB / 4) + tid] = staged;
+        if (more && tid < CHUNK_DW) lbuf[(buf ^ 1) * (CC * RB / 4) + tid] = staged;
         __syncthreads();
-        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * KG_BLOCK + rg * 16);
+        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * KG_BLOCK + rg * CC);
         uint32_t mx = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < CC / 4; k++) {
             const uint4 v = src[k];
             const uint32_t a0 = v.x > v.y ? v.x : v.y, a1 = v.z > v.w ? v.z : v.w;
             const uint32_t a2 = a0 > a1 ? a0 : a1;
@@ -723,7 +769,8 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         mx = dpp_max_step(mx, 2);
         mx = dpp_max_step(mx, 3);
         mx = dpp_max_step(mx, 4);
-        if (rg == 31 && rj < p1 - p0) {
+        if (G == 64) mx = dpp_max_step(mx, 5);
+        if (rg == G - 1 && rj < p1 - p0) {
             const int32_t row = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[rj].row;
             partials[(int64_t)row * a.tiles_total + tile] = mx;
         }
@@ -732,22 +779,25 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     }
 }
 
-template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1>
+template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE>
 __global__ __launch_bounds__(KG_BLOCK) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_cls_desc *__restrict__ descs,
                                                     const kg_cls_work *__restrict__ work,
                                                     const char *__restrict__ rows, uint64_t *__restrict__ mask,
                                                     uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
-    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_KCHUNK * KG_BLOCK];
-    __shared__ __attribute__((aligned(64))) char lrows[2 * KG_KCHUNK * 128];
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[CC * KG_BLOCK];
+    __shared__ __attribute__((aligned(64))) char lrows[2 * CC * 128];
+    __shared__ __attribute__((aligned(16))) uint16_t sstage[STAGE ? (KG_BLOCK / 64) * CC * 128 : 8];
     const kg_cls_work w = work[blockIdx.y];
     const kg_cls_desc d = descs[w.cls];
+#define KG_CLS_ARGS c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows, sstage
     switch (d.kind) {
-        case 0: cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1>(c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows); break;
-        case 1: cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1>(c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows); break;
-        case 2: cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1>(c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows); break;
-        default: cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1>(c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows); break;
+        case 0: cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS); break;
+        case 1: cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS); break;
+        case 2: cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS); break;
+        default: cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS); break;
     }
+#undef KG_CLS_ARGS
 }
 
 // Slow nodes (outside the fp64 exactness bounds) come out of k_eval2 as infeasible with
@@ -1474,18 +1524,24 @@ void launch_cls4(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint
     const kg_cls_desc *descs = (const kg_cls_desc *)m;
     const kg_cls_work *work = (const kg_cls_work *)(m + e->cls_work_off);
     const char *rows = m + e->cls_rows_off;
+    // matrix mode: 16-pod chunks, score segments staged in LDS and written as 1 KiB wave stores
     if (mask)
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts, e->pl,
-                           a, descs, work, rows, mask, scores, partials);
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, 16, true>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts,
+                           e->pl, a, descs, work, rows, mask, scores, partials);
     else
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts, e->pl,
-                           a, descs, work, rows, mask, scores, partials);
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, 16, false>), grid, dim3(KG_BLOCK), 0, e->stream,
+                           e->consts, e->pl, a, descs, work, rows, mask, scores, partials);
 }
 
 template <bool MOST, bool FIT_ON, bool LA_ON>
 void launch_cls3(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint16_t *scores, uint32_t *partials) {
-    // plugin weights 1 (the shipped profile): totals are plain sums
-    if (e->consts.weight_fit == 1 && e->consts.weight_la == 1) launch_cls4<MOST, FIT_ON, LA_ON, true>(e, grid, a, mask, scores, partials);
+    // plugin weights 1 and every Fit / LoadAware resource weight 1 (the shipped profile): all weighted
+    // sums are plain sums
+    bool unit = e->consts.weight_fit == 1 && e->consts.weight_la == 1;
+    if (LA_ON) unit = unit && e->consts.la_w[0] == 1 && e->consts.la_w[1] == 1;
+    for (const kg_cls_desc &d : e->cls_desc)
+        for (int f = 0; f < 4; f++) unit = unit && d.fit_w[f] <= 1u;
+    if (unit) launch_cls4<MOST, FIT_ON, LA_ON, true>(e, grid, a, mask, scores, partials);
     else launch_cls4<MOST, FIT_ON, LA_ON, false>(e, grid, a, mask, scores, partials);
 }
 
