@@ -192,7 +192,7 @@ typedef struct kg_config {
 
     /* engine knobs */
     int32_t device;            /* HIP device ordinal */
-    int32_t place_chunk;       /* pods per refresh in kg_place (0 ⇒ default 64) */
+    int32_t place_chunk;       /* pods per refresh in kg_place (0 ⇒ default 8) */
 
     /* Reservation (profile weight, config/manager/scheduler-config.yaml:82-91 ships 5000) */
     int32_t weight_reservation;

@@ -40,7 +40,7 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
                 aggregated: Optional[dict] = None,
                 weight_numa: int = 1, numa_strategy: str = "LeastAllocated",
                 numa_hint_strategy: str = "LeastAllocated", numa_resources: Optional[Dict[str, int]] = None,
-                weight_reservation: int = 1, device: int = 0, place_chunk: int = 64) -> np.ndarray:
+                weight_reservation: int = 1, device: int = 0, place_chunk: int = 8) -> np.ndarray:
     c = np.zeros((), dtype=nat.CONFIG)
     c["abi_version"] = nat.ABI_VERSION
     bits = 0

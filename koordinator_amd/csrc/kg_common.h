@@ -183,62 +183,81 @@ KG_HD double kg_scaled_ratio(int64_t num, int64_t den) {
 }
 
 // Derived planes of node i from its canonical row (host ingest and device commit share this).
-KG_HD void kg_finalize_node(const kg_consts &c, const kg_planes &pl, int64_t i) {
+// Split in parts so the placement resolve can derive them with one thread per part:
+//   kg_finalize_fit(r)  Fit planes and free_ of resource r (r < KG_NUM_RES) → bit 0: slow, bit 1: in fit_mask
+//   kg_finalize_la(r)   LoadAware planes of resource r (r < 2)             → slow
+//   kg_finalize_flags   dflags / fit_mask / metric from the parts' results
+KG_HD uint32_t kg_finalize_fit(const kg_consts &c, const kg_planes &pl, int64_t i, int r) {
     const kg_node_row &row = pl.rows[i];
     const int64_t cap = pl.cap;
+    uint32_t out = 0;
+    pl.free_[r * cap + i] = row.alloc[r] - row.requested[r];
+    double R = 0.0, F = 0.0;
+    int64_t a = row.alloc[r];
+    bool present = r < 3 || ((row.alloc_present >> r) & 1u);
+    if (c.fit_w[r] > 0 && present && a != 0) {
+        out |= 2u;
+        int64_t base = r < 2 ? row.nonzero_requested[r] : row.requested[r];
+        if (a < 0 || a >= KG_CAP_LIMIT || kg_abs64(base) >= KG_VAL_LIMIT) {
+            out |= 1u;
+        } else {
+            R = 100.0 / (double)a;
+            F = c.fit_most ? kg_scaled_ratio(base, a) : kg_scaled_ratio(a - base, a);
+        }
+    }
+    pl.fit_R[r * cap + i] = R;
+    pl.fit_F[r * cap + i] = F;
+    return out;
+}
+KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, int r) {
+    const kg_node_row &row = pl.rows[i];
+    const int64_t cap = pl.cap;
+    bool slow = false;
+    int64_t a = row.la_alloc[r];
+    double R = 0.0, F0 = 0.0, F1 = 0.0;
+    if (a != 0) {
+        if (a < 0 || a >= KG_CAP_LIMIT || kg_abs64(row.la_used[0][r]) >= KG_VAL_LIMIT ||
+            kg_abs64(row.la_used[1][r]) >= KG_VAL_LIMIT) {
+            slow = true;
+        } else {
+            R = 100.0 / (double)a;
+            F0 = kg_scaled_ratio(a - row.la_used[0][r], a);
+            F1 = kg_scaled_ratio(a - row.la_used[1][r], a);
+        }
+    }
+    pl.la_R[r * cap + i] = R;
+    pl.la_F[(0 * 2 + r) * cap + i] = F0;
+    pl.la_F[(1 * 2 + r) * cap + i] = F1;
+    return slow;
+}
+KG_HD void kg_finalize_flags(const kg_planes &pl, int64_t i, bool slow, uint32_t fmask) {
+    const kg_node_row &row = pl.rows[i];
     uint32_t df = 0;
     if (row.flags & KG_NODE_VALID) df |= KGD_VALID;
     if ((int64_t)row.pod_count + 1 > (int64_t)row.allowed_pods) df |= KGD_PODS_FULL;
-    bool slow = false;
-    uint32_t fmask = 0;
-    for (int r = 0; r < KG_NUM_RES; r++) {
-        int64_t fr = row.alloc[r] - row.requested[r];
-        pl.free_[r * cap + i] = fr;
-        if (r == KG_RES_CPU && fr < 0) df |= KGD_OVER_CPU;
-        if (r == KG_RES_MEMORY && fr < 0) df |= KGD_OVER_MEM;
-        if (r == KG_RES_EPHEMERAL_STORAGE && fr < 0) df |= KGD_OVER_EPH;
-        double R = 0.0, F = 0.0;
-        int64_t a = row.alloc[r];
-        bool present = r < 3 || ((row.alloc_present >> r) & 1u);
-        if (c.fit_w[r] > 0 && present && a != 0) {
-            fmask |= 1u << r;
-            int64_t base = r < 2 ? row.nonzero_requested[r] : row.requested[r];
-            if (a < 0 || a >= KG_CAP_LIMIT || kg_abs64(base) >= KG_VAL_LIMIT) {
-                slow = true;
-            } else {
-                R = 100.0 / (double)a;
-                F = c.fit_most ? kg_scaled_ratio(base, a) : kg_scaled_ratio(a - base, a);
-            }
-        }
-        pl.fit_R[r * cap + i] = R;
-        pl.fit_F[r * cap + i] = F;
-    }
-    for (int r = 0; r < 2; r++) {
-        int64_t a = row.la_alloc[r];
-        double R = 0.0, F0 = 0.0, F1 = 0.0;
-        if (a != 0) {
-            if (a < 0 || a >= KG_CAP_LIMIT || kg_abs64(row.la_used[0][r]) >= KG_VAL_LIMIT ||
-                kg_abs64(row.la_used[1][r]) >= KG_VAL_LIMIT) {
-                slow = true;
-            } else {
-                R = 100.0 / (double)a;
-                F0 = kg_scaled_ratio(a - row.la_used[0][r], a);
-                F1 = kg_scaled_ratio(a - row.la_used[1][r], a);
-            }
-        }
-        pl.la_R[r * cap + i] = R;
-        pl.la_F[(0 * 2 + r) * cap + i] = F0;
-        pl.la_F[(1 * 2 + r) * cap + i] = F1;
-    }
+    if (row.alloc[KG_RES_CPU] - row.requested[KG_RES_CPU] < 0) df |= KGD_OVER_CPU;
+    if (row.alloc[KG_RES_MEMORY] - row.requested[KG_RES_MEMORY] < 0) df |= KGD_OVER_MEM;
+    if (row.alloc[KG_RES_EPHEMERAL_STORAGE] - row.requested[KG_RES_EPHEMERAL_STORAGE] < 0) df |= KGD_OVER_EPH;
     if (slow) df |= KGD_SLOW;
-    if (pl.rsv_of && pl.rsv_of[i] >= 0) df = (df & ~(KGD_VALID | KGD_SLOW)) | KGD_RSV;  // kg_rsv_pair owns it
     if (row.flags & KG_NODE_HAS_METRIC) df |= KGD_HAS_METRIC;
     if (row.flags & KG_NODE_HAS_UPDATE_TIME) df |= KGD_HAS_UPDATE;
     if (row.flags & KG_NODE_LA_PASS_NONPROD) df |= KGD_LA_PASS_NP;
     if (row.flags & KG_NODE_LA_PASS_PROD) df |= KGD_LA_PASS_P;
+    if (pl.rsv_of && pl.rsv_of[i] >= 0) df = (df & ~(KGD_VALID | KGD_SLOW)) | KGD_RSV;  // kg_rsv_pair owns it
     pl.metric_ns[i] = row.metric_update_ns;
     pl.fit_mask[i] = fmask;
     pl.dflags[i] = df;
+}
+KG_HD void kg_finalize_node(const kg_consts &c, const kg_planes &pl, int64_t i) {
+    bool slow = false;
+    uint32_t fmask = 0;
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        const uint32_t f = kg_finalize_fit(c, pl, i, r);
+        slow = slow || (f & 1u);
+        if (f & 2u) fmask |= 1u << r;
+    }
+    for (int r = 0; r < 2; r++) slow = kg_finalize_la(c, pl, i, r) || slow;
+    kg_finalize_flags(pl, i, slow, fmask);
 }
 
 // Reserve delta: NodeInfo.AddPod (requested += request, nonzero += nonzero, pods += 1;

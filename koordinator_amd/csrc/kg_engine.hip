@@ -1130,6 +1130,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     __shared__ int64_t redo[KG_RESOLVE_THREADS / 64];
     __shared__ int32_t n_touched, n_rescan, gate_ok;
     __shared__ unsigned long long wbest;
+    __shared__ uint32_t fin[KG_NUM_RES + 2];
     const int tid = threadIdx.x;
     if (tid == 0) n_touched = 0;
     for (int j = 0; j < n; j++) {
@@ -1198,14 +1199,13 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             if (tid == 0 && rk > wbest) wbest = rk;
         }
         __syncthreads();
+        const unsigned long long w = wbest;
+        const int32_t node = w ? (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull)) : -1;
         if (tid == 0) {
-            const unsigned long long w = wbest;
             if (w) {
-                const int32_t node = (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull));
                 rsv_quota_commit(pl, ra, pd, node);
                 kg_numa_commit(c, pl.rows[node], pd);
                 kg_apply_commit(pl.rows[node], pd);
-                kg_finalize_node(c, pl, node);
                 bool seen = false;
                 for (int q = 0; q < n_touched; q++) seen |= touched[q] == node;
                 if (!seen) touched[n_touched++] = node;
@@ -1217,6 +1217,26 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             }
         }
         __syncthreads();
+        if (w) {
+            // re-derive the committed node's planes, one thread per resource (the int64 divisions of
+            // kg_scaled_ratio dominate a serial kg_finalize_node); the flags take their results
+            if (tid < KG_NUM_RES) {
+                const uint32_t f = kg_finalize_fit(c, pl, node, tid);
+                fin[tid] = f;
+            } else if (tid < KG_NUM_RES + 2) {
+                fin[tid] = kg_finalize_la(c, pl, node, tid - KG_NUM_RES) ? 1u : 0u;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                bool slow = false;
+                uint32_t fmask = 0;
+                for (int r = 0; r < KG_NUM_RES + 2; r++) slow = slow || (fin[r] & 1u);
+                for (int r = 0; r < KG_NUM_RES; r++)
+                    if (fin[r] & 2u) fmask |= 1u << r;
+                kg_finalize_flags(pl, node, slow, fmask);
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -2065,7 +2085,7 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
         return set_err(e, KG_ERR_STATE, "kg_place runs on the whole snapshot; use the chunk API for shards");
     const int32_t P = e->n_pods;
     if (P == 0) return KG_OK;
-    int32_t chunk = e->cfg.place_chunk > 0 ? e->cfg.place_chunk : 64;
+    int32_t chunk = e->cfg.place_chunk > 0 ? e->cfg.place_chunk : 8;
     if (chunk > KG_MAX_CHUNK) chunk = KG_MAX_CHUNK;
     const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4;
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };

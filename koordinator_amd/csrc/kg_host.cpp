@@ -363,7 +363,7 @@ void kg_config_default(kg_config *c) {
     c->numa_hint_strategy = KG_STRATEGY_LEAST_ALLOCATED;
     c->numa_resource_weight[KG_RES_CPU] = 1;
     c->numa_resource_weight[KG_RES_MEMORY] = 1;
-    c->place_chunk = 64;
+    c->place_chunk = 8;
 }
 
 void kg_config_shipped_profile(kg_config *c) {

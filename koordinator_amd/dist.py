@@ -134,6 +134,6 @@ def place(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, now_ns: 
     device = device or torch.device("cuda", torch.cuda.current_device())
     eng = sharded_engine(cfg, node_rows, pod_rows, device, group)
     try:
-        return place_sharded(eng, now_ns, device, chunk=int(cfg["place_chunk"]) or 64, group=group)
+        return place_sharded(eng, now_ns, device, chunk=int(cfg["place_chunk"]) or 8, group=group)
     finally:
         eng.close()
