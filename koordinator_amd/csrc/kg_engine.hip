@@ -885,6 +885,77 @@ __global__ __launch_bounds__(256) void k_eval_numa(kg_consts c, kg_planes pl, Ho
     if (tid < np) partials[(int64_t)(p0 + tid) * a.tiles_total + tile] = keys[tid];
 }
 
+// NodeNUMAResource enabled, pod per lane: a wave holds 64 pods and walks 256 nodes of a tile one
+// node at a time, so every node-side value (derived planes, canonical row with its zones) is
+// wave-uniform (one cache line per load, served to all 64 pods) and the NUMA hint enumeration runs
+// on the node's structure for 64 requests at once.  Outputs accumulate per lane along the pod's own
+// row: 64 feasibility bits per u64 word, 8 score pairs per 16-byte store, 16 NUMA scores per 16-byte
+// store, the per-(pod, tile) key as a lane-private max (one atomicMax per wave).
+#define KG_NUMA2_NODES 256
+__global__ __launch_bounds__(256) void k_eval_numa2(kg_consts c, kg_planes pl, HotArgs a,
+                                                    const kg_pod_dev *__restrict__ pods,
+                                                    const kg_node_row *__restrict__ rows,
+                                                    unsigned long long *__restrict__ mask,
+                                                    uint16_t *__restrict__ scores, uint8_t *__restrict__ numa_scores,
+                                                    uint32_t *__restrict__ partials) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t tile = (int64_t)a.tile_begin + blockIdx.x;
+    const int p = blockIdx.y * 64 + lane;
+    const bool live = p < a.n_pods;
+    const kg_pod_dev pd = pods[live ? p : 0];
+    const int64_t base = tile * KG_TILE + wave * KG_NUMA2_NODES;
+    const BatchMasks bm{0xFFu, 0xFFu};
+    uint32_t best = 0;
+    uint64_t mword = 0;
+    uint32_t sacc[4] = {0u, 0u, 0u, 0u};
+    uint32_t nacc[4] = {0u, 0u, 0u, 0u};
+    for (int k = 0; k < KG_NUMA2_NODES; k++) {
+        const int64_t node = base + k;
+        const bool in_range = node < a.node_end;
+        uint32_t fit = 0, la = 0, nsc = 0;
+        bool ok = false;
+        if (in_range) {  // wave-uniform branch
+            NodeRegs n;
+            load_node(c, pl, node, true, bm, a.now_ns, n);
+            ok = eval_pair(c, pl, pd, n, node, a.now_ns, fit, la);
+            kg_numa_out o;
+            kg_numa_pair(c, rows[node], pd, o);
+            ok = ok && o.feasible;
+            nsc = o.score;
+        }
+        const uint32_t local = (uint32_t)(node - tile * KG_TILE);
+        if (ok) {
+            const uint32_t key = ((total_of(c, fit, la, nsc) + 1u) << KG_TILE_SHIFT) | (KG_TILE - 1u - local);
+            best = best > key ? best : key;
+        }
+        mword |= (uint64_t)ok << (k & 63);
+        sacc[(k & 7) >> 1] |= (fit | (la << 8)) << ((k & 1) * 16);
+        nacc[(k & 15) >> 2] |= nsc << ((k & 3) * 8);
+        const int64_t col = node - a.col_begin;
+        if ((k & 7) == 7) {
+            const int64_t c0 = col - 7;
+            if (live && scores && c0 < a.score_stride)
+                *reinterpret_cast<uint4 *>(scores + (int64_t)p * a.score_stride + c0) =
+                    make_uint4(sacc[0], sacc[1], sacc[2], sacc[3]);
+            sacc[0] = sacc[1] = sacc[2] = sacc[3] = 0u;
+        }
+        if ((k & 15) == 15) {
+            const int64_t c0 = col - 15;
+            if (live && numa_scores && c0 < a.score_stride)
+                *reinterpret_cast<uint4 *>(numa_scores + (int64_t)p * a.score_stride + c0) =
+                    make_uint4(nacc[0], nacc[1], nacc[2], nacc[3]);
+            nacc[0] = nacc[1] = nacc[2] = nacc[3] = 0u;
+        }
+        if ((k & 63) == 63) {
+            const int64_t c0 = col - 63;
+            if (live && mask && c0 < (int64_t)a.mask_words * 64) mask[(int64_t)p * a.mask_words + (c0 >> 6)] = mword;
+            mword = 0;
+        }
+    }
+    if (live && best) atomicMax(&partials[(int64_t)p * a.tiles_total + tile], best);
+}
+
 __device__ __forceinline__ unsigned long long decode_partial(uint32_t k, int tile) {
     if (k == 0) return 0ull;
     const uint32_t node = (uint32_t)tile * KG_TILE + (KG_TILE - 1) - (k & (KG_TILE - 1));
@@ -1595,10 +1666,16 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     for (int s = 0; s < 8; s++) a.slot_res[s] = s < e->nslot ? e->slot_res[s] : -1;
     a.now_ns = now_ns;
     if (e->consts.plugins & KG_PLUGIN_NUMA) {
-        dim3 grid((unsigned)shard_tiles, (unsigned)((n + KG_NUMA_PODS - 1) / KG_NUMA_PODS));
         if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
-        hipLaunchKernelGGL(k_eval_numa, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
-                           (unsigned long long *)mask, scores, numa_scores, partials);
+        if (n >= 64) {  // pod per lane needs full waves of pods; placement chunks keep node per lane
+            dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64));
+            hipLaunchKernelGGL(k_eval_numa2, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
+                               e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials);
+        } else {
+            dim3 grid((unsigned)shard_tiles, (unsigned)((n + KG_NUMA_PODS - 1) / KG_NUMA_PODS));
+            hipLaunchKernelGGL(k_eval_numa, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
+                               (unsigned long long *)mask, scores, numa_scores, partials);
+        }
         HIP_TRY(e, hipGetLastError());
         if (e->profiling) {
             HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
