@@ -72,7 +72,7 @@ class ChunkBackend(Protocol):
                       score_ptr: int) -> None: ...
 
 
-def place_sharded(backend: ChunkBackend, now_ns: int, device: torch.device, chunk: int = 64,
+def place_sharded(backend: ChunkBackend, now_ns: int, device: torch.device, chunk: int = 8,
                   group=None) -> Tuple[np.ndarray, np.ndarray]:
     """Sequential-cycle placement of the backend's pod batch, node-sharded across the group.
 
@@ -106,12 +106,14 @@ class _nullctx:
 
 
 def sharded_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, device: torch.device,
-                   group=None):
+                   group=None, reservations: Optional[np.ndarray] = None, quotas: Optional[np.ndarray] = None):
     """A HIP engine on `device` holding the full snapshot, restricted to this rank's node shard.
 
     The engine is bound to a dedicated torch stream (``eng.torch_stream``); `place_sharded` runs the
     collectives and tensor ops on that same stream, so engine kernels and merges are ordered. (The
-    legacy null stream cannot be shared: ``kg_set_stream(NULL)`` means an engine-owned stream.)"""
+    legacy null stream cannot be shared: ``kg_set_stream(NULL)`` means an engine-owned stream.)
+    Reservation slots and ElasticQuota groups are replicated like the snapshot: every rank evaluates
+    all reservation nodes and applies the same quota gate in its (identical) resolve."""
     from .engine import Engine
 
     rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -122,6 +124,10 @@ def sharded_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray,
     eng.torch_stream = torch.cuda.Stream(device)
     eng.set_stream(eng.torch_stream.cuda_stream)
     eng.load_snapshot(node_rows)
+    if reservations is not None:
+        eng.set_reservations(reservations)
+    if quotas is not None:
+        eng.set_quotas(quotas)
     eng.set_pods(pod_rows)
     begin, end = shard_range(len(node_rows), rank, world)
     eng.set_shard(begin, end)
@@ -129,10 +135,11 @@ def sharded_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray,
 
 
 def place(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, now_ns: int,
-          device: Optional[torch.device] = None, group=None) -> Tuple[np.ndarray, np.ndarray]:
+          device: Optional[torch.device] = None, group=None, reservations: Optional[np.ndarray] = None,
+          quotas: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
     """Convenience wrapper: build the sharded engine, place the batch, release the engine."""
     device = device or torch.device("cuda", torch.cuda.current_device())
-    eng = sharded_engine(cfg, node_rows, pod_rows, device, group)
+    eng = sharded_engine(cfg, node_rows, pod_rows, device, group, reservations, quotas)
     try:
         return place_sharded(eng, now_ns, device, chunk=int(cfg["place_chunk"]) or 8, group=group)
     finally:

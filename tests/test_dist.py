@@ -149,3 +149,42 @@ def test_sharded_engine_two_ranks_one_gpu():
     for rank, placed_ok, top1_ok in res:
         assert placed_ok, f"rank {rank}: sharded placement differs from the sequential oracle"
         assert top1_ok, f"rank {rank}: merged top-1 differs from the oracle"
+
+
+def _gpu_rsv_worker(rank, world, port, q):
+    from oracle import oracle
+
+    _init(rank, world, port)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        cl = synth.make_rsv_cluster(5_000, 300, seed=72, n_quotas=8, quota_ratio=0.6)
+        cfg = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "Reservation", "ElasticQuota"))
+        idx = np.arange(300)
+        nodes = engine.build_node_rows(cfg, cl)
+        pods = engine.build_pod_rows(cfg, cl, idx)
+        got_n, got_s = kdist.place(cfg, nodes, pods, cl.now_ns, device=dev, reservations=cl.rsv_arr,
+                                   quotas=cl.quota_arr)
+        ref_n, ref_s, _, _ = oracle.schedule2(cfg, cl, idx, cl.now_ns)
+        q.put((rank, np.array_equal(got_n, ref_n) and np.array_equal(got_s, ref_s), bool((ref_n == -1).any())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_placement_reservation_quota_two_ranks_one_gpu():
+    """Config 5 through the node-sharded placement: replicated reservation / quota state, per-tile
+    partial keys merged over the ranks, identical resolves."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_rsv_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=110) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, placed_ok, some_rejected in res:
+        assert placed_ok, f"rank {rank}: sharded placement differs from the sequential oracle"
+        assert some_rejected
