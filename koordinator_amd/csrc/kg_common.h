@@ -518,8 +518,10 @@ KG_HD void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod
                     kg_numa_visit(c, row, p, best, a, true, full, false, true);
                     continue;
                 }
+                // a permutation with a & b == 0 is skipped by kg_numa_visit: test that before the
+                // (zone-sum) fit of b, so disjoint single-zone hints cost a bit test, not Z² sums
                 for (uint32_t b = (1u << L[1].k) - 1u; b; b = kg_combo_next(b, Z))
-                    if (kg_list_fits(row, L[1], b)) kg_numa_visit(c, row, p, best, a, true, b, true, true);
+                    if ((a & b) && kg_list_fits(row, L[1], b)) kg_numa_visit(c, row, p, best, a, true, b, true, true);
             }
         }
         if (!best.pref && policy == KG_NUMA_BEST_EFFORT) {
@@ -536,7 +538,7 @@ KG_HD void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod
                     const int kb0 = L[1].any ? 1 : 0, kb1 = L[1].any ? Z : 0;
                     for (int kb = kb0; kb <= kb1; kb++) {
                         for (uint32_t b = kb ? (1u << kb) - 1u : full; b; b = kb ? kg_combo_next(b, Z) : 0u) {
-                            if (kb && !kg_list_fits(row, L[1], b)) continue;
+                            if (!(a & b) || (kb && !kg_list_fits(row, L[1], b))) continue;
                             const bool pb = kb == L[1].k;
                             kg_numa_visit(c, row, p, best, a, ka != 0, b, kb != 0, pa && ka != 0 && pb && kb != 0);
                         }
