@@ -316,8 +316,24 @@ struct kg_numa_out {
     int64_t alloc[KG_MAX_ZONES][2];   // allocated cpu, memory
 };
 
-KG_HD int64_t kg_lr_i(int64_t req, int64_t cap) { return (cap == 0 || req > cap) ? 0 : ((cap - req) * 100) / cap; }
-KG_HD int64_t kg_mr_i(int64_t req, int64_t cap) { return cap == 0 ? 0 : ((req > cap ? cap : req) * 100) / cap; }
+// n / d (Go int64 division) for the score quotients: when 0 ≤ n < 128·d and d < 2^40 the quotient
+// is < 128, so one fp32 estimate (relative error < 2^-21, absolute < 2^-14) is off by at most one
+// and a single exact int64 multiply-compare settles it; every other operand takes the division
+KG_HD int64_t kg_qdiv(int64_t n, int64_t d) {
+    if (n < 0 || d <= 0 || d >= (1LL << 40) || n >= (d << 7)) return n / d;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float r = __builtin_amdgcn_rcpf((float)d);
+#else
+    const float r = 1.0f / (float)d;
+#endif
+    int64_t q = (int64_t)((float)n * r);
+    const int64_t t = q * d;
+    if (t > n) q--;
+    else if (t + d <= n) q++;
+    return q;
+}
+KG_HD int64_t kg_lr_i(int64_t req, int64_t cap) { return (cap == 0 || req > cap) ? 0 : kg_qdiv((cap - req) * 100, cap); }
+KG_HD int64_t kg_mr_i(int64_t req, int64_t cap) { return cap == 0 ? 0 : kg_qdiv((req > cap ? cap : req) * 100, cap); }
 
 // resourceAllocationScorer.score (scoring.go:187-226) where only cpu / memory can be allocatable
 // (zone sums): every other resource is either native with allocatable 0 or a missing scalar key.
@@ -330,7 +346,7 @@ KG_HD uint32_t kg_numa_score_zones(const kg_consts &c, bool most, const int64_t 
         s += (most ? kg_mr_i(rq, total[r]) : kg_lr_i(rq, total[r])) * c.numa_w[r];
         w += c.numa_w[r];
     }
-    return w ? (uint32_t)(s / w) : 0u;
+    return w ? (uint32_t)kg_qdiv(s, w) : 0u;
 }
 
 // the same over the node's Requested / Allocatable (policy None, or nothing allocated in zones)
@@ -347,7 +363,7 @@ KG_HD uint32_t kg_numa_score_node(const kg_consts &c, const kg_node_row &row, co
         s += (c.numa_most ? kg_mr_i(rq, a) : kg_lr_i(rq, a)) * c.numa_w[r];
         w += c.numa_w[r];
     }
-    return w ? (uint32_t)(s / w) : 0u;
+    return w ? (uint32_t)kg_qdiv(s, w) : 0u;
 }
 
 // zone total / available of resource r ∈ {cpu, memory} for zone i (available = max(total − allocated, 0))
@@ -377,6 +393,84 @@ KG_HD uint64_t kg_id_mask(const kg_node_row &row, uint32_t m) {
     return out;
 }
 
+// Zone-sum providers for the hint enumeration.  kg_zone_calc sums the canonical row's zones per
+// call (host, placement kernels); kg_zone_tab reads a per-node table of every index mask's sums, id
+// mask and the descending-total prefix sums, built once per node by kg_zone_tab_fill (k_eval_numa2
+// keeps it in LDS, so the per-pair enumeration over a wave's pods does table lookups).  Both derive
+// every value with the same functions, so the pair results are identical.
+struct kg_zone_calc {
+    const kg_node_row &row;
+    KG_HD void sums(uint32_t m, int64_t tot[2], int64_t av[2]) const { kg_mask_sums(row, m, tot, av); }
+    KG_HD uint64_t idmask(uint32_t m) const { return kg_id_mask(row, m); }
+    // minimum affinity of resource r ∈ {cpu, memory}: fewest zones whose largest totals cover q
+    KG_HD int min_k(int r, int64_t q, int Z) const {
+        int64_t t[KG_MAX_ZONES];
+        for (int i = 0; i < Z; i++) t[i] = kg_zone_total(row, i, r);
+        int64_t acc = 0;
+        for (int k = 1; k <= Z; k++) {
+            int best_i = 0;
+            for (int i = 1; i < Z; i++)
+                if (t[i] > t[best_i]) best_i = i;
+            acc += t[best_i];
+            t[best_i] = -1;
+            if (acc >= q) return k;
+        }
+        return Z;
+    }
+};
+
+#define KG_ZTAB_MASKS (1 << KG_MAX_ZONES)
+struct kg_zone_tab_data {
+    int64_t tot[2][KG_ZTAB_MASKS], av[2][KG_ZTAB_MASKS];
+    uint64_t idm[KG_ZTAB_MASKS];
+    int64_t pref[2][KG_MAX_ZONES + 1];   // pref[r][k]: the acc of kg_zone_calc::min_k after k picks
+};
+
+struct kg_zone_tab {
+    const kg_zone_tab_data &d;
+    KG_HD void sums(uint32_t m, int64_t tot[2], int64_t av[2]) const {
+        tot[0] = d.tot[0][m];
+        tot[1] = d.tot[1][m];
+        av[0] = d.av[0][m];
+        av[1] = d.av[1][m];
+    }
+    KG_HD uint64_t idmask(uint32_t m) const { return d.idm[m]; }
+    KG_HD int min_k(int r, int64_t q, int Z) const {
+        for (int k = 1; k <= Z; k++)
+            if (d.pref[r][k] >= q) return k;
+        return Z;
+    }
+};
+
+// one lane's share of the table: masks lane, lane + nlanes, ... below 2^Z; lanes 0 and 1 the prefix sums
+KG_HD void kg_zone_tab_fill(const kg_node_row &row, int lane, int nlanes, kg_zone_tab_data &d) {
+    const int Z = row.n_zones;
+    for (int m = lane; m < (1 << Z); m += nlanes) {
+        int64_t tot[2], av[2];
+        kg_mask_sums(row, (uint32_t)m, tot, av);
+        d.tot[0][m] = tot[0];
+        d.tot[1][m] = tot[1];
+        d.av[0][m] = av[0];
+        d.av[1][m] = av[1];
+        d.idm[m] = kg_id_mask(row, (uint32_t)m);
+    }
+    if (lane < 2) {
+        const int r = lane;
+        int64_t t[KG_MAX_ZONES];
+        for (int i = 0; i < Z; i++) t[i] = kg_zone_total(row, i, r);
+        int64_t acc = 0;
+        d.pref[r][0] = 0;
+        for (int k = 1; k <= Z; k++) {
+            int best_i = 0;
+            for (int i = 1; i < Z; i++)
+                if (t[i] > t[best_i]) best_i = i;
+            acc += t[best_i];
+            t[best_i] = -1;
+            d.pref[r][k] = acc;
+        }
+    }
+}
+
 // lexicographic successor of a k-combination of {0..Z-1} held as an index bitmask (0 when done):
 // bitmask.IterateBitMasks order within one size
 KG_HD uint32_t kg_combo_next(uint32_t m, int Z) {
@@ -395,11 +489,12 @@ struct kg_numa_list {
     int64_t req;
 };
 
-KG_HD bool kg_list_fits(const kg_node_row &row, const kg_numa_list &l, uint32_t m) {
+template <class ZS>
+KG_HD bool kg_list_fits(const ZS &zs, const kg_numa_list &l, uint32_t m) {
     if (l.req == 0) return true;
     if (l.res > 1) return false;
     int64_t tot[2], av[2];
-    kg_mask_sums(row, m, tot, av);
+    zs.sums(m, tot, av);
     return tot[l.res] >= l.req && av[l.res] >= l.req;
 }
 
@@ -419,24 +514,28 @@ KG_HD void kg_numa_fold(kg_numa_best &b, uint64_t m, bool pref, uint32_t score) 
 }
 
 // score of a hint mask (generateResourceHints: the NUMA scorer over requested = total − available)
-KG_HD uint32_t kg_hint_score(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, uint32_t m) {
+template <class ZS>
+KG_HD uint32_t kg_hint_score(const kg_consts &c, const ZS &zs, const kg_pod_dev &p, uint32_t m) {
     int64_t tot[2], av[2];
-    kg_mask_sums(row, m, tot, av);
+    zs.sums(m, tot, av);
     const int64_t used[2] = {tot[0] - av[0], tot[1] - av[1]};
     return kg_numa_score_zones(c, c.numa_hint_most != 0, used, tot, p);
 }
 
 // one permutation (masks a, b in index space; `full` stands for a nil hint of an empty list)
-KG_HD void kg_numa_visit(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_best &best,
+template <class ZS>
+KG_HD void kg_numa_visit(const kg_consts &c, const ZS &zs, const kg_pod_dev &p, kg_numa_best &best,
                          uint32_t a, bool a_hint, uint32_t b, bool b_hint, bool pref) {
     const uint32_t m = a & b;
     if (m == 0) return;
     const bool member = (a_hint && a == m) || (b_hint && b == m);
-    kg_numa_fold(best, kg_id_mask(row, m), pref, member ? kg_hint_score(c, row, p, m) : 0u);
+    kg_numa_fold(best, zs.idmask(m), pref, member ? kg_hint_score(c, zs, p, m) : 0u);
 }
 
 // Filter + Score of NodeNUMAResource for one pair; o.zone / o.alloc are what Reserve records.
-KG_HD void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o) {
+template <class ZS>
+KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
+                          const ZS &zs) {
     o.feasible = true;
     o.score = 0;
     o.n_alloc = 0;
@@ -472,25 +571,11 @@ KG_HD void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod
         kg_numa_list l{r, Z, false, q};
         bool keyed = false;   // some zone's total has the resource (totalResourceNames)
         if (r <= KG_RES_MEMORY) {
-            int64_t t[KG_MAX_ZONES];
-            int64_t tot_all = 0, av_all = 0;
-            for (int i = 0; i < Z; i++) {
-                t[i] = kg_zone_total(row, i, r);
-                tot_all += t[i];
-                av_all += kg_zone_avail(row, i, r);
-                if ((row.zone_keys >> (2 * i + r)) & 1u) keyed = true;
-            }
-            // minimum affinity: fewest zones whose largest totals cover the request
-            int64_t acc = 0;
-            for (int k = 1; k <= Z; k++) {
-                int best_i = 0;
-                for (int i = 1; i < Z; i++)
-                    if (t[i] > t[best_i]) best_i = i;
-                acc += t[best_i];
-                t[best_i] = -1;
-                if (acc >= q) { l.k = k; break; }
-            }
-            l.any = tot_all >= q && av_all >= q;
+            int64_t tot_all[2], av_all[2];
+            zs.sums(full, tot_all, av_all);
+            keyed = (row.zone_keys & (0x5555u << r) & ((1u << (2 * Z)) - 1u)) != 0;
+            l.k = zs.min_k(r, q, Z);   // minimum affinity: fewest zones whose largest totals cover q
+            l.any = tot_all[r] >= q && av_all[r] >= q;
         } else if (q == 0) {
             l.k = 1;       // a zero request fits every mask
             l.any = true;
@@ -503,7 +588,7 @@ KG_HD void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod
         L[nl++] = l;
     }
     const bool single = policy == KG_NUMA_SINGLE_NUMA_NODE;
-    const uint64_t dflt = kg_id_mask(row, full);
+    const uint64_t dflt = zs.idmask(full);
     kg_numa_best best{dflt, false, 0u};
     if (nl == 0) {
         best = kg_numa_best{dflt, true, 0u};   // no provider hints: any affinity, preferred
@@ -513,15 +598,15 @@ KG_HD void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod
             if (!L[i].any || (single && L[i].k != 1)) can_pref = false;
         if (can_pref) {
             for (uint32_t a = (1u << L[0].k) - 1u; a; a = kg_combo_next(a, Z)) {
-                if (!kg_list_fits(row, L[0], a)) continue;
+                if (!kg_list_fits(zs, L[0], a)) continue;
                 if (nl == 1) {
-                    kg_numa_visit(c, row, p, best, a, true, full, false, true);
+                    kg_numa_visit(c, zs, p, best, a, true, full, false, true);
                     continue;
                 }
                 // a permutation with a & b == 0 is skipped by kg_numa_visit: test that before the
                 // (zone-sum) fit of b, so disjoint single-zone hints cost a bit test, not Z² sums
                 for (uint32_t b = (1u << L[1].k) - 1u; b; b = kg_combo_next(b, Z))
-                    if ((a & b) && kg_list_fits(row, L[1], b)) kg_numa_visit(c, row, p, best, a, true, b, true, true);
+                    if ((a & b) && kg_list_fits(zs, L[1], b)) kg_numa_visit(c, zs, p, best, a, true, b, true, true);
             }
         }
         if (!best.pref && policy == KG_NUMA_BEST_EFFORT) {
@@ -529,18 +614,18 @@ KG_HD void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod
             const int ka0 = L[0].any ? 1 : 0, ka1 = L[0].any ? Z : 0;
             for (int ka = ka0; ka <= ka1; ka++) {
                 for (uint32_t a = ka ? (1u << ka) - 1u : full; a; a = ka ? kg_combo_next(a, Z) : 0u) {
-                    if (ka && !kg_list_fits(row, L[0], a)) continue;
+                    if (ka && !kg_list_fits(zs, L[0], a)) continue;
                     const bool pa = ka == L[0].k;
                     if (nl == 1) {
-                        kg_numa_visit(c, row, p, best, a, ka != 0, full, false, pa && ka != 0);
+                        kg_numa_visit(c, zs, p, best, a, ka != 0, full, false, pa && ka != 0);
                         continue;
                     }
                     const int kb0 = L[1].any ? 1 : 0, kb1 = L[1].any ? Z : 0;
                     for (int kb = kb0; kb <= kb1; kb++) {
                         for (uint32_t b = kb ? (1u << kb) - 1u : full; b; b = kb ? kg_combo_next(b, Z) : 0u) {
-                            if (!(a & b) || (kb && !kg_list_fits(row, L[1], b))) continue;
+                            if (!(a & b) || (kb && !kg_list_fits(zs, L[1], b))) continue;
                             const bool pb = kb == L[1].k;
-                            kg_numa_visit(c, row, p, best, a, ka != 0, b, kb != 0, pa && ka != 0 && pb && kb != 0);
+                            kg_numa_visit(c, zs, p, best, a, ka != 0, b, kb != 0, pa && ka != 0 && pb && kb != 0);
                         }
                     }
                 }
@@ -601,6 +686,17 @@ KG_HD void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod
     } else {
         o.score = kg_numa_score_node(c, row, p);
     }
+}
+
+// Out of line on the device: the sequential k_resolve and the placement-chunk kernel keep their own
+// register budget instead of inheriting the hint enumeration's
+#if defined(__HIPCC__)
+static __host__ __device__ __noinline__
+#else
+inline
+#endif
+void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o) {
+    kg_numa_pair_z(c, row, p, o, kg_zone_calc{row});
 }
 
 // Reserve of NodeNUMAResource (plugin.go:375-419): record the zone allocations of the chosen node

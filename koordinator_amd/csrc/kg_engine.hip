@@ -892,7 +892,7 @@ __global__ __launch_bounds__(256) void k_eval_numa(kg_consts c, kg_planes pl, Ho
 // row: 64 feasibility bits per u64 word, 8 score pairs per 16-byte store, 16 NUMA scores per 16-byte
 // store, the per-(pod, tile) key as a lane-private max (one atomicMax per wave).
 #define KG_NUMA2_NODES 256
-__global__ __launch_bounds__(256) void k_eval_numa2(kg_consts c, kg_planes pl, HotArgs a,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_eval_numa2(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_pod_dev *__restrict__ pods,
                                                     const kg_node_row *__restrict__ rows,
                                                     unsigned long long *__restrict__ mask,
@@ -906,6 +906,10 @@ __global__ __launch_bounds__(256) void k_eval_numa2(kg_consts c, kg_planes pl, H
     const kg_pod_dev pd = pods[live ? p : 0];
     const int64_t base = tile * KG_TILE + wave * KG_NUMA2_NODES;
     const BatchMasks bm{0xFFu, 0xFFu};
+    // per-wave zone table of the current node (every index mask's sums and id mask, prefix sums of
+    // the descending totals): filled by the wave's 64 lanes, read by the hint enumeration of its pods
+    __shared__ kg_zone_tab_data ztab[256 / 64];
+    kg_zone_tab_data &zt = ztab[wave];
     uint32_t best = 0;
     uint64_t mword = 0;
     uint32_t sacc[4] = {0u, 0u, 0u, 0u};
@@ -919,8 +923,18 @@ __global__ __launch_bounds__(256) void k_eval_numa2(kg_consts c, kg_planes pl, H
             NodeRegs n;
             load_node(c, pl, node, true, bm, a.now_ns, n);
             ok = eval_pair(c, pl, pd, n, node, a.now_ns, fit, la);
-            kg_numa_out o;
-            kg_numa_pair(c, rows[node], pd, o);
+            const kg_node_row &row = rows[node];
+            const bool zoned = (row.flags & KG_NODE_NUMA_OPTIONS) && row.numa_policy != KG_NUMA_NONE &&
+                               row.n_zones > 0;   // n_zones ≤ KG_MAX_ZONES (kg_build_node_rows)
+            if (zoned) {  // wave-uniform; the previous node's reads precede these writes (in-order LDS per wave)
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                kg_zone_tab_fill(row, lane, 64, zt);
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+            }
+            kg_numa_out o;   // a node without zones returns before the hint enumeration reads the table
+            kg_numa_pair_z(c, row, pd, o, kg_zone_tab{zt});
             ok = ok && o.feasible;
             nsc = o.score;
         }
