@@ -393,6 +393,17 @@ KG_HD uint64_t kg_id_mask(const kg_node_row &row, uint32_t m) {
     return out;
 }
 
+// lexicographic successor of a k-combination of {0..Z-1} held as an index bitmask (0 when done):
+// bitmask.IterateBitMasks order within one size
+KG_HD uint32_t kg_combo_next(uint32_t m, int Z) {
+    int cnt = 0, t = Z - 1;
+    while (t >= 0 && ((m >> t) & 1u)) { cnt++; t--; }
+    int b = t;
+    while (b >= 0 && !((m >> b) & 1u)) b--;
+    if (b < 0) return 0;
+    return (m & ((1u << b) - 1u)) | (((1u << (cnt + 1)) - 1u) << (b + 1));
+}
+
 // Zone-sum providers for the hint enumeration.  kg_zone_calc sums the canonical row's zones per
 // call (host, placement kernels); kg_zone_tab reads a per-node table of every index mask's sums, id
 // mask and the descending-total prefix sums, built once per node by kg_zone_tab_fill (k_eval_numa2
@@ -402,6 +413,7 @@ struct kg_zone_calc {
     const kg_node_row &row;
     KG_HD void sums(uint32_t m, int64_t tot[2], int64_t av[2]) const { kg_mask_sums(row, m, tot, av); }
     KG_HD uint64_t idmask(uint32_t m) const { return kg_id_mask(row, m); }
+    KG_HD uint32_t next(uint32_t m, int Z) const { return kg_combo_next(m, Z); }
     // minimum affinity of resource r ∈ {cpu, memory}: fewest zones whose largest totals cover q
     KG_HD int min_k(int r, int64_t q, int Z) const {
         int64_t t[KG_MAX_ZONES];
@@ -423,6 +435,7 @@ struct kg_zone_calc {
 struct kg_zone_tab_data {
     int64_t tot[2][KG_ZTAB_MASKS], av[2][KG_ZTAB_MASKS];
     uint64_t idm[KG_ZTAB_MASKS];
+    uint8_t succ[KG_ZTAB_MASKS];         // kg_combo_next(m, n_zones)
     int64_t pref[2][KG_MAX_ZONES + 1];   // pref[r][k]: the acc of kg_zone_calc::min_k after k picks
 };
 
@@ -435,6 +448,7 @@ struct kg_zone_tab {
         av[1] = d.av[1][m];
     }
     KG_HD uint64_t idmask(uint32_t m) const { return d.idm[m]; }
+    KG_HD uint32_t next(uint32_t m, int) const { return d.succ[m]; }
     KG_HD int min_k(int r, int64_t q, int Z) const {
         for (int k = 1; k <= Z; k++)
             if (d.pref[r][k] >= q) return k;
@@ -453,6 +467,7 @@ KG_HD void kg_zone_tab_fill(const kg_node_row &row, int lane, int nlanes, kg_zon
         d.av[0][m] = av[0];
         d.av[1][m] = av[1];
         d.idm[m] = kg_id_mask(row, (uint32_t)m);
+        d.succ[m] = (uint8_t)kg_combo_next((uint32_t)m, Z);
     }
     if (lane < 2) {
         const int r = lane;
@@ -469,17 +484,6 @@ KG_HD void kg_zone_tab_fill(const kg_node_row &row, int lane, int nlanes, kg_zon
             d.pref[r][k] = acc;
         }
     }
-}
-
-// lexicographic successor of a k-combination of {0..Z-1} held as an index bitmask (0 when done):
-// bitmask.IterateBitMasks order within one size
-KG_HD uint32_t kg_combo_next(uint32_t m, int Z) {
-    int cnt = 0, t = Z - 1;
-    while (t >= 0 && ((m >> t) & 1u)) { cnt++; t--; }
-    int b = t;
-    while (b >= 0 && !((m >> b) & 1u)) b--;
-    if (b < 0) return 0;
-    return (m & ((1u << b) - 1u)) | (((1u << (cnt + 1)) - 1u) << (b + 1));
 }
 
 struct kg_numa_list {
@@ -597,7 +601,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
         for (int i = 0; i < nl; i++)
             if (!L[i].any || (single && L[i].k != 1)) can_pref = false;
         if (can_pref) {
-            for (uint32_t a = (1u << L[0].k) - 1u; a; a = kg_combo_next(a, Z)) {
+            for (uint32_t a = (1u << L[0].k) - 1u; a; a = zs.next(a, Z)) {
                 if (!kg_list_fits(zs, L[0], a)) continue;
                 if (nl == 1) {
                     kg_numa_visit(c, zs, p, best, a, true, full, false, true);
@@ -605,7 +609,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
                 }
                 // a permutation with a & b == 0 is skipped by kg_numa_visit: test that before the
                 // (zone-sum) fit of b, so disjoint single-zone hints cost a bit test, not Z² sums
-                for (uint32_t b = (1u << L[1].k) - 1u; b; b = kg_combo_next(b, Z))
+                for (uint32_t b = (1u << L[1].k) - 1u; b; b = zs.next(b, Z))
                     if ((a & b) && kg_list_fits(zs, L[1], b)) kg_numa_visit(c, zs, p, best, a, true, b, true, true);
             }
         }
@@ -613,7 +617,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
             // no preferred permutation: the full fold, hints of every size in IterateBitMasks order
             const int ka0 = L[0].any ? 1 : 0, ka1 = L[0].any ? Z : 0;
             for (int ka = ka0; ka <= ka1; ka++) {
-                for (uint32_t a = ka ? (1u << ka) - 1u : full; a; a = ka ? kg_combo_next(a, Z) : 0u) {
+                for (uint32_t a = ka ? (1u << ka) - 1u : full; a; a = ka ? zs.next(a, Z) : 0u) {
                     if (ka && !kg_list_fits(zs, L[0], a)) continue;
                     const bool pa = ka == L[0].k;
                     if (nl == 1) {
@@ -622,7 +626,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
                     }
                     const int kb0 = L[1].any ? 1 : 0, kb1 = L[1].any ? Z : 0;
                     for (int kb = kb0; kb <= kb1; kb++) {
-                        for (uint32_t b = kb ? (1u << kb) - 1u : full; b; b = kb ? kg_combo_next(b, Z) : 0u) {
+                        for (uint32_t b = kb ? (1u << kb) - 1u : full; b; b = kb ? zs.next(b, Z) : 0u) {
                             if (!(a & b) || (kb && !kg_list_fits(zs, L[1], b))) continue;
                             const bool pb = kb == L[1].k;
                             kg_numa_visit(c, zs, p, best, a, ka != 0, b, kb != 0, pa && ka != 0 && pb && kb != 0);
