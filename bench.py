@@ -78,7 +78,7 @@ def cpu_model() -> str:
 def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
     """BASELINE config 3: the shipped profile with NodeNUMAResource (weight 1) over 100k nodes with
     4/6/8 NUMA zones (synth.make_numa_cluster, seed 3).  Matrix mode: feasibility + Fit / LoadAware /
-    NUMA score planes + top-1 (k_eval_numa); placement: sequential cycle with zone Reserve."""
+    NUMA score planes + top-1 (k_eval_numa2: pod per lane, per-wave LDS zone table); placement: sequential cycle with zone Reserve."""
     import torch
 
     from koordinator_amd import _native as nat
@@ -120,7 +120,7 @@ def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
     return {"workload": f"config3: {P} pods x {N} nodes, 4/6/8 NUMA zones, policy mix 40% SingleNUMANode / 30% "
                         "Restricted / 30% None, 60% LS / 40% batch pods, shipped profile + NodeNUMAResource",
             "evals_per_s": round(P * N / ((t1 - t0) / steps), 1), "ms_per_step": round((t1 - t0) / steps * 1e3, 3),
-            "kernel": "k_eval_numa", "kernel_ms": round(k_ms, 3), "feasible_frac_sample": round(feasible, 4),
+            "kernel": "k_eval_numa2", "kernel_ms": round(k_ms, 3), "feasible_frac_sample": round(feasible, 4),
             "placement": {"pods": P, "seconds": round(tp1 - tp0, 4), "pods_placed_per_s": round(P / (tp1 - tp0), 1),
                           "placed": int((nodes >= 0).sum())}}
 

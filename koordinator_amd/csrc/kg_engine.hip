@@ -892,6 +892,7 @@ __global__ __launch_bounds__(256) void k_eval_numa(kg_consts c, kg_planes pl, Ho
 // row: 64 feasibility bits per u64 word, 8 score pairs per 16-byte store, 16 NUMA scores per 16-byte
 // store, the per-(pod, tile) key as a lane-private max (one atomicMax per wave).
 #define KG_NUMA2_NODES 256
+#define KG_NUMA2_MIN_PODS 1   // below it: k_eval_numa (node per lane)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_eval_numa2(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_pod_dev *__restrict__ pods,
                                                     const kg_node_row *__restrict__ rows,
@@ -904,7 +905,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const int p = blockIdx.y * 64 + lane;
     const bool live = p < a.n_pods;
     const kg_pod_dev pd = pods[live ? p : 0];
-    const int64_t base = tile * KG_TILE + wave * KG_NUMA2_NODES;
+    // blockIdx.z splits each wave's 256 nodes into gridDim.z runs of ≥ 64 (whole mask words), so
+    // small placement chunks (one pod block) still put ≥ 1.5 waves on every SIMD
+    const int npw = KG_NUMA2_NODES / (int)gridDim.z;
+    const int64_t base = tile * KG_TILE + wave * KG_NUMA2_NODES + (int64_t)blockIdx.z * npw;
     const BatchMasks bm{0xFFu, 0xFFu};
     // per-wave zone table of the current node (every index mask's sums and id mask, prefix sums of
     // the descending totals): filled by the wave's 64 lanes, read by the hint enumeration of its pods
@@ -914,7 +918,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     uint64_t mword = 0;
     uint32_t sacc[4] = {0u, 0u, 0u, 0u};
     uint32_t nacc[4] = {0u, 0u, 0u, 0u};
-    for (int k = 0; k < KG_NUMA2_NODES; k++) {
+    for (int k = 0; k < npw; k++) {
         const int64_t node = base + k;
         const bool in_range = node < a.node_end;
         uint32_t fit = 0, la = 0, nsc = 0;
@@ -1681,8 +1685,8 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     a.now_ns = now_ns;
     if (e->consts.plugins & KG_PLUGIN_NUMA) {
         if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
-        if (n >= 64) {  // pod per lane needs full waves of pods; placement chunks keep node per lane
-            dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64));
+        if (n >= KG_NUMA2_MIN_PODS) {  // pod per lane; a single pod block splits the node runs 4 ways
+            dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), n <= 64 ? 4u : 1u);
             hipLaunchKernelGGL(k_eval_numa2, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
                                e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials);
         } else {
