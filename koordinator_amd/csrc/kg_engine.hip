@@ -913,6 +913,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     // per-wave zone table of the current node (every index mask's sums and id mask, prefix sums of
     // the descending totals): filled by the wave's 64 lanes, read by the hint enumeration of its pods
     __shared__ kg_zone_tab_data ztab[256 / 64];
+    __shared__ __attribute__((aligned(16))) kg_node_row lrow_s[256 / 64];
+    static_assert(sizeof(kg_node_row) % 16 == 0, "rows are staged as 16-byte words");
     kg_zone_tab_data &zt = ztab[wave];
     uint32_t best = 0;
     uint64_t mword = 0;
@@ -927,7 +929,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             NodeRegs n;
             load_node(c, pl, node, true, bm, a.now_ns, n);
             ok = eval_pair(c, pl, pd, n, node, a.now_ns, fit, la);
-            const kg_node_row &row = rows[node];
+            // the node's canonical row, staged once into the wave's LDS: the hint enumeration re-reads
+            // its zone fields in every loop of every lane
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            if (lane < (int)(sizeof(kg_node_row) / 16))
+                reinterpret_cast<uint4 *>(&lrow_s[wave])[lane] = reinterpret_cast<const uint4 *>(rows + node)[lane];
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const kg_node_row &row = lrow_s[wave];
             const bool zoned = (row.flags & KG_NODE_NUMA_OPTIONS) && row.numa_policy != KG_NUMA_NONE &&
                                row.n_zones > 0;   // n_zones ≤ KG_MAX_ZONES (kg_build_node_rows)
             if (zoned) {  // wave-uniform; the previous node's reads precede these writes (in-order LDS per wave)
