@@ -607,8 +607,21 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
                     kg_numa_visit(c, zs, p, best, a, true, full, false, true);
                     continue;
                 }
+                if (L[0].k == 1) {
+                    // a = {i}: every b it meets merges to m = a with a's own score, and repeating a
+                    // candidate right after folding it is a no-op, so one visit iff some fitting b ⊇ a
+                    bool hit = false;
+                    if (L[1].k == 1) {
+                        hit = kg_list_fits(zs, L[1], a);
+                    } else {
+                        for (uint32_t b = (1u << L[1].k) - 1u; b && !hit; b = zs.next(b, Z))
+                            hit = (a & b) && kg_list_fits(zs, L[1], b);
+                    }
+                    if (hit) kg_numa_visit(c, zs, p, best, a, true, a, true, true);
+                    continue;
+                }
                 // a permutation with a & b == 0 is skipped by kg_numa_visit: test that before the
-                // (zone-sum) fit of b, so disjoint single-zone hints cost a bit test, not Z² sums
+                // (zone-sum) fit of b, so disjoint hints cost a bit test, not a zone sum
                 for (uint32_t b = (1u << L[1].k) - 1u; b; b = zs.next(b, Z))
                     if ((a & b) && kg_list_fits(zs, L[1], b)) kg_numa_visit(c, zs, p, best, a, true, b, true, true);
             }
