@@ -898,12 +898,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                                                     const kg_node_row *__restrict__ rows,
                                                     unsigned long long *__restrict__ mask,
                                                     uint16_t *__restrict__ scores, uint8_t *__restrict__ numa_scores,
-                                                    uint32_t *__restrict__ partials) {
+                                                    uint32_t *__restrict__ partials, const int32_t *__restrict__ perm) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t tile = (int64_t)a.tile_begin + blockIdx.x;
-    const int p = blockIdx.y * 64 + lane;
-    const bool live = p < a.n_pods;
+    const int slot = blockIdx.y * 64 + lane;
+    const bool live = slot < a.n_pods;
+    const int p = live && perm ? perm[slot] : slot;   // the pod row this lane evaluates and writes
     const kg_pod_dev pd = pods[live ? p : 0];
     // blockIdx.z splits each wave's 256 nodes into gridDim.z runs of ≥ 64 (whole mask words), so
     // small placement chunks (one pod block) still put ≥ 1.5 waves on every SIMD
@@ -1366,6 +1367,8 @@ struct kg_engine {
     int32_t slot_res[8] = {0, 1, -1, -1, -1, -1, -1, -1};
     int32_t n_pods = 0, pods_cap = 0;
     size_t hot_bytes = 0;
+    int32_t *numa_perm = nullptr;   // NodeNUMAResource matrix mode: pod rows grouped by hint-list shape
+    bool numa_perm_on = false;
     BatchMasks bm{0, 0};
     bool la_prod = false;           // some pod of the batch scores with the prod-usage variant
     bool pow2 = true;               // every Fit / LoadAware weight sum of the batch is a power of two
@@ -1698,7 +1701,8 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
         if (n >= KG_NUMA2_MIN_PODS) {  // pod per lane; a single pod block splits the node runs 4 ways
             dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), n <= 64 ? 4u : 1u);
             hipLaunchKernelGGL(k_eval_numa2, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
-                               e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials);
+                               e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials,
+                               e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr);
         } else {
             dim3 grid((unsigned)shard_tiles, (unsigned)((n + KG_NUMA_PODS - 1) / KG_NUMA_PODS));
             hipLaunchKernelGGL(k_eval_numa, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
@@ -1825,6 +1829,7 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->rsv_mem) (void)hipFree(e->rsv_mem);
     if (e->quota) (void)hipFree(e->quota);
     if (e->gate) (void)hipFree(e->gate);
+    if (e->numa_perm) (void)hipFree(e->numa_perm);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     for (int k = 0; k < kg_engine::kRing; k++) {
         if (e->ev0[k]) (void)hipEventDestroy(e->ev0[k]);
@@ -2013,20 +2018,41 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
         if (e->pods) HIP_TRY(e, hipFree(e->pods));
         if (e->hot) HIP_TRY(e, hipFree(e->hot));
         if (e->gate) HIP_TRY(e, hipFree(e->gate));
+        if (e->numa_perm) HIP_TRY(e, hipFree(e->numa_perm));
         e->pods = nullptr;
         e->hot = nullptr;
         e->gate = nullptr;
+        e->numa_perm = nullptr;
         e->pods_cap = 0;
         e->hot_bytes = 0;
         HIP_TRY(e, hipMalloc(&e->pods, sizeof(kg_pod_dev) * (size_t)(n > 0 ? n : 1)));
         HIP_TRY(e, hipMalloc(&e->hot, sizeof(kg_pod_hot_t<8>) * (size_t)(n > 0 ? n : 1)));
         HIP_TRY(e, hipMalloc(&e->gate, 2 * (size_t)(n > 0 ? n : 1)));
+        HIP_TRY(e, hipMalloc(&e->numa_perm, sizeof(int32_t) * (size_t)(n > 0 ? n : 1)));
         e->pods_cap = n;
         e->hot_bytes = sizeof(kg_pod_hot_t<8>) * (size_t)(n > 0 ? n : 1);
     }
     if (n) {
         HIP_TRY(e, hipMemcpyAsync(e->pods, dev.data(), sizeof(kg_pod_dev) * (size_t)n, hipMemcpyHostToDevice, e->stream));
         HIP_TRY(e, hipMemcpyAsync(e->hot, hot.data(), hot.size(), hipMemcpyHostToDevice, e->stream));
+    }
+    // k_eval_numa2 runs a wave's 64 pods in lockstep through the hint enumeration, whose trip counts
+    // depend on the pod's hint lists: matrix mode visits the pods grouped by (list count, cpu,
+    // memory request), so a wave's lanes mostly share one loop shape (outputs stay in pod-row order)
+    std::vector<int32_t> order;
+    e->numa_perm_on = (e->cfg.enabled_plugins & KG_PLUGIN_NUMA) && n > 64;
+    if (e->numa_perm_on) {
+        order.resize((size_t)n);
+        for (int32_t i = 0; i < n; i++) order[i] = i;
+        auto lists = [&](int32_t i) { return (rows[i].flags & KG_POD_NUMA_SKIP) ? 0 : kg_numa_list_count(rows[i]); };
+        std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+            const int lx = lists(x), ly = lists(y);
+            if (lx != ly) return lx < ly;
+            if (dev[x].numa_req[KG_RES_CPU] != dev[y].numa_req[KG_RES_CPU])
+                return dev[x].numa_req[KG_RES_CPU] < dev[y].numa_req[KG_RES_CPU];
+            return dev[x].numa_req[KG_RES_MEMORY] < dev[y].numa_req[KG_RES_MEMORY];
+        });
+        HIP_TRY(e, hipMemcpyAsync(e->numa_perm, order.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, e->stream));
     }
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     e->nslot = nslot;

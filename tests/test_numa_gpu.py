@@ -65,6 +65,16 @@ def test_matrix_numa_edge_cases(seed, kw):
     _check_matrix3(numa_config(**kw), cl, 64)
 
 
+@pytest.mark.parametrize("seed,pods", [(14, 160), (15, 333)])
+def test_matrix_numa_grouped_pods(seed, pods):
+    # > 64 pods: k_eval_numa2 walks the batch in hint-list-grouped order (kg_pods_set's numa_perm) and
+    # must still write every pod's own row
+    cl = make_numa_edge_cluster(2_100, pods, seed=seed)
+    _check_matrix3(numa_config(), cl, pods)
+    cl3 = synth.make_numa_cluster(2_000, pods, seed=seed)
+    _check_matrix3(numa_config(), cl3, pods)
+
+
 def test_matrix_numa_shard():
     cl = make_numa_edge_cluster(2_500, 40, seed=13)
     _check_matrix3(numa_config(), cl, 40, begin=1024, end=2500)
