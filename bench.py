@@ -350,7 +350,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK, 4),
                          "traffic": None if traffic is None else int(traffic), "traffic_unit": "bytes per launch (PMC)",
                          "traffic_source": traffic_src,
-                         "kernel": "k_eval", "kernel_ms": round(k_ms, 4),
+                         "kernel": "k_eval3", "kernel_ms": round(k_ms, 4),
                          "algorithmic_bytes_per_launch": int(algo_bytes)},
             "cpu_baseline": cpu_baseline,
             "placement": placement,
