@@ -456,19 +456,32 @@ struct kg_zone_tab {
     }
 };
 
-// one lane's share of the table: masks lane, lane + nlanes, ... below 2^Z; lanes 0 and 1 the prefix sums
-KG_HD void kg_zone_tab_fill(const kg_node_row &row, int lane, int nlanes, kg_zone_tab_data &d) {
+// the table of one node, filled by `nlanes` cooperating lanes (1 on the host): the sums and id masks
+// by subset recurrence over the highest zone, table[2^b | x] = table[x] + zone b for x < 2^b, in the
+// ascending-zone order kg_mask_sums adds them; `sync` orders the rounds (a wave barrier on the device);
+// the combination successors per mask; lanes 0 and 1 the prefix sums of the descending totals
+template <class Sync>
+KG_HD void kg_zone_tab_fill(const kg_node_row &row, int lane, int nlanes, kg_zone_tab_data &d, Sync sync) {
     const int Z = row.n_zones;
-    for (int m = lane; m < (1 << Z); m += nlanes) {
-        int64_t tot[2], av[2];
-        kg_mask_sums(row, (uint32_t)m, tot, av);
-        d.tot[0][m] = tot[0];
-        d.tot[1][m] = tot[1];
-        d.av[0][m] = av[0];
-        d.av[1][m] = av[1];
-        d.idm[m] = kg_id_mask(row, (uint32_t)m);
-        d.succ[m] = (uint8_t)kg_combo_next((uint32_t)m, Z);
+    if (lane == 0) {
+        d.tot[0][0] = d.tot[1][0] = d.av[0][0] = d.av[1][0] = 0;
+        d.idm[0] = 0;
     }
+    for (int b = 0; b < Z; b++) {
+        sync();
+        const int64_t t0 = kg_zone_total(row, b, 0), t1 = kg_zone_total(row, b, 1);
+        const int64_t a0 = kg_zone_avail(row, b, 0), a1 = kg_zone_avail(row, b, 1);
+        const uint64_t id = 1ull << row.zone_id[b];
+        for (int x = lane; x < (1 << b); x += nlanes) {
+            const int m = (1 << b) | x;
+            d.tot[0][m] = d.tot[0][x] + t0;
+            d.tot[1][m] = d.tot[1][x] + t1;
+            d.av[0][m] = d.av[0][x] + a0;
+            d.av[1][m] = d.av[1][x] + a1;
+            d.idm[m] = d.idm[x] | id;
+        }
+    }
+    for (int m = lane; m < (1 << Z); m += nlanes) d.succ[m] = (uint8_t)kg_combo_next((uint32_t)m, Z);
     if (lane < 2) {
         const int r = lane;
         int64_t t[KG_MAX_ZONES];

@@ -944,7 +944,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             if (zoned) {  // wave-uniform; the previous node's reads precede these writes (in-order LDS per wave)
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
-                kg_zone_tab_fill(row, lane, 64, zt);
+                kg_zone_tab_fill(row, lane, 64, zt, [] {
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                });
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
             }
