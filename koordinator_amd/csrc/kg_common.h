@@ -459,7 +459,7 @@ struct kg_zone_tab {
 // the table of one node, filled by `nlanes` cooperating lanes (1 on the host): the sums and id masks
 // by subset recurrence over the highest zone, table[2^b | x] = table[x] + zone b for x < 2^b, in the
 // ascending-zone order kg_mask_sums adds them; `sync` orders the rounds (a wave barrier on the device);
-// the combination successors per mask; lanes 0 and 1 the prefix sums of the descending totals
+// the combination successors per mask; the prefix sums of the descending totals (cpu, memory)
 template <class Sync>
 KG_HD void kg_zone_tab_fill(const kg_node_row &row, int lane, int nlanes, kg_zone_tab_data &d, Sync sync) {
     const int Z = row.n_zones;
@@ -482,8 +482,7 @@ KG_HD void kg_zone_tab_fill(const kg_node_row &row, int lane, int nlanes, kg_zon
         }
     }
     for (int m = lane; m < (1 << Z); m += nlanes) d.succ[m] = (uint8_t)kg_combo_next((uint32_t)m, Z);
-    if (lane < 2) {
-        const int r = lane;
+    for (int r = lane; r < 2; r += nlanes) {
         int64_t t[KG_MAX_ZONES];
         for (int i = 0; i < Z; i++) t[i] = kg_zone_total(row, i, r);
         int64_t acc = 0;

@@ -608,8 +608,12 @@ kg_status kg_row_eval(const kg_config *cfg, const kg_node_row *node, const kg_po
     kg_pair_exact(k, row, dflags, pd, now_ns, ok, fit, la);
     if (pd.flags & KGP_RSV_REQUIRED) ok = false;  // no reservation on this node can match
     if (k.plugins & KG_PLUGIN_NUMA) {
+        // through the zone-table provider of k_eval_numa2 (the table filled by one lane), so the CPU
+        // row tests pin that path too; kg_row_commit keeps k_resolve's per-call zone sums
+        kg_zone_tab_data zt;
+        if (row.n_zones > 0) kg_zone_tab_fill(row, 0, 1, zt, [] {});
         kg_numa_out o;
-        kg_numa_pair(k, row, pd, o);
+        kg_numa_pair_z(k, row, pd, o, kg_zone_tab{zt});
         ok = ok && o.feasible;
         numa = o.score;
     }
