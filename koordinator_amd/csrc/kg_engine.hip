@@ -831,68 +831,13 @@ __global__ void k_fix_slow(kg_consts c, kg_planes pl, const kg_pod_dev *__restri
     }
 }
 
-// NodeNUMAResource enabled (config 3): Fit + LoadAware as in k_eval2 (fast planes, exact row for
-// slow nodes) plus kg_numa_pair on the canonical row, all in one pass.  A 256-thread workgroup
-// covers one 1024-node tile in four 256-node passes and KG_NUMA_PODS pods; per-(pod, tile) keys
-// are reduced in LDS.  The hint merge is branchy per-lane integer work over the row's zones (the
-// rows stay L2-resident across the workgroup's pods), so this path is latency-, not HBM-bound.
-#define KG_NUMA_PODS 16
-__global__ __launch_bounds__(256) void k_eval_numa(kg_consts c, kg_planes pl, HotArgs a,
-                                                   const kg_pod_dev *__restrict__ pods,
-                                                   unsigned long long *__restrict__ mask, uint16_t *__restrict__ scores,
-                                                   uint8_t *__restrict__ numa_scores, uint32_t *__restrict__ partials) {
-    __shared__ uint32_t keys[KG_NUMA_PODS];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int64_t tile = (int64_t)a.tile_begin + blockIdx.x;
-    const int p0 = blockIdx.y * KG_NUMA_PODS;
-    const int np = min(KG_NUMA_PODS, a.n_pods - p0);
-    if (tid < KG_NUMA_PODS) keys[tid] = 0u;
-    __syncthreads();
-    const BatchMasks bm{0xFFu, 0xFFu};
-    for (int k = 0; k < KG_TILE / 256; k++) {
-        const int local = k * 256 + tid;
-        const int64_t node = tile * KG_TILE + local;
-        const bool in_range = node < a.node_end;
-        const int64_t col = node - a.col_begin;
-        NodeRegs n;
-        load_node(c, pl, node, in_range, bm, a.now_ns, n);
-        for (int j = 0; j < np; j++) {
-            const kg_pod_dev &pd = pods[p0 + j];
-            uint32_t fit = 0, la = 0;
-            kg_numa_out o;
-            o.feasible = false;
-            o.score = 0;
-            bool ok = false;
-            if (in_range) {
-                ok = eval_pair(c, pl, pd, n, node, a.now_ns, fit, la);
-                kg_numa_pair(c, pl.rows[node], pd, o);
-                ok = ok && o.feasible;
-            }
-            const unsigned long long bits = __ballot(ok);
-            const int64_t prow = (int64_t)(p0 + j);
-            if (mask && lane == 0 && col < a.node_end - a.col_begin)
-                mask[prow * a.mask_words + (col >> 6)] = bits;
-            if (in_range) {
-                if (scores) scores[prow * a.score_stride + col] = (uint16_t)(fit | (la << 8));
-                if (numa_scores) numa_scores[prow * a.score_stride + col] = (uint8_t)o.score;
-            }
-            uint32_t key = ok ? ((total_of(c, fit, la, o.score) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local) : 0u;
-            key = wave_max_u32(key);
-            if (lane == 0 && key) atomicMax(&keys[j], key);
-        }
-    }
-    __syncthreads();
-    if (tid < np) partials[(int64_t)(p0 + tid) * a.tiles_total + tile] = keys[tid];
-}
-
-// NodeNUMAResource enabled, pod per lane: a wave holds 64 pods and walks 256 nodes of a tile one
+// NodeNUMAResource enabled (config 3; matrix mode and placement chunks), pod per lane: a wave holds 64 pods and walks 256 nodes of a tile one
 // node at a time, so every node-side value (derived planes, canonical row with its zones) is
 // wave-uniform (one cache line per load, served to all 64 pods) and the NUMA hint enumeration runs
 // on the node's structure for 64 requests at once.  Outputs accumulate per lane along the pod's own
 // row: 64 feasibility bits per u64 word, 8 score pairs per 16-byte store, 16 NUMA scores per 16-byte
 // store, the per-(pod, tile) key as a lane-private max (one atomicMax per wave).
 #define KG_NUMA2_NODES 256
-#define KG_NUMA2_MIN_PODS 1   // below it: k_eval_numa (node per lane)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_eval_numa2(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_pod_dev *__restrict__ pods,
                                                     const kg_node_row *__restrict__ rows,
@@ -1701,15 +1646,11 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     a.now_ns = now_ns;
     if (e->consts.plugins & KG_PLUGIN_NUMA) {
         if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
-        if (n >= KG_NUMA2_MIN_PODS) {  // pod per lane; a single pod block splits the node runs 4 ways
+        {  // pod per lane; a single pod block splits each wave's node run 4 ways
             dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), n <= 64 ? 4u : 1u);
             hipLaunchKernelGGL(k_eval_numa2, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
                                e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials,
                                e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr);
-        } else {
-            dim3 grid((unsigned)shard_tiles, (unsigned)((n + KG_NUMA_PODS - 1) / KG_NUMA_PODS));
-            hipLaunchKernelGGL(k_eval_numa, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
-                               (unsigned long long *)mask, scores, numa_scores, partials);
         }
         HIP_TRY(e, hipGetLastError());
         if (e->profiling) {

@@ -1,6 +1,6 @@
 """NodeNUMAResource (BASELINE config 3) on the HIP engine against the oracle restatement.
 
-Matrix mode (k_eval_numa: feasibility, Fit / LoadAware / NUMA score planes, top-1 keys), placement
+Matrix mode (k_eval_numa2: feasibility, Fit / LoadAware / NUMA score planes, top-1 keys), placement
 (k_resolve with zone-allocation Reserve), node shards, and the host-side rejections of pods the
 engine path does not cover (cpuset binding, more than two hint lists).
 """
