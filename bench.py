@@ -296,7 +296,7 @@ def main():
         dist.barrier()
         torch.cuda.synchronize(dev)
         tp0 = time.perf_counter()
-        nodes, tot = kdist.place_sharded(deng, now, dev, chunk=int(cfg["place_chunk"]))
+        nodes, tot = kdist.place_sharded(deng, now, dev, chunk=kdist.place_chunk_of(cfg))
         dist.barrier()
         tp1 = time.perf_counter()
         deng.close()

@@ -55,6 +55,9 @@ extern "C" {
 
 #define KG_ABI_VERSION 3
 
+/* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
+#define KG_PLACE_CHUNK_MAX 1024
+
 /* ------------------------------------------------------------------ */
 /* status codes                                                          */
 /* ------------------------------------------------------------------ */
@@ -192,7 +195,7 @@ typedef struct kg_config {
 
     /* engine knobs */
     int32_t device;            /* HIP device ordinal */
-    int32_t place_chunk;       /* pods per refresh in kg_place (0 ⇒ default 8) */
+    int32_t place_chunk;       /* pods per refresh in kg_place (0 ⇒ default 8; at most KG_PLACE_CHUNK_MAX) */
 
     /* Reservation (profile weight, config/manager/scheduler-config.yaml:82-91 ships 5000) */
     int32_t weight_reservation;
@@ -408,7 +411,10 @@ typedef struct kg_engine kg_engine;
  *   mask     [P][W] uint64: bit (c % 64) of word c/64 ⇔ pod p feasible on node B + c
  *            (AND of every enabled Filter plugin)
  *   scores   [P][64·W][2] uint8: {NodeResourcesFit score, LoadAwareScheduling score} ∈ [0,100]
- *            (0 where a plugin is disabled; row stride 64·W pairs)
+ *            (0 where a plugin is disabled; row stride 64·W pairs).  Like the reference, where Score
+ *            runs only on the nodes that passed Filter, a score is meaningful only where the pair's
+ *            mask bit is set: the planes of a pod failing a node-independent gate (ElasticQuota
+ *            PreFilter, a required reservation) keep the per-pair plugin scores of the plain nodes.
  *   numa_scores [P][64·W] uint8: NodeNUMAResource score (when KG_PLUGIN_NUMA is enabled)
  *   top1     [P] uint64: (total+1) << 32 | (0xFFFFFFFF − node) of the best feasible node,
  *            total = Σ weight·score, ties → lowest node index; 0 ⇔ no feasible node

@@ -39,6 +39,7 @@ NODE_NUMA_OPTIONS, NODE_NUMA_TOPO_VALID = 0x40, 0x80
 
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE, CODE_UNSCHEDULABLE_AND_UNRESOLVABLE = 0, 1, 2, 3
 TILE = 1024
+PLACE_CHUNK_MAX = 1024
 
 RESOURCE_LIST = np.dtype([("v", "<i8", (NUM_RES,)), ("present", "<u4"), ("_pad", "<u4")], align=True)
 

@@ -36,7 +36,7 @@
 
 #define KG_POD_CHUNK 64          // pods between two LDS partial combines in k_eval
 #define KG_RESOLVE_THREADS 1024
-#define KG_MAX_CHUNK 1024        // max pods per resolve call (touched-list capacity)
+#define KG_MAX_CHUNK KG_PLACE_CHUNK_MAX   // max pods per resolve call (touched-list capacity)
 #define KG_MAX_TILES 4096        // max tiles per snapshot in k_resolve (2M nodes)
 
 // ---------------------------------------------------------------------------------------
@@ -2312,6 +2312,8 @@ kg_status kg_commit(kg_engine *e, int32_t pod, int32_t node) {
     kg_status st = check_engine(e);
     if (st) return st;
     if (pod < 0 || pod >= e->n_pods || node < 0 || node >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "bad commit");
+    st = quota_ready(e);   // the pod's quota group must exist before its usage is committed
+    if (st) return st;
     hipLaunchKernelGGL(k_commit_one, dim3(1), dim3(1), 0, e->stream, e->consts, e->pl, e->pods, pod, node, rsv_args(e));
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipStreamSynchronize(e->stream));

@@ -414,6 +414,8 @@ kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
         return fail("plugin weight out of range (each >= 0, sum <= 40000)");
     if (c->fit_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->fit_strategy != KG_STRATEGY_MOST_ALLOCATED)
         return fail("unsupported NodeResourcesFit scoring strategy");
+    // kg_place: 0 ⇒ the default chunk (8); at most the resolve kernel's touched-list capacity
+    if (c->place_chunk < 0 || c->place_chunk > KG_PLACE_CHUNK_MAX) return fail("place_chunk out of range (0..1024)");
     return KG_OK;
 }
 

@@ -78,6 +78,8 @@ def place_sharded(backend: ChunkBackend, now_ns: int, device: torch.device, chun
 
     The backend must hold the full (replicated) snapshot with its evaluation restricted to this
     rank's `shard_range`. Returns (node or −1, total or −1) per pod, identical on every rank."""
+    if chunk < 1 or chunk > nat.PLACE_CHUNK_MAX:
+        raise ValueError(f"chunk {chunk} outside 1..{nat.PLACE_CHUNK_MAX}")
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     P, tiles = backend.n_pods, backend.num_tiles
     stream = getattr(backend, "torch_stream", None)
@@ -103,6 +105,15 @@ class _nullctx:
 
     def __exit__(self, *a):
         return False
+
+
+def place_chunk_of(cfg: np.ndarray) -> int:
+    """kg_place's rule for the chunk size: 0 ⇒ 8, capped at KG_PLACE_CHUNK_MAX (negative values are
+    rejected by kg_config_validate)."""
+    chunk = int(cfg["place_chunk"])
+    if chunk < 0:
+        raise ValueError(f"place_chunk {chunk} < 0")
+    return min(chunk if chunk > 0 else 8, nat.PLACE_CHUNK_MAX)
 
 
 def sharded_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, device: torch.device,
@@ -141,6 +152,6 @@ def place(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, now_ns: 
     device = device or torch.device("cuda", torch.cuda.current_device())
     eng = sharded_engine(cfg, node_rows, pod_rows, device, group, reservations, quotas)
     try:
-        return place_sharded(eng, now_ns, device, chunk=int(cfg["place_chunk"]) or 8, group=group)
+        return place_sharded(eng, now_ns, device, chunk=place_chunk_of(cfg), group=group)
     finally:
         eng.close()

@@ -12,6 +12,14 @@ Config 1/2 distributions:
          (Burstable → LS → prod), 20 % BestEffort batch pods requesting only
          batch-cpu / batch-memory.
 Every quantity is an exact integer in its base unit (cpu in milli).
+
+Node-side LoadAware inputs beyond the base distributions (``decorate``, on by default) so that every
+branch of the node terms is exercised at scale: a fraction of the nodes carry already-assigned pods
+(podAssignCache entries assigned long before, inside the report interval before, or after the
+NodeMetric UpdateTime), PodsMetric entries (for most of those pods, plus NotFound and duplicated
+ones), AggregatedNodeUsages (one or two durations, some percentile types missing), best-effort pods
+that make NonZeroRequested exceed Requested, custom usage-threshold annotations (valid and
+unparsable) and raw-allocatable annotations (EstimateNode ≠ Allocatable).
 """
 from __future__ import annotations
 
@@ -30,13 +38,14 @@ MI = 1 << 20
 class SynthView:
     """Same attribute surface as objects.FlatView (pods, containers, nodes, c_view …)."""
 
-    def __init__(self, pods, containers, nodes, now_ns, numa=None, reservations=None, quotas=None):
+    def __init__(self, pods, containers, nodes, now_ns, numa=None, reservations=None, quotas=None, aggregated=None,
+                 pod_metrics=None, assigned=None):
         self.pods = pods
         self.containers = containers
         self.nodes = nodes
-        self.aggregated_arr = np.zeros(0, dtype=nat.AGGREGATED_USAGE)
-        self.pod_metrics_arr = np.zeros(0, dtype=nat.POD_METRIC)
-        self.assigned_arr = np.zeros(0, dtype=nat.ASSIGNED_POD)
+        self.aggregated_arr = np.zeros(0, dtype=nat.AGGREGATED_USAGE) if aggregated is None else aggregated
+        self.pod_metrics_arr = np.zeros(0, dtype=nat.POD_METRIC) if pod_metrics is None else pod_metrics
+        self.assigned_arr = np.zeros(0, dtype=nat.ASSIGNED_POD) if assigned is None else assigned
         self.numa_arr = np.zeros(0, dtype=nat.NUMA_SPEC) if numa is None else numa
         self.rsv_arr = np.zeros(0, dtype=nat.RESERVATION) if reservations is None else reservations
         self.quota_arr = np.zeros(0, dtype=nat.QUOTA) if quotas is None else quotas
@@ -44,9 +53,14 @@ class SynthView:
         self.c_view = nat.make_view(self.pods, self.containers, self.nodes, self.aggregated_arr, self.pod_metrics_arr,
                                     self.assigned_arr, self.numa_arr, self.rsv_arr, self.quota_arr)
 
+    def with_nodes(self, nodes: np.ndarray, pods: Optional[np.ndarray] = None) -> "SynthView":
+        """The same cluster with other node (and pod) specs; every side array is kept, so the nodes'
+        indices into them stay valid."""
+        return SynthView(self.pods if pods is None else pods, self.containers, nodes, self.now_ns, self.numa_arr,
+                         self.rsv_arr, self.quota_arr, self.aggregated_arr, self.pod_metrics_arr, self.assigned_arr)
+
     def subset_nodes(self, begin: int, end: int) -> "SynthView":
-        nodes = np.ascontiguousarray(self.nodes[begin:end])
-        return SynthView(self.pods, self.containers, nodes, self.now_ns, self.numa_arr)
+        return self.with_nodes(np.ascontiguousarray(self.nodes[begin:end]))
 
 
 def _rl_fill(arr, r, values, mask=None):
@@ -132,10 +146,115 @@ def make_pods(p: int, seed: int):
     return pods, cont
 
 
-def make_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, **kw) -> SynthView:
+def decorate(nodes: np.ndarray, pods: np.ndarray, cont: np.ndarray, seed: int, assigned_frac: float = 0.2,
+             aggregated_frac: float = 0.3, besteffort_frac: float = 0.3, custom_frac: float = 0.04,
+             raw_alloc_frac: float = 0.02):
+    """Node-side LoadAware inputs (see the module docstring), in place on `nodes`.  Existing pods are
+    appended after the pending ones (pods[len(pods):]), so pending pod i keeps index i.  Returns
+    (pods, containers, aggregated, pod_metrics, assigned)."""
+    rng = np.random.default_rng(seed + 313)
+    n, p0, c0 = len(nodes), len(pods), len(cont)
+    metric = (nodes["has_node_metric"] != 0) & (nodes["has_node_metric_info"] != 0)
+    upd = nodes["update_time_ns"]
+    cpu = nodes["allocatable"]["v"][:, nat.RES_CPU]
+    mem = nodes["allocatable"]["v"][:, nat.RES_MEMORY]
+    # NonZeroRequested > Requested: best-effort pods count 100m / 200Mi each (schedutil.GetNonzeroRequests)
+    be = np.where(rng.random(n) < besteffort_frac, rng.integers(1, 4, n), 0)
+    nodes["nonzero_requested"][:, 0] += be * 100
+    nodes["nonzero_requested"][:, 1] += be * 200 * MI
+    nodes["pod_count"] = np.minimum(nodes["pod_count"] + be, 100)
+    # already-assigned pods (podAssignCache) with their PodsMetric
+    host = np.flatnonzero(metric & (rng.random(n) < assigned_frac))
+    k = rng.integers(1, 5, len(host))
+    m = int(k.sum())
+    xp, xc = make_pods(m, seed + 17)
+    xp["first_container"] += c0
+    xp["first_init_container"] += c0
+    xp["name_id"] = np.arange(m) + 20_000_000 + 1_000_000 * (seed % 7)
+    pods = np.concatenate([pods, xp])
+    cont = np.concatenate([cont, xc])
+    owner = np.repeat(host, k)
+    assigned = np.zeros(m, dtype=nat.ASSIGNED_POD)
+    assigned["pod"] = p0 + np.arange(m)
+    interval = nodes["report_interval_seconds"][owner] * 10**9
+    when = rng.random(m)   # long before / inside the report interval before / after UpdateTime
+    assigned["timestamp_ns"] = np.where(when < 0.4, upd[owner] - 5 * interval,
+                                        np.where(when < 0.7, upd[owner] - interval // 3, upd[owner] + 5 * 10**9))
+    first = np.zeros(n, np.int64)
+    first[host] = np.concatenate([[0], np.cumsum(k)[:-1]])
+    nodes["first_assigned"][host] = first[host]
+    nodes["n_assigned"][host] = k
+    # PodsMetric: 80 % of the assigned pods, plus NotFound entries and repeated names on some nodes
+    rq = xc["requests"]["v"]
+    req_cpu = np.maximum(rq[:, nat.RES_CPU], rq[:, nat.RES_BATCH_CPU])
+    req_mem = np.maximum(rq[:, nat.RES_MEMORY], rq[:, nat.RES_BATCH_MEMORY])
+    reported = rng.random(m) < 0.8
+    extra = rng.random(len(host)) < 0.3
+    entries = []
+    pos = 0
+    for h_i, node in enumerate(host):
+        idx = np.arange(pos, pos + k[h_i])
+        pos += k[h_i]
+        mine = [(int(xp["name_id"][j]), int(p0 + j), j) for j in idx if reported[j]]
+        if extra[h_i]:
+            mine.append((90_000_000 + int(node), -1, -1))            # lister NotFound: skipped
+            if mine[0][2] >= 0:
+                mine.append(mine[0])                                  # repeated name: the last one wins
+        entries.append(mine)
+    pm_count = np.array([len(e) for e in entries], np.int64)
+    pm = np.zeros(int(pm_count.sum()), dtype=nat.POD_METRIC)
+    flat = [x for e in entries for x in e]
+    if flat:
+        pm["name_id"] = [x[0] for x in flat]
+        pm["lister_pod"] = [x[1] for x in flat]
+        src = np.array([x[2] for x in flat])
+        scale = rng.integers(30, 121, len(flat))
+        ucpu = np.where(src >= 0, req_cpu[np.maximum(src, 0)] * scale // 100, 1000)
+        umem = np.where(src >= 0, (req_mem[np.maximum(src, 0)] // 100) * scale, GI)
+        _rl_fill(pm["usage"], nat.RES_CPU, ucpu)
+        _rl_fill(pm["usage"], nat.RES_MEMORY, umem)
+    pfirst = np.concatenate([[0], np.cumsum(pm_count)[:-1]]) if len(host) else np.zeros(0, np.int64)
+    nodes["first_pod_metric"][host] = pfirst
+    nodes["n_pod_metric"][host] = pm_count
+    # AggregatedNodeUsages: one or two durations; p95 missing on some
+    ag_nodes = np.flatnonzero(metric & (rng.random(n) < aggregated_frac))
+    na = rng.integers(1, 3, len(ag_nodes))
+    agg = np.zeros(int(na.sum()), dtype=nat.AGGREGATED_USAGE)
+    owner_a = np.repeat(ag_nodes, na)
+    slot = np.concatenate([np.arange(c) for c in na]) if len(na) else np.zeros(0, np.int64)
+    agg["duration_ns"] = np.where(slot == 0, 300, 600) * 10**9
+    ucpu = nodes["node_usage"]["v"][owner_a, nat.RES_CPU]
+    umem = nodes["node_usage"]["v"][owner_a, nat.RES_MEMORY]
+    drop_p95 = rng.random(len(agg)) < 0.2
+    for t, f in ((nat.AGG_AVG, 80), (nat.AGG_P50, 85), (nat.AGG_P90, 100), (nat.AGG_P95, 105), (nat.AGG_P99, 110)):
+        live = ~drop_p95 if t == nat.AGG_P95 else np.ones(len(agg), bool)
+        _rl_fill(agg["usage"][:, t], nat.RES_CPU, np.minimum(ucpu * f // 100, cpu[owner_a]), live)
+        _rl_fill(agg["usage"][:, t], nat.RES_MEMORY, np.minimum((umem // 100) * f, mem[owner_a]), live)
+    afirst = np.concatenate([[0], np.cumsum(na)[:-1]]) if len(na) else np.zeros(0, np.int64)
+    nodes["first_aggregated"][ag_nodes] = afirst
+    nodes["n_aggregated"][ag_nodes] = na
+    # annotations: custom usage thresholds (valid / unparsable) and raw allocatable
+    u = rng.random(n)
+    custom = u < custom_frac
+    nodes["custom_thresholds_state"] = np.where(custom, 1, np.where(u < custom_frac * 1.25, -1, 0))
+    _rl_fill(nodes["custom_usage_thresholds"], nat.RES_CPU, np.full(n, 70), custom)
+    _rl_fill(nodes["custom_usage_thresholds"], nat.RES_MEMORY, np.full(n, 90), custom)
+    prod_thr = custom & (rng.random(n) < 0.3)
+    _rl_fill(nodes["custom_prod_usage_thresholds"], nat.RES_CPU, np.full(n, 50), prod_thr)
+    raw = rng.random(n) < raw_alloc_frac
+    nodes["raw_allocatable_state"] = np.where(raw, 1, 0)
+    _rl_fill(nodes["raw_allocatable"], nat.RES_CPU, cpu * 6 // 5, raw)
+    return pods, cont, agg, pm, assigned
+
+
+def make_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, decorated: bool = True,
+                 **kw) -> SynthView:
     nodes = make_nodes(n_nodes, seed, now_ns, **kw)
     pods, cont = make_pods(n_pods, seed)
-    return SynthView(pods, cont, nodes, now_ns)
+    if not decorated:
+        return SynthView(pods, cont, nodes, now_ns)
+    pods, cont, agg, pm, asg = decorate(nodes, pods, cont, seed)
+    return SynthView(pods, cont, nodes, now_ns, aggregated=agg, pod_metrics=pm, assigned=asg)
 
 
 def make_numa_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, zones=(4, 6, 8),

@@ -1215,14 +1215,18 @@ int kgo_eval_matrix3(const kg_config *c, const kg_cluster_view *v, const int32_t
         for (int32_t j = node_begin; j < node_end; j++) {
             const kg_node_spec *n = &v->nodes[j];
             int64_t o = (int64_t)p * W + (j - node_begin);
-            mask[o] = (uint8_t)pair_feasible(c, v, pod, n, now_ns);
+            /* NodeNUMAResource Filter and Score come out of one evaluation of the pair */
+            int64_t s = 0;
+            const int numa_ok = !(c->enabled_plugins & KG_PLUGIN_NUMA) || kgo_numa_eval(c, v, pod, n, &s);
+            int ok = numa_ok;
+            if (ok && (c->enabled_plugins & KG_PLUGIN_FIT) && kgo_fit_filter(v, pod, n) != KG_CODE_SUCCESS) ok = 0;
+            if (ok && (c->enabled_plugins & KG_PLUGIN_LOADAWARE) &&
+                kgo_loadaware_filter(c, v, pod, n, now_ns) != KG_CODE_SUCCESS)
+                ok = 0;
+            mask[o] = (uint8_t)ok;
             fit[o] = (c->enabled_plugins & KG_PLUGIN_FIT) ? (uint8_t)kgo_fit_score(c, v, pod, n) : 0;
             la[o] = (c->enabled_plugins & KG_PLUGIN_LOADAWARE) ? (uint8_t)kgo_loadaware_score(c, v, pod, n, now_ns) : 0;
-            if (numa) {
-                int64_t s = 0;
-                if (c->enabled_plugins & KG_PLUGIN_NUMA) kgo_numa_eval(c, v, pod, n, &s);
-                numa[o] = (uint8_t)s;
-            }
+            if (numa) numa[o] = (uint8_t)s;
         }
     }
     return 0;

@@ -77,14 +77,14 @@ def test_matrix_slow_path_huge_nodes():
     cl.nodes["allocatable"]["v"][big, 1] = (1 << 43) + 12345
     cl.nodes["requested"]["v"][big, 1] = (1 << 42) + 777
     cl.nodes["nonzero_requested"][big, 1] = (1 << 42) + 777
-    cl = synth.SynthView(cl.pods, cl.containers, cl.nodes, cl.now_ns)
+    cl = cl.with_nodes(cl.nodes)
     _check_matrix(shipped_profile(), cl, np.arange(40), cl.now_ns)
 
 
 def test_matrix_daemonset_and_prod_score_variant():
     cl = synth.make_cluster(1_000, 64, seed=9)
     cl.pods["is_daemonset"][::5] = 1
-    cl = synth.SynthView(cl.pods, cl.containers, cl.nodes, cl.now_ns)
+    cl = cl.with_nodes(cl.nodes)
     cfg = shipped_profile(score_according_prod_usage=True, prod_usage_thresholds={"cpu": 40})
     _check_matrix(cfg, cl, np.arange(64), cl.now_ns)
 

@@ -115,3 +115,22 @@ def test_rsv_commit_one():
             eng.commit(0, int(ref_nodes[0]))
             np.testing.assert_array_equal(eng.download_reservations()["allocated"]["v"], ref_rsv["allocated"]["v"])
             np.testing.assert_array_equal(eng.download_quotas()["used"]["v"], ref_q["used"]["v"])
+
+
+def test_commit_needs_every_quota_group():
+    """kg_commit checks that the pod's quota group exists (quota_ready), like kg_eval and kg_place do:
+    a commit after kg_quota_set got fewer groups than the pods reference fails with KG_ERR_STATE."""
+    cl = rsv_cluster(200, 8, seed=66, rsv_node_frac=1.0, n_quotas=3)
+    cfg = shipped_profile(plugins=RSV_EQ)
+    eng = engine.Engine(cfg)
+    try:
+        eng.load_snapshot(engine.build_node_rows(cfg, cl))
+        eng.set_reservations(cl.rsv_arr)
+        eng.set_quotas(cl.quota_arr[:1])
+        rows = engine.build_pod_rows(cfg, cl, np.arange(8))
+        rows["quota"][:] = 2
+        eng.set_pods(rows)
+        with pytest.raises(engine.EngineError, match="quota index"):
+            eng.commit(0, 0)
+    finally:
+        eng.close()
