@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 3
+#define KG_ABI_VERSION 4
 
 /* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
 #define KG_PLACE_CHUNK_MAX 1024
@@ -295,8 +295,14 @@ typedef struct kg_numa_spec {
     kg_resource_list zone_total[KG_MAX_ZONES];       /* NUMANodeResources[i].Resources (before amplification) */
     kg_resource_list zone_allocated[KG_MAX_ZONES];   /* allocatedResources[zone] (present == 0 ⇔ none) */
     double cpu_amplification_ratio;                  /* annotation resource-amplification-ratio cpu (≤ 1 ⇔ none) */
-    int32_t cpu_topology_valid;                      /* CPUTopology.IsValid(): Reserve records allocations only then */
-    int32_t _pad;
+    int32_t cpu_topology_valid;                      /* TopologyOptions.CPUTopology: 1 valid (IsValid()), 0 reported but
+                                                        invalid, −1 nil (no NodeResourceTopology).  Reserve records
+                                                        allocations only when valid; with a cpu amplification ratio
+                                                        > 1, 0 makes filterAmplifiedCPUs reject cpu requests
+                                                        (plugin.go:359-362, resource_manager.go:390-397) */
+    int32_t cpuset_cpus;                             /* |NodeAllocation.allocatedCPUs|: CPUs held by cpuset pods
+                                                        (GetAvailableCPUs' allocated, no preferred CPUs) */
+    int32_t zone_cpuset_cpus[KG_MAX_ZONES];          /* allocatedCPUs.CPUsInNUMANodes(zone_id[z]) (node_allocation.go:165) */
 } kg_numa_spec;
 
 /* One reservation as the reservation cache holds it (frameworkext.ReservationInfo). */
@@ -377,6 +383,7 @@ typedef struct kg_pod_row {
 #define KG_NODE_LA_AGG_MISSING 0x20u     /* score aggregation requested but not reported (info) */
 #define KG_NODE_NUMA_OPTIONS 0x40u       /* the node has NodeNUMAResource topology options */
 #define KG_NODE_NUMA_TOPO_VALID 0x80u    /* CPUTopology valid: Reserve records zone allocations */
+#define KG_NODE_NUMA_TOPO_INVALID 0x100u /* CPUTopology reported but invalid (GetAvailableCPUs fails) */
 
 typedef struct kg_node_row {
     int64_t alloc[KG_NUM_RES];          /* NodeInfo.Allocatable */
@@ -398,6 +405,12 @@ typedef struct kg_node_row {
     uint32_t zone_keys;                 /* bit 2z+r: zone z's total has resource r (cpu 0, memory 1) */
     uint32_t zone_alloc_keys;           /* bit 2z+r: zone z's allocation has resource r */
     double cpu_amplification_ratio;     /* ≤ 1 ⇔ none */
+    /* cpuset pods on the node (the amplified-CPU terms of filterAmplifiedCPUs / scoreWithAmplifiedCPUs /
+       getAvailableNUMANodeResources); zero unless the CPU topology is valid */
+    int64_t cpuset_milli;               /* cpuset_cpus · 1000 */
+    int64_t cpuset_amp_milli;           /* Amplify(cpuset_milli, ratio) */
+    int64_t zone_cpuset_amp[KG_MAX_ZONES]; /* Amplify(c, ratio) − c, c = zone z's cpuset CPUs · 1000: added to the
+                                              zone's allocated cpu while the zone has an allocation entry */
 } kg_node_row;
 
 /* ------------------------------------------------------------------ */

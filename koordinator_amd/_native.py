@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 NUM_RES = 8
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
  RES_EXTENDED) = range(8)
@@ -35,7 +35,7 @@ MAX_ZONES = 8
 POD_HAS_REQUEST, POD_DAEMONSET, POD_PROD, POD_LA_PROD_SCORE, POD_VALID = 0x1, 0x2, 0x4, 0x8, 0x80000000
 POD_NUMA_SKIP, POD_NUMA_CPU_BIND, POD_NON_PREEMPTIBLE = 0x10, 0x20, 0x40
 NODE_VALID, NODE_HAS_METRIC, NODE_HAS_UPDATE_TIME, NODE_LA_PASS_NONPROD, NODE_LA_PASS_PROD = 0x1, 0x2, 0x4, 0x8, 0x10
-NODE_NUMA_OPTIONS, NODE_NUMA_TOPO_VALID = 0x40, 0x80
+NODE_NUMA_OPTIONS, NODE_NUMA_TOPO_VALID, NODE_NUMA_TOPO_INVALID = 0x40, 0x80, 0x100
 
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE, CODE_UNSCHEDULABLE_AND_UNRESOLVABLE = 0, 1, 2, 3
 TILE = 1024
@@ -88,7 +88,8 @@ NODE_SPEC = np.dtype([
 NUMA_SPEC = np.dtype([
     ("policy", "<i4"), ("n_zones", "<i4"), ("zone_id", "<i4", (MAX_ZONES,)),
     ("zone_total", RESOURCE_LIST, (MAX_ZONES,)), ("zone_allocated", RESOURCE_LIST, (MAX_ZONES,)),
-    ("cpu_amplification_ratio", "<f8"), ("cpu_topology_valid", "<i4"), ("_pad", "<i4"),
+    ("cpu_amplification_ratio", "<f8"), ("cpu_topology_valid", "<i4"), ("cpuset_cpus", "<i4"),
+    ("zone_cpuset_cpus", "<i4", (MAX_ZONES,)),
 ], align=True)
 
 POD_ROW = np.dtype([
@@ -105,6 +106,7 @@ NODE_ROW = np.dtype([
     ("numa_policy", "<i4"), ("n_zones", "<i4"), ("zone_id", "<i4", (MAX_ZONES,)),
     ("zone_total", "<i8", (MAX_ZONES, 2)), ("zone_allocated", "<i8", (MAX_ZONES, 2)),
     ("zone_keys", "<u4"), ("zone_alloc_keys", "<u4"), ("cpu_amplification_ratio", "<f8"),
+    ("cpuset_milli", "<i8"), ("cpuset_amp_milli", "<i8"), ("zone_cpuset_amp", "<i8", (MAX_ZONES,)),
 ], align=True)
 
 RESERVATION = np.dtype([

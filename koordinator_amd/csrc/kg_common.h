@@ -350,7 +350,9 @@ KG_HD uint32_t kg_numa_score_zones(const kg_consts &c, bool most, const int64_t 
 }
 
 // the same over the node's Requested / Allocatable (policy None, or nothing allocated in zones)
-KG_HD uint32_t kg_numa_score_node(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p) {
+// `amplified`: scoreWithAmplifiedCPUs (scoring.go:99-116), the node's cpuset CPUs counted amplified
+KG_HD uint32_t kg_numa_score_node(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p,
+                                  bool amplified = false) {
     int64_t s = 0, w = 0;
     for (int r = 0; r < KG_NUM_RES; r++) {
         if (c.numa_w[r] <= 0) continue;
@@ -359,7 +361,8 @@ KG_HD uint32_t kg_numa_score_node(const kg_consts &c, const kg_node_row &row, co
         if (scalar && (pr == 0 || !((row.alloc_present >> r) & 1u))) continue;
         const int64_t a = row.alloc[r];
         if (a == 0) continue;
-        const int64_t rq = row.requested[r] + pr;
+        int64_t rq = row.requested[r] + pr;
+        if (amplified && r == KG_RES_CPU) rq += row.cpuset_amp_milli - row.cpuset_milli;
         s += (c.numa_most ? kg_mr_i(rq, a) : kg_lr_i(rq, a)) * c.numa_w[r];
         w += c.numa_w[r];
     }
@@ -370,8 +373,21 @@ KG_HD uint32_t kg_numa_score_node(const kg_consts &c, const kg_node_row &row, co
 KG_HD int64_t kg_zone_total(const kg_node_row &row, int i, int r) {
     return ((row.zone_keys >> (2 * i + r)) & 1u) ? row.zone_total[i][r] : 0;
 }
+// allocated resource r of zone i as getAvailableNUMANodeResources reads it (node_allocation.go:155-177):
+// with a cpu amplification ratio > 1, a zone with an allocation entry counts its cpuset CPUs amplified
+KG_HD int64_t kg_zone_alloc(const kg_node_row &row, int i, int r) {
+    int64_t a = row.zone_allocated[i][r];
+    if (r == KG_RES_CPU && row.cpu_amplification_ratio > 1.0 && ((row.zone_alloc_keys >> (2 * i)) & 3u))
+        a += row.zone_cpuset_amp[i];
+    return a;
+}
+// key set of those allocations: the amplified entry always carries a cpu quantity
+KG_HD uint32_t kg_zone_alloc_keys(const kg_node_row &row) {
+    const uint32_t k = row.zone_alloc_keys;
+    return row.cpu_amplification_ratio > 1.0 ? k | ((k | (k >> 1)) & 0x5555u) : k;
+}
 KG_HD int64_t kg_zone_avail(const kg_node_row &row, int i, int r) {
-    const int64_t a = kg_zone_total(row, i, r) - row.zone_allocated[i][r];
+    const int64_t a = kg_zone_total(row, i, r) - kg_zone_alloc(row, i, r);
     return a > 0 ? a : 0;
 }
 
@@ -558,15 +574,25 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
     if (p.flags & KG_POD_NUMA_SKIP) return;
     const bool opts = (row.flags & KG_NODE_NUMA_OPTIONS) != 0;
     const int policy = opts ? row.numa_policy : KG_NUMA_NONE;
-    // filterAmplifiedCPUs without cpuset allocations (plugin.go:340-373)
+    // filterAmplifiedCPUs (plugin.go:340-373) for a pod without cpuset binding
     const double ratio = opts ? row.cpu_amplification_ratio : 0.0;
     const int64_t pcpu = p.numa_req[KG_RES_CPU];
-    if (pcpu != 0 && ratio > 1.0 && pcpu > row.alloc[KG_RES_CPU] - row.requested[KG_RES_CPU]) {
-        o.feasible = false;
-        return;
+    const bool amplified = pcpu != 0 && ratio > 1.0;
+    if (amplified) {
+        if (row.flags & KG_NODE_NUMA_TOPO_INVALID) {   // GetAvailableCPUs: invalid CPU topology
+            o.feasible = false;
+            return;
+        }
+        int64_t rq = row.requested[KG_RES_CPU];
+        const int64_t am = row.cpuset_milli;
+        if (rq >= am && am > 0) rq += row.cpuset_amp_milli - am;
+        if (pcpu > row.alloc[KG_RES_CPU] - rq) {
+            o.feasible = false;
+            return;
+        }
     }
     if (policy == KG_NUMA_NONE) {
-        o.score = kg_numa_score_node(c, row, p);
+        o.score = kg_numa_score_node(c, row, p, amplified);
         return;
     }
     const int Z = row.n_zones;
@@ -681,7 +707,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
             left &= ~(1u << zi);
             int64_t got[2] = {0, 0};
             for (int r = 0; r < 2; r++) {
-                if (!want[r] || !(((row.zone_keys | row.zone_alloc_keys) >> (2 * zi + r)) & 1u)) continue;
+                if (!want[r] || !(((row.zone_keys | kg_zone_alloc_keys(row)) >> (2 * zi + r)) & 1u)) continue;
                 inter[r] = true;
                 const int64_t a = kg_zone_avail(row, zi, r);
                 got[r] = a < req[r] ? a : req[r];
@@ -707,7 +733,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
             const int zi = o.zone[j];
             for (int r = 0; r < 2; r++) {
                 tot[r] += kg_zone_total(row, zi, r);
-                const int64_t u = row.zone_allocated[zi][r];
+                const int64_t u = kg_zone_alloc(row, zi, r);
                 used[r] += u > 0 ? u : 0;
             }
         }

@@ -556,7 +556,21 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
             const kg_numa_spec &nm = view->numa[ns.numa];
             if (nm.n_zones < 0 || nm.n_zones > KG_MAX_ZONES) return KG_ERR_RANGE;
             row.flags |= KG_NODE_NUMA_OPTIONS;
-            if (nm.cpu_topology_valid) row.flags |= KG_NODE_NUMA_TOPO_VALID;
+            if (nm.cpu_topology_valid < -1 || nm.cpu_topology_valid > 1) return KG_ERR_INVALID_ARG;
+            if (nm.cpu_topology_valid == 1) row.flags |= KG_NODE_NUMA_TOPO_VALID;
+            if (nm.cpu_topology_valid == 0) row.flags |= KG_NODE_NUMA_TOPO_INVALID;
+            // cpuset allocations are recorded only on a valid topology (resourceManager.Update)
+            if (nm.cpuset_cpus < 0 || (nm.cpuset_cpus > 0 && nm.cpu_topology_valid != 1)) return KG_ERR_INVALID_ARG;
+            const double ratio = nm.cpu_amplification_ratio;
+            const auto amplify = [ratio](int64_t x) { return ratio > 1.0 ? (int64_t)ceil((double)x * ratio) : x; };
+            row.cpuset_milli = (int64_t)nm.cpuset_cpus * 1000;
+            row.cpuset_amp_milli = amplify(row.cpuset_milli);
+            for (int z = 0; z < KG_MAX_ZONES; z++) {
+                const int32_t zc = z < nm.n_zones ? nm.zone_cpuset_cpus[z] : 0;
+                if (zc < 0 || zc > nm.cpuset_cpus || (z >= nm.n_zones && nm.zone_cpuset_cpus[z] != 0))
+                    return KG_ERR_INVALID_ARG;
+                row.zone_cpuset_amp[z] = amplify((int64_t)zc * 1000) - (int64_t)zc * 1000;
+            }
             row.numa_policy = nm.policy;
             row.n_zones = nm.n_zones;
             row.cpu_amplification_ratio = nm.cpu_amplification_ratio;

@@ -124,7 +124,9 @@ class Node:
     numa_zone_ids: Optional[List[int]] = None               # NUMANodeResource.Node (default 0..Z-1)
     numa_allocated: Optional[Dict[int, Dict[str, object]]] = None   # allocatedResources by zone id
     cpu_amplification_ratio: float = 0.0
-    cpu_topology_valid: bool = True
+    cpu_topology_valid: bool = True          # CPUTopology.IsValid() of the NodeResourceTopology (nil without zones)
+    cpuset_cpus: int = 0                     # CPUs held by cpuset pods (NodeAllocation.allocatedCPUs)
+    zone_cpuset_cpus: Optional[Dict[int, int]] = None   # those CPUs by zone id
 
 
 NUMA_POLICY = {"": nat.NUMA_NONE, "BestEffort": nat.NUMA_BEST_EFFORT, "Restricted": nat.NUMA_RESTRICTED,
@@ -143,7 +145,11 @@ def numa_spec_record(n: "Node") -> np.ndarray:
         if n.numa_allocated and zid in n.numa_allocated:
             rec["zone_allocated"][z] = resource_list(n.numa_allocated[zid])
     rec["cpu_amplification_ratio"] = n.cpu_amplification_ratio
-    rec["cpu_topology_valid"] = int(n.cpu_topology_valid)
+    # no NodeResourceTopology (a node with only the amplification annotation): CPUTopology is nil
+    rec["cpu_topology_valid"] = -1 if n.numa_zones is None else int(n.cpu_topology_valid)
+    rec["cpuset_cpus"] = n.cpuset_cpus
+    for z, zid in enumerate(ids):
+        rec["zone_cpuset_cpus"][z] = (n.zone_cpuset_cpus or {}).get(zid, 0)
     return rec
 
 
@@ -286,7 +292,7 @@ class Cluster:
                 fv.assigned.append(rec)
             ns["n_assigned"] = len(self.assigned.get(n.name, []))
             ns["numa"] = -1
-            if n.numa_zones is not None:
+            if n.numa_zones is not None or n.cpu_amplification_ratio > 1:
                 ns["numa"] = len(fv.numa)
                 fv.numa.append(numa_spec_record(n))
         fv.nodes = nodes

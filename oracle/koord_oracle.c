@@ -619,6 +619,11 @@ typedef struct {
     kg_resource_list avail[KG_MAX_ZONES];
 } numa_zones;
 
+/* extension.Amplify (apis/extension/node_resource_amplification.go:170-175) */
+static int64_t amplify(int64_t x, double ratio) {
+    return ratio > 1.0 ? (int64_t)ceil((double)x * ratio) : x;
+}
+
 /* TopologyOptions after amplifyNUMANodeResources + NodeAllocation.getAvailableNUMANodeResources */
 static void numa_zones_of(const kg_numa_spec *s, numa_zones *z) {
     memset(z, 0, sizeof(*z));
@@ -630,6 +635,12 @@ static void numa_zones_of(const kg_numa_spec *s, numa_zones *z) {
             z->total[i].v[KG_RES_CPU] = (int64_t)ceil((double)get(&z->total[i], KG_RES_CPU) * s->cpu_amplification_ratio);
         z->allocated[i] = s->zone_allocated[i];
         z->has_alloc[i] = s->zone_allocated[i].present != 0;
+        if (z->has_alloc[i] && s->cpu_amplification_ratio > 1.0) {
+            /* node_allocation.go:164-170: the zone's cpuset CPUs count amplified */
+            int64_t cs = (int64_t)s->zone_cpuset_cpus[i] * 1000;
+            z->allocated[i].v[KG_RES_CPU] = get(&z->allocated[i], KG_RES_CPU) - cs + amplify(cs, s->cpu_amplification_ratio);
+            z->allocated[i].present |= 1u << KG_RES_CPU;
+        }
         kg_resource_list none;
         memset(&none, 0, sizeof(none));
         rl_sub_nonneg(&z->total[i], z->has_alloc[i] ? &z->allocated[i] : &none, &z->avail[i]);
@@ -916,10 +927,19 @@ static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_
     hint->score = 0;
     if (numa_skip(&preq)) return 1;
     int policy = numa ? numa->policy : KG_NUMA_NONE;
-    /* filterAmplifiedCPUs (plugin.go:340-373) without cpuset allocations */
+    /* filterAmplifiedCPUs (plugin.go:340-373); the pod binds no cpuset, the node's cpuset pods are
+     * NodeAllocation.allocatedCPUs (GetAvailableCPUs: nil topology ⇒ none, invalid ⇒ error) */
     double ratio = numa ? numa->cpu_amplification_ratio : 0.0;
     int64_t pcpu = get(&preq, KG_RES_CPU);
-    if (pcpu != 0 && ratio > 1.0 && pcpu > get(&n->allocatable, KG_RES_CPU) - get(&n->requested, KG_RES_CPU)) return 0;
+    int amplified = pcpu != 0 && ratio > 1.0;
+    int64_t cs_milli = 0;
+    if (amplified) {
+        if (numa->cpu_topology_valid == 0) return 0;
+        cs_milli = numa->cpu_topology_valid == 1 ? (int64_t)numa->cpuset_cpus * 1000 : 0;
+        int64_t rq = get(&n->requested, KG_RES_CPU);
+        if (rq >= cs_milli && cs_milli > 0) rq = rq - cs_milli + amplify(cs_milli, ratio);
+        if (pcpu > get(&n->allocatable, KG_RES_CPU) - rq) return 0;
+    }
     numa_zones z;
     if (policy != KG_NUMA_NONE) {
         if (!numa || numa->n_zones == 0) return 0; /* node(s) missing NUMA resources */
@@ -946,8 +966,16 @@ static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_
             *score = numa_scorer(c, c->numa_strategy, &req, &alloc, &preq);
             return 1;
         }
+        *score = numa_scorer(c, c->numa_strategy, &n->requested, &n->allocatable, &preq);
+        return 1;
     }
-    *score = numa_scorer(c, c->numa_strategy, &n->requested, &n->allocatable, &preq);
+    /* policy none: scoreWithAmplifiedCPUs (scoring.go:99-116) */
+    kg_resource_list rq = n->requested;
+    if (amplified) {
+        rq.v[KG_RES_CPU] = get(&rq, KG_RES_CPU) - cs_milli + amplify(cs_milli, ratio);
+        rq.present |= 1u << KG_RES_CPU;
+    }
+    *score = numa_scorer(c, c->numa_strategy, &rq, &n->allocatable, &preq);
     return 1;
 }
 

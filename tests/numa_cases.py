@@ -8,7 +8,9 @@ nodes
   * CPU amplification ratio 1.5 (zone cpu amplified; filterAmplifiedCPUs active)
   * zones over-allocated (available clipped at 0), zones without a memory key, no allocation entry
   * a Restricted node with no zones (Filter: node(s) missing NUMA resources)
-  * invalid CPU topology (Reserve records nothing)
+  * invalid CPU topology (Reserve records nothing; filterAmplifiedCPUs rejects cpu requests)
+  * cpuset pods on the node (whole CPUs per zone, some outside the zones): amplified node / zone cpu
+  * an amplification annotation without NodeResourceTopology (nil CPU topology, no zones)
 pods
   * large requests spanning several zones (minimum affinity > 1, SingleNUMANode rejects)
   * memory-only and cpu-only pods, a present-but-zero cpu key (hint list over every mask)
@@ -53,6 +55,23 @@ def make_numa_edge_cluster(n_nodes: int, n_pods: int, seed: int):
             numa["n_zones"][j] = 0
         if rng.random() < 0.1:
             numa["cpu_topology_valid"][j] = 0
+        elif rng.random() < 0.3:
+            # cpuset pods hold whole CPUs out of the zones' cpu allocations; amplified nodes mostly
+            for z in range(int(numa["n_zones"][j])):
+                al = numa["zone_allocated"][j, z]
+                if al["present"] & np.uint32(1 << nat.RES_CPU):
+                    numa["zone_cpuset_cpus"][j, z] = rng.integers(0, al["v"][nat.RES_CPU] // 1000 + 1)
+            numa["cpuset_cpus"][j] = numa["zone_cpuset_cpus"][j].sum() + rng.integers(0, 3)
+            if rng.random() < 0.6:
+                numa["cpu_amplification_ratio"][j] = rng.choice([1.5, 2.0, 1.25])
+        if rng.random() < 0.04:
+            # amplification annotation without a NodeResourceTopology (CPUTopology nil)
+            numa["policy"][j] = nat.NUMA_NONE
+            numa["n_zones"][j] = 0
+            numa["cpu_topology_valid"][j] = -1
+            numa["cpuset_cpus"][j] = 0
+            numa["zone_cpuset_cpus"][j] = 0
+            numa["cpu_amplification_ratio"][j] = 2.0
     # pods: keep the LS / batch mix, then reshape some LS requests
     rq, lm = cl.containers["requests"], cl.containers["limits"]
     prng = np.random.default_rng(seed + 9)

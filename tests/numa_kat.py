@@ -42,3 +42,56 @@ def merge_lists(providers):
         for res, hints in prov.items():
             lists.append(None if hints is None else [(h[0], h[1]) for h in hints])
     return lists
+
+
+def _amplify(x, ratio):
+    """extension.Amplify (apis/extension/node_resource_amplification.go:170-175)."""
+    import math
+    return x if ratio <= 1 else int(math.ceil(float(x) * float(ratio)))
+
+
+def _amp_pod(name, req, cpuset):
+    # makePodOnNode (plugin_test.go:122-135): prod priority; a cpuset pod is LSR
+    labels = {"koordinator.sh/qosClass": "LSR"} if cpuset else {}
+    return Pod(name=name, containers=[Container(requests=dict(req))], priority=9999, labels=labels)
+
+
+def _amp_node(name, cpu, memory, ratio, nrt, cpuset_cpus):
+    """makeNode (plugin_test.go:114-120) and, for nrt nodes, the TopologyOptions the KATs install:
+    buildCPUTopologyForTest(2, 1, 8, 2) — CPUs 0-15 in NUMA node 0, 16-31 in node 1 — with zones of
+    Amplify(16, ratio) cpus and 20Gi; an existing cpuset pod holds CPUs 0..n-1."""
+    cpu_m = _amplify(quantity_value("cpu", cpu), ratio)
+    node = Node(name, allocatable={"cpu": f"{cpu_m}m", "memory": memory}, cpu_amplification_ratio=ratio)
+    if nrt:
+        zone = {"cpu": str(_amplify(16, ratio)), "memory": "20Gi"}
+        node.numa_zones = [dict(zone), dict(zone)]
+        node.cpu_topology_valid = True
+        node.cpuset_cpus = cpuset_cpus
+        node.zone_cpuset_cpus = {0: min(cpuset_cpus, 16), 1: max(cpuset_cpus - 16, 0)}
+    return node
+
+
+def amplified_score_cluster(case):
+    cl = Cluster()
+    for nd in case["nodes"]:
+        ex = [e for e in case["existing"] if e["node"] == nd["name"]]
+        cs = sum(quantity_value("cpu", e["cpu"]) // 1000 for e in ex if e["cpuset"])
+        pods = [_amp_pod(f"e{i}-{nd['name']}", {"cpu": e["cpu"], "memory": e["memory"]}, e["cpuset"])
+                for i, e in enumerate(ex)]
+        cl.add_node_with_pods(_amp_node(nd["name"], nd["cpu"], nd["memory"], nd["ratio"], nd["nrt"], cs), pods)
+    pod = _amp_pod("p", case["pod"], case["pod_cpuset"])
+    view = cl.view(extra_pods=[pod])
+    cfg = make_config(plugins=("NodeNUMAResource",), numa_strategy=case["strategy"])
+    return cfg, view, view.pod_index(pod), cl
+
+
+def amplified_filter_cluster(case):
+    """TestFilterWithAmplifiedCPUs: one node of cpuTopology.NumCPUs (32) cpus and 40Gi."""
+    cl = Cluster()
+    cs = sum(quantity_value("cpu", e["cpu"]) // 1000 for e in case["existing"] if e["cpuset"])
+    pods = [_amp_pod(f"e{i}", {"cpu": e["cpu"]}, e["cpuset"]) for i, e in enumerate(case["existing"])]
+    cl.add_node_with_pods(_amp_node("node-1", "32", "40Gi", case["ratio"], case["nrt"], cs), pods)
+    pod = _amp_pod("p", case["pod"], case["pod_cpuset"]) if case["pod"] else Pod(name="p")
+    view = cl.view(extra_pods=[pod])
+    cfg = make_config(plugins=("NodeNUMAResource",))
+    return cfg, view, view.pod_index(pod), cl

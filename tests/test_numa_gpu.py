@@ -9,7 +9,7 @@ import pytest
 
 from kat import load
 from numa_cases import make_numa_edge_cluster, numa_config
-from numa_kat import numa_score_cluster
+from numa_kat import amplified_filter_cluster, amplified_score_cluster, numa_score_cluster
 from koordinator_amd import _native as nat
 from koordinator_amd import engine, synth
 from oracle import oracle
@@ -17,6 +17,7 @@ from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 SCORE = load("numa_score_kat.json")
+AMP = load("numa_amplified_kat.json")
 
 
 def _engine_for(cfg, view, pod_index):
@@ -89,6 +90,32 @@ def test_kat_numa_node_score(case):
     k = len(case["nodes"])
     assert list(res["numa_scores"][0, :k]) == case["want"]
     assert engine.unpack_mask(res["mask"], k).all()
+
+
+@pytest.mark.parametrize("case", AMP["score_cases"], ids=lambda c: c["name"])
+def test_kat_amplified_score(case):
+    """TestScoreWithAmplifiedCPUs through kg_eval; a scheduled cpuset pod is rejected at kg_pods_set."""
+    cfg, view, pi, cl = amplified_score_cluster(case)
+    if case["pod_cpuset"]:
+        with engine.Engine(cfg) as eng:
+            eng.load_snapshot(engine.build_node_rows(cfg, view))
+            with pytest.raises(engine.EngineError, match="cpuset"):
+                eng.set_pods(engine.build_pod_rows(cfg, view, [pi]))
+        return
+    with _engine_for(cfg, view, [pi]) as eng:
+        res = eng.eval(0)
+    k = len(case["nodes"])
+    assert list(res["numa_scores"][0, :k]) == case["want"]
+    assert engine.unpack_mask(res["mask"], k).all()
+
+
+@pytest.mark.parametrize("case", [c for c in AMP["filter_cases"] if not c["pod_cpuset"]], ids=lambda c: c["name"])
+def test_kat_amplified_filter(case):
+    """TestFilterWithAmplifiedCPUs through kg_eval (NodeNUMAResource alone)."""
+    cfg, view, pi, cl = amplified_filter_cluster(case)
+    with _engine_for(cfg, view, [pi]) as eng:
+        res = eng.eval(0)
+    assert bool(engine.unpack_mask(res["mask"], 1)[0, 0]) == case["want"]
 
 
 @pytest.mark.parametrize("chunk", [1, 16, 64])

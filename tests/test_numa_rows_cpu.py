@@ -9,11 +9,13 @@ import pytest
 
 from kat import load
 from numa_cases import make_numa_edge_cluster, numa_config
-from numa_kat import numa_score_cluster
+from numa_kat import amplified_filter_cluster, amplified_score_cluster, numa_score_cluster
+from koordinator_amd import _native as nat
 from koordinator_amd import engine, synth
 from oracle import oracle
 
 SCORE = load("numa_score_kat.json")
+AMP = load("numa_amplified_kat.json")
 
 CONFIGS = {
     "least": dict(),
@@ -95,3 +97,47 @@ def test_row_commit_numa_matches_sequential_oracle(seed):
     np.testing.assert_array_equal(np.array(got_n), ref_n)
     np.testing.assert_array_equal(np.array(got_s), ref_s)
     assert (nodes["zone_allocated"] != engine.build_node_rows(cfg, cl)["zone_allocated"]).any()
+
+
+@pytest.mark.parametrize("case", AMP["score_cases"], ids=lambda c: c["name"])
+def test_row_eval_amplified_score_kat(case):
+    """TestScoreWithAmplifiedCPUs through the engine's per-pair code; a scheduled pod that binds a
+    cpuset (LSR prod, integer cpus) is flagged for rejection at kg_pods_set instead."""
+    cfg, view, pi, cl = amplified_score_cluster(case)
+    nodes = engine.build_node_rows(cfg, view)
+    pods = engine.build_pod_rows(cfg, view, [pi])
+    if case["pod_cpuset"]:
+        assert pods["flags"][0] & nat.POD_NUMA_CPU_BIND
+        return
+    assert not pods["flags"][0] & nat.POD_NUMA_CPU_BIND
+    got = [engine.row_eval(cfg, nodes[j:j + 1], pods, 0) for j in range(len(case["nodes"]))]
+    assert all(g[0] for g in got)
+    assert [g[3] for g in got] == case["want"]
+
+
+@pytest.mark.parametrize("case", AMP["filter_cases"], ids=lambda c: c["name"])
+def test_row_eval_amplified_filter_kat(case):
+    cfg, view, pi, cl = amplified_filter_cluster(case)
+    nodes = engine.build_node_rows(cfg, view)
+    pods = engine.build_pod_rows(cfg, view, [pi])
+    if case["pod_cpuset"]:
+        assert pods["flags"][0] & nat.POD_NUMA_CPU_BIND
+        return
+    assert bool(engine.row_eval(cfg, nodes, pods, 0)[0]) == case["want"]
+
+
+def test_edge_cases_reach_the_cpuset_terms():
+    """The edge clusters exercise the amplified cpuset terms: zeroing the cpuset counts changes some
+    feasibility bits and some scores."""
+    P, N = 60, 200
+    cl = make_numa_edge_cluster(N, P, seed=13)
+    cfg = numa_config()
+    m, f, l, n = oracle.eval_matrix3(cfg, cl, np.arange(P), cl.now_ns)
+    numa = cl.numa_arr.copy()
+    numa["cpuset_cpus"] = 0
+    numa["zone_cpuset_cpus"] = 0
+    bare = synth.SynthView(cl.pods, cl.containers, cl.nodes, cl.now_ns, numa)
+    m0, f0, l0, n0 = oracle.eval_matrix3(cfg, bare, np.arange(P), cl.now_ns)
+    assert (m != m0).any()
+    assert (n != n0).any()
+    assert (cl.numa_arr["cpu_topology_valid"] == -1).any()

@@ -7,7 +7,7 @@ WHAT=${2:-all}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [[ $WHAT == all || $WHAT == tests ]]; then
-  timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
     > gpurun_out/tests_$TAG.log 2>&1 || { tail -30 gpurun_out/tests_$TAG.log; exit 1; }
   tail -3 gpurun_out/tests_$TAG.log
 fi
