@@ -477,13 +477,14 @@ kg_status kg_row_eval(const kg_config *cfg, const kg_node_row *node, const kg_po
 
 /* Reservation-aware Filter + Score of one (pod, node) pair on host rows through the kernels' per-pair
  * code (kg_rsv_pair): the node's reservation slots `rsv` (≤ KG_MAX_RSV_PER_NODE, in cache order) are
- * restored for the pod (transformer.go:49-291), Fit / LoadAware / Reservation.Filter run on the
- * restored NodeInfo, and *rsv_raw / *order / *nominated are the pod's PreScore inputs for this node
+ * restored for the pod (transformer.go:49-291), Fit / LoadAware / NodeNUMAResource / Reservation.Filter
+ * run on the restored NodeInfo, and *rsv_raw / *order / *nominated are the pod's PreScore inputs for this node
  * (scoreReservation of the nominated reservation, its order label, its slot; −1 none).  The
  * preferred-node override and NormalizeScore are per-pod reductions over nodes (not per pair). */
 kg_status kg_row_eval_rsv(const kg_config *cfg, const kg_node_row *node, const kg_reservation *rsv, int32_t n_rsv,
                           const kg_pod_row *pod, int64_t now_ns, int32_t *feasible, int32_t *fit_score,
-                          int32_t *la_score, int32_t *rsv_raw, int64_t *order, int32_t *nominated);
+                          int32_t *la_score, int32_t *numa_score, int32_t *rsv_raw, int64_t *order,
+                          int32_t *nominated);
 
 /* Engine lifecycle. */
 kg_status kg_engine_create(const kg_config *cfg, kg_engine **out);

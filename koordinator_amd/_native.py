@@ -213,7 +213,7 @@ def lib() -> ctypes.CDLL:
         "kg_set_profiling": (i32, [vp, i32]), "kg_eval_kernel_times": (i32, [vp, vp, i32]),
         "kg_rsv_set": (i32, [vp, vp, i32]), "kg_rsv_download": (i32, [vp, vp, i32]),
         "kg_quota_set": (i32, [vp, vp, i32]), "kg_quota_download": (i32, [vp, vp, i32]),
-        "kg_row_eval_rsv": (i32, [vp, vp, vp, i32, vp, i64, vp, vp, vp, vp, vp, vp]),
+        "kg_row_eval_rsv": (i32, [vp, vp, vp, i32, vp, i64, vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -352,7 +352,8 @@ KG_HD uint32_t kg_numa_score_zones(const kg_consts &c, bool most, const int64_t 
 // the same over the node's Requested / Allocatable (policy None, or nothing allocated in zones)
 // `amplified`: scoreWithAmplifiedCPUs (scoring.go:99-116), the node's cpuset CPUs counted amplified
 KG_HD uint32_t kg_numa_score_node(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p,
-                                  bool amplified = false) {
+                                  bool amplified = false, const int64_t *requested = nullptr) {
+    if (!requested) requested = row.requested;
     int64_t s = 0, w = 0;
     for (int r = 0; r < KG_NUM_RES; r++) {
         if (c.numa_w[r] <= 0) continue;
@@ -361,7 +362,7 @@ KG_HD uint32_t kg_numa_score_node(const kg_consts &c, const kg_node_row &row, co
         if (scalar && (pr == 0 || !((row.alloc_present >> r) & 1u))) continue;
         const int64_t a = row.alloc[r];
         if (a == 0) continue;
-        int64_t rq = row.requested[r] + pr;
+        int64_t rq = requested[r] + pr;
         if (amplified && r == KG_RES_CPU) rq += row.cpuset_amp_milli - row.cpuset_milli;
         s += (c.numa_most ? kg_mr_i(rq, a) : kg_lr_i(rq, a)) * c.numa_w[r];
         w += c.numa_w[r];
@@ -565,9 +566,12 @@ KG_HD void kg_numa_visit(const kg_consts &c, const ZS &zs, const kg_pod_dev &p, 
 }
 
 // Filter + Score of NodeNUMAResource for one pair; o.zone / o.alloc are what Reserve records.
+// `requested`: NodeInfo.Requested the plugin sees (default the row's; the Reservation restore's view on a
+// node with reservations, transformer.go:49-291 restores the snapshot NodeInfo every plugin reads).
 template <class ZS>
 KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
-                          const ZS &zs) {
+                          const ZS &zs, const int64_t *requested = nullptr) {
+    if (!requested) requested = row.requested;
     o.feasible = true;
     o.score = 0;
     o.n_alloc = 0;
@@ -583,7 +587,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
             o.feasible = false;
             return;
         }
-        int64_t rq = row.requested[KG_RES_CPU];
+        int64_t rq = requested[KG_RES_CPU];
         const int64_t am = row.cpuset_milli;
         if (rq >= am && am > 0) rq += row.cpuset_amp_milli - am;
         if (pcpu > row.alloc[KG_RES_CPU] - rq) {
@@ -592,7 +596,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
         }
     }
     if (policy == KG_NUMA_NONE) {
-        o.score = kg_numa_score_node(c, row, p, amplified);
+        o.score = kg_numa_score_node(c, row, p, amplified, requested);
         return;
     }
     const int Z = row.n_zones;
@@ -739,7 +743,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
         }
         o.score = kg_numa_score_zones(c, c.numa_most != 0, used, tot, p);
     } else {
-        o.score = kg_numa_score_node(c, row, p);
+        o.score = kg_numa_score_node(c, row, p, false, requested);
     }
 }
 
@@ -750,8 +754,9 @@ static __host__ __device__ __noinline__
 #else
 inline
 #endif
-void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o) {
-    kg_numa_pair_z(c, row, p, o, kg_zone_calc{row});
+void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
+                  const int64_t *requested = nullptr) {
+    kg_numa_pair_z(c, row, p, o, kg_zone_calc{row}, requested);
 }
 
 // Reserve of NodeNUMAResource (plugin.go:375-419): record the zone allocations of the chosen node
@@ -1005,7 +1010,7 @@ KG_HD int kg_rsv_nominate(const kg_node_row &row, const kg_rsv_view &v, const kg
 
 struct kg_rsv_out {
     bool feasible;
-    uint32_t fit, la;       // plugin scores on the restored NodeInfo
+    uint32_t fit, la, numa; // plugin scores on the restored NodeInfo
     uint32_t raw;           // Reservation.Score before the preferred-node override and NormalizeScore
     int64_t order;          // PreScore node order (INT64_MAX: none)
     int32_t nominated;      // slot of the nominated reservation, −1 none
@@ -1018,6 +1023,15 @@ KG_HD void kg_rsv_pair(const kg_consts &c, const kg_node_row &row, uint32_t df, 
     kg_rsv_restore(row, rs, nr, p, v);
     bool feas;
     kg_pair_view(c, row, v.requested, v.nonzero, v.pod_count, df, p, now_ns, feas, o.fit, o.la);
+    o.numa = 0;
+    if (c.plugins & KG_PLUGIN_NUMA) {
+        // NodeNUMAResource on the restored NodeInfo; its own RestoreReservation hands back only the
+        // reservations' cpusets (reservation.go:68-122), which reservations of non-binding pods do not hold
+        kg_numa_out no;
+        kg_numa_pair(c, row, p, no, v.requested);
+        feas = feas && no.feasible;
+        o.numa = no.score;
+    }
     if (v.n_matched == 0) feas = feas && p.rsv_aff < 0;  // Reservation.Filter (plugin.go:351-369)
     else feas = feas && kg_rsv_filter_with(row, v, rs, v.matched, v.n_matched, p.rsv_aff >= 0, p);
     o.feasible = feas;

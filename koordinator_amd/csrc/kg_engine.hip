@@ -999,7 +999,7 @@ __device__ __forceinline__ void rsv_entry(const kg_consts &c, const kg_planes &p
     const int32_t node = ra.rnode[k];
     kg_rsv_out r;
     kg_rsv_pair(c, pl.rows[node], pl.dflags[node], ra.rsv + ra.rfirst[k], ra.rfirst[k + 1] - ra.rfirst[k], p, now_ns, r);
-    const uint32_t base = total_of(c, r.fit, r.la);
+    const uint32_t base = total_of(c, r.fit, r.la, r.numa);
     e = r.feasible ? ((unsigned long long)(base + 1u) << 32) | ((unsigned long long)r.raw << 16) |
                          (unsigned long long)(uint32_t)(r.nominated + 1)
                    : 0ull;
@@ -1091,8 +1091,8 @@ __device__ unsigned long long rsv_best_block(const kg_consts &c, const unsigned 
 // entries of pods [0, P) × every reservation node; matrix mode also writes their planes
 __global__ __launch_bounds__(256) void k_rsv_eval(kg_consts c, kg_planes pl, RsvArgs ra, const kg_pod_dev *pods,
                                                   int32_t P, int64_t now_ns, unsigned long long *mask,
-                                                  uint16_t *scores, int64_t col_begin, int64_t col_end,
-                                                  int32_t mask_words, int64_t score_stride) {
+                                                  uint16_t *scores, uint8_t *numa_scores, int64_t col_begin,
+                                                  int64_t col_end, int32_t mask_words, int64_t score_stride) {
     const int32_t k = blockIdx.x * 256 + threadIdx.x;
     const int32_t p = blockIdx.y;
     if (k >= ra.n_rn || p >= P) return;
@@ -1106,6 +1106,7 @@ __global__ __launch_bounds__(256) void k_rsv_eval(kg_consts c, kg_planes pl, Rsv
     if (scores && node >= col_begin && node < col_end) {
         const int64_t col = node - col_begin;
         scores[(int64_t)p * score_stride + col] = (uint16_t)(r.fit | (r.la << 8));
+        if (numa_scores) numa_scores[(int64_t)p * score_stride + col] = (uint8_t)r.numa;
         if (r.feasible) atomicOr(&mask[(int64_t)p * mask_words + (col >> 6)], 1ull << (col & 63));
     }
 }
@@ -1713,12 +1714,13 @@ kg_status quota_ready(kg_engine *e) {
 
 // entries of pods [pod_begin, pod_begin + n) (n ≤ KG_RSV_POD_CHUNK) for every reservation node
 kg_status rsv_eval_chunk(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
-                         int32_t mask_words, int64_t score_stride) {
+                         uint8_t *numa_scores, int32_t mask_words, int64_t score_stride) {
     const RsvArgs ra = rsv_args(e);
     if (!ra.rsv || n <= 0) return KG_OK;
     dim3 grid((unsigned)((ra.n_rn + 255) / 256), (unsigned)n);
     hipLaunchKernelGGL(k_rsv_eval, grid, dim3(256), 0, e->stream, e->consts, e->pl, ra, e->pods + pod_begin, n, now_ns,
-                       (unsigned long long *)mask, scores, e->shard_begin, e->shard_end, mask_words, score_stride);
+                       (unsigned long long *)mask, scores, numa_scores, e->shard_begin, e->shard_end, mask_words,
+                       score_stride);
     HIP_TRY(e, hipGetLastError());
     return KG_OK;
 }
@@ -2091,7 +2093,8 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
         for (int32_t b = 0; b < P; b += KG_RSV_POD_CHUNK) {
             const int32_t n = P - b < KG_RSV_POD_CHUNK ? P - b : KG_RSV_POD_CHUNK;
             st = rsv_eval_chunk(e, now_ns, b, n, mask ? mask + (int64_t)b * mask_words : nullptr,
-                                scores ? scores + (int64_t)b * stride : nullptr, mask_words, stride);
+                                scores ? scores + (int64_t)b * stride : nullptr,
+                                numa_on && numa ? numa + (int64_t)b * stride : nullptr, mask_words, stride);
             if (st) return st;
             hipLaunchKernelGGL(k_rsv_reduce, dim3((unsigned)n), dim3(256), 0, e->stream, e->consts, ra, n,
                                tdst ? tdst + b : nullptr, rsvp ? rsvp + (int64_t)b * stride : nullptr, e->shard_begin,
@@ -2127,7 +2130,7 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
     // ranks in the multi-GPU placement, so each rank holds all of them), rows 0..n of E / O
     if (rsv_args(e).rsv) {
         if (n > KG_RSV_POD_CHUNK) return set_err(e, KG_ERR_RANGE, "chunk larger than the reservation entry buffer");
-        return rsv_eval_chunk(e, now_ns, pod_begin, n, nullptr, nullptr, 0, 0);
+        return rsv_eval_chunk(e, now_ns, pod_begin, n, nullptr, nullptr, nullptr, 0, 0);
     }
     return KG_OK;
 }

@@ -386,8 +386,6 @@ kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
     if (c->enabled_plugins &
         ~(KG_PLUGIN_FIT | KG_PLUGIN_LOADAWARE | KG_PLUGIN_NUMA | KG_PLUGIN_RESERVATION | KG_PLUGIN_ELASTICQUOTA))
         return fail("unsupported plugin bit");
-    if ((c->enabled_plugins & KG_PLUGIN_RESERVATION) && (c->enabled_plugins & KG_PLUGIN_NUMA))
-        return fail("Reservation together with NodeNUMAResource is not supported by the engine");
     if (c->eq_check_parent_quota) return fail("ElasticQuota EnableCheckParentQuota is not supported by the engine");
     int64_t fw = 0, lw = 0, nw = 0;
     for (int r = 0; r < KG_NUM_RES; r++) {
@@ -642,7 +640,8 @@ kg_status kg_row_eval(const kg_config *cfg, const kg_node_row *node, const kg_po
 
 kg_status kg_row_eval_rsv(const kg_config *cfg, const kg_node_row *node, const kg_reservation *rsv, int32_t n_rsv,
                           const kg_pod_row *pod, int64_t now_ns, int32_t *feasible, int32_t *fit_score,
-                          int32_t *la_score, int32_t *rsv_raw, int64_t *order, int32_t *nominated) {
+                          int32_t *la_score, int32_t *numa_score, int32_t *rsv_raw, int64_t *order,
+                          int32_t *nominated) {
     if (!cfg || !node || !pod || !feasible || n_rsv < 0 || n_rsv > KG_MAX_RSV_PER_NODE || (n_rsv > 0 && !rsv))
         return KG_ERR_INVALID_ARG;
     kg_consts k;
@@ -660,6 +659,7 @@ kg_status kg_row_eval_rsv(const kg_config *cfg, const kg_node_row *node, const k
     *feasible = o.feasible ? 1 : 0;
     if (fit_score) *fit_score = (int32_t)o.fit;
     if (la_score) *la_score = (int32_t)o.la;
+    if (numa_score) *numa_score = (int32_t)o.numa;
     if (rsv_raw) *rsv_raw = (int32_t)o.raw;
     if (order) *order = o.order;
     if (nominated) *nominated = o.nominated;

@@ -49,14 +49,16 @@ def row_eval(cfg: np.ndarray, node_row: np.ndarray, pod_row: np.ndarray, now_ns:
 
 
 def row_eval_rsv(cfg: np.ndarray, node_row: np.ndarray, rsv: np.ndarray, pod_row: np.ndarray, now_ns: int):
-    """(feasible, fit, la, raw, order, nominated) of one pair with the node's reservation slots (host rows)."""
+    """(feasible, fit, la, numa, raw, order, nominated) of one pair with the node's reservation slots
+    (host rows)."""
     rsv = np.ascontiguousarray(rsv, dtype=nat.RESERVATION)
-    f, a, b, r, nm = (ctypes.c_int32() for _ in range(5))
+    f, a, b, n, r, nm = (ctypes.c_int32() for _ in range(6))
     o = ctypes.c_int64()
     _check(nat.lib().kg_row_eval_rsv(nat.ptr(cfg), nat.ptr(node_row), nat.ptr(rsv) if len(rsv) else None, len(rsv),
                                      nat.ptr(pod_row), int(now_ns), ctypes.byref(f), ctypes.byref(a), ctypes.byref(b),
-                                     ctypes.byref(r), ctypes.byref(o), ctypes.byref(nm)), what="kg_row_eval_rsv")
-    return bool(f.value), a.value, b.value, r.value, o.value, nm.value
+                                     ctypes.byref(n), ctypes.byref(r), ctypes.byref(o), ctypes.byref(nm)),
+           what="kg_row_eval_rsv")
+    return bool(f.value), a.value, b.value, n.value, r.value, o.value, nm.value
 
 
 class Engine:

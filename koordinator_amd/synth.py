@@ -331,6 +331,26 @@ def make_rsv_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS,
     group's total demand (min = half of it); `non_preemptible_frac` are non-preemptible."""
     rng = np.random.default_rng(seed + 555)
     nodes = make_nodes(n_nodes, seed, now_ns)
+    rsv = _reservations(nodes, rng, rsv_node_frac, owner_classes, (nat.RES_BATCH_CPU, nat.RES_BATCH_MEMORY))
+    pods, cont = make_pods(n_pods, seed)
+    rq, lm = cont["requests"], cont["limits"]
+    cpu_r = np.where(rq["present"] & (1 << nat.RES_CPU), rq["v"][:, nat.RES_CPU], rq["v"][:, nat.RES_BATCH_CPU])
+    mem_r = np.where(rq["present"] & (1 << nat.RES_MEMORY), rq["v"][:, nat.RES_MEMORY], rq["v"][:, nat.RES_BATCH_MEMORY])
+    for arr in (rq, lm):
+        arr["v"][:] = 0
+        arr["present"][:] = 0
+    for arr in (rq, lm):
+        _rl_fill(arr, nat.RES_BATCH_CPU, cpu_r)
+        _rl_fill(arr, nat.RES_BATCH_MEMORY, mem_r)
+    quotas = _owners_and_quotas(pods, cont, seed, owner_classes, n_quotas, quota_ratio, owned_frac, affinity_frac,
+                                non_preemptible_frac)
+    return SynthView(pods, cont, nodes, now_ns, reservations=rsv, quotas=quotas)
+
+
+def _reservations(nodes, rng, rsv_node_frac, owner_classes, res):
+    """`rsv_node_frac` of the nodes carry 1–2 reservations of the two resources `res` (10–30 % of the
+    node's allocatable of them); the reserve pods and their assigned pods are pods of the node."""
+    n_nodes = len(nodes)
     rn = np.sort(rng.choice(n_nodes, int(round(rsv_node_frac * n_nodes)), replace=False))
     node_of = np.repeat(rn, rng.integers(1, 3, len(rn)))
     R = len(node_of)
@@ -350,37 +370,42 @@ def make_rsv_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS,
     rsv["owner_classes"] = owners
     rsv["affinity_classes"] = owners
     rsv["order"] = np.where(rng.random(R) < 0.3, rng.integers(1, 101, R), 0)
-    bcpu = nodes["allocatable"]["v"][node_of, nat.RES_BATCH_CPU]
-    bmem = nodes["allocatable"]["v"][node_of, nat.RES_BATCH_MEMORY]
+    r0, r1 = res
+    bcpu = nodes["allocatable"]["v"][node_of, r0]
+    bmem = nodes["allocatable"]["v"][node_of, r1]
     ac = bcpu * rng.integers(10, 31, R) // 100
     am = (bmem // 100) * rng.integers(10, 31, R)
-    _rl_fill(rsv["allocatable"], nat.RES_BATCH_CPU, ac)
-    _rl_fill(rsv["allocatable"], nat.RES_BATCH_MEMORY, am)
+    if r0 == nat.RES_CPU:
+        ac = ac // 1000 * 1000
+    _rl_fill(rsv["allocatable"], r0, ac)
+    _rl_fill(rsv["allocatable"], r1, am)
     assigned = rng.integers(0, 4, R)
     fill = np.where(assigned > 0, rng.integers(0, 101, R), 0)
     xc = ac * fill // 100
     xm = (am // 100) * fill
     has = assigned > 0
-    _rl_fill(rsv["allocated"], nat.RES_BATCH_CPU, xc, has)
-    _rl_fill(rsv["allocated"], nat.RES_BATCH_MEMORY, xm, has)
+    _rl_fill(rsv["allocated"], r0, xc, has)
+    _rl_fill(rsv["allocated"], r1, xm, has)
     rsv["n_assigned"] = assigned
     rv = nodes["requested"]["v"]
-    np.add.at(rv[:, nat.RES_BATCH_CPU], node_of, ac + xc)
-    np.add.at(rv[:, nat.RES_BATCH_MEMORY], node_of, am + xm)
-    np.add.at(nodes["nonzero_requested"][:, 0], node_of, 100 * (1 + assigned))
-    np.add.at(nodes["nonzero_requested"][:, 1], node_of, 200 * MI * (1 + assigned))
+    np.add.at(rv[:, r0], node_of, ac + xc)
+    np.add.at(rv[:, r1], node_of, am + xm)
+    if r0 == nat.RES_CPU:
+        np.add.at(nodes["nonzero_requested"][:, 0], node_of, ac + xc)
+        np.add.at(nodes["nonzero_requested"][:, 1], node_of, am + xm)
+    else:
+        np.add.at(nodes["nonzero_requested"][:, 0], node_of, 100 * (1 + assigned))
+        np.add.at(nodes["nonzero_requested"][:, 1], node_of, 200 * MI * (1 + assigned))
     np.add.at(nodes["pod_count"], node_of, 1 + assigned)
+    return rsv
 
-    pods, cont = make_pods(n_pods, seed)
-    rq, lm = cont["requests"], cont["limits"]
-    cpu_r = np.where(rq["present"] & (1 << nat.RES_CPU), rq["v"][:, nat.RES_CPU], rq["v"][:, nat.RES_BATCH_CPU])
-    mem_r = np.where(rq["present"] & (1 << nat.RES_MEMORY), rq["v"][:, nat.RES_MEMORY], rq["v"][:, nat.RES_BATCH_MEMORY])
-    for arr in (rq, lm):
-        arr["v"][:] = 0
-        arr["present"][:] = 0
-    for arr in (rq, lm):
-        _rl_fill(arr, nat.RES_BATCH_CPU, cpu_r)
-        _rl_fill(arr, nat.RES_BATCH_MEMORY, mem_r)
+
+def _owners_and_quotas(pods, cont, seed, owner_classes, n_quotas, quota_ratio, owned_frac, affinity_frac,
+                       non_preemptible_frac):
+    """Reservation owner / affinity classes, quota groups and non-preemptible flags of the pods; each
+    group's runtime (used limit) is `quota_ratio` of its total demand of every requested resource
+    (min = half of it)."""
+    n_pods = len(pods)
     prng = np.random.default_rng(seed + 4242)
     owned = prng.random(n_pods) < owned_frac
     owner = prng.integers(0, owner_classes, n_pods)
@@ -390,15 +415,35 @@ def make_rsv_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS,
     pods["quota"] = q
     pods["non_preemptible"] = prng.random(n_pods) < non_preemptible_frac
     quotas = np.zeros(n_quotas, dtype=nat.QUOTA)
-    dc = np.bincount(q, weights=cpu_r, minlength=n_quotas).astype(np.int64)
-    dm = np.bincount(q, weights=mem_r, minlength=n_quotas).astype(np.int64)
-    lim_c = (dc * int(quota_ratio * 100)) // 100
-    lim_m = (dm // 100) * int(quota_ratio * 100)
-    _rl_fill(quotas["used_limit"], nat.RES_BATCH_CPU, lim_c)
-    _rl_fill(quotas["used_limit"], nat.RES_BATCH_MEMORY, lim_m)
-    _rl_fill(quotas["min"], nat.RES_BATCH_CPU, lim_c // 2)
-    _rl_fill(quotas["min"], nat.RES_BATCH_MEMORY, lim_m // 2)
-    return SynthView(pods, cont, nodes, now_ns, reservations=rsv, quotas=quotas)
+    rq = cont["requests"]
+    for r in (nat.RES_CPU, nat.RES_MEMORY, nat.RES_BATCH_CPU, nat.RES_BATCH_MEMORY):
+        has = (rq["present"] & np.uint32(1 << r)) != 0
+        if not has.any():
+            continue
+        d = np.bincount(q, weights=np.where(has, rq["v"][:, r], 0), minlength=n_quotas).astype(np.int64)
+        lim = (d * int(quota_ratio * 100)) // 100 if r in (nat.RES_CPU, nat.RES_BATCH_CPU) else \
+            (d // 100) * int(quota_ratio * 100)
+        _rl_fill(quotas["used_limit"], r, lim)
+        _rl_fill(quotas["min"], r, lim // 2)
+    return quotas
+
+
+def make_profile_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, rsv_node_frac: float = 0.1,
+                         owner_classes: int = 16, n_quotas: int = 32, quota_ratio: float = 0.8,
+                         owned_frac: float = 0.6, affinity_frac: float = 0.1, non_preemptible_frac: float = 0.1,
+                         zones=(2, 4, 8)) -> SynthView:
+    """The shipped profile with every engine plugin (Fit, LoadAware, NodeNUMAResource, Reservation,
+    ElasticQuota): config-3 nodes (NUMA zones, policy mix) and LS / batch pods, with reservations of
+    cpu / memory on `rsv_node_frac` of the nodes (so the restored NodeInfo moves NodeNUMAResource's
+    node-level terms), owner / affinity classes and quota groups over every requested resource."""
+    cl = make_numa_cluster(n_nodes, n_pods, seed, now_ns, zones=zones)
+    nodes = cl.nodes
+    rng = np.random.default_rng(seed + 556)
+    rsv = _reservations(nodes, rng, rsv_node_frac, owner_classes, (nat.RES_CPU, nat.RES_MEMORY))
+    pods, cont = cl.pods, cl.containers
+    quotas = _owners_and_quotas(pods, cont, seed, owner_classes, n_quotas, quota_ratio, owned_frac, affinity_frac,
+                                non_preemptible_frac)
+    return SynthView(pods, cont, nodes, now_ns, numa=cl.numa_arr, reservations=rsv, quotas=quotas)
 
 
 # BASELINE.json configs (single-GPU bench uses config 2)

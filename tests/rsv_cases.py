@@ -70,19 +70,22 @@ def rows_matrix5(cfg, view, pod_index, now_ns):
     mask = np.zeros((P, N), bool)
     fit = np.zeros((P, N), np.uint8)
     la = np.zeros((P, N), np.uint8)
+    numa = np.zeros((P, N), np.uint8)
     rsvp = np.zeros((P, N), np.uint8)
     top1 = np.zeros(P, np.uint64)
     wf, wl, wr = int(cfg["weight_fit"]), int(cfg["weight_loadaware"]), int(cfg["weight_reservation"])
+    wn = int(cfg["weight_numa"]) if int(cfg["enabled_plugins"]) & nat.PLUGIN_NUMA else 0
     for p in range(P):
         raw = np.zeros(N, np.int64)
         order = np.full(N, INT64_MAX, np.int64)
         for j in range(N):
             if j in by_node:
-                f, a, b, rr, o, _ = engine.row_eval_rsv(cfg, rows[j:j + 1], np.array(by_node[j]), prow[p:p + 1], now_ns)
+                f, a, b, n, rr, o, _ = engine.row_eval_rsv(cfg, rows[j:j + 1], np.array(by_node[j]), prow[p:p + 1],
+                                                           now_ns)
                 raw[j], order[j] = rr, o
             else:
-                f, a, b, _ = engine.row_eval(cfg, rows[j:j + 1], prow[p:p + 1], now_ns)
-            mask[p, j], fit[p, j], la[p, j] = f, a, b
+                f, a, b, n = engine.row_eval(cfg, rows[j:j + 1], prow[p:p + 1], now_ns)
+            mask[p, j], fit[p, j], la[p, j], numa[p, j] = f, a, b, n
         feas = mask[p]
         cand = np.where(feas & (order != INT64_MAX))[0]
         if len(cand):
@@ -91,9 +94,9 @@ def rows_matrix5(cfg, view, pod_index, now_ns):
         mx = int(raw[feas].max()) if feas.any() else 0
         s = np.where(feas, (100 * raw) // mx if mx else 0, 0)
         rsvp[p] = s
-        total = wf * fit[p].astype(np.int64) + wl * la[p].astype(np.int64) + wr * s
+        total = wf * fit[p].astype(np.int64) + wl * la[p].astype(np.int64) + wn * numa[p].astype(np.int64) + wr * s
         if feas.any():
             t = np.where(feas, total, -1)
             j = int(t.argmax())
             top1[p] = ((int(t[j]) + 1) << 32) | (0xFFFFFFFF - j)
-    return mask, fit, la, rsvp, top1
+    return mask, fit, la, numa, rsvp, top1

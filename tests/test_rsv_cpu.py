@@ -4,7 +4,7 @@ engine's per-pod reduction against the oracle on seeded config-5 clusters."""
 import numpy as np
 import pytest
 
-from koordinator_amd import engine
+from koordinator_amd import engine, synth
 from koordinator_amd.config import make_config, shipped_profile
 from oracle import oracle
 from rsv_cases import kat_cluster, kat_doc, rows_matrix5, rsv_cluster
@@ -21,7 +21,7 @@ def test_reservation_score_kat(case):
     assert raw == case["want"]
     rows = engine.build_node_rows(cfg, view)
     prow = engine.build_pod_rows(cfg, view, [0])
-    f, _, _, raw2, _, nom2 = engine.row_eval_rsv(cfg, rows[0:1], view.rsv_arr, prow[0:1], view.now_ns)
+    f, _, _, _, raw2, _, nom2 = engine.row_eval_rsv(cfg, rows[0:1], view.rsv_arr, prow[0:1], view.now_ns)
     assert (f, raw2, nom2) == (ok, raw, nom)
 
 
@@ -31,10 +31,24 @@ def test_rows_match_oracle_matrix(seed):
     cfg = shipped_profile(plugins=RSV)
     idx = np.arange(24)
     got = rows_matrix5(cfg, cl, idx, cl.now_ns)
-    m, fit, la, _, rsv, top1 = oracle.eval_matrix5(cfg, cl, idx, cl.now_ns)
-    for a, b in zip(got, (m, fit, la, rsv, top1)):
+    m, fit, la, numa, rsv, top1 = oracle.eval_matrix5(cfg, cl, idx, cl.now_ns)
+    for a, b in zip(got, (m, fit, la, numa, rsv, top1)):
         np.testing.assert_array_equal(a, b)
     assert rsv.max() == 100 and m.any()
+
+
+@pytest.mark.parametrize("seed", [54, 55])
+def test_rows_match_oracle_matrix_with_numa(seed):
+    """Reservation + NodeNUMAResource (the shipped profile's filter set without ElasticQuota): the
+    NUMA terms of reservation nodes run on the restored NodeInfo (kg_rsv_pair → kg_numa_pair)."""
+    cl = synth.make_profile_cluster(400, 24, seed=seed, rsv_node_frac=0.4)
+    cfg = shipped_profile(plugins=RSV + ("NodeNUMAResource",), weight_numa=2)
+    idx = np.arange(24)
+    got = rows_matrix5(cfg, cl, idx, cl.now_ns)
+    m, fit, la, numa, rsv, top1 = oracle.eval_matrix5(cfg, cl, idx, cl.now_ns)
+    for a, b in zip(got, (m, fit, la, numa, rsv, top1)):
+        np.testing.assert_array_equal(a, b)
+    assert rsv.max() == 100 and m.any() and numa.any()
 
 
 def test_oracle_quota_gate_and_reserve():

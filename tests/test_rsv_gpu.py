@@ -4,7 +4,8 @@ quota state after the last Reserve, snapshot rows)."""
 import numpy as np
 import pytest
 
-from koordinator_amd import engine
+from koordinator_amd import _native as nat
+from koordinator_amd import engine, synth
 from koordinator_amd.config import make_config, shipped_profile
 from oracle import oracle
 from rsv_cases import kat_cluster, kat_doc, rsv_cluster
@@ -13,6 +14,7 @@ pytestmark = pytest.mark.gpu
 
 RSV = ("NodeResourcesFit", "LoadAwareScheduling", "Reservation")
 RSV_EQ = RSV + ("ElasticQuota",)
+PROFILE = RSV_EQ + ("NodeNUMAResource",)   # the shipped profile's engine plugins
 
 
 def _engine(cfg, view, idx):
@@ -30,10 +32,12 @@ def _check_matrix(cfg, cl, idx):
     N = len(cl.nodes)
     with _engine(cfg, cl, idx) as eng:
         res = eng.eval(cl.now_ns)
-    m, fit, la, _, rsv, top1 = oracle.eval_matrix5(cfg, cl, idx, cl.now_ns)
+    m, fit, la, numa, rsv, top1 = oracle.eval_matrix5(cfg, cl, idx, cl.now_ns)
     np.testing.assert_array_equal(engine.unpack_mask(res["mask"], N), m)
     np.testing.assert_array_equal(res["scores"][:, :N, 0], fit)
     np.testing.assert_array_equal(res["scores"][:, :N, 1], la)
+    if int(cfg["enabled_plugins"]) & nat.PLUGIN_NUMA:
+        np.testing.assert_array_equal(res["numa_scores"][:, :N], numa)
     np.testing.assert_array_equal(res["rsv_scores"][:, :N], rsv)
     np.testing.assert_array_equal(res["top1"], top1)
     return m, rsv
@@ -134,3 +138,32 @@ def test_commit_needs_every_quota_group():
             eng.commit(0, 0)
     finally:
         eng.close()
+
+
+def test_profile_matrix_parity():
+    """Every engine plugin of the shipped profile at once (Fit, LoadAware, NodeNUMAResource, Reservation,
+    ElasticQuota): NUMA planes of reservation nodes come from the restored NodeInfo."""
+    cl = synth.make_profile_cluster(2600, 72, seed=71, rsv_node_frac=0.25, n_quotas=8, quota_ratio=0.3)
+    m, rsv = _check_matrix(shipped_profile(plugins=PROFILE, weight_numa=2), cl, np.arange(72))
+    assert m.any() and rsv.max() == 100
+
+
+@pytest.mark.parametrize("chunk", [1, 8, 64])
+def test_profile_placement_matches_sequential_cycle(chunk):
+    cl = synth.make_profile_cluster(900, 260, seed=72, rsv_node_frac=0.3, n_quotas=6, quota_ratio=0.5)
+    cfg = shipped_profile(plugins=PROFILE, weight_numa=2, place_chunk=chunk)
+    idx = np.arange(260)
+    with _engine(cfg, cl, idx) as eng:
+        nodes, scores = eng.place(cl.now_ns)
+        rsv_after = eng.download_reservations()
+        q_after = eng.download_quotas()
+        rows_after = eng.download()
+    ref_nodes, ref_scores, ref_rsv, ref_q = oracle.schedule2(cfg, cl, idx, cl.now_ns)
+    np.testing.assert_array_equal(nodes, ref_nodes)
+    np.testing.assert_array_equal(scores, ref_scores)
+    np.testing.assert_array_equal(rsv_after["n_assigned"], ref_rsv["n_assigned"])
+    np.testing.assert_array_equal(rsv_after["allocated"]["v"], ref_rsv["allocated"]["v"])
+    np.testing.assert_array_equal(q_after["used"]["v"], ref_q["used"]["v"])
+    rnodes = set(cl.rsv_arr["node"].tolist())
+    assert any(n in rnodes for n in nodes.tolist())
+    assert (rows_after["zone_allocated"] != engine.build_node_rows(cfg, cl)["zone_allocated"]).any()
