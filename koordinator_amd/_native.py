@@ -189,10 +189,14 @@ def lib() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(ENGINE_SO):
-        raise RuntimeError(f"{ENGINE_SO} is missing: build it with `python koordinator_amd/build.py` "
+    # test hook (tests/test_sanitizers_cpu.py): a sanitizer build of the host code alone; the engine
+    # entry points are absent from it, so any GPU call fails
+    host_only = os.environ.get("KG_SANITIZED_HOST_SO")
+    so = host_only or ENGINE_SO
+    if not os.path.exists(so):
+        raise RuntimeError(f"{so} is missing: build it with `python koordinator_amd/build.py` "
                            "(there is no CPU fallback for the engine)")
-    L = ctypes.CDLL(ENGINE_SO)
+    L = ctypes.CDLL(so)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     sig = {
         "kg_abi_version": (i32, []), "kg_struct_size": (i64, [i32]),
@@ -216,6 +220,8 @@ def lib() -> ctypes.CDLL:
         "kg_row_eval_rsv": (i32, [vp, vp, vp, i32, vp, i64, vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
+        if host_only and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

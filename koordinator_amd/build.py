@@ -68,6 +68,30 @@ def build_oracle(force: bool = False) -> str:
     return ORACLE_SO
 
 
+# AddressSanitizer + UndefinedBehaviorSanitizer builds of the host code (kg_host.cpp: row builders,
+# config validation, the per-pair row evaluation shared with the kernels) and of the oracle, for the CPU
+# test suite (tests/test_sanitizers_cpu.py).  Host code only: GPU sanitizers are not available.
+SAN_DIR = os.path.join(ROOT, "build", "sanitize")
+SAN_HOST_SO = os.path.join(SAN_DIR, "libkoordhost_asan.so")
+SAN_ORACLE_SO = os.path.join(SAN_DIR, "libkoordoracle_asan.so")
+SAN_FLAGS = ["-O1", "-g", "-fPIC", "-shared", "-ffp-contract=off", "-fno-omit-frame-pointer",
+             "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+
+
+def build_sanitized(force: bool = False) -> tuple[str, str]:
+    os.makedirs(SAN_DIR, exist_ok=True)
+    inc = ["-I", os.path.join(ROOT, "include")]
+    host_src = os.path.join(CSRC, "kg_host.cpp")
+    if force or _newer(SAN_HOST_SO, engine_sources()):
+        _run(["g++", "-std=c++17", *SAN_FLAGS, *inc, host_src, "-o", SAN_HOST_SO + ".tmp"])
+        os.replace(SAN_HOST_SO + ".tmp", SAN_HOST_SO)
+    src = os.path.join(ORACLE_DIR, "koord_oracle.c")
+    if force or _newer(SAN_ORACLE_SO, [src, os.path.join(ROOT, "include", "koord_gpu.h")]):
+        _run(["gcc", "-std=c11", *SAN_FLAGS, *inc, src, "-o", SAN_ORACLE_SO + ".tmp", "-lm", "-lpthread"])
+        os.replace(SAN_ORACLE_SO + ".tmp", SAN_ORACLE_SO)
+    return SAN_HOST_SO, SAN_ORACLE_SO
+
+
 def build_all(force: bool = False) -> None:
     build_oracle(force)
     build_engine(force)

@@ -14,9 +14,10 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(ORACLE_SO):
-            raise RuntimeError(f"{ORACLE_SO} missing: run `python koordinator_amd/build.py`")
-        L = ctypes.CDLL(ORACLE_SO)
+        so = os.environ.get("KGO_SANITIZED_SO") or ORACLE_SO   # tests/test_sanitizers_cpu.py
+        if not os.path.exists(so):
+            raise RuntimeError(f"{so} missing: run `python koordinator_amd/build.py`")
+        L = ctypes.CDLL(so)
         vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
         L.kgo_loadaware_filter.restype = ctypes.c_int
         L.kgo_loadaware_filter.argtypes = [vp, vp, vp, vp, i64]
