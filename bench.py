@@ -7,9 +7,16 @@ config 2 = 10k pods × 100k nodes per GPU.
 A step = one matrix-mode pass: every (pod, node) pair of the resident pod batch against the
 resident node shard → feasibility bit plane + {Fit, LoadAware} u8 score planes + per-pod best
 node key; with N > 1 the per-pod keys of all shards are merged with an RCCL all-gather.
-Weak scaling: every rank owns its own 100k-node shard (global nodes = N × 100k).
 
-  python bench.py [--gpus N --steps K --warmup W]
+Scaling modes (--scaling):
+  strong  (default; BASELINE's metric "at 100k nodes, 1/2/4/8 GPU") — one 100k-node cluster (seed 2)
+          sharded over the N ranks, rank r owning nodes [r·100k/N, (r+1)·100k/N);
+  config4 — BASELINE config 4: a 1M-node cluster sharded the same way (125k nodes per rank at N = 8);
+  weak    — every rank owns its own 100k-node cluster (global nodes = N × 100k).
+Placement (pods placed/s) runs over the same global node set: one GPU, or dist.place_sharded with
+the snapshot replicated and the tile range sharded.
+
+  python bench.py [--gpus N --steps K --warmup W] [--scaling strong|config4|weak]
   torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -38,11 +45,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--pods", type=int, default=10_000)
-    ap.add_argument("--nodes", type=int, default=100_000, help="nodes per GPU")
+    ap.add_argument("--nodes", type=int, default=100_000,
+                    help="global nodes (strong) or nodes per GPU (weak); config4 uses 1M")
+    ap.add_argument("--scaling", choices=("strong", "config4", "weak"), default="strong")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: CPU rehearsal of N > 1)")
     ap.add_argument("--no-placement", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=12.0,
+                    help="CPU-baseline budget per baseline: one timed run ≈ budget / 6 (warm-up + median of 5)")
     ap.add_argument("--c3-pods", type=int, default=1_000, help="config-3 (NodeNUMAResource) pods; 0 skips it")
+    ap.add_argument("--c3-large-pods", type=int, default=10_000, help="config-3 matrix run at this many pods; 0 skips")
     ap.add_argument("--c5-pods", type=int, default=100_000,
                     help="config-5 (Reservation + ElasticQuota) pods placed in sequence; 0 skips it")
     ap.add_argument("--c5-matrix-pods", type=int, default=1_000, help="config-5 matrix-mode pods")
@@ -73,6 +85,36 @@ def cpu_model() -> str:
     except OSError:
         pass
     return platform.processor()
+
+
+def host_info() -> dict:
+    """The CPU the baselines ran on: model, logical CPUs of the machine and of this process."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count()
+    return {"model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": avail}
+
+
+def cpu_median(run, cap, target_s=2.0, runs=5, start=4):
+    """SURVEY §8d CPU-baseline method: grow the sample k until one run takes about `target_s`
+    (k ≤ cap), one warm-up run at that size, then `runs` timed runs; returns (k, median s, all s)."""
+    k = max(1, min(start, cap))
+    while True:
+        t0 = time.perf_counter()
+        run(k)
+        dt = time.perf_counter() - t0
+        if dt >= target_s / 4 or k >= cap:
+            break
+        k = min(cap, k * 2)
+    k = max(1, min(cap, int(k * target_s / max(dt, 1e-3))))
+    run(k)
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        run(k)
+        ts.append(time.perf_counter() - t0)
+    return k, float(np.median(ts)), [round(t, 3) for t in ts]
 
 
 def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
@@ -117,12 +159,56 @@ def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
     nodes, _ = eng.place(cl.now_ns)
     tp1 = time.perf_counter()
     eng.close()
-    return {"workload": f"config3: {P} pods x {N} nodes, 4/6/8 NUMA zones, policy mix 40% SingleNUMANode / 30% "
-                        "Restricted / 30% None, 60% LS / 40% batch pods, shipped profile + NodeNUMAResource",
-            "evals_per_s": round(P * N / ((t1 - t0) / steps), 1), "ms_per_step": round((t1 - t0) / steps * 1e3, 3),
-            "kernel": "k_eval_numa2", "kernel_ms": round(k_ms, 3), "feasible_frac_sample": round(feasible, 4),
-            "placement": {"pods": P, "seconds": round(tp1 - tp0, 4), "pods_placed_per_s": round(P / (tp1 - tp0), 1),
-                          "placed": int((nodes >= 0).sum())}}
+    out = {"workload": f"config3: {P} pods x {N} nodes, 4/6/8 NUMA zones, policy mix 40% SingleNUMANode / 30% "
+                       "Restricted / 30% None, 60% LS / 40% batch pods, shipped profile + NodeNUMAResource",
+           "evals_per_s": round(P * N / ((t1 - t0) / steps), 1), "ms_per_step": round((t1 - t0) / steps * 1e3, 3),
+           "kernel": "k_eval_numa2", "kernel_ms": round(k_ms, 3), "feasible_frac_sample": round(feasible, 4),
+           "placement": {"pods": P, "seconds": round(tp1 - tp0, 4), "pods_placed_per_s": round(P / (tp1 - tp0), 1),
+                         "placed": int((nodes >= 0).sum())}}
+    del mask, scores, numa
+    if args.c3_large_pods > 0:
+        # the top of SURVEY's 1k–10k pod range, matrix mode only
+        PL = args.c3_large_pods
+        cl_l = synth.make_numa_cluster(N, PL, seed=3)
+        eng = engine.Engine(cfg)
+        eng.set_stream(stream.cuda_stream)
+        eng.load_snapshot(rows)
+        eng.set_pods(engine.build_pod_rows(cfg, cl_l, np.arange(PL)))
+        mask = torch.empty((PL, W), dtype=torch.int64, device=dev)
+        scores = torch.empty((PL, W * 64, 2), dtype=torch.uint8, device=dev)
+        numa = torch.empty((PL, W * 64), dtype=torch.uint8, device=dev)
+        top1 = torch.zeros(PL, dtype=torch.int64, device=dev)
+        step = lambda: eng.eval_device(cl.now_ns, mask.data_ptr(), scores.data_ptr(), top1.data_ptr(), numa.data_ptr())
+        step()
+        torch.cuda.synchronize(dev)
+        eng.set_profiling(True)
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize(dev)
+        tl = time.perf_counter() - t0
+        kl = float(np.mean(eng.eval_kernel_times(1)))
+        eng.close()
+        del mask, scores, numa
+        out["large"] = {"pods": PL, "evals_per_s": round(PL * N / tl, 1), "ms_per_step": round(tl * 1e3, 3),
+                        "kernel_ms": round(kl, 3)}
+    if not args.no_cpu_baseline:
+        from oracle import oracle  # CPU restatement, timed as the baseline only
+        workers = min(16, os.cpu_count() or 1)
+        k, med, ts = cpu_median(lambda k: oracle.eval_parallel(cfg, cl, np.arange(k), cl.now_ns, workers), P,
+                                target_s=args.cpu_budget_s / 6)
+        out["cpu_baseline"] = {"value": round(k * N / med, 1), "unit": "evals/s", "cores": workers, "kind": "port",
+                               "sample": f"first {k} pods x {N} nodes of the same config-3 cluster, Filter+Score of "
+                                         f"every pair with NodeNUMAResource, {workers}-thread node fan-out "
+                                         f"(kgo_eval_parallel); median of {len(ts)} runs", "runs_s": ts,
+                               "host": host_info()}
+        k2, m2, t2s = cpu_median(lambda k: oracle.schedule_parallel(cfg, cl, np.arange(k), cl.now_ns, workers), P,
+                                 target_s=args.cpu_budget_s / 6)
+        out["placement"]["cpu_baseline"] = {
+            "value": round(k2 / m2, 2), "unit": "pods placed/s", "cores": workers, "kind": "port",
+            "sample": f"first {k2} pods, sequential cycle with zone Reserve and a {workers}-thread Parallelizer "
+                      f"fan-out over nodes per pod (kgo_schedule_parallel); median of {len(t2s)} runs",
+            "runs_s": t2s}
+    return out
 
 
 def bench_config5(args, engine, synth, shipped_profile, dev, stream, cpu_model):
@@ -183,17 +269,12 @@ def bench_config5(args, engine, synth, shipped_profile, dev, stream, cpu_model):
            "matrix": {"pods": PM, "evals_per_s": round(PM * N / tm, 1), "ms_per_step": round(tm * 1e3, 3)}}
     if not args.no_cpu_baseline:
         from oracle import oracle  # CPU restatement of the sequential cycle, timed as the baseline only
-        k, tc = 4, 0.0
-        while True:
-            tc0 = time.perf_counter()
-            oracle.schedule2(cfg, cl, np.arange(k), cl.now_ns)
-            tc = time.perf_counter() - tc0
-            if tc > args.cpu_budget_s / 4 or k >= P:
-                break
-            k = min(P, k * 2)
-        out["cpu_baseline"] = {"value": round(k / tc, 2), "unit": "pods placed/s", "cores": 1, "kind": "port",
+        k, med, ts = cpu_median(lambda k: oracle.schedule2(cfg, cl, np.arange(k), cl.now_ns), P,
+                                target_s=args.cpu_budget_s / 6)
+        out["cpu_baseline"] = {"value": round(k / med, 2), "unit": "pods placed/s", "cores": 1, "kind": "port",
                                "sample": f"first {k} pods of the same burst, sequential cycle over all {N} nodes "
-                                         f"(oracle/koord_oracle.c kgo_schedule2), {tc:.1f}s on {cpu_model()}"}
+                                         f"(oracle/koord_oracle.c kgo_schedule2); median of {len(ts)} runs",
+                               "runs_s": ts, "host": host_info()}
     return out
 
 
@@ -208,19 +289,35 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev if args.backend == "gloo" else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(args.backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
-    P, N = args.pods, args.nodes
-    seed = 2 + 7919 * rank            # rank 0 = BASELINE config 2 (seed 2)
-    cl = synth.make_cluster(N, P, seed=seed)
-    pods_cl = synth.make_cluster(1, P, seed=2)   # the same pod batch on every rank
-    cfg = shipped_profile(device=local)
-    node_rows = engine.build_node_rows(cfg, cl)
+    P = args.pods
+    cfg = shipped_profile(device=gpu)
+    pods_cl = synth.make_cluster(1, P, seed=2)   # the same pod batch on every rank (config-2 pods)
     pod_rows = engine.build_pod_rows(cfg, pods_cl, np.arange(P))
+    if args.scaling == "weak":
+        N = args.nodes
+        total = N * world
+        cl = synth.make_cluster(N, P, seed=2 + 7919 * rank)   # rank 0 = BASELINE config 2 (seed 2)
+        global_rows = None
+        node_rows = engine.build_node_rows(cfg, cl)
+        offset = rank * N
+    else:
+        total = 1_000_000 if args.scaling == "config4" else args.nodes
+        cl = synth.make_cluster(total, P, seed=4 if args.scaling == "config4" else 2)
+        global_rows = engine.build_node_rows(cfg, cl)
+        offset, end = rank * total // world, (rank + 1) * total // world
+        N = end - offset
+        node_rows = np.ascontiguousarray(global_rows[offset:end])
     now = cl.now_ns
 
     eng = engine.Engine(cfg)
@@ -237,12 +334,15 @@ def main():
     scores = torch.empty((P, words * 64, 2), dtype=torch.uint8, device=dev)
     top1 = torch.zeros(P, dtype=torch.int64, device=dev)
     gathered = torch.zeros((world, P), dtype=torch.int64, device=dev) if world > 1 else None
-    offset = rank * N
 
     def step():
         eng.eval_device(now, mask.data_ptr(), scores.data_ptr(), top1.data_ptr())
         if world > 1:
             keys = torch.where(top1 != 0, top1 - offset, top1)       # local → global node index
+            if args.backend != "nccl":          # gloo rehearsal: the equivalent max all-reduce
+                from koordinator_amd import dist as kdist
+                kdist.merge_top1_(keys)
+                return keys
             dist.all_gather_into_tensor(gathered.view(-1), keys)
             return gathered.max(dim=0).values
         return top1
@@ -269,7 +369,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
-    evals_per_s = P * N * world / (elapsed / args.steps)
+    evals_per_s = P * total / (elapsed / args.steps)
 
     k_ms = float(np.mean(kernel_ms)) if len(kernel_ms) else float("nan")
     algo_bytes = P * N * BYTES_PER_PAIR + N * BYTES_PER_NODE + P * BYTES_PER_POD
@@ -290,8 +390,8 @@ def main():
         # node-sharded sequential cycle over the union of every rank's shard (replicated snapshot,
         # per-tile partial keys merged with RCCL all_reduce(MAX), replicated resolve: koordinator_amd/dist.py)
         from koordinator_amd import dist as kdist
-        all_rows = np.concatenate([engine.build_node_rows(cfg, synth.make_cluster(N, 1, seed=2 + 7919 * r))
-                                   for r in range(world)])
+        all_rows = global_rows if global_rows is not None else np.concatenate(
+            [engine.build_node_rows(cfg, synth.make_cluster(N, 1, seed=2 + 7919 * r)) for r in range(world)])
         deng = kdist.sharded_engine(cfg, all_rows, pod_rows, dev)
         dist.barrier()
         torch.cuda.synchronize(dev)
@@ -300,7 +400,7 @@ def main():
         dist.barrier()
         tp1 = time.perf_counter()
         deng.close()
-        placement = {"pods": P, "nodes": N * world, "seconds": round(tp1 - tp0, 6),
+        placement = {"pods": P, "nodes": total, "seconds": round(tp1 - tp0, 6),
                      "pods_placed_per_s": round(P / (tp1 - tp0), 1), "placed": int((nodes >= 0).sum()),
                      "chunk": int(cfg["place_chunk"]), "mode": f"dist.place_sharded over {world} ranks"}
 
@@ -308,17 +408,29 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle  # CPU restatement, timed as the baseline only
         workers = min(16, os.cpu_count() or 1)
-        budget = args.cpu_budget_s
-        done, tc0 = 0, time.perf_counter()
-        while time.perf_counter() - tc0 < budget and done < P:
-            k = min(workers, P - done)
-            oracle.eval_parallel(cfg, cl, np.arange(done, done + k), now, workers)
-            done += k
-        tc = time.perf_counter() - tc0
-        cpu_baseline = {"value": round(done * N / tc, 1), "unit": "evals/s", "cores": workers, "kind": "port",
-                        "sample": f"{done} pods x {N} nodes of the same config-2 cluster, Filter+Score of every pair, "
+        k, med, ts = cpu_median(lambda k: oracle.eval_parallel(cfg, cl, np.arange(k), now, workers), P,
+                                target_s=args.cpu_budget_s / 6)
+        cpu_baseline = {"value": round(k * N / med, 1), "unit": "evals/s", "cores": workers, "kind": "port",
+                        "sample": f"first {k} pods x {N} nodes of the same config-2 cluster, Filter+Score of every pair, "
                                   f"Parallelizer-faithful {workers}-thread node fan-out (oracle/koord_oracle.c "
-                                  f"kgo_eval_parallel), {tc:.1f}s on {cpu_model()}"}
+                                  f"kgo_eval_parallel); median of {len(ts)} runs after a warm-up",
+                        "runs_s": ts, "host": host_info()}
+        if placement is not None:
+            # placement baselines: the sequential cycle, single-threaded and with the 16-thread
+            # Parallelizer fan-out over nodes per pod (kgo_schedule_parallel), on a pod prefix
+            k1, m1, t1s = cpu_median(lambda k: oracle.schedule(cfg, cl, np.arange(k), now), P,
+                                     target_s=args.cpu_budget_s / 6)
+            k2, m2, t2s = cpu_median(lambda k: oracle.schedule_parallel(cfg, cl, np.arange(k), now, workers), P,
+                                     target_s=args.cpu_budget_s / 6)
+            placement["cpu_baseline"] = {
+                "sequential": {"value": round(k1 / m1, 2), "unit": "pods placed/s", "cores": 1, "kind": "port",
+                               "sample": f"first {k1} pods, sequential cycle over all {N} nodes (kgo_schedule); "
+                                         f"median of {len(t1s)} runs", "runs_s": t1s},
+                "parallel": {"value": round(k2 / m2, 2), "unit": "pods placed/s", "cores": workers, "kind": "port",
+                             "sample": f"first {k2} pods, sequential cycle with a {workers}-thread Parallelizer fan-out "
+                                       f"over nodes per pod (kgo_schedule_parallel); median of {len(t2s)} runs",
+                             "runs_s": t2s},
+                "host": host_info()}
 
     config3 = None
     if args.c3_pods > 0 and world == 1:
@@ -339,13 +451,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.scaling == "weak" else "strong",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic",
-            "config": {"workload": f"config2: {P} pods x {N} nodes per GPU ({N * world} nodes total), shipped-profile "
-                                   "args, outputs: feasibility bits + Fit/LoadAware u8 scores + per-pod top-1",
-                       "pods": P, "nodes_per_gpu": N, "parallelism": f"node-shard x{world}"},
+            "config": {"workload": (f"{'config4' if args.scaling == 'config4' else 'config2'}: {P} pods x {total} nodes "
+                                    f"({N} on rank 0 of {world}, {args.scaling} scaling), shipped-profile args, "
+                                    "outputs: feasibility bits + Fit/LoadAware u8 scores + per-pod top-1"),
+                       "pods": P, "nodes": total, "nodes_per_gpu": N, "parallelism": f"node-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK, 4),
                          "traffic": None if traffic is None else int(traffic), "traffic_unit": "bytes per launch (PMC)",

@@ -27,6 +27,7 @@
  * reference test in the tree (parity unpinned beyond its in-repo mirrors).
  * Built with -ffp-contract=off so float64 expressions round like Go's.
  */
+#define _POSIX_C_SOURCE 200809L /* pthread barriers of the CPU baselines under -std=c11 */
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -1430,6 +1431,62 @@ int kgo_eval_matrix5(const kg_config *c, const kg_cluster_view *v, const int32_t
     return 0;
 }
 
+/* Reserve of the chosen node for one pod: AssumePod, NodeNUMAResource zones, Reservation, ElasticQuota,
+ * LoadAware assign (the sequential cycle's state updates). */
+static void reserve_pod(const kg_config *c, kg_cluster_view *vv, const kg_cluster_view *v, node_state *st,
+                        rsv_index *ri, kg_quota *quotas, const kg_pod_spec *pod, int32_t best_n, int nom,
+                        int64_t now_ns) {
+    /* Reserve: AssumePod → NodeInfo.AddPod (calculateResource) */
+    node_state *s = &st[best_n];
+    fw_resource req;
+    fit_pod_request(vv, pod, &req);
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        if (r < 3 || ((req.scalar_keys >> r) & 1u)) {
+            s->spec.requested.v[r] = get(&s->spec.requested, r) + req.v[r];
+            if (r >= 3) s->spec.requested.present |= 1u << r;
+        }
+    }
+    s->spec.requested.present |= 0x7u;
+    for (int r = 0; r < 2; r++) {
+        int64_t nz = 0;
+        for (int k = 0; k < pod->n_containers; k++)
+            nz += request_for_resource(r, &v->containers[pod->first_container + k].requests, 1);
+        for (int k = 0; k < pod->n_init_containers; k++) {
+            int64_t x = request_for_resource(r, &v->containers[pod->first_init_container + k].requests, 1);
+            if (x > nz) nz = x;
+        }
+        if (pod->overhead.present && has(&pod->overhead, r)) nz += pod->overhead.v[r];
+        s->spec.nonzero_requested[r] += nz;
+    }
+    s->spec.pod_count += 1;
+    /* NodeNUMAResource.Reserve → resourceManager.Update: zone allocations of the stored hint (the
+     * zone state is the one the pod was filtered on, so re-admitting reproduces that hint) */
+    if ((c->enabled_plugins & KG_PLUGIN_NUMA) && s->has_numa) numa_reserve(c, vv, pod, &s->numa);
+    kg_resource_list preq;
+    numa_pod_requests(vv, pod, &preq);
+    /* Reservation.Reserve → reservationCache.assumePod → ReservationInfo.AddAssignedPod
+     * (plugin.go:525-560, reservation_info.go:379-388) on the nominated reservation */
+    if ((c->enabled_plugins & KG_PLUGIN_RESERVATION) && nom >= 0) {
+        kg_reservation *r = &ri->of[best_n][nom]->r;
+        kg_resource_list m = preq;
+        m.present &= r->allocatable.present;
+        rl_add(&r->allocated, &m);
+        r->n_assigned += 1;
+    }
+    /* ElasticQuota.Reserve → GroupQuotaManager.ReservePod → used += requests */
+    if (c->enabled_plugins & KG_PLUGIN_ELASTICQUOTA) quota_reserve(pod, &preq, quotas);
+    /* LoadAware.Reserve → podAssignCache.assign(nodeName, pod) with timestamp now */
+    if (!pod->is_terminated) {
+        if (s->n_assigned == s->cap_assigned) {
+            s->cap_assigned *= 2;
+            s->assigned = (assigned_ref *)realloc(s->assigned, sizeof(assigned_ref) * (size_t)s->cap_assigned);
+        }
+        s->assigned[s->n_assigned].pod = pod;
+        s->assigned[s->n_assigned].ts = now_ns;
+        s->n_assigned++;
+    }
+}
+
 /* Sequential reference cycle over pod_index[0..P) in queue order.
  * out_node[p] = chosen node or -1; out_score[p] = weighted total or -1.  out_rsv / out_quota
  * (may be NULL) receive the reservation / quota states after the last Reserve. */
@@ -1450,55 +1507,7 @@ int kgo_schedule2(const kg_config *c, const kg_cluster_view *v, const int32_t *p
         out_node[p] = best_n;
         out_score[p] = best_n < 0 ? -1 : best;
         if (best_n < 0) continue;
-        /* Reserve: AssumePod → NodeInfo.AddPod (calculateResource) */
-        node_state *s = &st[best_n];
-        fw_resource req;
-        fit_pod_request(&vv, pod, &req);
-        for (int r = 0; r < KG_NUM_RES; r++) {
-            if (r < 3 || ((req.scalar_keys >> r) & 1u)) {
-                s->spec.requested.v[r] = get(&s->spec.requested, r) + req.v[r];
-                if (r >= 3) s->spec.requested.present |= 1u << r;
-            }
-        }
-        s->spec.requested.present |= 0x7u;
-        for (int r = 0; r < 2; r++) {
-            int64_t nz = 0;
-            for (int k = 0; k < pod->n_containers; k++)
-                nz += request_for_resource(r, &v->containers[pod->first_container + k].requests, 1);
-            for (int k = 0; k < pod->n_init_containers; k++) {
-                int64_t x = request_for_resource(r, &v->containers[pod->first_init_container + k].requests, 1);
-                if (x > nz) nz = x;
-            }
-            if (pod->overhead.present && has(&pod->overhead, r)) nz += pod->overhead.v[r];
-            s->spec.nonzero_requested[r] += nz;
-        }
-        s->spec.pod_count += 1;
-        /* NodeNUMAResource.Reserve → resourceManager.Update: zone allocations of the stored hint (the
-         * zone state is the one the pod was filtered on, so re-admitting reproduces that hint) */
-        if ((c->enabled_plugins & KG_PLUGIN_NUMA) && s->has_numa) numa_reserve(c, &vv, pod, &s->numa);
-        kg_resource_list preq;
-        numa_pod_requests(&vv, pod, &preq);
-        /* Reservation.Reserve → reservationCache.assumePod → ReservationInfo.AddAssignedPod
-         * (plugin.go:525-560, reservation_info.go:379-388) on the nominated reservation */
-        if ((c->enabled_plugins & KG_PLUGIN_RESERVATION) && nom >= 0) {
-            kg_reservation *r = &ri.of[best_n][nom]->r;
-            kg_resource_list m = preq;
-            m.present &= r->allocatable.present;
-            rl_add(&r->allocated, &m);
-            r->n_assigned += 1;
-        }
-        /* ElasticQuota.Reserve → GroupQuotaManager.ReservePod → used += requests */
-        if (c->enabled_plugins & KG_PLUGIN_ELASTICQUOTA) quota_reserve(pod, &preq, quotas);
-        /* LoadAware.Reserve → podAssignCache.assign(nodeName, pod) with timestamp now */
-        if (!pod->is_terminated) {
-            if (s->n_assigned == s->cap_assigned) {
-                s->cap_assigned *= 2;
-                s->assigned = (assigned_ref *)realloc(s->assigned, sizeof(assigned_ref) * (size_t)s->cap_assigned);
-            }
-            s->assigned[s->n_assigned].pod = pod;
-            s->assigned[s->n_assigned].ts = now_ns;
-            s->n_assigned++;
-        }
+        reserve_pod(c, &vv, v, st, &ri, quotas, pod, best_n, nom, now_ns);
     }
     if (out_rsv)
         for (int32_t i = 0; i < v->n_reservations; i++) out_rsv[i] = ri.states[i].r;
@@ -1593,5 +1602,132 @@ int kgo_eval_parallel(const kg_config *c, const kg_cluster_view *v, const int32_
     free(th);
     free(args);
     free(best);
+    return 0;
+}
+
+/* ---------------------------------------------------------------- */
+/* CPU placement baseline: the sequential cycle with the reference's  */
+/* Parallelizer fan-out over nodes inside each pod (Filter + Score of */
+/* every node on `workers` threads, selectHost, then Reserve on the   */
+/* calling thread).  Plugins: Fit, LoadAware, NodeNUMAResource.       */
+/* ---------------------------------------------------------------- */
+typedef struct {
+    const kg_config *c;
+    kg_cluster_view *vv;
+    node_state *st;
+    const kg_pod_spec *pod;
+    int64_t now_ns;
+    int32_t n, chunk, workers;
+    int32_t next;
+    int stop;
+    int64_t *best;
+    pthread_barrier_t start, done;
+} sched_pool;
+
+typedef struct { sched_pool *pool; int w; } sched_arg;
+
+/* Filter + weighted Score of one plain node on its current state (oracle_pod without reservations) */
+static int node_total(const kg_config *c, kg_cluster_view *vv, node_state *s, const kg_pod_spec *pod, int64_t now_ns,
+                      int64_t *total) {
+    kg_node_spec *n = &s->spec;
+    int64_t numa_score = 0;
+    if (c->enabled_plugins & KG_PLUGIN_NUMA) {
+        numa_hint h;
+        if (!numa_pair(c, vv, pod, n, s->has_numa ? &s->numa : NULL, &numa_score, &h)) return 0;
+    }
+    if ((c->enabled_plugins & KG_PLUGIN_FIT) && kgo_fit_filter(vv, pod, n) != KG_CODE_SUCCESS) return 0;
+    if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && kgo_loadaware_filter(c, vv, pod, n, now_ns) != KG_CODE_SUCCESS)
+        return 0;
+    int64_t fit = (c->enabled_plugins & KG_PLUGIN_FIT) ? kgo_fit_score(c, vv, pod, n) : 0;
+    int64_t la = (c->enabled_plugins & KG_PLUGIN_LOADAWARE)
+                     ? loadaware_score_impl(c, vv, pod, n, s->assigned, s->n_assigned, now_ns) : 0;
+    *total = c->weight_fit * fit + c->weight_loadaware * la + c->weight_numa * numa_score;
+    return 1;
+}
+
+static void *sched_worker(void *arg) {
+    sched_arg *a = (sched_arg *)arg;
+    sched_pool *pl = a->pool;
+    for (;;) {
+        pthread_barrier_wait(&pl->start);
+        if (pl->stop) break;
+        int64_t best = -1;
+        for (;;) {
+            int32_t s0 = __atomic_fetch_add(&pl->next, pl->chunk, __ATOMIC_RELAXED);
+            if (s0 >= pl->n) break;
+            int32_t e = s0 + pl->chunk < pl->n ? s0 + pl->chunk : pl->n;
+            for (int32_t k = s0; k < e; k++) {
+                int64_t total;
+                if (!node_total(pl->c, pl->vv, &pl->st[k], pl->pod, pl->now_ns, &total)) continue;
+                int64_t key = ((total + 1) << 32) | (int64_t)(0xFFFFFFFFu - (uint32_t)k);
+                if (key > best) best = key;
+            }
+        }
+        pl->best[a->w] = best;
+        pthread_barrier_wait(&pl->done);
+    }
+    return NULL;
+}
+
+/* Same outputs as kgo_schedule; returns -2 for plugins outside Fit / LoadAware / NodeNUMAResource. */
+int kgo_schedule_parallel(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P,
+                          int64_t now_ns, int32_t workers, int32_t *out_node, int64_t *out_score) {
+    if (c->enabled_plugins & (KG_PLUGIN_RESERVATION | KG_PLUGIN_ELASTICQUOTA)) return -2;
+    if (workers < 1) workers = 1;
+    int32_t N = v->n_nodes;
+    node_state *st = states_build(v, N);
+    kg_cluster_view vv = *v;
+    rsv_index ri;
+    if (rsv_index_build(v, N, &ri) != 0) { rsv_index_free(&ri); states_free(st, N); return -1; }
+    sched_pool pl;
+    memset(&pl, 0, sizeof(pl));
+    pl.c = c;
+    pl.vv = &vv;
+    pl.st = st;
+    pl.now_ns = now_ns;
+    pl.n = N;
+    pl.workers = workers;
+    pl.chunk = (int32_t)sqrt((double)N);   /* parallelize.chunkSizeFor */
+    if (N / workers + 1 < pl.chunk) pl.chunk = N / workers + 1;
+    if (pl.chunk < 1) pl.chunk = 1;
+    pl.best = (int64_t *)malloc(sizeof(int64_t) * (size_t)workers);
+    pthread_barrier_init(&pl.start, NULL, (unsigned)workers + 1);
+    pthread_barrier_init(&pl.done, NULL, (unsigned)workers + 1);
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)workers);
+    sched_arg *args = (sched_arg *)malloc(sizeof(sched_arg) * (size_t)workers);
+    for (int w = 0; w < workers; w++) {
+        args[w].pool = &pl;
+        args[w].w = w;
+        pthread_create(&th[w], NULL, sched_worker, &args[w]);
+    }
+    for (int32_t p = 0; p < P; p++) {
+        const kg_pod_spec *pod = &v->pods[pod_index[p]];
+        pl.pod = pod;
+        pl.next = 0;
+        pthread_barrier_wait(&pl.start);
+        pthread_barrier_wait(&pl.done);
+        int64_t b = -1;
+        for (int w = 0; w < workers; w++)
+            if (pl.best[w] > b) b = pl.best[w];
+        if (b < 0) {
+            out_node[p] = -1;
+            out_score[p] = -1;
+            continue;
+        }
+        int32_t node = (int32_t)(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFF));
+        out_node[p] = node;
+        out_score[p] = (b >> 32) - 1;
+        reserve_pod(c, &vv, v, st, &ri, NULL, pod, node, -1, now_ns);
+    }
+    pl.stop = 1;
+    pthread_barrier_wait(&pl.start);
+    for (int w = 0; w < workers; w++) pthread_join(th[w], NULL);
+    pthread_barrier_destroy(&pl.start);
+    pthread_barrier_destroy(&pl.done);
+    free(th);
+    free(args);
+    free(pl.best);
+    rsv_index_free(&ri);
+    states_free(st, N);
     return 0;
 }

@@ -218,3 +218,20 @@ def rsv_pair(cfg, view, pod_i, node_j):
     if ok < 0:
         raise RuntimeError("kgo_rsv_pair failed")
     return bool(ok), raw.value, nom.value
+
+
+def schedule_parallel(cfg, view, pod_index, now_ns, workers):
+    """The sequential cycle with a `workers`-thread Parallelizer fan-out over nodes per pod (CPU
+    placement baseline; Fit / LoadAware / NodeNUMAResource)."""
+    idx = np.ascontiguousarray(pod_index, dtype=np.int32)
+    nodes = np.zeros(len(idx), np.int32)
+    scores = np.zeros(len(idx), np.int64)
+    L = lib()
+    L.kgo_schedule_parallel.restype = ctypes.c_int
+    L.kgo_schedule_parallel.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32] + \
+        [ctypes.c_void_p] * 2
+    st = L.kgo_schedule_parallel(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, len(idx), now_ns, int(workers),
+                                 nodes.ctypes.data, scores.ctypes.data)
+    if st != 0:
+        raise RuntimeError(f"kgo_schedule_parallel failed ({st})")
+    return nodes, scores

@@ -1,0 +1,29 @@
+"""The CPU placement baseline (oracle kgo_schedule_parallel: the sequential cycle with a Parallelizer
+fan-out over nodes per pod) places exactly like the sequential oracle cycle."""
+import numpy as np
+import pytest
+
+from numa_cases import make_numa_edge_cluster, numa_config
+from koordinator_amd import synth
+from koordinator_amd.config import shipped_profile
+from oracle import oracle
+
+
+@pytest.mark.parametrize("workers", [1, 3, 8])
+def test_parallel_cycle_matches_sequential(workers):
+    cl = synth.make_cluster(1_500, 80, seed=12)
+    cfg = shipped_profile()
+    ref = oracle.schedule(cfg, cl, np.arange(80), cl.now_ns)
+    got = oracle.schedule_parallel(cfg, cl, np.arange(80), cl.now_ns, workers)
+    np.testing.assert_array_equal(got[0], ref[0])
+    np.testing.assert_array_equal(got[1], ref[1])
+
+
+def test_parallel_cycle_matches_sequential_numa():
+    cl = make_numa_edge_cluster(300, 120, seed=14)
+    cfg = numa_config(weight_numa=2)
+    ref = oracle.schedule(cfg, cl, np.arange(120), cl.now_ns)
+    got = oracle.schedule_parallel(cfg, cl, np.arange(120), cl.now_ns, 6)
+    np.testing.assert_array_equal(got[0], ref[0])
+    np.testing.assert_array_equal(got[1], ref[1])
+    assert (ref[0] >= 0).any()
