@@ -58,6 +58,12 @@ extern "C" {
 /* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
 #define KG_PLACE_CHUNK_MAX 1024
 
+/* kg_place_chunk_eval / _resolve partial buffer: KG_PARTIAL_SLOTS uint32 per (pod, 1024-node tile) —
+ * the tile's best keys in descending order, 0-padded (nodes outside the fp64 fast-path bounds are not
+ * listed: the resolve re-scores them from the engine's slow-node list).  Slots of a tile come from one
+ * rank only, so ranks merge buffers with an element-wise max. */
+#define KG_PARTIAL_SLOTS 16
+
 /* ------------------------------------------------------------------ */
 /* status codes                                                          */
 /* ------------------------------------------------------------------ */
@@ -515,8 +521,9 @@ kg_status kg_eval(kg_engine *eng, int64_t now_ns, const kg_eval_out *out);
 kg_status kg_place(kg_engine *eng, int64_t now_ns, int32_t *out_node, int64_t *out_score);
 
 /* Multi-GPU building blocks of kg_place (see koordinator_amd/dist.py):
- * chunk_eval writes per-(pod, 512-node tile) partial keys of the shard for pods
- * [pod_begin, pod_begin+n) into partial_dev ([n][tiles_total] uint32, tile index global);
+ * chunk_eval writes per-(pod, 1024-node tile) partial keys of the shard for pods
+ * [pod_begin, pod_begin+n) into partial_dev ([n][tiles_total][KG_PARTIAL_SLOTS] uint32, tile index
+ * global; the caller zeroes nothing, chunk_eval clears the buffer's n rows itself);
  * chunk_resolve commits those pods sequentially given the partials of ALL tiles. */
 int32_t kg_num_tiles(const kg_engine *eng);
 kg_status kg_place_chunk_eval(kg_engine *eng, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev);

@@ -40,6 +40,7 @@ NODE_NUMA_OPTIONS, NODE_NUMA_TOPO_VALID, NODE_NUMA_TOPO_INVALID = 0x40, 0x80, 0x
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE, CODE_UNSCHEDULABLE_AND_UNRESOLVABLE = 0, 1, 2, 3
 TILE = 1024
 PLACE_CHUNK_MAX = 1024
+PARTIAL_SLOTS = 16      # KG_PARTIAL_SLOTS: uint32 per (pod, tile) in the placement-chunk partial buffer
 
 RESOURCE_LIST = np.dtype([("v", "<i8", (NUM_RES,)), ("present", "<u4"), ("_pad", "<u4")], align=True)
 

@@ -174,11 +174,41 @@ struct kg_planes {
 
 KG_HD int64_t kg_abs64(int64_t x) { return x < 0 ? -x : x; }
 
+// Exact truncating int64 quotient and remainder of n / d (d > 0) — the device has no int64 divide
+// instruction: an fp64 estimate (relative error ≈ 2^-52, so off by ≤ |n/d|·2^-51 + 1) is corrected
+// with exact int64 arithmetic, the residual's own fp64 quotient and a final ±1 step.
+// Valid for |n| < 2^57 and 0 < d < 2^53 (the finalize operands: |100·(a − base)| < 2^57, a < 2^41).
+KG_HD void kg_divmod64_fp(int64_t n, int64_t d, int64_t &q, int64_t &r) {
+    int64_t q0 = (int64_t)((double)n / (double)d);
+    int64_t r0 = n - q0 * d;
+    const int64_t q1 = (int64_t)((double)r0 / (double)d);
+    q0 += q1;
+    r0 -= q1 * d;
+    // C truncation: the remainder takes the sign of n and |r| < d
+    if (n >= 0) {
+        if (r0 < 0) { q0 -= 1; r0 += d; }
+        else if (r0 >= d) { q0 += 1; r0 -= d; }
+    } else {
+        if (r0 > 0) { q0 += 1; r0 -= d; }
+        else if (r0 <= -d) { q0 -= 1; r0 += d; }
+    }
+    q = q0;
+    r = r0;
+}
+KG_HD void kg_divmod64(int64_t n, int64_t d, int64_t &q, int64_t &r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    kg_divmod64_fp(n, d, q, r);
+#else
+    q = n / d;
+    r = n % d;
+#endif
+}
+
 // RN(100*num/den + eps) from an exact int64 quotient and remainder (|100*num| < 2^63)
 KG_HD double kg_scaled_ratio(int64_t num, int64_t den) {
     int64_t n100 = num * 100;
-    int64_t q = n100 / den;
-    int64_t r = n100 % den;
+    int64_t q, r;
+    kg_divmod64(n100, den, q, r);
     return (double)q + ((double)r / (double)den + KG_EPS);
 }
 
@@ -187,11 +217,15 @@ KG_HD double kg_scaled_ratio(int64_t num, int64_t den) {
 //   kg_finalize_fit(r)  Fit planes and free_ of resource r (r < KG_NUM_RES) → bit 0: slow, bit 1: in fit_mask
 //   kg_finalize_la(r)   LoadAware planes of resource r (r < 2)             → slow
 //   kg_finalize_flags   dflags / fit_mask / metric from the parts' results
-KG_HD uint32_t kg_finalize_fit(const kg_consts &c, const kg_planes &pl, int64_t i, int r) {
+// (free / R / F out: optional copies of the written plane values, for the resolve kernel's node cache)
+KG_HD uint32_t kg_finalize_fit(const kg_consts &c, const kg_planes &pl, int64_t i, int r, int64_t *free_out = nullptr,
+                               double *R_out = nullptr, double *F_out = nullptr) {
     const kg_node_row &row = pl.rows[i];
     const int64_t cap = pl.cap;
     uint32_t out = 0;
-    pl.free_[r * cap + i] = row.alloc[r] - row.requested[r];
+    const int64_t fr = row.alloc[r] - row.requested[r];
+    pl.free_[r * cap + i] = fr;
+    if (free_out) *free_out = fr;
     double R = 0.0, F = 0.0;
     int64_t a = row.alloc[r];
     bool present = r < 3 || ((row.alloc_present >> r) & 1u);
@@ -207,9 +241,12 @@ KG_HD uint32_t kg_finalize_fit(const kg_consts &c, const kg_planes &pl, int64_t 
     }
     pl.fit_R[r * cap + i] = R;
     pl.fit_F[r * cap + i] = F;
+    if (R_out) *R_out = R;
+    if (F_out) *F_out = F;
     return out;
 }
-KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, int r) {
+KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, int r, double *R_out = nullptr,
+                          double *F0_out = nullptr, double *F1_out = nullptr) {
     const kg_node_row &row = pl.rows[i];
     const int64_t cap = pl.cap;
     bool slow = false;
@@ -228,7 +265,18 @@ KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, in
     pl.la_R[r * cap + i] = R;
     pl.la_F[(0 * 2 + r) * cap + i] = F0;
     pl.la_F[(1 * 2 + r) * cap + i] = F1;
+    if (R_out) {
+        *R_out = R;
+        *F0_out = F0;
+        *F1_out = F1;
+    }
     return slow;
+}
+// the bits of dflags a Reserve can change, from the committed row values
+#define KGD_DYNAMIC (KGD_PODS_FULL | KGD_OVER_CPU | KGD_OVER_MEM | KGD_OVER_EPH | KGD_SLOW)
+KG_HD uint32_t kg_dflags_dynamic(bool pods_full, const bool over[3], bool slow) {
+    return (pods_full ? KGD_PODS_FULL : 0u) | (over[0] ? KGD_OVER_CPU : 0u) | (over[1] ? KGD_OVER_MEM : 0u) |
+           (over[2] ? KGD_OVER_EPH : 0u) | (slow ? KGD_SLOW : 0u);
 }
 KG_HD void kg_finalize_flags(const kg_planes &pl, int64_t i, bool slow, uint32_t fmask) {
     const kg_node_row &row = pl.rows[i];
@@ -568,9 +616,10 @@ KG_HD void kg_numa_visit(const kg_consts &c, const ZS &zs, const kg_pod_dev &p, 
 // Filter + Score of NodeNUMAResource for one pair; o.zone / o.alloc are what Reserve records.
 // `requested`: NodeInfo.Requested the plugin sees (default the row's; the Reservation restore's view on a
 // node with reservations, transformer.go:49-291 restores the snapshot NodeInfo every plugin reads).
+// `reserve`: the Reserve path (Allocate on the stored hint, plugin.go:406-416) — no Filter-only checks.
 template <class ZS>
 KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
-                          const ZS &zs, const int64_t *requested = nullptr) {
+                          const ZS &zs, const int64_t *requested = nullptr, bool reserve = false) {
     if (!requested) requested = row.requested;
     o.feasible = true;
     o.score = 0;
@@ -582,7 +631,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
     const double ratio = opts ? row.cpu_amplification_ratio : 0.0;
     const int64_t pcpu = p.numa_req[KG_RES_CPU];
     const bool amplified = pcpu != 0 && ratio > 1.0;
-    if (amplified) {
+    if (amplified && !reserve) {
         if (row.flags & KG_NODE_NUMA_TOPO_INVALID) {   // GetAvailableCPUs: invalid CPU topology
             o.feasible = false;
             return;
@@ -755,8 +804,8 @@ static __host__ __device__ __noinline__
 inline
 #endif
 void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
-                  const int64_t *requested = nullptr) {
-    kg_numa_pair_z(c, row, p, o, kg_zone_calc{row}, requested);
+                  const int64_t *requested = nullptr, bool reserve = false) {
+    kg_numa_pair_z(c, row, p, o, kg_zone_calc{row}, requested, reserve);
 }
 
 // Reserve of NodeNUMAResource (plugin.go:375-419): record the zone allocations of the chosen node
@@ -765,7 +814,7 @@ KG_HD void kg_numa_commit(const kg_consts &c, kg_node_row &row, const kg_pod_dev
         !(row.flags & KG_NODE_NUMA_TOPO_VALID))
         return;
     kg_numa_out o;
-    kg_numa_pair(c, row, p, o);
+    kg_numa_pair(c, row, p, o, nullptr, true);
     if (!o.feasible) return;
     for (int j = 0; j < o.n_alloc; j++) {
         const int zi = o.zone[j];

@@ -35,7 +35,7 @@
 #include "kg_host.h"
 
 #define KG_POD_CHUNK 64          // pods between two LDS partial combines in k_eval
-#define KG_RESOLVE_THREADS 1024
+#define KG_RESOLVE_THREADS 512
 #define KG_MAX_CHUNK KG_PLACE_CHUNK_MAX   // max pods per resolve call (touched-list capacity)
 #define KG_MAX_TILES 4096        // max tiles per snapshot in k_resolve (2M nodes)
 
@@ -98,6 +98,22 @@ struct BatchMasks {
     uint32_t fit;   // Fit score resources
 };
 
+// node-only filter bits and LoadAware validity from dflags (and the NodeMetric expiry at `now`)
+__device__ __forceinline__ void node_regs_status(const kg_consts &c, uint32_t df, bool expired, NodeRegs &n) {
+    bool base = (df & KGD_VALID) != 0;
+    if (c.plugins & KG_PLUGIN_FIT) base = base && !(df & KGD_PODS_FULL);
+    uint32_t ok = base ? 4u : 0u;
+    if (c.plugins & KG_PLUGIN_LOADAWARE) {
+        ok |= (base && kg_la_pass(c, df, expired, 0)) ? 1u : 0u;
+        ok |= (base && kg_la_pass(c, df, expired, 1)) ? 2u : 0u;
+        n.la_valid = kg_la_valid(c, df, expired);
+    } else {
+        ok |= base ? 3u : 0u;
+        n.la_valid = false;
+    }
+    n.ok_bits = ok;
+}
+
 __device__ __forceinline__ void load_node(const kg_consts &c, const kg_planes &pl, int64_t i, bool in_range,
                                           const BatchMasks &bm, int64_t now_ns, NodeRegs &n) {
     const int64_t cap = pl.cap;
@@ -134,18 +150,7 @@ __device__ __forceinline__ void load_node(const kg_consts &c, const kg_planes &p
             }
         }
     }
-    bool base = (df & KGD_VALID) != 0;
-    if (c.plugins & KG_PLUGIN_FIT) base = base && !(df & KGD_PODS_FULL);
-    uint32_t ok = base ? 4u : 0u;
-    if (c.plugins & KG_PLUGIN_LOADAWARE) {
-        ok |= (base && kg_la_pass(c, df, expired, 0)) ? 1u : 0u;
-        ok |= (base && kg_la_pass(c, df, expired, 1)) ? 2u : 0u;
-        n.la_valid = kg_la_valid(c, df, expired);
-    } else {
-        ok |= base ? 3u : 0u;
-        n.la_valid = false;
-    }
-    n.ok_bits = ok;
+    node_regs_status(c, df, expired, n);
 }
 
 __device__ __forceinline__ int lr_q(double neg_pr, double R, double F) {
@@ -395,7 +400,7 @@ __device__ __forceinline__ bool eval_hot(const kg_consts &c, const HotArgs &a, c
 
 // Pods [p0, p1) against the lane's two nodes (n0 = wave base + lane, n1 = n0 + 64).
 // seg0 / seg1: the wave's two 64-node segments lie inside the output rows (wave-uniform).
-template <int S, bool FAST, bool LA_PROD, bool FULL, bool OUT>
+template <int S, bool FAST, bool LA_PROD, bool FULL, bool OUT, bool TOPK>
 __device__ __forceinline__ void hot_loop2(const kg_consts &c, const HotArgs &a, const kg_pod_hot_t<S> *__restrict__ pods,
                                           uint64_t *__restrict__ mrow, uint16_t *__restrict__ srow,
                                           const HotNode<S, LA_PROD> &n0, const HotNode<S, LA_PROD> &n1,
@@ -425,18 +430,49 @@ __device__ __forceinline__ void hot_loop2(const kg_consts &c, const HotArgs &a, 
         }
         const uint32_t k0 = ok0 ? (tot0 << KG_TILE_SHIFT) + kb0 : 0u;
         const uint32_t k1 = ok1 ? (tot1 << KG_TILE_SHIFT) + kb1 : 0u;
-        kbuf[(p - p0) * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
+        if (TOPK) {   // every key of the tile: [pod][1024], node-local order irrelevant
+            kbuf[(p - p0) * 2 * KG_BLOCK + tid] = k0;
+            kbuf[(p - p0) * 2 * KG_BLOCK + KG_BLOCK + tid] = k1;
+        } else {
+            kbuf[(p - p0) * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
+        }
     }
+}
+
+#define KG_TOPK KG_PARTIAL_SLOTS   // best keys per (pod, tile) in placement chunks
+
+// Placement chunks: the KG_TOPK best keys of one pod's 1024 tile keys, by one wave, in descending order
+// into lanes 0..KG_TOPK−1 of the result (0 where the tile has fewer feasible nodes).  Keys are unique
+// (they carry the local node), so each round removes exactly one.
+__device__ __forceinline__ uint32_t tile_topk(const uint32_t *keys) {
+    const int lane = threadIdx.x & 63;
+    uint32_t v[KG_TILE / 64];
+#pragma unroll
+    for (int i = 0; i < KG_TILE / 64; i++) v[i] = keys[lane + 64 * i];
+    uint32_t out = 0;
+    for (int r = 0; r < KG_TOPK; r++) {
+        uint32_t m = v[0];
+#pragma unroll
+        for (int i = 1; i < KG_TILE / 64; i++) m = m > v[i] ? m : v[i];
+        m = wave_max_u32(m);
+        if (m == 0) break;   // wave-uniform
+        out = lane == r ? m : out;
+#pragma unroll
+        for (int i = 0; i < KG_TILE / 64; i++) v[i] = v[i] == m ? 0u : v[i];
+    }
+    return out;
 }
 
 #define KG_KCHUNK 16   // pods per LDS key buffer
 
-template <int S, bool FAST, bool LA_PROD, bool OUT>
+// TOPK (placement chunks, no planes): the partials hold KG_TOPK best keys per (pod, tile) instead of one
+template <int S, bool FAST, bool LA_PROD, bool OUT, bool TOPK>
 __global__ __launch_bounds__(KG_BLOCK) void k_eval2(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_pod_hot_t<S> *__restrict__ pods,
                                                     uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
                                                     uint32_t *__restrict__ partials) {
-    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_KCHUNK * KG_BLOCK];
+    static_assert(!(TOPK && OUT), "top-k partials are a placement-chunk mode");
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_KCHUNK * KG_BLOCK * (TOPK ? 2 : 1)];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -470,12 +506,20 @@ __global__ __launch_bounds__(KG_BLOCK) void k_eval2(kg_consts c, kg_planes pl, H
     for (int p0 = pb; p0 < pe; p0 += KG_KCHUNK) {
         const int p1 = min(p0 + KG_KCHUNK, pe);
         if (full)
-            hot_loop2<S, FAST, LA_PROD, true, OUT>(c, a, pods, mrow, srow, n0, n1, kb0, kb1, mask_lanes, seg0, seg1,
-                                                   p0, p1, kbuf);
+            hot_loop2<S, FAST, LA_PROD, true, OUT, TOPK>(c, a, pods, mrow, srow, n0, n1, kb0, kb1, mask_lanes, seg0,
+                                                         seg1, p0, p1, kbuf);
         else
-            hot_loop2<S, FAST, LA_PROD, false, OUT>(c, a, pods, mrow, srow, n0, n1, kb0, kb1, mask_lanes, seg0, seg1,
-                                                    p0, p1, kbuf);
+            hot_loop2<S, FAST, LA_PROD, false, OUT, TOPK>(c, a, pods, mrow, srow, n0, n1, kb0, kb1, mask_lanes, seg0,
+                                                          seg1, p0, p1, kbuf);
         __syncthreads();
+        if (TOPK) {
+            for (int pp = wave; pp < p1 - p0; pp += KG_BLOCK / 64) {
+                const uint32_t t = tile_topk(kbuf + pp * 2 * KG_BLOCK);
+                if (lane < KG_TOPK) partials[((int64_t)(p0 + pp) * a.tiles_total + tile) * KG_PARTIAL_SLOTS + lane] = t;
+            }
+            __syncthreads();
+            continue;
+        }
         const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * KG_BLOCK + rg * 16);
         uint32_t mx = 0;
 #pragma unroll
@@ -808,15 +852,17 @@ __global__ void k_slow_list(const uint32_t *__restrict__ dflags, int64_t begin, 
     if (i < end && (dflags[i] & KGD_SLOW) && (dflags[i] & KGD_VALID)) list[atomicAdd(count, 1)] = (int32_t)i;
 }
 
+// (the list covers the whole snapshot; columns outside the evaluated range [col_begin, col_end) are skipped)
 __global__ void k_fix_slow(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t n_pods,
                            const int32_t *__restrict__ list, const int32_t *__restrict__ count, int64_t col_begin,
-                           int32_t mask_words, int64_t score_stride, int32_t tiles_total, int64_t now_ns,
-                           unsigned long long *mask, uint16_t *scores, uint32_t *partials) {
+                           int64_t col_end, int32_t mask_words, int64_t score_stride, int32_t tiles_total,
+                           int64_t now_ns, unsigned long long *mask, uint16_t *scores, uint32_t *partials) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_pods) return;
     const int32_t n = *count;
     for (int32_t k = 0; k < n; k++) {
         const int64_t node = list[k];
+        if (node < col_begin || node >= col_end) continue;
         bool feas;
         uint32_t fit, la;
         kg_pair_exact(c, pl.rows[node], pl.dflags[node], pods[p], now_ns, feas, fit, la);
@@ -1151,9 +1197,8 @@ __global__ void k_quota_apply(const uint8_t *__restrict__ gate, int32_t P, unsig
 // Reserve of the Reservation (nominated slot) and ElasticQuota (used) parts on `node`.
 // Reservation.Reserve takes the nomination of PreScore, or runs NominateReservation itself when
 // scheduleOne skipped scoring (plugin.go:525-560): on a feasible node both are kg_rsv_nominate
-// over the same restored state.
-__device__ __forceinline__ void rsv_quota_commit(const kg_planes &pl, const RsvArgs &ra, const kg_pod_dev &p,
-                                                 int32_t node) {
+// over the same restored state (the pre-Reserve row: call before the AssumePod delta).
+__device__ __forceinline__ void rsv_commit(const kg_planes &pl, const RsvArgs &ra, const kg_pod_dev &p, int32_t node) {
     if (ra.rsv && pl.rsv_of) {
         const int32_t k = pl.rsv_of[node];
         if (k >= 0) {
@@ -1164,61 +1209,168 @@ __device__ __forceinline__ void rsv_quota_commit(const kg_planes &pl, const RsvA
             if (nom >= 0) kg_rsv_commit(ra.rsv[ra.rfirst[k] + nom], p);
         }
     }
+}
+__device__ __forceinline__ void rsv_quota_commit(const kg_planes &pl, const RsvArgs &ra, const kg_pod_dev &p,
+                                                 int32_t node) {
+    rsv_commit(pl, ra, p, node);
     if (ra.quota && p.quota >= 0) kg_quota_commit(ra.quota[p.quota], p);
 }
 
 // Sequential commit of pods [pod_begin, pod_begin + n) given their per-tile partial keys.
+// The resolve keeps the derived planes of the first KG_NCACHE nodes a chunk commits in LDS, written by
+// the commit threads themselves, so later pods of the chunk re-score those nodes without a global round
+// trip (the canonical row and the global planes are written as well).
+#define KG_NCACHE 16
+struct NodeCacheEntry {
+    NodeRegs n;          // ok_bits / la_valid are derived at use (they depend on `now`)
+    int64_t metric_ns;
+};
+
+__device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c, const kg_planes &pl, const kg_pod_dev &p,
+                                                              const NodeCacheEntry &ce, int64_t node, int64_t now_ns) {
+    NodeRegs n = ce.n;
+    const bool expired = (c.plugins & KG_PLUGIN_LOADAWARE) ? kg_metric_expired(c, n.df, ce.metric_ns, now_ns) : false;
+    node_regs_status(c, n.df, expired, n);
+    uint32_t fit, la, numa = 0;
+    if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
+    if (c.plugins & KG_PLUGIN_NUMA) {
+        kg_numa_out o;
+        kg_numa_pair(c, pl.rows[node], p, o);
+        if (!o.feasible) return 0ull;
+        numa = o.score;
+    }
+    return ((unsigned long long)(total_of(c, fit, la, numa) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
+}
+
+// Sequential commit of pods [pod_begin, pod_begin + n) given their per-tile partial keys (kslots per
+// (pod, tile): 1 = the tile's best key, KG_PARTIAL_SLOTS = the top-KG_TOPK list + slow slot).
+// One workgroup; per pod: (A) every tile's best untouched candidate and the re-scored touched nodes →
+// block max; (B) Reserve, one thread per part, and the committed node's planes.  The next pod's row
+// and tile keys are prefetched while the current pod is resolved.
 __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_planes pl,
                                                                 const kg_pod_dev *__restrict__ pods, int32_t pod_begin,
                                                                 int32_t n, const uint32_t *partials, int32_t tiles_total,
                                                                 int64_t n_nodes, int64_t now_ns, int32_t *out_node,
-                                                                int64_t *out_score, RsvArgs ra) {
+                                                                int64_t *out_score, RsvArgs ra, int32_t kslots,
+                                                                int32_t *slow_list, int32_t *slow_count) {
+    constexpr int POD_DW = (int)(sizeof(kg_pod_dev) / 4);
+    static_assert(sizeof(kg_pod_dev) % 4 == 0 && POD_DW <= KG_RESOLVE_THREADS, "pod rows are staged one dword per thread");
     __shared__ int32_t touched[KG_MAX_CHUNK];
     __shared__ int32_t rescan[KG_MAX_TILES];
     __shared__ unsigned long long red[KG_RESOLVE_THREADS / 64];
     __shared__ int64_t redo[KG_RESOLVE_THREADS / 64];
-    __shared__ int32_t n_touched, n_rescan, gate_ok;
-    __shared__ unsigned long long wbest;
+    // the quota gate and the rescan counter alternate between two slots by pod parity: a pod that
+    // commits nothing ends without a barrier, so the next pod must not overwrite what a slower wave of
+    // this pod may still read
+    __shared__ int32_t n_touched, n_rescan[2], gate_ok[2];
     __shared__ uint32_t fin[KG_NUM_RES + 2];
+    __shared__ int32_t fl_pods_full;
+    __shared__ uint32_t fl_over[3];
+    __shared__ uint32_t fl_old_df;
+    __shared__ __attribute__((aligned(16))) kg_pod_dev lpod[2];
+    __shared__ NodeCacheEntry ncache[KG_NCACHE];
+    __shared__ int32_t n_slow;
     const int tid = threadIdx.x;
-    if (tid == 0) n_touched = 0;
-    for (int j = 0; j < n; j++) {
-        if (tid == 0) {
-            n_rescan = 0;
-            const kg_pod_dev &pq = pods[pod_begin + j];
-            // ElasticQuota PreFilter on the quota state after every earlier Reserve
-            gate_ok = !ra.quota || pq.quota < 0 || kg_quota_pass(ra.quota[pq.quota], pq);
-        }
-        __syncthreads();
-        if (!gate_ok) {
-            if (tid == 0) {
-                out_node[j] = -1;
-                out_score[j] = -1;
+    // tile keys of the next pod, prefetched into registers by the thread owning the tile
+    const bool key_prefetch = tiles_total <= KG_RESOLVE_THREADS;
+    const int ks = kslots == 1 ? 1 : KG_PARTIAL_SLOTS;
+    uint32_t kcur[KG_PARTIAL_SLOTS], knxt[KG_PARTIAL_SLOTS];
+    auto load_keys = [&](int jj, uint32_t (&dst)[KG_PARTIAL_SLOTS]) {
+        if (!key_prefetch || tid >= tiles_total || jj >= n) return;
+        if (ks == 1) {
+            dst[0] = partials[(int64_t)jj * tiles_total + tid];
+        } else {
+            const uint4 *src = reinterpret_cast<const uint4 *>(partials + ((int64_t)jj * tiles_total + tid) * KG_PARTIAL_SLOTS);
+#pragma unroll
+            for (int q = 0; q < KG_PARTIAL_SLOTS / 4; q++) {
+                const uint4 v = src[q];
+                dst[4 * q] = v.x;
+                dst[4 * q + 1] = v.y;
+                dst[4 * q + 2] = v.z;
+                dst[4 * q + 3] = v.w;
             }
-            __syncthreads();
-            continue;
         }
-        const kg_pod_dev &pd = pods[pod_begin + j];
+    };
+    if (tid == 0) {
+        n_touched = 0;
+        n_rescan[0] = n_rescan[1] = 0;
+        n_slow = *slow_count;
+    }
+    if (tid < POD_DW && n > 0) reinterpret_cast<uint32_t *>(&lpod[0])[tid] = reinterpret_cast<const uint32_t *>(pods + pod_begin)[tid];
+    load_keys(0, kcur);
+    __syncthreads();
+    for (int j = 0; j < n; j++) {
+        const int par = j & 1;
+        const kg_pod_dev &pd = lpod[par];
+        if (tid == 0)  // ElasticQuota PreFilter on the quota state after every earlier Reserve (read after the sync below)
+            gate_ok[par] = !ra.quota || pd.quota < 0 || kg_quota_pass(ra.quota[pd.quota], pd);
+        // prefetch pod j + 1 (its slot's last reader, pod j − 1, is past this pod's first barrier... see the
+        // note above: a barrier-free pod j − 1 reads its row only before its own second barrier)
+        if (j + 1 < n && tid >= KG_RESOLVE_THREADS - POD_DW)
+            reinterpret_cast<uint32_t *>(&lpod[par ^ 1])[tid - (KG_RESOLVE_THREADS - POD_DW)] =
+                reinterpret_cast<const uint32_t *>(pods + pod_begin + j + 1)[tid - (KG_RESOLVE_THREADS - POD_DW)];
+        load_keys(j + 1, knxt);
         unsigned long long best = 0;
         const int nt = n_touched;
         // a pod that requires a reservation can only land on reservation nodes (rsv part below)
         const bool plain_ok = !(pd.flags & KGP_RSV_REQUIRED);
         for (int t = tid; t < tiles_total; t += KG_RESOLVE_THREADS) {
-            const unsigned long long k = decode_partial(partials[(int64_t)j * tiles_total + t], t);
-            if (!k) continue;
-            const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
-            bool hit = false;
-            for (int q = 0; q < nt; q++) hit |= touched[q] == node;
-            if (hit) rescan[atomicAdd(&n_rescan, 1)] = t;
-            else best = best > k ? best : k;
+            if (!key_prefetch) {   // more tiles than threads: this thread's tiles straight from memory
+                if (ks == 1) {
+                    kcur[0] = partials[(int64_t)j * tiles_total + t];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < KG_PARTIAL_SLOTS; q++)
+                        kcur[q] = partials[((int64_t)j * tiles_total + t) * KG_PARTIAL_SLOTS + q];
+                }
+            }
+            if (ks == 1) {   // one key per tile: a touched best node forces a rescan of its tile
+                const unsigned long long k = decode_partial(kcur[0], t);
+                if (!k) continue;
+                const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
+                bool hit = false;
+                for (int q = 0; q < nt; q++) hit |= touched[q] == node;
+                if (hit) rescan[atomicAdd(&n_rescan[par], 1)] = t;
+                else best = best > k ? best : k;
+                continue;
+            }
+            // the tile's KG_TOPK best keys (descending, 0-padded): the first untouched key is the tile's
+            // best untouched fast node; the tile is rescanned only when every key of a full list was touched
+            // (fully unrolled: the list stays in registers)
+            unsigned long long cand = 0;
+            bool found = false, ended = false;
+#pragma unroll
+            for (int s = 0; s < KG_TOPK; s++) {
+                const unsigned long long k = decode_partial(kcur[s], t);
+                ended = ended || k == 0;
+                if (!found && !ended) {
+                    const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
+                    bool hit = false;
+                    for (int q = 0; q < nt; q++) hit |= touched[q] == node;
+                    if (!hit) {
+                        cand = k;
+                        found = true;
+                    }
+                }
+            }
+            const bool need = !found && !ended;
+            if (need) rescan[atomicAdd(&n_rescan[par], 1)] = t;
+            else best = best > cand ? best : cand;
         }
         if (!plain_ok) best = 0;
         for (int q = tid; q < nt && plain_ok; q += KG_RESOLVE_THREADS) {
-            const unsigned long long k = pair_key(c, pl, pd, touched[q], n_nodes, now_ns);
+            const unsigned long long k = q < KG_NCACHE ? pair_key_cached(c, pl, pd, ncache[q], touched[q], now_ns)
+                                                       : pair_key(c, pl, pd, touched[q], n_nodes, now_ns);
+            best = best > k ? best : k;
+        }
+        // nodes outside the fp64 bounds are not in the lists: re-scored exactly, every pod
+        const int ns = (ks == 1 || !plain_ok) ? 0 : n_slow;
+        for (int q = tid; q < ns; q += KG_RESOLVE_THREADS) {
+            const unsigned long long k = pair_key(c, pl, pd, slow_list[q], n_nodes, now_ns);
             best = best > k ? best : k;
         }
         __syncthreads();
-        const int nr = plain_ok ? n_rescan : 0;
+        const int nr = plain_ok ? n_rescan[par] : 0;
         for (int q = tid; q < nr * KG_TILE; q += KG_RESOLVE_THREADS) {
             const int64_t node = (int64_t)rescan[q / KG_TILE] * KG_TILE + (q % KG_TILE);
             const unsigned long long k = pair_key(c, pl, pd, node, n_nodes, now_ns);
@@ -1227,13 +1379,14 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         best = wave_max_u64(best);
         if ((tid & 63) == 0) red[tid >> 6] = best;
         __syncthreads();
-        if (tid == 0) {
-            unsigned long long w = 0;
-            for (int q = 0; q < KG_RESOLVE_THREADS / 64; q++) w = w > red[q] ? w : red[q];
-            wbest = w;
-        }
-        __syncthreads();
+        // every thread takes the block maximum itself (no broadcast barrier)
+        unsigned long long wb = 0;
+        for (int q = 0; q < KG_RESOLVE_THREADS / 64; q++) wb = wb > red[q] ? wb : red[q];
+        if (tid == 0) n_rescan[par] = 0;   // pod j + 2's counter: every reader of it is past the sync above
+#pragma unroll
+        for (int q = 0; q < KG_PARTIAL_SLOTS; q++) kcur[q] = knxt[q];
         if (ra.rsv && ra.n_rn > 0) {
+            __syncthreads();
             // nodes with reservations: refresh this pod's entries of the nodes earlier pods touched,
             // then PreScore / Score / NormalizeScore over every reservation node
             unsigned long long *E = ra.E + (int64_t)j * ra.n_rn;
@@ -1245,47 +1398,95 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             __syncthreads();
             const unsigned long long rk =
                 rsv_best_block<KG_RESOLVE_THREADS>(c, E, O, ra.rnode, ra.n_rn, nullptr, 0, 0, red, redo);
-            if (tid == 0 && rk > wbest) wbest = rk;
+            wb = wb > rk ? wb : rk;
         }
-        __syncthreads();
-        const unsigned long long w = wbest;
+        const unsigned long long w = gate_ok[par] ? wb : 0ull;   // a pod failing the quota gate is unschedulable
         const int32_t node = w ? (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull)) : -1;
-        if (tid == 0) {
-            if (w) {
-                rsv_quota_commit(pl, ra, pd, node);
-                kg_numa_commit(c, pl.rows[node], pd);
-                kg_apply_commit(pl.rows[node], pd);
-                bool seen = false;
-                for (int q = 0; q < n_touched; q++) seen |= touched[q] == node;
-                if (!seen) touched[n_touched++] = node;
-                out_node[j] = node;
-                out_score[j] = (int64_t)(w >> 32) - 1;
-            } else {
+        if (!w) {
+            if (tid == 0) {
                 out_node[j] = -1;
                 out_score[j] = -1;
             }
+            continue;   // nothing changed: the next pod's first barrier orders the outputs
+        }
+        // Reserve.  The Reservation nomination (restore) and NodeNUMAResource's zone commit (its
+        // amplified-cpu filter) read the pre-Reserve node, so they go first when enabled.
+        if ((ra.rsv && ra.n_rn > 0) || (c.plugins & KG_PLUGIN_NUMA)) {
+            if (tid == 0) {
+                rsv_commit(pl, ra, pd, node);
+                kg_numa_commit(c, pl.rows[node], pd);
+            }
+            __syncthreads();
+        }
+        // the node's slot in the touched list (and node cache): its position, or the next one
+        int slot = nt;
+        for (int q = 0; q < nt; q++)
+            if (touched[q] == node) slot = q;
+        NodeCacheEntry *ce = slot < KG_NCACHE ? &ncache[slot] : nullptr;
+        // AssumePod / LoadAware deltas and the committed node's derived planes, one thread per part:
+        // thread 64 + r owns resource r's fields of the row and its Fit planes, 64 + 8 + r the LoadAware
+        // terms of r; thread 0 the reservation / quota Reserve, the pod count and the outputs
+        kg_node_row &row = pl.rows[node];
+        if (tid >= 64 && tid < 64 + KG_NUM_RES) {
+            const int r = tid - 64;
+            const int64_t req = row.requested[r] + pd.req[r];
+            row.requested[r] = req;
+            if (r < 2) row.nonzero_requested[r] += pd.nonzero[r];
+            if (r < 3) fl_over[r] = row.alloc[r] - req < 0 ? 1u : 0u;
+            int64_t fr;
+            double R, F;
+            fin[r] = kg_finalize_fit(c, pl, node, r, &fr, &R, &F);
+            if (ce) {
+                ce->n.free_[r] = fr;
+                ce->n.fit_R[r] = R;
+                ce->n.fit_F[r] = F;
+            }
+        } else if (tid >= 64 + KG_NUM_RES && tid < 64 + KG_NUM_RES + 2) {
+            const int r = tid - 64 - KG_NUM_RES;
+            row.la_used[0][r] += pd.la_est_i[r];
+            if (pd.flags & KG_POD_PROD) row.la_used[1][r] += pd.la_est_i[r];
+            double R, F0, F1;
+            fin[KG_NUM_RES + r] = kg_finalize_la(c, pl, node, r, &R, &F0, &F1) ? 1u : 0u;
+            if (ce) {
+                ce->n.la_R[r] = R;
+                ce->n.la_F0[r] = F0;
+                ce->n.la_F1[r] = F1;
+            }
+        } else if (tid == 0) {
+            if (ra.quota && pd.quota >= 0) kg_quota_commit(ra.quota[pd.quota], pd);
+            const int32_t pc = row.pod_count + 1;
+            row.pod_count = pc;
+            fl_pods_full = (int64_t)pc + 1 > (int64_t)row.allowed_pods ? 1 : 0;
+            fl_old_df = pl.dflags[node];
+            if (ce) ce->metric_ns = pl.metric_ns[node];
+            if (slot == nt) touched[n_touched++] = node;
+            out_node[j] = node;
+            out_score[j] = (int64_t)(w >> 32) - 1;
         }
         __syncthreads();
-        if (w) {
-            // re-derive the committed node's planes, one thread per resource (the int64 divisions of
-            // kg_scaled_ratio dominate a serial kg_finalize_node); the flags take their results
-            if (tid < KG_NUM_RES) {
-                const uint32_t f = kg_finalize_fit(c, pl, node, tid);
-                fin[tid] = f;
-            } else if (tid < KG_NUM_RES + 2) {
-                fin[tid] = kg_finalize_la(c, pl, node, tid - KG_NUM_RES) ? 1u : 0u;
+        if (tid == 0) {   // kg_finalize_flags from the parts (metric and the static bits are unchanged)
+            bool slow = false;
+            uint32_t fmask = 0;
+            for (int r = 0; r < KG_NUM_RES + 2; r++) slow = slow || (fin[r] & 1u);
+            for (int r = 0; r < KG_NUM_RES; r++)
+                if (fin[r] & 2u) fmask |= 1u << r;
+            const bool over[3] = {fl_over[0] != 0, fl_over[1] != 0, fl_over[2] != 0};
+            const uint32_t old = fl_old_df;
+            uint32_t dyn = kg_dflags_dynamic(fl_pods_full != 0, over, slow);
+            if (old & KGD_RSV) dyn &= ~KGD_SLOW;   // kg_rsv_pair owns reservation nodes
+            const uint32_t df = (old & ~KGD_DYNAMIC) | dyn;
+            pl.dflags[node] = df;
+            pl.fit_mask[node] = fmask;
+            if ((df & KGD_SLOW) && !(old & KGD_SLOW)) {   // the node left the fast paths: list it
+                slow_list[n_slow++] = node;
+                *slow_count = n_slow;
             }
-            __syncthreads();
-            if (tid == 0) {
-                bool slow = false;
-                uint32_t fmask = 0;
-                for (int r = 0; r < KG_NUM_RES + 2; r++) slow = slow || (fin[r] & 1u);
-                for (int r = 0; r < KG_NUM_RES; r++)
-                    if (fin[r] & 2u) fmask |= 1u << r;
-                kg_finalize_flags(pl, node, slow, fmask);
+            if (ce) {
+                ce->n.df = df;
+                ce->n.fit_mask = fmask;
             }
-            __syncthreads();
         }
+        __syncthreads();
     }
 }
 
@@ -1333,8 +1534,10 @@ struct kg_engine {
     size_t cls_mem_bytes = 0;
     int32_t cls_nwork = 0;
     size_t cls_work_off = 0, cls_rows_off = 0;
-    int32_t *slow_list = nullptr;   // [cap] nodes outside the fast-path bounds (rebuilt per eval)
+    int32_t *slow_list = nullptr;   // [cap] nodes outside the fast-path bounds, whole snapshot
     int32_t *slow_count = nullptr;
+    bool slow_valid = false;        // the list matches the planes (rebuilt lazily after host-side changes;
+                                    // the placement resolve appends the nodes its commits make slow)
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
     bool profiling = false;
@@ -1398,28 +1601,31 @@ int pods_per_block_for(int64_t n_pods, int64_t tiles) {
 
 template <int S, bool FAST, bool LA_PROD>
 void launch_hot_div(kg_engine *e, dim3 grid, const HotArgs &a, int32_t pod_begin, uint64_t *mask, uint16_t *scores,
-                    uint32_t *partials) {
+                    uint32_t *partials, bool topk) {
     const kg_pod_hot_t<S> *pods = reinterpret_cast<const kg_pod_hot_t<S> *>(e->hot) + pod_begin;
     if (mask)
-        hipLaunchKernelGGL((k_eval2<S, FAST, LA_PROD, true>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts, e->pl, a,
-                           pods, mask, scores, partials);
+        hipLaunchKernelGGL((k_eval2<S, FAST, LA_PROD, true, false>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts,
+                           e->pl, a, pods, mask, scores, partials);
+    else if (topk)
+        hipLaunchKernelGGL((k_eval2<S, FAST, LA_PROD, false, true>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts,
+                           e->pl, a, pods, mask, scores, partials);
     else
-        hipLaunchKernelGGL((k_eval2<S, FAST, LA_PROD, false>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts, e->pl, a,
-                           pods, mask, scores, partials);
+        hipLaunchKernelGGL((k_eval2<S, FAST, LA_PROD, false, false>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts,
+                           e->pl, a, pods, mask, scores, partials);
 }
 
 template <int S>
 void launch_hot(kg_engine *e, dim3 grid, const HotArgs &a, int32_t pod_begin, uint64_t *mask, uint16_t *scores,
-                uint32_t *partials) {
+                uint32_t *partials, bool topk) {
     const kg_consts &c = e->consts;
     const bool fast = e->pow2 && !c.fit_most && c.weight_fit == 1 && c.weight_la == 1 &&
                       (c.plugins & (KG_PLUGIN_FIT | KG_PLUGIN_LOADAWARE)) == (KG_PLUGIN_FIT | KG_PLUGIN_LOADAWARE);
     if (e->la_prod) {
-        if (fast) launch_hot_div<S, true, true>(e, grid, a, pod_begin, mask, scores, partials);
-        else launch_hot_div<S, false, true>(e, grid, a, pod_begin, mask, scores, partials);
+        if (fast) launch_hot_div<S, true, true>(e, grid, a, pod_begin, mask, scores, partials, topk);
+        else launch_hot_div<S, false, true>(e, grid, a, pod_begin, mask, scores, partials, topk);
     } else {
-        if (fast) launch_hot_div<S, true, false>(e, grid, a, pod_begin, mask, scores, partials);
-        else launch_hot_div<S, false, false>(e, grid, a, pod_begin, mask, scores, partials);
+        if (fast) launch_hot_div<S, true, false>(e, grid, a, pod_begin, mask, scores, partials, topk);
+        else launch_hot_div<S, false, false>(e, grid, a, pod_begin, mask, scores, partials, topk);
     }
 }
 
@@ -1627,8 +1833,22 @@ void launch_cls(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint1
 }
 
 // mask and scores are both produced or both omitted (the host path provides scratch for a missing one)
+// the slow-node list of the whole snapshot, rebuilt when host-side changes invalidated it
+kg_status slow_refresh(kg_engine *e) {
+    if (e->slow_valid) return KG_OK;
+    HIP_TRY(e, hipMemsetAsync(e->slow_count, 0, sizeof(int32_t), e->stream));
+    if (e->n_nodes > 0)
+        hipLaunchKernelGGL(k_slow_list, dim3((unsigned)((e->n_nodes + 255) / 256)), dim3(256), 0, e->stream, e->pl.dflags,
+                           (int64_t)0, e->n_nodes, e->slow_list, e->slow_count);
+    HIP_TRY(e, hipGetLastError());
+    e->slow_valid = true;
+    return KG_OK;
+}
+
+// topk: placement chunk (partials of KG_PARTIAL_SLOTS per (pod, tile) on the non-NUMA path; the NUMA
+// kernel writes one key per (pod, tile), slot 0 of a dense [n][tiles] layout — see partial_slots)
 kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
-                      uint32_t *partials, bool use_cls = false, uint8_t *numa_scores = nullptr) {
+                      uint32_t *partials, bool use_cls = false, uint8_t *numa_scores = nullptr, bool topk = false) {
     if (n <= 0) return KG_OK;
     if ((mask == nullptr) != (scores == nullptr)) return set_err(e, KG_ERR_INVALID_ARG, "mask and scores go together");
     const int64_t shard_tiles = (e->shard_end - e->shard_begin + KG_TILE - 1) / KG_TILE;
@@ -1668,23 +1888,25 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     dim3 grid((unsigned)shard_tiles, use_cls ? (unsigned)e->cls_nwork : (unsigned)((n + a.pods_per_block - 1) / a.pods_per_block));
     if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
     if (use_cls) launch_cls(e, grid, a, mask, scores, partials);
-    else if (e->nslot == 2) launch_hot<2>(e, grid, a, pod_begin, mask, scores, partials);
-    else if (e->nslot == 4) launch_hot<4>(e, grid, a, pod_begin, mask, scores, partials);
-    else launch_hot<8>(e, grid, a, pod_begin, mask, scores, partials);
+    else if (e->nslot == 2) launch_hot<2>(e, grid, a, pod_begin, mask, scores, partials, topk);
+    else if (e->nslot == 4) launch_hot<4>(e, grid, a, pod_begin, mask, scores, partials, topk);
+    else launch_hot<8>(e, grid, a, pod_begin, mask, scores, partials, topk);
     HIP_TRY(e, hipGetLastError());
     if (e->profiling) {
         HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
         e->ev_count++;
     }
-    // exact re-evaluation of the (rare) nodes outside the fp64 fast-path bounds
-    const int64_t width = e->shard_end - e->shard_begin;
-    HIP_TRY(e, hipMemsetAsync(e->slow_count, 0, sizeof(int32_t), e->stream));
-    hipLaunchKernelGGL(k_slow_list, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, e->stream, e->pl.dflags,
-                       e->shard_begin, e->shard_end, e->slow_list, e->slow_count);
-    hipLaunchKernelGGL(k_fix_slow, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->consts, e->pl,
-                       e->pods + pod_begin, n, e->slow_list, e->slow_count, e->shard_begin, a.mask_words, a.score_stride,
-                       a.tiles_total, now_ns, (unsigned long long *)mask, scores, partials);
-    HIP_TRY(e, hipGetLastError());
+    // exact re-evaluation of the (rare) nodes outside the fp64 fast-path bounds; a placement chunk
+    // leaves them to the resolve, which re-scores the slow-node list itself
+    kg_status st = slow_refresh(e);
+    if (st) return st;
+    if (!topk) {
+        hipLaunchKernelGGL(k_fix_slow, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->consts, e->pl,
+                           e->pods + pod_begin, n, e->slow_list, e->slow_count, e->shard_begin, e->shard_end,
+                           a.mask_words, a.score_stride, a.tiles_total, now_ns, (unsigned long long *)mask, scores,
+                           partials);
+        HIP_TRY(e, hipGetLastError());
+    }
     return KG_OK;
 }
 
@@ -1860,6 +2082,7 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
                        (int64_t)0, cap);
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->slow_valid = false;
     return KG_OK;
 }
 
@@ -1881,6 +2104,7 @@ kg_status kg_snapshot_upsert(kg_engine *e, const int32_t *node_index, const kg_n
                        (const kg_node_row *)s, (const int32_t *)(s + (rb + 255) / 256 * 256), n);
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipStreamSynchronize(e->stream));  // staging buffer reuse
+    e->slow_valid = false;
     return KG_OK;
 }
 
@@ -2123,8 +2347,12 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
     if (st) return st;
     if (pod_begin < 0 || n < 0 || pod_begin + (int64_t)n > e->n_pods || (n > 0 && !partial_dev))
         return set_err(e, KG_ERR_RANGE, "bad chunk");
-    HIP_TRY(e, hipMemsetAsync(partial_dev, 0, (size_t)n * (size_t)tiles_total(e) * 4, e->stream));
-    st = launch_eval(e, now_ns, pod_begin, n, nullptr, nullptr, partial_dev);
+    // the top-k kernel writes every slot of every tile of its shard; the NUMA kernel merges with atomics
+    // and a shard leaves the other ranks' tiles to the merge: those start from zeros
+    const bool whole = e->shard_begin == 0 && e->shard_end == e->n_nodes;
+    if ((e->consts.plugins & KG_PLUGIN_NUMA) || !whole)
+        HIP_TRY(e, hipMemsetAsync(partial_dev, 0, (size_t)n * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS, e->stream));
+    st = launch_eval(e, now_ns, pod_begin, n, nullptr, nullptr, partial_dev, false, nullptr, true);
     if (st) return st;
     // reservation nodes: entries of every reservation node (the snapshot is replicated across
     // ranks in the multi-GPU placement, so each rank holds all of them), rows 0..n of E / O
@@ -2148,8 +2376,11 @@ kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin
     if (ra.rsv) {  // this chunk's entries were written by kg_place_chunk_eval from row 0
         if (n > KG_RSV_POD_CHUNK) return set_err(e, KG_ERR_RANGE, "chunk larger than the reservation entry buffer");
     }
+    st = slow_refresh(e);
+    if (st) return st;
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream, e->consts, e->pl, e->pods, pod_begin, n,
-                       partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev, ra);
+                       partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev, ra,
+                       (e->consts.plugins & KG_PLUGIN_NUMA) ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count);
     HIP_TRY(e, hipGetLastError());
     return KG_OK;
 }
@@ -2165,7 +2396,7 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
     if (P == 0) return KG_OK;
     int32_t chunk = e->cfg.place_chunk > 0 ? e->cfg.place_chunk : 8;
     if (chunk > KG_MAX_CHUNK) chunk = KG_MAX_CHUNK;
-    const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4;
+    const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS;
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
     st = ensure_scratch(e, up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + 256);
     if (st) return st;
@@ -2271,6 +2502,7 @@ kg_status kg_rsv_set(kg_engine *e, const kg_reservation *rsv, int32_t n) {
                        e->pl, (int64_t)0, e->pl.cap);
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->slow_valid = false;
     return KG_OK;
 }
 
@@ -2318,6 +2550,7 @@ kg_status kg_commit(kg_engine *e, int32_t pod, int32_t node) {
     st = quota_ready(e);   // the pod's quota group must exist before its usage is committed
     if (st) return st;
     hipLaunchKernelGGL(k_commit_one, dim3(1), dim3(1), 0, e->stream, e->consts, e->pl, e->pods, pod, node, rsv_args(e));
+    e->slow_valid = false;
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     return KG_OK;

@@ -65,6 +65,7 @@ class ChunkBackend(Protocol):
 
     n_pods: int
     num_tiles: int
+    partial_slots: int     # uint32 keys per (pod, tile) in the partial buffer
 
     def chunk_eval(self, now_ns: int, pod_begin: int, n: int, partial_ptr: int) -> None: ...
 
@@ -84,7 +85,8 @@ def place_sharded(backend: ChunkBackend, now_ns: int, device: torch.device, chun
     P, tiles = backend.n_pods, backend.num_tiles
     stream = getattr(backend, "torch_stream", None)
     with torch.cuda.stream(stream) if stream is not None else _nullctx():
-        partial = torch.zeros((max(chunk, 1), tiles), dtype=torch.int32, device=device)
+        slots = getattr(backend, "partial_slots", 1)
+        partial = torch.zeros((max(chunk, 1), tiles, slots), dtype=torch.int32, device=device)
         nodes = torch.full((max(P, 1),), -1, dtype=torch.int32, device=device)
         scores = torch.full((max(P, 1),), -1, dtype=torch.int64, device=device)
         for b in range(0, P, chunk):

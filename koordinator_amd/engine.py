@@ -136,6 +136,8 @@ class Engine:
     def num_tiles(self) -> int:
         return nat.lib().kg_num_tiles(self._h)
 
+    partial_slots = nat.PARTIAL_SLOTS   # uint32 per (pod, tile) of kg_place_chunk_eval's buffer
+
     # pods -------------------------------------------------------------------------------
     def set_pods(self, rows: np.ndarray) -> None:
         rows = np.ascontiguousarray(rows, dtype=nat.POD_ROW)

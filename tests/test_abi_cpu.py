@@ -37,6 +37,15 @@ def test_library_exports_every_declared_function():
     assert sorted(decl) == sorted(nat.EXPORTED)
 
 
+def test_header_constants_match_python():
+    import re
+    text = open(HEADER).read()
+    consts = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define (KG_\w+) (\d+)\b", text)}
+    assert consts["KG_ABI_VERSION"] == nat.ABI_VERSION
+    assert consts["KG_PLACE_CHUNK_MAX"] == nat.PLACE_CHUNK_MAX
+    assert consts["KG_PARTIAL_SLOTS"] == nat.PARTIAL_SLOTS
+
+
 def test_struct_layouts_match():
     nat.check_abi()
     assert nat.lib().kg_abi_version() == nat.ABI_VERSION

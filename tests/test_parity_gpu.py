@@ -119,6 +119,36 @@ def test_placement_matches_sequential_cycle(chunk):
     np.testing.assert_array_equal(after, rows)
 
 
+@pytest.mark.parametrize("chunk", [15, 16, 17])
+def test_placement_slow_nodes_and_list_depth(chunk):
+    """Placement with nodes outside the fp64 bounds from the start (cap ≥ 2^41 B) and nodes whose score
+    base crosses 2^50 on their first commit (the resolve lists them as slow), at chunk sizes around the
+    top-k list depth (KG_PARTIAL_SLOTS = 16: a 17th pod can find every listed node of a tile touched)."""
+    cl = synth.make_cluster(2_500, 300, seed=24)
+    big = np.arange(0, 2_500, 11)
+    cl.nodes["allocatable"]["v"][big, 1] = (1 << 43) + 12345
+    cl.nodes["requested"]["v"][big, 1] = (1 << 42) + 777
+    cl.nodes["nonzero_requested"][big, 1] = (1 << 42) + 777
+    edge = np.arange(5, 2_500, 13)
+    cl.nodes["nonzero_requested"][edge, 1] = (1 << 50) - (64 << 20)
+    cl = cl.with_nodes(cl.nodes)
+    cfg = shipped_profile(place_chunk=chunk)
+    idx = np.arange(300)
+    with _engine_for(cfg, cl, idx) as eng:
+        nodes, scores = eng.place(cl.now_ns)
+        after = eng.download()
+    ref_nodes, ref_scores = oracle.schedule(cfg, cl, idx, cl.now_ns)
+    np.testing.assert_array_equal(nodes, ref_nodes)
+    np.testing.assert_array_equal(scores, ref_scores)
+    assert np.isin(nodes, big).any() and np.isin(nodes, edge).any()
+    rows = engine.build_node_rows(cfg, cl)
+    prow = engine.build_pod_rows(cfg, cl, idx)
+    for p, n in enumerate(nodes):
+        if n >= 0:
+            engine.row_commit(cfg, rows[n:n + 1], prow[p:p + 1])
+    np.testing.assert_array_equal(after, rows)
+
+
 def test_placement_tight_cluster_with_unschedulable_pods():
     """Few small nodes: pods run out of room, later pods become unschedulable (−1)."""
     cl = synth.make_cluster(10, 1200, seed=33, no_metric_frac=0.3)

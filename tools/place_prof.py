@@ -1,0 +1,28 @@
+"""One kg_place run (config 2: 10k pods × 100k nodes, or config 3 with "c3": 1k pods, NodeNUMAResource)
+for rocprofv3 kernel traces of the placement path."""
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, ".")
+from koordinator_amd import _native as nat  # noqa: E402
+from koordinator_amd import engine, synth  # noqa: E402
+from koordinator_amd.config import shipped_profile  # noqa: E402
+
+C3 = len(sys.argv) > 1 and sys.argv[1] == "c3"
+P = int(sys.argv[2]) if len(sys.argv) > 2 else (1_000 if C3 else 10_000)
+cl = synth.make_numa_cluster(100_000, P, seed=3) if C3 else synth.make_cluster(100_000, P, seed=2)
+cfg = shipped_profile()
+if C3:
+    cfg["enabled_plugins"] |= nat.PLUGIN_NUMA
+rows = engine.build_node_rows(cfg, cl)
+pods = engine.build_pod_rows(cfg, cl, np.arange(P))
+with engine.Engine(cfg) as eng:
+    eng.load_snapshot(rows)
+    eng.set_pods(pods)
+    eng.sync()
+    t0 = time.perf_counter()
+    nodes, scores = eng.place(cl.now_ns)
+    dt = time.perf_counter() - t0
+print(f"{'config3' if C3 else 'config2'} placement: {P} pods in {dt:.3f} s = {P / dt:.0f} pods/s", flush=True)

@@ -15,7 +15,7 @@ C3 = len(sys.argv) > 2 and sys.argv[2] == "c3"
 cl = synth.make_numa_cluster(100_000, P, seed=3) if C3 else synth.make_cluster(100_000, P, seed=2)
 rows = None
 ref = None
-for chunk in ((2, 4, 8, 16) if C3 else (4, 8, 16, 32, 64)):
+for chunk in ((2, 4, 8, 16) if C3 else (4, 8, 12, 16, 24, 32)):
     cfg = shipped_profile(place_chunk=chunk)
     if C3:
         cfg["enabled_plugins"] |= nat.PLUGIN_NUMA
