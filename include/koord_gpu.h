@@ -455,7 +455,7 @@ enum kg_struct_id {
     KG_SID_RESOURCE_LIST = 0, KG_SID_CONFIG, KG_SID_CONTAINER, KG_SID_POD_SPEC,
     KG_SID_AGGREGATED_USAGE, KG_SID_POD_METRIC, KG_SID_ASSIGNED_POD, KG_SID_NODE_SPEC,
     KG_SID_CLUSTER_VIEW, KG_SID_POD_ROW, KG_SID_NODE_ROW, KG_SID_EVAL_OUT, KG_SID_NUMA_SPEC,
-    KG_SID_RESERVATION, KG_SID_QUOTA, KG_SID_COUNT
+    KG_SID_RESERVATION, KG_SID_QUOTA, KG_SID_RSV_RESTORED, KG_SID_COUNT
 };
 int64_t kg_struct_size(int32_t sid);
 
@@ -491,6 +491,22 @@ kg_status kg_row_eval_rsv(const kg_config *cfg, const kg_node_row *node, const k
                           const kg_pod_row *pod, int64_t now_ns, int32_t *feasible, int32_t *fit_score,
                           int32_t *la_score, int32_t *numa_score, int32_t *rsv_raw, int64_t *order,
                           int32_t *nominated);
+
+/* The Reservation restore of one (pod, node) pair as the plugins see it (BeforePreFilter,
+ * transformer.go:49-291): NodeInfo after restoring the unmatched reservations' remainders and removing
+ * the matched reserve pods, and the nodeReservationState the Filter / nomination read. */
+typedef struct kg_rsv_restored {
+    int64_t requested[KG_NUM_RES];      /* NodeInfo.Requested after the restore */
+    int64_t pod_requested[KG_NUM_RES];  /* nodeRState.podRequested (after the unmatched part) */
+    int64_t r_allocated[KG_NUM_RES];    /* nodeRState.rAllocated (Σ Allocated of the matched) */
+    int64_t nonzero[2];                 /* NodeInfo.NonZeroRequested after the restore */
+    int32_t pod_count;                  /* len(NodeInfo.Pods) after the restore */
+    int32_t n_matched;                  /* matched reservations (their slots: rsv[] order) */
+    int32_t has_state;                  /* nodeReservationStates has the node */
+    int32_t _pad;
+} kg_rsv_restored;
+kg_status kg_row_rsv_restore(const kg_config *cfg, const kg_node_row *node, const kg_reservation *rsv, int32_t n_rsv,
+                             const kg_pod_row *pod, kg_rsv_restored *out);
 
 /* Engine lifecycle. */
 kg_status kg_engine_create(const kg_config *cfg, kg_engine **out);

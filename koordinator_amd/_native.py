@@ -120,8 +120,13 @@ QUOTA = np.dtype([
     ("non_preemptible_used", RESOURCE_LIST),
 ], align=True)
 
+RSV_RESTORED = np.dtype([
+    ("requested", "<i8", (NUM_RES,)), ("pod_requested", "<i8", (NUM_RES,)), ("r_allocated", "<i8", (NUM_RES,)),
+    ("nonzero", "<i8", (2,)), ("pod_count", "<i4"), ("n_matched", "<i4"), ("has_state", "<i4"), ("_pad", "<i4"),
+], align=True)
+
 STRUCT_IDS = [RESOURCE_LIST, CONFIG, CONTAINER, POD_SPEC, AGGREGATED_USAGE, POD_METRIC, ASSIGNED_POD, NODE_SPEC,
-              None, POD_ROW, NODE_ROW, None, NUMA_SPEC, RESERVATION, QUOTA]
+              None, POD_ROW, NODE_ROW, None, NUMA_SPEC, RESERVATION, QUOTA, RSV_RESTORED]
 
 
 class ClusterView(ctypes.Structure):
@@ -179,7 +184,7 @@ EXPORTED = [
     "kg_last_error", "kg_set_stream", "kg_sync", "kg_snapshot_reset", "kg_snapshot_upsert", "kg_snapshot_remove",
     "kg_snapshot_download", "kg_set_shard", "kg_pods_set", "kg_eval", "kg_place", "kg_num_tiles",
     "kg_place_chunk_eval", "kg_place_chunk_resolve", "kg_commit", "kg_set_profiling", "kg_eval_kernel_times",
-    "kg_rsv_set", "kg_rsv_download", "kg_quota_set", "kg_quota_download", "kg_row_eval_rsv",
+    "kg_rsv_set", "kg_rsv_download", "kg_quota_set", "kg_quota_download", "kg_row_eval_rsv", "kg_row_rsv_restore",
 ]
 
 _lib = None
@@ -219,6 +224,7 @@ def lib() -> ctypes.CDLL:
         "kg_rsv_set": (i32, [vp, vp, i32]), "kg_rsv_download": (i32, [vp, vp, i32]),
         "kg_quota_set": (i32, [vp, vp, i32]), "kg_quota_download": (i32, [vp, vp, i32]),
         "kg_row_eval_rsv": (i32, [vp, vp, vp, i32, vp, i64, vp, vp, vp, vp, vp, vp, vp]),
+        "kg_row_rsv_restore": (i32, [vp, vp, vp, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if host_only and not hasattr(L, name):

@@ -1017,6 +1017,50 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
     return ((unsigned long long)(total_of(c, fit, la, numa) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
 }
 
+// NodeNUMAResource placement chunks (≤ KG_NUMA_CHUNK_PODS pods): node per lane, so all 64 lanes work
+// on a small pod chunk (the matrix kernel's pod-per-lane layout would leave most lanes idle); each
+// thread holds 4 nodes of a 1024-node tile, the chunk's pod rows sit in LDS, and the per-pod top-k
+// keys of the tile go to the partial lists like k_eval2's.  The hint enumeration reads each lane's own
+// canonical row (kg_zone_calc).
+#define KG_NUMA_CHUNK_PODS 16
+__global__ __launch_bounds__(256) void k_eval_numa_chunk(kg_consts c, kg_planes pl, HotArgs a,
+                                                         const kg_pod_dev *__restrict__ pods,
+                                                         uint32_t *__restrict__ partials) {
+    constexpr int POD_DW = (int)(sizeof(kg_pod_dev) / 4);
+    __shared__ __attribute__((aligned(16))) kg_pod_dev lp[KG_NUMA_CHUNK_PODS];
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_NUMA_CHUNK_PODS * KG_TILE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = a.n_pods;   // ≤ KG_NUMA_CHUNK_PODS (host-checked)
+    for (int k = tid; k < n * POD_DW; k += 256)
+        reinterpret_cast<uint32_t *>(lp)[k] = reinterpret_cast<const uint32_t *>(pods)[k];
+    __syncthreads();
+    const int tile = a.tile_begin + blockIdx.x;
+    const BatchMasks bm{0xFFu, 0xFFu};
+    for (int v = 0; v < KG_TILE / 256; v++) {
+        const int local = v * 256 + tid;
+        const int64_t node = (int64_t)tile * KG_TILE + local;
+        const bool in_range = node < a.node_end;
+        NodeRegs nr;
+        load_node(c, pl, node, in_range, bm, a.now_ns, nr);
+        for (int p = 0; p < n; p++) {
+            uint32_t key = 0;
+            uint32_t fit, la;
+            if (in_range && eval_pair(c, pl, lp[p], nr, node, a.now_ns, fit, la)) {
+                kg_numa_out o;
+                kg_numa_pair(c, pl.rows[node], lp[p], o);
+                if (o.feasible)
+                    key = ((total_of(c, fit, la, o.score) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local);
+            }
+            kbuf[p * KG_TILE + local] = key;
+        }
+    }
+    __syncthreads();
+    for (int p = wave; p < n; p += 4) {
+        const uint32_t t = tile_topk(kbuf + p * KG_TILE);
+        if (lane < KG_TOPK) partials[((int64_t)p * a.tiles_total + tile) * KG_PARTIAL_SLOTS + lane] = t;
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // Reservation + ElasticQuota (BASELINE config 5)
 // ---------------------------------------------------------------------------------------
@@ -1252,7 +1296,8 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                                                                 int32_t n, const uint32_t *partials, int32_t tiles_total,
                                                                 int64_t n_nodes, int64_t now_ns, int32_t *out_node,
                                                                 int64_t *out_score, RsvArgs ra, int32_t kslots,
-                                                                int32_t *slow_list, int32_t *slow_count) {
+                                                                int32_t *slow_list, int32_t *slow_count,
+                                                                int32_t rescore_slow) {
     constexpr int POD_DW = (int)(sizeof(kg_pod_dev) / 4);
     static_assert(sizeof(kg_pod_dev) % 4 == 0 && POD_DW <= KG_RESOLVE_THREADS, "pod rows are staged one dword per thread");
     __shared__ int32_t touched[KG_MAX_CHUNK];
@@ -1364,7 +1409,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             best = best > k ? best : k;
         }
         // nodes outside the fp64 bounds are not in the lists: re-scored exactly, every pod
-        const int ns = (ks == 1 || !plain_ok) ? 0 : n_slow;
+        const int ns = (!rescore_slow || !plain_ok) ? 0 : n_slow;
         for (int q = tid; q < ns; q += KG_RESOLVE_THREADS) {
             const unsigned long long k = pair_key(c, pl, pd, slow_list[q], n_nodes, now_ns);
             best = best > k ? best : k;
@@ -1865,6 +1910,17 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     a.fit_cap = e->consts.fit_most ? 100u : 0xFFFFFFFFu;
     for (int s = 0; s < 8; s++) a.slot_res[s] = s < e->nslot ? e->slot_res[s] : -1;
     a.now_ns = now_ns;
+    if ((e->consts.plugins & KG_PLUGIN_NUMA) && topk && n <= KG_NUMA_CHUNK_PODS) {
+        if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
+        hipLaunchKernelGGL(k_eval_numa_chunk, dim3((unsigned)shard_tiles), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                           e->pods + pod_begin, partials);
+        HIP_TRY(e, hipGetLastError());
+        if (e->profiling) {
+            HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
+            e->ev_count++;
+        }
+        return KG_OK;
+    }
     if (e->consts.plugins & KG_PLUGIN_NUMA) {
         if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
         {  // pod per lane; a single pod block splits each wave's node run 4 ways
@@ -2350,7 +2406,7 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
     // the top-k kernel writes every slot of every tile of its shard; the NUMA kernel merges with atomics
     // and a shard leaves the other ranks' tiles to the merge: those start from zeros
     const bool whole = e->shard_begin == 0 && e->shard_end == e->n_nodes;
-    if ((e->consts.plugins & KG_PLUGIN_NUMA) || !whole)
+    if (((e->consts.plugins & KG_PLUGIN_NUMA) && n > KG_NUMA_CHUNK_PODS) || !whole)
         HIP_TRY(e, hipMemsetAsync(partial_dev, 0, (size_t)n * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS, e->stream));
     st = launch_eval(e, now_ns, pod_begin, n, nullptr, nullptr, partial_dev, false, nullptr, true);
     if (st) return st;
@@ -2378,9 +2434,11 @@ kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin
     }
     st = slow_refresh(e);
     if (st) return st;
+    const bool numa = (e->consts.plugins & KG_PLUGIN_NUMA) != 0;
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream, e->consts, e->pl, e->pods, pod_begin, n,
                        partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev, ra,
-                       (e->consts.plugins & KG_PLUGIN_NUMA) ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count);
+                       numa && n > KG_NUMA_CHUNK_PODS ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count,
+                       numa ? 0 : 1);   // the NUMA chunk kernels list slow nodes themselves (exact pair path)
     HIP_TRY(e, hipGetLastError());
     return KG_OK;
 }

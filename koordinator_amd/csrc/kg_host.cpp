@@ -334,6 +334,7 @@ int64_t kg_struct_size(int32_t sid) {
         case KG_SID_NUMA_SPEC: return sizeof(kg_numa_spec);
         case KG_SID_RESERVATION: return sizeof(kg_reservation);
         case KG_SID_QUOTA: return sizeof(kg_quota);
+        case KG_SID_RSV_RESTORED: return sizeof(kg_rsv_restored);
     }
     return -1;
 }
@@ -663,6 +664,28 @@ kg_status kg_row_eval_rsv(const kg_config *cfg, const kg_node_row *node, const k
     if (rsv_raw) *rsv_raw = (int32_t)o.raw;
     if (order) *order = o.order;
     if (nominated) *nominated = o.nominated;
+    return KG_OK;
+}
+
+kg_status kg_row_rsv_restore(const kg_config *cfg, const kg_node_row *node, const kg_reservation *rsv, int32_t n_rsv,
+                             const kg_pod_row *pod, kg_rsv_restored *out) {
+    if (!cfg || !node || !pod || !out || n_rsv < 0 || n_rsv > KG_MAX_RSV_PER_NODE || (n_rsv > 0 && !rsv))
+        return KG_ERR_INVALID_ARG;
+    kg_pod_dev pd;
+    kg_pod_dev_from_row(*cfg, *pod, pd);
+    kg_rsv_view v;
+    kg_rsv_restore(*node, rsv, n_rsv, pd, v);
+    memset(out, 0, sizeof(*out));
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        out->requested[r] = v.requested[r];
+        out->pod_requested[r] = v.pod_requested[r];
+        out->r_allocated[r] = v.r_allocated[r];
+    }
+    out->nonzero[0] = v.nonzero[0];
+    out->nonzero[1] = v.nonzero[1];
+    out->pod_count = (int32_t)v.pod_count;
+    out->n_matched = v.n_matched;
+    out->has_state = v.has_state ? 1 : 0;
     return KG_OK;
 }
 

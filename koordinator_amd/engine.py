@@ -61,6 +61,15 @@ def row_eval_rsv(cfg: np.ndarray, node_row: np.ndarray, rsv: np.ndarray, pod_row
     return bool(f.value), a.value, b.value, n.value, r.value, o.value, nm.value
 
 
+def row_rsv_restore(cfg: np.ndarray, node_row: np.ndarray, rsv: np.ndarray, pod_row: np.ndarray) -> np.ndarray:
+    """The Reservation restore of one pair (kg_row_rsv_restore): a RSV_RESTORED record."""
+    rsv = np.ascontiguousarray(rsv, dtype=nat.RESERVATION)
+    out = np.zeros((), dtype=nat.RSV_RESTORED)
+    _check(nat.lib().kg_row_rsv_restore(nat.ptr(cfg), nat.ptr(node_row), nat.ptr(rsv) if len(rsv) else None, len(rsv),
+                                        nat.ptr(pod_row), nat.ptr(out)), what="kg_row_rsv_restore")
+    return out
+
+
 class Engine:
     """One engine = one GPU, one HIP stream, one HBM-resident node snapshot."""
 

@@ -1411,6 +1411,33 @@ int kgo_rsv_pair(const kg_config *c, const kg_cluster_view *v, int32_t pod_i, in
     return ok;
 }
 
+/* The BeforePreFilter restore of one pair on the view's initial state (TestRestoreReservation):
+ * the restored NodeInfo's requested / non-zero requested / pod count and nodeRState. */
+int kgo_rsv_restore(const kg_config *c, const kg_cluster_view *v, int32_t pod_i, int32_t node_j,
+                    kg_rsv_restored *out) {
+    const int32_t N = v->n_nodes;
+    rsv_index ri;
+    if (rsv_index_build(v, N, &ri) != 0) { rsv_index_free(&ri); return -1; }
+    kg_node_spec n = v->nodes[node_j];
+    rsv_node_state rst;
+    memset(&rst, 0, sizeof(rst));
+    if (ri.n_of[node_j]) rsv_restore(&v->pods[pod_i], ri.of[node_j], ri.n_of[node_j], &n, &rst);
+    memset(out, 0, sizeof(*out));
+    for (int q = 0; q < KG_NUM_RES; q++) {
+        out->requested[q] = get(&n.requested, q);
+        out->pod_requested[q] = rst.pod_requested[q];
+        out->r_allocated[q] = rst.r_allocated[q];
+    }
+    out->nonzero[0] = n.nonzero_requested[0];
+    out->nonzero[1] = n.nonzero_requested[1];
+    out->pod_count = n.pod_count;
+    out->n_matched = rst.n_matched;
+    out->has_state = rst.has_state;
+    (void)c;
+    rsv_index_free(&ri);
+    return 0;
+}
+
 /* Matrix mode with every plugin (mask / per-plugin planes [P][N], top1 [P]); nothing committed. */
 int kgo_eval_matrix5(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
                      uint8_t *mask, uint8_t *fit, uint8_t *la, uint8_t *numa, uint8_t *rsv, uint64_t *top1) {

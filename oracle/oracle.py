@@ -220,6 +220,18 @@ def rsv_pair(cfg, view, pod_i, node_j):
     return bool(ok), raw.value, nom.value
 
 
+def rsv_restore(cfg, view, pod_i, node_j):
+    """The restored NodeInfo of one pair (kgo_rsv_restore) as a RSV_RESTORED record."""
+    from koordinator_amd import _native as nat
+    L = lib()
+    L.kgo_rsv_restore.restype = ctypes.c_int
+    L.kgo_rsv_restore.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
+    out = np.zeros((), dtype=nat.RSV_RESTORED)
+    if L.kgo_rsv_restore(_cfg(cfg), ctypes.byref(view.c_view), int(pod_i), int(node_j), out.ctypes.data) < 0:
+        raise RuntimeError("kgo_rsv_restore failed")
+    return out
+
+
 def schedule_parallel(cfg, view, pod_index, now_ns, workers):
     """The sequential cycle with a `workers`-thread Parallelizer fan-out over nodes per pod (CPU
     placement baseline; Fit / LoadAware / NodeNUMAResource)."""

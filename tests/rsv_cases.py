@@ -100,3 +100,74 @@ def rows_matrix5(cfg, view, pod_index, now_ns):
             j = int(t.argmax())
             top1[p] = ((int(t[j]) + 1) << 32) | (0xFFFFFFFF - j)
     return mask, fit, la, numa, rsvp, top1
+
+
+def restore_filter_doc():
+    with open(os.path.join(HERE, "golden", "reservation_restore_filter_kat.json")) as f:
+        return json.load(f)
+
+
+def _kat_view(node_docs, rsv_docs, pod, affinity=False):
+    """Nodes from {allocatable, requested, nonzero, pod_count, allowed_pods} dicts, reservations
+    from {node, allocatable, allocated, n_assigned, matches_pod, policy, order} dicts, one
+    single-container pod (owner class 0; affinity class 0 when `affinity`)."""
+    nodes = np.zeros(len(node_docs), dtype=nat.NODE_SPEC)
+    nodes["numa"] = -1
+    for j, d in enumerate(node_docs):
+        nodes[j]["allocatable"] = _rl(d["allocatable"])
+        req = d.get("requested", {})
+        nodes[j]["requested"] = _rl(req)
+        nz = d.get("nonzero", req)
+        nodes[j]["nonzero_requested"] = (nz.get("cpu", 0), nz.get("memory", 0))
+        nodes[j]["pod_count"] = d.get("pod_count", 0)
+        nodes[j]["allowed_pods"] = d.get("allowed_pods", 110)
+    pods = np.zeros(1, dtype=nat.POD_SPEC)
+    pods["n_containers"] = 1
+    pods["label_priority_class"] = -1
+    pods["label_qos"] = -1
+    pods["rsv_owner_class"] = 0
+    pods["rsv_affinity_class"] = 0 if affinity else -1
+    pods["quota"] = -1
+    cont = np.zeros(1, dtype=nat.CONTAINER)
+    cont[0]["requests"] = _rl(pod)
+    rsv = np.zeros(len(rsv_docs), dtype=nat.RESERVATION)
+    pol = {"Default": nat.RSV_POLICY_DEFAULT, "Aligned": nat.RSV_POLICY_ALIGNED,
+           "Restricted": nat.RSV_POLICY_RESTRICTED}
+    for i, d in enumerate(rsv_docs):
+        rsv[i]["node"] = d.get("node", 0)
+        rsv[i]["flags"] = nat.RSV_AVAILABLE
+        rsv[i]["policy"] = pol[d.get("policy", "Default")]
+        rsv[i]["owner_classes"] = 1 if d.get("matches_pod", True) else 0
+        rsv[i]["affinity_classes"] = 1 if d.get("matches_pod", True) else 0
+        rsv[i]["order"] = d.get("order", 0)
+        rsv[i]["allocatable"] = _rl(d["allocatable"])
+        rsv[i]["allocated"] = _rl(d.get("allocated"))
+        rsv[i]["n_assigned"] = d.get("n_assigned", 0)
+    return synth.SynthView(pods, cont, nodes, synth.NOW_NS, reservations=rsv)
+
+
+def restore_view(doc):
+    r = doc["restore"]
+    return _kat_view([r["node"]], r["reservations"], r["pod"])
+
+
+def filter_view(doc, case):
+    f = doc["filter"]
+    node = dict(f["node"], requested=case["pod_requested"])
+    return _kat_view([node], [dict(f["reservation"], policy=case["policy"])], case["pod"], affinity=case["affinity"])
+
+
+def order_view(doc):
+    s = doc["score_with_order"]
+    rsv = [dict(s["reservation"], node=j, order=o) for j, o in enumerate(s["orders"])]
+    return _kat_view([s["node"]] * len(rsv), rsv, s["pod"])
+
+
+def restored_dict(rec):
+    """RSV_RESTORED → the JSON's units ({cpu, memory} maps, zero entries dropped)."""
+    def rl(a):
+        return {k: int(a[r]) for k, r in (("cpu", nat.RES_CPU), ("memory", nat.RES_MEMORY)) if int(a[r])}
+    return {"pod_requested": rl(rec["pod_requested"]), "r_allocated": rl(rec["r_allocated"]),
+            "requested": rl(rec["requested"]), "nonzero": rl(rec["nonzero"]),
+            "pod_count": int(rec["pod_count"]), "n_matched": int(rec["n_matched"]),
+            "has_state": bool(rec["has_state"])}

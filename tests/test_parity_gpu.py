@@ -132,7 +132,8 @@ def test_placement_slow_nodes_and_list_depth(chunk):
     edge = np.arange(5, 2_500, 13)
     cl.nodes["nonzero_requested"][edge, 1] = (1 << 50) - (64 << 20)
     cl = cl.with_nodes(cl.nodes)
-    cfg = shipped_profile(place_chunk=chunk)
+    # MostAllocated: a huge score base clamps to 100, so the edge nodes attract pods and cross the bound
+    cfg = shipped_profile(place_chunk=chunk, fit_strategy="MostAllocated")
     idx = np.arange(300)
     with _engine_for(cfg, cl, idx) as eng:
         nodes, scores = eng.place(cl.now_ns)

@@ -8,7 +8,7 @@ from koordinator_amd import _native as nat
 from koordinator_amd import engine, synth
 from koordinator_amd.config import make_config, shipped_profile
 from oracle import oracle
-from rsv_cases import kat_cluster, kat_doc, rsv_cluster
+from rsv_cases import filter_view, kat_cluster, kat_doc, order_view, restore_filter_doc, rsv_cluster
 
 pytestmark = pytest.mark.gpu
 
@@ -167,3 +167,26 @@ def test_profile_placement_matches_sequential_cycle(chunk):
     rnodes = set(cl.rsv_arr["node"].tolist())
     assert any(n in rnodes for n in nodes.tolist())
     assert (rows_after["zone_allocated"] != engine.build_node_rows(cfg, cl)["zone_allocated"]).any()
+
+
+RF = restore_filter_doc()
+
+
+@pytest.mark.parametrize("case", RF["filter"]["cases"], ids=lambda c: c["name"])
+def test_filter_with_reservations_kat_gpu(case):
+    """Test_filterWithReservations cases through kg_eval (Reservation alone)."""
+    cfg = make_config(plugins=("Reservation",))
+    view = filter_view(RF, case)
+    with _engine(cfg, view, [0]) as eng:
+        res = eng.eval(view.now_ns)
+    assert bool(engine.unpack_mask(res["mask"], 1)[0, 0]) == case["want"]
+
+
+def test_score_with_order_kat_gpu():
+    """TestScoreWithOrder through kg_eval: normalized 10/10/10/100, best node test-node-4."""
+    cfg = make_config(plugins=("Reservation",))
+    view = order_view(RF)
+    with _engine(cfg, view, [0]) as eng:
+        res = eng.eval(view.now_ns)
+    assert list(res["rsv_scores"][0, :4]) == RF["score_with_order"]["want"]
+    assert engine.decode_top1(res["top1"])[0][0] == 3
