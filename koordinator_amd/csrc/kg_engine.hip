@@ -823,8 +823,11 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     }
 }
 
-template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE>
-__global__ __launch_bounds__(KG_BLOCK) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
+// One launch per class kind (the work table is grouped by kind): each kernel is register-allocated for
+// its own kind, so the common 2-compare / 2-score kind runs at 6 waves per SIMD (≤ 80 VGPRs, LDS
+// ≤ 53 KiB per workgroup) instead of inheriting the 4-resource kinds' budget.
+template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE, int KIND>
+__global__ __launch_bounds__(KG_BLOCK) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? 6 : KIND == 2 ? 5 : 4))) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_cls_desc *__restrict__ descs,
                                                     const kg_cls_work *__restrict__ work,
                                                     const char *__restrict__ rows, uint64_t *__restrict__ mask,
@@ -835,12 +838,10 @@ __global__ __launch_bounds__(KG_BLOCK) void k_eval3(kg_consts c, kg_planes pl, H
     const kg_cls_work w = work[blockIdx.y];
     const kg_cls_desc d = descs[w.cls];
 #define KG_CLS_ARGS c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows, sstage
-    switch (d.kind) {
-        case 0: cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS); break;
-        case 1: cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS); break;
-        case 2: cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS); break;
-        default: cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS); break;
-    }
+    if constexpr (KIND == 0) cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS);
+    else if constexpr (KIND == 1) cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS);
+    else if constexpr (KIND == 2) cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS);
+    else cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS);
 #undef KG_CLS_ARGS
 }
 
@@ -1018,45 +1019,50 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
 }
 
 // NodeNUMAResource placement chunks (≤ KG_NUMA_CHUNK_PODS pods): node per lane, so all 64 lanes work
-// on a small pod chunk (the matrix kernel's pod-per-lane layout would leave most lanes idle); each
-// thread holds 4 nodes of a 1024-node tile, the chunk's pod rows sit in LDS, and the per-pod top-k
-// keys of the tile go to the partial lists like k_eval2's.  The hint enumeration reads each lane's own
-// canonical row (kg_zone_calc).
+// on a small pod chunk (the matrix kernel's pod-per-lane layout would leave most lanes idle).  One
+// workgroup per (tile, pod): each thread holds 4 nodes of the 1024-node tile, the tile's keys sit in
+// LDS and wave 0 writes the pod's top-k list of the tile (k_eval2's partial layout).  The hint
+// enumeration reads each lane's own canonical row (kg_zone_calc).  XCD-aware order: hardware hands
+// workgroup b to XCD b % 8, so the n pods of one tile are consecutive workgroups of ONE XCD and its
+// L2 serves the tile's rows to all of them.
 #define KG_NUMA_CHUNK_PODS 16
+#define KG_XCDS 8
 __global__ __launch_bounds__(256) void k_eval_numa_chunk(kg_consts c, kg_planes pl, HotArgs a,
-                                                         const kg_pod_dev *__restrict__ pods,
+                                                         const kg_pod_dev *__restrict__ pods, int32_t shard_tiles,
                                                          uint32_t *__restrict__ partials) {
+    __shared__ __attribute__((aligned(16))) kg_pod_dev lp;
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_TILE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int n = a.n_pods;   // 1..KG_NUMA_CHUNK_PODS (host-checked)
+    const int b = blockIdx.x, xcd = b % KG_XCDS, r = b / KG_XCDS;
+    const int tile_rel = (r / n) * KG_XCDS + xcd, p = r % n;
+    if (tile_rel >= shard_tiles) return;   // grid padded to a multiple of 8 tiles; block-uniform
     constexpr int POD_DW = (int)(sizeof(kg_pod_dev) / 4);
-    __shared__ __attribute__((aligned(16))) kg_pod_dev lp[KG_NUMA_CHUNK_PODS];
-    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_NUMA_CHUNK_PODS * KG_TILE];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n = a.n_pods;   // ≤ KG_NUMA_CHUNK_PODS (host-checked)
-    for (int k = tid; k < n * POD_DW; k += 256)
-        reinterpret_cast<uint32_t *>(lp)[k] = reinterpret_cast<const uint32_t *>(pods)[k];
+    for (int k = tid; k < POD_DW; k += 256)
+        reinterpret_cast<uint32_t *>(&lp)[k] = reinterpret_cast<const uint32_t *>(pods + p)[k];
     __syncthreads();
-    const int tile = a.tile_begin + blockIdx.x;
+    const int tile = a.tile_begin + tile_rel;
     const BatchMasks bm{0xFFu, 0xFFu};
+#pragma unroll 1
     for (int v = 0; v < KG_TILE / 256; v++) {
         const int local = v * 256 + tid;
         const int64_t node = (int64_t)tile * KG_TILE + local;
         const bool in_range = node < a.node_end;
         NodeRegs nr;
         load_node(c, pl, node, in_range, bm, a.now_ns, nr);
-        for (int p = 0; p < n; p++) {
-            uint32_t key = 0;
-            uint32_t fit, la;
-            if (in_range && eval_pair(c, pl, lp[p], nr, node, a.now_ns, fit, la)) {
-                kg_numa_out o;
-                kg_numa_pair(c, pl.rows[node], lp[p], o);
-                if (o.feasible)
-                    key = ((total_of(c, fit, la, o.score) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local);
-            }
-            kbuf[p * KG_TILE + local] = key;
+        uint32_t key = 0;
+        uint32_t fit, la;
+        if (in_range && eval_pair(c, pl, lp, nr, node, a.now_ns, fit, la)) {
+            kg_numa_out o;
+            kg_numa_pair(c, pl.rows[node], lp, o);
+            if (o.feasible)
+                key = ((total_of(c, fit, la, o.score) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local);
         }
+        kbuf[local] = key;
     }
     __syncthreads();
-    for (int p = wave; p < n; p += 4) {
-        const uint32_t t = tile_topk(kbuf + p * KG_TILE);
+    if (tid < 64) {
+        const uint32_t t = tile_topk(kbuf);
         if (lane < KG_TOPK) partials[((int64_t)p * a.tiles_total + tile) * KG_PARTIAL_SLOTS + lane] = t;
     }
 }
@@ -1271,7 +1277,8 @@ struct NodeCacheEntry {
 };
 
 __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c, const kg_planes &pl, const kg_pod_dev &p,
-                                                              const NodeCacheEntry &ce, int64_t node, int64_t now_ns) {
+                                                              const NodeCacheEntry &ce, const kg_node_row &crow,
+                                                              int64_t node, int64_t now_ns) {
     NodeRegs n = ce.n;
     const bool expired = (c.plugins & KG_PLUGIN_LOADAWARE) ? kg_metric_expired(c, n.df, ce.metric_ns, now_ns) : false;
     node_regs_status(c, n.df, expired, n);
@@ -1279,7 +1286,7 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
     if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
     if (c.plugins & KG_PLUGIN_NUMA) {
         kg_numa_out o;
-        kg_numa_pair(c, pl.rows[node], p, o);
+        kg_numa_pair(c, crow, p, o);   // the LDS copy of the canonical row
         if (!o.feasible) return 0ull;
         numa = o.score;
     }
@@ -1314,6 +1321,12 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     __shared__ uint32_t fl_old_df;
     __shared__ __attribute__((aligned(16))) kg_pod_dev lpod[2];
     __shared__ NodeCacheEntry ncache[KG_NCACHE];
+    // NodeNUMAResource: canonical rows of the cached nodes (the hint enumeration of a re-score reads
+    // LDS, not a chain of dependent global loads) and the committed node's row for the zone commit
+    __shared__ __attribute__((aligned(16))) kg_node_row nrow[KG_NCACHE + 1];
+    constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16);
+    static_assert(sizeof(kg_node_row) % 16 == 0 && ROW_U4 <= 64, "rows are staged as 16-byte words by one wave");
+    const bool numa_on = (c.plugins & KG_PLUGIN_NUMA) != 0;
     __shared__ int32_t n_slow;
     const int tid = threadIdx.x;
     // tile keys of the next pod, prefetched into registers by the thread owning the tile
@@ -1404,7 +1417,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         }
         if (!plain_ok) best = 0;
         for (int q = tid; q < nt && plain_ok; q += KG_RESOLVE_THREADS) {
-            const unsigned long long k = q < KG_NCACHE ? pair_key_cached(c, pl, pd, ncache[q], touched[q], now_ns)
+            const unsigned long long k = q < KG_NCACHE ? pair_key_cached(c, pl, pd, ncache[q], nrow[q], touched[q], now_ns)
                                                        : pair_key(c, pl, pd, touched[q], n_nodes, now_ns);
             best = best > k ? best : k;
         }
@@ -1456,10 +1469,15 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         }
         // Reserve.  The Reservation nomination (restore) and NodeNUMAResource's zone commit (its
         // amplified-cpu filter) read the pre-Reserve node, so they go first when enabled.
-        if ((ra.rsv && ra.n_rn > 0) || (c.plugins & KG_PLUGIN_NUMA)) {
+        kg_node_row &srow = nrow[KG_NCACHE];
+        if (numa_on) {   // stage the node's row for the zone commit
+            if (tid < ROW_U4) reinterpret_cast<uint4 *>(&srow)[tid] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
+            __syncthreads();
+        }
+        if ((ra.rsv && ra.n_rn > 0) || numa_on) {
             if (tid == 0) {
                 rsv_commit(pl, ra, pd, node);
-                kg_numa_commit(c, pl.rows[node], pd);
+                kg_numa_commit(c, srow, pd);
             }
             __syncthreads();
         }
@@ -1497,6 +1515,11 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 ce->n.la_F0[r] = F0;
                 ce->n.la_F1[r] = F1;
             }
+        } else if (numa_on && tid >= 128 && tid < 128 + KG_MAX_ZONES) {   // the zone commit, back to the row
+            const int zi = tid - 128;
+            row.zone_allocated[zi][0] = srow.zone_allocated[zi][0];
+            row.zone_allocated[zi][1] = srow.zone_allocated[zi][1];
+            if (zi == 0) row.zone_alloc_keys = srow.zone_alloc_keys;
         } else if (tid == 0) {
             if (ra.quota && pd.quota >= 0) kg_quota_commit(ra.quota[pd.quota], pd);
             const int32_t pc = row.pod_count + 1;
@@ -1509,6 +1532,8 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             out_score[j] = (int64_t)(w >> 32) - 1;
         }
         __syncthreads();
+        if (numa_on && ce && tid >= 128 && tid < 128 + ROW_U4)   // the committed row into the node cache
+            reinterpret_cast<uint4 *>(&nrow[slot])[tid - 128] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid - 128];
         if (tid == 0) {   // kg_finalize_flags from the parts (metric and the static bits are unchanged)
             bool slow = false;
             uint32_t fmask = 0;
@@ -1578,6 +1603,7 @@ struct kg_engine {
     void *cls_mem = nullptr;                // device: descs | work | rows
     size_t cls_mem_bytes = 0;
     int32_t cls_nwork = 0;
+    int32_t cls_kind_work[4][2] = {};   // [kind] = (first work item, count)
     size_t cls_work_off = 0, cls_rows_off = 0;
     int32_t *slow_list = nullptr;   // [cap] nodes outside the fast-path bounds, whole snapshot
     int32_t *slow_count = nullptr;
@@ -1799,9 +1825,16 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
     for (size_t c = 0; c < descs.size(); c++) {
         descs[c].rows_offset = (int64_t)rows_bytes;
         rows_bytes += (size_t)descs[c].row_bytes * (size_t)descs[c].count;
-        const int32_t n = descs[c].count;
-        const int32_t ppb = pods_per_block_for(n, shard_tiles);
-        for (int32_t b = 0; b < n; b += ppb) work.push_back(kg_cls_work{(int32_t)c, b, b + ppb < n ? b + ppb : n, 0});
+    }
+    for (int kind = 0; kind < 4; kind++) {   // the work table grouped by kind: one launch per kind
+        e->cls_kind_work[kind][0] = (int32_t)work.size();
+        for (size_t c = 0; c < descs.size(); c++) {
+            if (descs[c].kind != kind) continue;
+            const int32_t n = descs[c].count;
+            const int32_t ppb = pods_per_block_for(n, shard_tiles);
+            for (int32_t b = 0; b < n; b += ppb) work.push_back(kg_cls_work{(int32_t)c, b, b + ppb < n ? b + ppb : n, 0});
+        }
+        e->cls_kind_work[kind][1] = (int32_t)work.size() - e->cls_kind_work[kind][0];
     }
     std::vector<char> rows(rows_bytes ? rows_bytes : 64, 0);
     for (size_t c = 0; c < descs.size(); c++) {
@@ -1840,19 +1873,31 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
     return KG_OK;
 }
 
+template <bool MOST, bool FIT_ON, bool LA_ON, bool W1, int KIND>
+void launch_cls_kind(kg_engine *e, dim3 grid, const HotArgs &a, const kg_cls_desc *descs, const kg_cls_work *work,
+                     const char *rows, uint64_t *mask, uint16_t *scores, uint32_t *partials) {
+    const int32_t first = e->cls_kind_work[KIND][0], count = e->cls_kind_work[KIND][1];
+    if (count == 0) return;
+    grid.y = (unsigned)count;
+    // matrix mode: 8-pod chunks, score segments staged in LDS and written as 1 KiB wave stores
+    if (mask)
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, 8, true, KIND>), grid, dim3(KG_BLOCK), 0, e->stream,
+                           e->consts, e->pl, a, descs, work + first, rows, mask, scores, partials);
+    else
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, 16, false, KIND>), grid, dim3(KG_BLOCK), 0, e->stream,
+                           e->consts, e->pl, a, descs, work + first, rows, mask, scores, partials);
+}
+
 template <bool MOST, bool FIT_ON, bool LA_ON, bool W1>
 void launch_cls4(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint16_t *scores, uint32_t *partials) {
     const char *m = (const char *)e->cls_mem;
     const kg_cls_desc *descs = (const kg_cls_desc *)m;
     const kg_cls_work *work = (const kg_cls_work *)(m + e->cls_work_off);
     const char *rows = m + e->cls_rows_off;
-    // matrix mode: 16-pod chunks, score segments staged in LDS and written as 1 KiB wave stores
-    if (mask)
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, 16, true>), grid, dim3(KG_BLOCK), 0, e->stream, e->consts,
-                           e->pl, a, descs, work, rows, mask, scores, partials);
-    else
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, 16, false>), grid, dim3(KG_BLOCK), 0, e->stream,
-                           e->consts, e->pl, a, descs, work, rows, mask, scores, partials);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 0>(e, grid, a, descs, work, rows, mask, scores, partials);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 1>(e, grid, a, descs, work, rows, mask, scores, partials);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 2>(e, grid, a, descs, work, rows, mask, scores, partials);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 3>(e, grid, a, descs, work, rows, mask, scores, partials);
 }
 
 template <bool MOST, bool FIT_ON, bool LA_ON>
@@ -1912,8 +1957,9 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     a.now_ns = now_ns;
     if ((e->consts.plugins & KG_PLUGIN_NUMA) && topk && n <= KG_NUMA_CHUNK_PODS) {
         if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
-        hipLaunchKernelGGL(k_eval_numa_chunk, dim3((unsigned)shard_tiles), dim3(256), 0, e->stream, e->consts, e->pl, a,
-                           e->pods + pod_begin, partials);
+        const unsigned blocks = (unsigned)((shard_tiles + KG_XCDS - 1) / KG_XCDS * KG_XCDS * n);
+        hipLaunchKernelGGL(k_eval_numa_chunk, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                           e->pods + pod_begin, (int32_t)shard_tiles, partials);
         HIP_TRY(e, hipGetLastError());
         if (e->profiling) {
             HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
