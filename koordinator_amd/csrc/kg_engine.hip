@@ -649,6 +649,32 @@ __device__ __forceinline__ void cls_scores(const kg_consts &c, const kg_cls_desc
     }
 }
 
+typedef uint16_t kg_u16x2 __attribute__((ext_vector_type(2)));
+
+// FULL + UNIT scores of one pair packed as H = fit | la << 16 (u16 halves): the Fit sum and the
+// LoadAware sum << 16 meet in one v_add3 (every term ≤ 100, so each half holds its sum without carry),
+// and one v_pk_lshrrev_b16 applies both plugins' weight-sum shifts (shifts = fit_shift | la_shift << 16)
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON>
+__device__ __forceinline__ uint32_t cls_packed(const kg_pod_cls_t<NC, NF> &pd, const ClsNode<NC, NF> &n,
+                                               kg_u16x2 shifts) {
+    uint32_t sf = 0;
+    if (FIT_ON) {
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n.R[f], n.F[f]));
+            if (MOST) q = q < 100u ? q : 100u;
+            sf += q;
+        }
+    }
+    uint32_t sl = 0;
+    if (LA_ON) {
+        const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la[0], n.laR[0], n.laF[0]));
+        const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la[1], n.laR[1], n.laF[1]));
+        sl = (q0 + q1) << 16;
+    }
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(kg_u16x2, sf + sl) >> shifts);
+}
+
 // v_cndmask_b32 with a wave lane mask as the condition: v where the lane's bit is set, else 0
 __device__ __forceinline__ uint32_t sel_lanes(unsigned long long m, uint32_t v) {
     uint32_t r;
@@ -673,7 +699,7 @@ __device__ __forceinline__ void write_lanes(uint32_t (&mb)[4], uint32_t lane, un
 // Pods [p0, p1) of one class against the lane's two nodes; rows come from the LDS chunk buffer.
 // The feasibility ballots of the chunk are collected into lanes (p − p0) of four VGPRs and written
 // once per chunk; EDGE workgroups (the shard's last tile) check that a segment lies in the row.
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool STAGE>
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool STAGE, int CC, bool UNR>
 __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> &n0,
                                          const ClsNode<NC, NF> &n1, unsigned long long okm0, unsigned long long okm1,
                                          const char *lrows, int p0, int p1, uint16_t *__restrict__ scores,
@@ -681,12 +707,40 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
                                          uint32_t *kbuf, uint32_t (&mb)[4], uint16_t *sst) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    for (int p = p0; p < p1; p++) {
+    // UNR: a whole chunk, unrolled, so every LDS address (pod row, key buffer, score staging) and
+    // every write-lane select is an immediate
+    const int np = UNR ? CC : p1 - p0;
+    const kg_u16x2 shifts = {(uint16_t)d.fit_shift, (uint16_t)c.la_shift};
+    auto pod = [&](const int i) {
         const kg_pod_cls_t<NC, NF> pd =
-            *reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(lrows + (p - p0) * (int)sizeof(kg_pod_cls_t<NC, NF>));
-        uint32_t fit0, la0, fit1, la1;
+            *reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(lrows + i * (int)sizeof(kg_pod_cls_t<NC, NF>));
         const unsigned long long m0 = cls_ok_mask<NC, NF>(pd, n0, okm0);
         const unsigned long long m1 = cls_ok_mask<NC, NF>(pd, n1, okm1);
+        if (FULL && W1) {
+            // packed pair scores: key = dot2(H, {1024, 1024}) + kb = (fit + la) << 10 + kb in one
+            // v_dot2_u32_u16; the staged u16 is the perm of H's low bytes (fit | la << 8)
+            const uint32_t h0 = cls_packed<NC, NF, MOST, FIT_ON, LA_ON>(pd, n0, shifts);
+            const uint32_t h1 = cls_packed<NC, NF, MOST, FIT_ON, LA_ON>(pd, n1, shifts);
+            const kg_u16x2 kw = {(uint16_t)(1u << KG_TILE_SHIFT), (uint16_t)(1u << KG_TILE_SHIFT)};
+            const uint32_t k0 = sel_lanes(m0, __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h0), kw, kb0, false));
+            const uint32_t k1 = sel_lanes(m1, __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h1), kw, kb1, false));
+            kbuf[i * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
+            if (OUT) {
+                write_lanes(mb, (uint32_t)i, m0, m1);
+                const uint16_t s0 = (uint16_t)__builtin_amdgcn_perm(h0, h0, 0x0c0c0200u);
+                const uint16_t s1 = (uint16_t)__builtin_amdgcn_perm(h1, h1, 0x0c0c0200u);
+                if (STAGE) {
+                    sst[i * 128 + lane] = s0;
+                    sst[i * 128 + 64 + lane] = s1;
+                } else {
+                    uint16_t *srow = scores + pd.score_off;
+                    if (seg0) srow[scol] = s0;
+                    if (seg1) srow[scol + 64] = s1;
+                }
+            }
+            return;
+        }
+        uint32_t fit0, la0, fit1, la1;
         cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n0, fit0, la0);
         cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n1, fit1, la1);
         uint32_t tot0, tot1;
@@ -699,18 +753,24 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
         }
         const uint32_t k0 = sel_lanes(m0, (tot0 << KG_TILE_SHIFT) + kb0);
         const uint32_t k1 = sel_lanes(m1, (tot1 << KG_TILE_SHIFT) + kb1);
-        kbuf[(p - p0) * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
+        kbuf[i * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
         if (OUT) {
-            write_lanes(mb, (uint32_t)(p - p0), m0, m1);
+            write_lanes(mb, (uint32_t)i, m0, m1);
             if (STAGE) {  // the wave's 128-column score segment of this pod, written out per chunk
-                sst[(p - p0) * 128 + lane] = (uint16_t)(fit0 | (la0 << 8));
-                sst[(p - p0) * 128 + 64 + lane] = (uint16_t)(fit1 | (la1 << 8));
+                sst[i * 128 + lane] = (uint16_t)(fit0 | (la0 << 8));
+                sst[i * 128 + 64 + lane] = (uint16_t)(fit1 | (la1 << 8));
             } else {
                 uint16_t *srow = scores + pd.score_off;
                 if (seg0) srow[scol] = (uint16_t)(fit0 | (la0 << 8));
                 if (seg1) srow[scol + 64] = (uint16_t)(fit1 | (la1 << 8));
             }
         }
+    };
+    if constexpr (UNR) {
+#pragma unroll
+        for (int i = 0; i < CC; i++) pod(i);
+    } else {
+        for (int i = 0; i < np; i++) pod(i);
     }
 }
 
@@ -768,12 +828,13 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         }
         const char *cur = lrows + buf * (CC * RB);
         uint32_t mb[4] = {0u, 0u, 0u, 0u};
-        if (full)
-            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, true, W1, STAGE>(c, d, n0, n1, okm0, okm1, cur, p0, p1, scores,
-                                                                              scol, seg0, seg1, kb0, kb1, kbuf, mb, sst);
-        else
-            cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, false, W1, STAGE>(c, d, n0, n1, okm0, okm1, cur, p0, p1, scores,
-                                                                               scol, seg0, seg1, kb0, kb1, kbuf, mb, sst);
+#define KG_CLS_PODS(FULL_, UNR_)                                                                                    \
+    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, STAGE, CC, UNR_>(c, d, n0, n1, okm0, okm1, cur, p0, p1, scores, \
+                                                                          scol, seg0, seg1, kb0, kb1, kbuf, mb, sst)
+        if (full && p1 - p0 == CC) KG_CLS_PODS(true, true);
+        else if (full) KG_CLS_PODS(true, false);
+        else KG_CLS_PODS(false, false);
+#undef KG_CLS_PODS
         if (OUT && STAGE) {
             // 16 lanes × 16 B cover one pod's 128 columns: four pods per wave-wide 1 KiB store.  The
             // reads see the other lanes' ds_writes: a wave's LDS operations complete in order.
