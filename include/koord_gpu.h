@@ -520,6 +520,13 @@ kg_status kg_snapshot_reset(kg_engine *eng, int32_t n_nodes);
 kg_status kg_snapshot_upsert(kg_engine *eng, const int32_t *node_index, const kg_node_row *rows, int32_t n);
 kg_status kg_snapshot_remove(kg_engine *eng, int32_t node_index);
 kg_status kg_snapshot_download(kg_engine *eng, int32_t first, int32_t n, kg_node_row *out);
+/* Snapshot generation (SURVEY §5 error contract; replaces the Go cache's generation check in
+ * Cache.UpdateSnapshot, a per-cycle staleness test): the count of successful snapshot mutations —
+ * kg_snapshot_reset, kg_snapshot_upsert / _remove, kg_commit and each placement resolve (kg_place,
+ * kg_place_chunk_resolve).  After a HIP error the device state is stale: this returns KG_ERR_STATE (with
+ * the generation reached), every other entry point fails with KG_ERR_STATE, and the caller falls back to
+ * the CPU plugins until kg_snapshot_reset + upsert reload the snapshot. */
+kg_status kg_snapshot_generation(kg_engine *eng, uint64_t *out);
 /* Restrict kg_eval/kg_place evaluation to nodes [begin, end) (node sharding across GPUs);
  * node indices stay global.  begin must be a multiple of 1024 unless the shard is empty. */
 kg_status kg_set_shard(kg_engine *eng, int32_t begin, int32_t end);

@@ -185,6 +185,7 @@ EXPORTED = [
     "kg_snapshot_download", "kg_set_shard", "kg_pods_set", "kg_eval", "kg_place", "kg_num_tiles",
     "kg_place_chunk_eval", "kg_place_chunk_resolve", "kg_commit", "kg_set_profiling", "kg_eval_kernel_times",
     "kg_rsv_set", "kg_rsv_download", "kg_quota_set", "kg_quota_download", "kg_row_eval_rsv", "kg_row_rsv_restore",
+    "kg_snapshot_generation",
 ]
 
 _lib = None
@@ -225,6 +226,7 @@ def lib() -> ctypes.CDLL:
         "kg_quota_set": (i32, [vp, vp, i32]), "kg_quota_download": (i32, [vp, vp, i32]),
         "kg_row_eval_rsv": (i32, [vp, vp, vp, i32, vp, i64, vp, vp, vp, vp, vp, vp, vp]),
         "kg_row_rsv_restore": (i32, [vp, vp, vp, i32, vp, vp]),
+        "kg_snapshot_generation": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         if host_only and not hasattr(L, name):

@@ -1672,6 +1672,11 @@ struct kg_engine {
                                     // the placement resolve appends the nodes its commits make slow)
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
+    // SURVEY §5 error contract: every successful snapshot mutation (reset, upsert / remove, commit,
+    // placement resolve) advances the generation; a HIP error marks the device state stale, and every
+    // entry point but kg_snapshot_reset then fails with KG_ERR_STATE until the snapshot is reloaded
+    uint64_t generation = 0;
+    bool stale = false;
     bool profiling = false;
     // Reservation / ElasticQuota (config 5)
     void *rsv_mem = nullptr;            // slots | rfirst | rnode | E | O
@@ -1700,7 +1705,10 @@ kg_status set_err(kg_engine *e, kg_status code, const char *fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, sizeof(buf), fmt, ap);
     va_end(ap);
-    if (e) e->err = buf;
+    if (e) {
+        e->err = buf;
+        if (code == KG_ERR_HIP) e->stale = true;
+    }
     return code;
 }
 
@@ -2110,8 +2118,11 @@ kg_status rsv_eval_chunk(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_
     return KG_OK;
 }
 
-kg_status check_engine(kg_engine *e) {
+kg_status check_engine(kg_engine *e, bool reloading = false) {
     if (!e) return KG_ERR_INVALID_ARG;
+    if (e->stale && !reloading)
+        return set_err(e, KG_ERR_STATE, "device state is stale after a HIP error (%s): reload it with kg_snapshot_reset",
+                       e->err.c_str());
     HIP_TRY(e, hipSetDevice(e->device));
     return KG_OK;
 }
@@ -2194,7 +2205,7 @@ kg_status kg_sync(kg_engine *e) {
 }
 
 kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
-    kg_status st = check_engine(e);
+    kg_status st = check_engine(e, true);
     if (st) return st;
     if (n_nodes < 0) return set_err(e, KG_ERR_INVALID_ARG, "negative node count");
     HIP_TRY(e, hipStreamSynchronize(e->stream));
@@ -2246,7 +2257,15 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     e->slow_valid = false;
+    e->stale = false;
+    e->generation++;
     return KG_OK;
+}
+
+kg_status kg_snapshot_generation(kg_engine *e, uint64_t *out) {
+    if (!e || !out) return KG_ERR_INVALID_ARG;
+    *out = e->generation;
+    return e->stale ? KG_ERR_STATE : KG_OK;
 }
 
 kg_status kg_snapshot_upsert(kg_engine *e, const int32_t *node_index, const kg_node_row *rows, int32_t n) {
@@ -2268,6 +2287,7 @@ kg_status kg_snapshot_upsert(kg_engine *e, const int32_t *node_index, const kg_n
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipStreamSynchronize(e->stream));  // staging buffer reuse
     e->slow_valid = false;
+    e->generation++;
     return KG_OK;
 }
 
@@ -2547,6 +2567,7 @@ kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin
                        numa && n > KG_NUMA_CHUNK_PODS ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count,
                        numa ? 0 : 1);   // the NUMA chunk kernels list slow nodes themselves (exact pair path)
     HIP_TRY(e, hipGetLastError());
+    e->generation++;   // the resolve commits the chunk's winners to the snapshot
     return KG_OK;
 }
 
@@ -2718,6 +2739,7 @@ kg_status kg_commit(kg_engine *e, int32_t pod, int32_t node) {
     e->slow_valid = false;
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->generation++;
     return KG_OK;
 }
 

@@ -126,6 +126,12 @@ class Engine:
         _check(nat.lib().kg_snapshot_download(self._h, first, n, nat.ptr(out)), self, "kg_snapshot_download")
         return out
 
+    def generation(self) -> int:
+        """kg_snapshot_generation: successful snapshot mutations so far; raises once the state is stale."""
+        g = ctypes.c_uint64(0)
+        _check(nat.lib().kg_snapshot_generation(self._h, ctypes.byref(g)), self, "kg_snapshot_generation")
+        return int(g.value)
+
     def set_shard(self, begin: int, end: int) -> None:
         _check(nat.lib().kg_set_shard(self._h, begin, end), self, "kg_set_shard")
         self.shard = (begin, end)

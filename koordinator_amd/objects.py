@@ -115,6 +115,8 @@ class Node:
     allocatable: Dict[str, object] = dataclasses.field(default_factory=dict)
     pods: int = 110
     annotations_raw_allocatable: Optional[Dict[str, object]] = None   # node.koordinator.sh/raw-allocatable
+    raw_allocatable_invalid: bool = False                             # that annotation does not unmarshal
+    custom_thresholds_invalid: bool = False                           # usage-thresholds does not unmarshal
     custom_usage_thresholds: Optional[Dict[str, int]] = None          # scheduling.koordinator.sh/usage-thresholds
     custom_prod_usage_thresholds: Optional[Dict[str, int]] = None
     custom_aggregated: Optional[dict] = None   # {"usageThresholds": {...}, "usageAggregationType": "p95", "usageAggregatedDuration": seconds}
@@ -241,10 +243,14 @@ class Cluster:
                                                quantity_value("memory", nz.get("memory", 0))]
             ns["pod_count"] = info["pods"]
             ns["allowed_pods"] = n.pods
-            if n.annotations_raw_allocatable is not None:
+            if n.raw_allocatable_invalid:
+                ns["raw_allocatable_state"] = -1
+            elif n.annotations_raw_allocatable is not None:
                 ns["raw_allocatable_state"] = 1
                 ns["raw_allocatable"] = resource_list(n.annotations_raw_allocatable)
-            if (n.custom_usage_thresholds or n.custom_prod_usage_thresholds or n.custom_aggregated) is not None:
+            if n.custom_thresholds_invalid:
+                ns["custom_thresholds_state"] = -1
+            elif (n.custom_usage_thresholds or n.custom_prod_usage_thresholds or n.custom_aggregated) is not None:
                 ns["custom_thresholds_state"] = 1
                 ns["custom_usage_thresholds"] = _thresholds(n.custom_usage_thresholds)
                 ns["custom_prod_usage_thresholds"] = _thresholds(n.custom_prod_usage_thresholds)

@@ -179,3 +179,24 @@ def test_snapshot_upsert_remove_and_commit():
     assert got[17]["flags"] == 0
     mask = engine.unpack_mask(res["mask"], 2000)
     assert not mask[:, 17].any()
+
+
+def test_snapshot_generation_counts_mutations():
+    """kg_snapshot_generation: reset, upsert / remove, commit and each placement resolve
+    advance it; evaluations do not."""
+    cl = synth.make_cluster(1_500, 16, seed=9)
+    cfg = shipped_profile()
+    idx = np.arange(16)
+    with engine.Engine(cfg) as eng:
+        assert eng.generation() == 0
+        eng.load_snapshot(engine.build_node_rows(cfg, cl))       # reset + upsert
+        g0 = eng.generation()
+        assert g0 == 2
+        eng.set_pods(engine.build_pod_rows(cfg, cl, idx))
+        eng.eval(cl.now_ns)
+        assert eng.generation() == g0
+        eng.remove(5)
+        eng.commit(0, 7)
+        assert eng.generation() == g0 + 2
+        eng.place(cl.now_ns)                                      # 16 pods in 8-pod chunks: 2 resolves
+        assert eng.generation() == g0 + 4
