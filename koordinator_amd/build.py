@@ -57,13 +57,17 @@ def build_engine(force: bool = False) -> str:
     return ENGINE_SO
 
 
+def oracle_sources() -> list[str]:
+    return [os.path.join(ORACLE_DIR, "koord_oracle.c"), os.path.join(ORACLE_DIR, "cpu_accumulator.c")]
+
+
 def build_oracle(force: bool = False) -> str:
-    src = os.path.join(ORACLE_DIR, "koord_oracle.c")
+    srcs = oracle_sources()
     os.makedirs(os.path.dirname(ORACLE_SO), exist_ok=True)
-    if not force and not _newer(ORACLE_SO, [src, os.path.join(ROOT, "include", "koord_gpu.h")]):
+    if not force and not _newer(ORACLE_SO, [*srcs, os.path.join(ROOT, "include", "koord_gpu.h")]):
         return ORACLE_SO
     tmp = ORACLE_SO + ".tmp"
-    _run(["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-ffp-contract=off", "-Wall", src, "-o", tmp, "-lm", "-lpthread"])
+    _run(["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-ffp-contract=off", "-Wall", *srcs, "-o", tmp, "-lm", "-lpthread"])
     os.replace(tmp, ORACLE_SO)
     return ORACLE_SO
 
@@ -85,9 +89,9 @@ def build_sanitized(force: bool = False) -> tuple[str, str]:
     if force or _newer(SAN_HOST_SO, engine_sources()):
         _run(["g++", "-std=c++17", *SAN_FLAGS, *inc, host_src, "-o", SAN_HOST_SO + ".tmp"])
         os.replace(SAN_HOST_SO + ".tmp", SAN_HOST_SO)
-    src = os.path.join(ORACLE_DIR, "koord_oracle.c")
-    if force or _newer(SAN_ORACLE_SO, [src, os.path.join(ROOT, "include", "koord_gpu.h")]):
-        _run(["gcc", "-std=c11", *SAN_FLAGS, *inc, src, "-o", SAN_ORACLE_SO + ".tmp", "-lm", "-lpthread"])
+    srcs = oracle_sources()
+    if force or _newer(SAN_ORACLE_SO, [*srcs, os.path.join(ROOT, "include", "koord_gpu.h")]):
+        _run(["gcc", "-std=c11", *SAN_FLAGS, *inc, *srcs, "-o", SAN_ORACLE_SO + ".tmp", "-lm", "-lpthread"])
         os.replace(SAN_ORACLE_SO + ".tmp", SAN_ORACLE_SO)
     return SAN_HOST_SO, SAN_ORACLE_SO
 

@@ -39,6 +39,12 @@ def lib():
         L.kgo_numa_merge.argtypes = [ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
         L.kgo_eval_matrix3.restype = ctypes.c_int
         L.kgo_eval_matrix3.argtypes = [vp, vp, vp, i32, i32, i32, i64, vp, vp, vp, vp]
+        L.kgo_take_cpus.restype = ctypes.c_int
+        L.kgo_take_cpus.argtypes = [vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, vp]
+        L.kgo_take_preferred_cpus.restype = ctypes.c_int
+        L.kgo_take_preferred_cpus.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, vp]
         _lib = L
     return _lib
 
@@ -247,3 +253,64 @@ def schedule_parallel(cfg, view, pod_index, now_ns, workers):
     if st != 0:
         raise RuntimeError(f"kgo_schedule_parallel failed ({st})")
     return nodes, scores
+
+
+# ---- NodeNUMAResource cpuset take (oracle/cpu_accumulator.c) ---------------------------------------
+
+BIND = {"": 0, "FullPCPUs": 1, "SpreadByPCPUs": 2}
+EXCLUSIVE = {"": 0, "None": 0, "PCPULevel": 1, "NUMANodeLevel": 2}
+NUMA_STRATEGY = {"LeastAllocated": 0, "MostAllocated": 1}
+
+
+class CPUTopo(ctypes.Structure):
+    _fields_ = [("n_cpus", ctypes.c_int32), ("socket", ctypes.c_void_p), ("node", ctypes.c_void_p),
+                ("core", ctypes.c_void_p)]
+
+
+def cpu_topology(socket, node, core):
+    """(socket, node, core) id arrays indexed by cpu id → (ctypes struct, keep-alive arrays)."""
+    arrs = [np.ascontiguousarray(x, dtype=np.int32) for x in (socket, node, core)]
+    t = CPUTopo(len(arrs[0]), *(a.ctypes.data for a in arrs))
+    return t, arrs
+
+
+def test_topology(num_sockets, nodes_per_socket, cores_per_node, cpus_per_core):
+    """buildCPUTopologyForTest (cpu_accumulator_test.go:30-57): dense ids socket → node → core → cpu."""
+    s, n, c = [], [], []
+    node_id = core_id = 0
+    for sk in range(num_sockets):
+        for _ in range(nodes_per_socket):
+            for _ in range(cores_per_node):
+                for _ in range(cpus_per_core):
+                    s.append(sk), n.append(node_id), c.append(core_id)
+                core_id += 1
+            node_id += 1
+    return s, n, c
+
+
+def _mask(n, cpus):
+    m = np.zeros(n, np.uint8)
+    for x in cpus or ():
+        m[x] = 1
+    return m
+
+
+def take_cpus(topo, max_ref, available, need, bind, excl="None", strategy="MostAllocated", alloc_ref=None,
+              alloc_excl=None, preferred=None):
+    """takeCPUs / takePreferredCPUs → sorted cpu list, or None on failure.  topo = (socket, node, core)."""
+    t, keep = cpu_topology(*topo)
+    n = t.n_cpus
+    av = _mask(n, available)
+    ref = np.zeros(n, np.int32) if alloc_ref is None else np.ascontiguousarray(alloc_ref, np.int32)
+    ex = np.zeros(n, np.int8) if alloc_excl is None else np.ascontiguousarray(alloc_excl, np.int8)
+    out = np.zeros(n, np.uint8)
+    L = lib()
+    args = [ctypes.byref(t), max_ref, av.ctypes.data]
+    if preferred is None:
+        st = L.kgo_take_cpus(*args, ref.ctypes.data, ex.ctypes.data, need, BIND[bind], EXCLUSIVE[excl],
+                             NUMA_STRATEGY[strategy], out.ctypes.data)
+    else:
+        pf = _mask(n, preferred)
+        st = L.kgo_take_preferred_cpus(*args, pf.ctypes.data, ref.ctypes.data, ex.ctypes.data, need, BIND[bind],
+                                       EXCLUSIVE[excl], NUMA_STRATEGY[strategy], out.ctypes.data)
+    return None if st != 0 else [int(i) for i in np.flatnonzero(out)]
