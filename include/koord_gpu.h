@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 4
+#define KG_ABI_VERSION 5
 
 /* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
 #define KG_PLACE_CHUNK_MAX 1024
@@ -153,6 +153,22 @@ enum kg_scoring_strategy {
 
 /* NUMA topology policies (apis/extension/numa_aware.go; node label node.koordinator.sh/numa-topology-policy
  * or the NodeResourceTopology kubelet policy, pkg/scheduler/plugins/nodenumaresource/util.go:52-58) */
+/* CPU bind policies of NodeNUMAResource (apis/extension/numa_aware.go:86-118) */
+enum kg_cpu_bind_policy {          /* ResourceSpec Required/PreferredCPUBindPolicy, args.DefaultCPUBindPolicy */
+    KG_CPU_BIND_UNSET = 0,         /* "" */
+    KG_CPU_BIND_DEFAULT = 1,       /* "Default" (the plugin's DefaultCPUBindPolicy) */
+    KG_CPU_BIND_FULL_PCPUS = 2,
+    KG_CPU_BIND_SPREAD_BY_PCPUS = 3,
+    KG_CPU_BIND_CONSTRAINED_BURST = 4,
+};
+enum kg_cpu_exclusive_policy {     /* ResourceSpec.PreferredCPUExclusivePolicy / CPUInfo.ExclusivePolicy */
+    KG_CPU_EXCL_UNSET = 0, KG_CPU_EXCL_NONE = 1, KG_CPU_EXCL_PCPU_LEVEL = 2, KG_CPU_EXCL_NUMA_NODE_LEVEL = 3,
+};
+enum kg_node_cpu_bind_policy {     /* GetNodeCPUBindPolicy: label node.koordinator.sh/cpu-bind-policy, or the
+                                      kubelet static policy with full-pcpus-only (numa_aware.go:314-325) */
+    KG_NODE_CPU_BIND_NONE = 0, KG_NODE_CPU_BIND_FULL_PCPUS_ONLY = 1, KG_NODE_CPU_BIND_SPREAD_BY_PCPUS = 2,
+};
+
 enum kg_numa_policy {
     KG_NUMA_NONE = 0,
     KG_NUMA_BEST_EFFORT = 1,
@@ -160,6 +176,7 @@ enum kg_numa_policy {
     KG_NUMA_SINGLE_NUMA_NODE = 3
 };
 #define KG_MAX_ZONES 8
+#define KG_MAX_NODE_CPUS 1024     /* logical CPUs of one node in kg_cluster_view.cpus */
 
 /* ------------------------------------------------------------------ */
 /* engine configuration = plugin args (pkg/scheduler/apis/config/types.go)  */
@@ -196,7 +213,7 @@ typedef struct kg_config {
     int32_t weight_numa;                      /* profile score weight of NodeNUMAResource */
     int32_t numa_strategy;                    /* ScoringStrategy.Type (node / allocated-zone score) */
     int32_t numa_hint_strategy;               /* NUMAScoringStrategy.Type (per-mask hint score) */
-    int32_t _pad1;
+    int32_t numa_default_cpu_bind_policy;     /* DefaultCPUBindPolicy (kg_cpu_bind_policy; v1beta2 default FullPCPUs) */
     int64_t numa_resource_weight[KG_NUM_RES]; /* ScoringStrategy.Resources (0 ⇔ absent) */
 
     /* engine knobs */
@@ -228,7 +245,8 @@ typedef struct kg_pod_spec {
     int32_t status_qos;                         /* kg_kube_qos of Status.QOSClass (UNSET ⇒ computed) */
     int32_t is_daemonset;                       /* an OwnerReference of Kind DaemonSet */
     int32_t is_terminated;                      /* util.IsPodTerminated */
-    int32_t _pad;
+    int32_t cpu_bind_required;                  /* annotation scheduling.koordinator.sh/resource-spec
+                                                   RequiredCPUBindPolicy (kg_cpu_bind_policy) */
     int64_t name_id;                            /* identity of namespace/name */
     /* Reservation: the pod's owner class (reservation.Match(pod) ⇔ bit owner_class of the reservation's
      * owner_classes; −1 ⇔ matches none) and its required reservation affinity class (−1 ⇔ no
@@ -239,6 +257,8 @@ typedef struct kg_pod_spec {
     /* ElasticQuota: index into kg_cluster_view.quotas (−1 ⇔ no quota: PreFilter skips) */
     int32_t quota;
     int32_t non_preemptible;                    /* extension.IsPodNonPreemptible */
+    int32_t cpu_bind_preferred;                 /* ResourceSpec.PreferredCPUBindPolicy (kg_cpu_bind_policy) */
+    int32_t cpu_exclusive;                      /* ResourceSpec.PreferredCPUExclusivePolicy (kg_cpu_exclusive_policy) */
 } kg_pod_spec;
 
 typedef struct kg_aggregated_usage { /* slov1alpha1.AggregatedUsage */
@@ -309,7 +329,22 @@ typedef struct kg_numa_spec {
     int32_t cpuset_cpus;                             /* |NodeAllocation.allocatedCPUs|: CPUs held by cpuset pods
                                                         (GetAvailableCPUs' allocated, no preferred CPUs) */
     int32_t zone_cpuset_cpus[KG_MAX_ZONES];          /* allocatedCPUs.CPUsInNUMANodes(zone_id[z]) (node_allocation.go:165) */
+    /* cpuset binding (the CPU accumulator's inputs): the node's CPU bind policy, TopologyOptions.MaxRefCount,
+       and its logical CPUs (CPUTopology.CPUDetails + NodeAllocation.allocatedCPUs + ReservedCPUs) as
+       kg_cluster_view.cpus[first_cpu, first_cpu + n_cpus), cpu id = position; n_cpus == 0 ⇔ no detail
+       (the count fields above then stand alone) */
+    int32_t node_cpu_bind_policy;                    /* kg_node_cpu_bind_policy */
+    int32_t max_ref_count;                           /* ≥ 1 */
+    int32_t first_cpu, n_cpus;
 } kg_numa_spec;
+
+/* One logical CPU of a node (CPUInfo of cpu_topology.go + the node allocation's view of it). */
+typedef struct kg_cpu_info {
+    int32_t socket, node, core;   /* SocketID, NodeID (NUMA node = zone id), CoreID as reported */
+    int32_t refcount;             /* NodeAllocation.allocatedCPUs[cpu].RefCount (0 ⇔ not allocated) */
+    int32_t exclusive;            /* its ExclusivePolicy (kg_cpu_exclusive_policy) while allocated */
+    int32_t reserved;             /* in TopologyOptions.ReservedCPUs (kubelet / node reservation / system QoS) */
+} kg_cpu_info;
 
 /* One reservation as the reservation cache holds it (frameworkext.ReservationInfo). */
 enum kg_rsv_policy { /* schedulingv1alpha1.ReservationAllocatePolicy */
@@ -350,6 +385,7 @@ typedef struct kg_cluster_view {
     const kg_numa_spec *numa;                int32_t n_numa;       int32_t _p6;
     const kg_reservation *reservations;      int32_t n_reservations; int32_t _p7;
     const kg_quota *quotas;                  int32_t n_quotas;     int32_t _p8;
+    const kg_cpu_info *cpus;                 int32_t n_cpus;       int32_t _p9;
 } kg_cluster_view;
 
 /* ------------------------------------------------------------------ */
@@ -360,7 +396,10 @@ typedef struct kg_cluster_view {
 #define KG_POD_PROD 0x4u           /* GetPodPriorityClassWithDefault == koord-prod */
 #define KG_POD_LA_PROD_SCORE 0x8u  /* prodPod && ScoreAccordingProdUsage (load_aware.go:291) */
 #define KG_POD_NUMA_SKIP 0x10u     /* NodeNUMAResource PreFilter skip: all requests zero (plugin.go:225-231) */
-#define KG_POD_NUMA_CPU_BIND 0x20u /* the pod asks for cpuset binding (LSE/LSR prod, plugin.go:232-262): unsupported */
+#define KG_POD_NUMA_CPU_BIND 0x20u /* PreFilter requestCPUBind: LSE/LSR prod with a FullPCPUs / SpreadByPCPUs
+                                      policy and a cpu request (plugin.go:232-262) */
+#define KG_POD_NUMA_BIND_INVALID 0x100u /* PreFilter ErrInvalidRequestedCPUs (cpu request not whole cores):
+                                           NodeNUMAResource fails on every node */
 #define KG_POD_NON_PREEMPTIBLE 0x40u /* ElasticQuota: extension.IsPodNonPreemptible (min gate) */
 #define KG_POD_VALID 0x80000000u
 
@@ -374,7 +413,8 @@ typedef struct kg_pod_row {
     int64_t numa_request[KG_NUM_RES];   /* PodRequestsAndLimits requests (NodeNUMAResource PreFilter,
                                            Reservation podRequests, ElasticQuota podRequest) */
     uint32_t numa_request_present;      /* key set of those requests */
-    uint32_t _pad;
+    uint32_t cpu_bind;                  /* PreFilter state: required policy | preferred (effective) policy << 4 |
+                                           exclusive policy << 8 (kg_cpu_bind_policy / kg_cpu_exclusive_policy) */
     int32_t rsv_owner_class;            /* kg_pod_spec.rsv_owner_class */
     int32_t rsv_affinity_class;         /* kg_pod_spec.rsv_affinity_class */
     int32_t quota;                      /* kg_pod_spec.quota */
@@ -417,6 +457,13 @@ typedef struct kg_node_row {
     int64_t cpuset_amp_milli;           /* Amplify(cpuset_milli, ratio) */
     int64_t zone_cpuset_amp[KG_MAX_ZONES]; /* Amplify(c, ratio) − c, c = zone z's cpuset CPUs · 1000: added to the
                                               zone's allocated cpu while the zone has an allocation entry */
+    /* cpuset binding on a node without a NUMA topology policy (the Filter's Allocate reduces to counts:
+       takeCPUs always succeeds on a large enough available set, and the required-policy filter leaves
+       whole free cores / one CPU per core with a free CPU) */
+    int32_t node_cpu_bind;              /* kg_node_cpu_bind_policy */
+    int32_t cpus_per_core;              /* CPUTopology.CPUsPerCore() (0 ⇔ no CPU detail) */
+    int32_t cpuset_full_free_cpus;      /* CPUs of the cores whose every CPU is available (getAvailableCPUs) */
+    int32_t cpuset_free_cores;          /* cores with at least one available CPU */
 } kg_node_row;
 
 /* ------------------------------------------------------------------ */
@@ -455,7 +502,7 @@ enum kg_struct_id {
     KG_SID_RESOURCE_LIST = 0, KG_SID_CONFIG, KG_SID_CONTAINER, KG_SID_POD_SPEC,
     KG_SID_AGGREGATED_USAGE, KG_SID_POD_METRIC, KG_SID_ASSIGNED_POD, KG_SID_NODE_SPEC,
     KG_SID_CLUSTER_VIEW, KG_SID_POD_ROW, KG_SID_NODE_ROW, KG_SID_EVAL_OUT, KG_SID_NUMA_SPEC,
-    KG_SID_RESERVATION, KG_SID_QUOTA, KG_SID_RSV_RESTORED, KG_SID_COUNT
+    KG_SID_RESERVATION, KG_SID_QUOTA, KG_SID_RSV_RESTORED, KG_SID_CPU_INFO, KG_SID_COUNT
 };
 int64_t kg_struct_size(int32_t sid);
 

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 NUM_RES = 8
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
  RES_EXTENDED) = range(8)
@@ -33,7 +33,10 @@ NUMA_NONE, NUMA_BEST_EFFORT, NUMA_RESTRICTED, NUMA_SINGLE_NUMA_NODE = range(4)
 MAX_ZONES = 8
 
 POD_HAS_REQUEST, POD_DAEMONSET, POD_PROD, POD_LA_PROD_SCORE, POD_VALID = 0x1, 0x2, 0x4, 0x8, 0x80000000
-POD_NUMA_SKIP, POD_NUMA_CPU_BIND, POD_NON_PREEMPTIBLE = 0x10, 0x20, 0x40
+POD_NUMA_SKIP, POD_NUMA_CPU_BIND, POD_NON_PREEMPTIBLE, POD_NUMA_BIND_INVALID = 0x10, 0x20, 0x40, 0x100
+CPU_BIND_UNSET, CPU_BIND_DEFAULT, CPU_BIND_FULL_PCPUS, CPU_BIND_SPREAD_BY_PCPUS, CPU_BIND_CONSTRAINED_BURST = range(5)
+CPU_EXCL_UNSET, CPU_EXCL_NONE, CPU_EXCL_PCPU_LEVEL, CPU_EXCL_NUMA_NODE_LEVEL = range(4)
+NODE_CPU_BIND_NONE, NODE_CPU_BIND_FULL_PCPUS_ONLY, NODE_CPU_BIND_SPREAD_BY_PCPUS = range(3)
 NODE_VALID, NODE_HAS_METRIC, NODE_HAS_UPDATE_TIME, NODE_LA_PASS_NONPROD, NODE_LA_PASS_PROD = 0x1, 0x2, 0x4, 0x8, 0x10
 NODE_NUMA_OPTIONS, NODE_NUMA_TOPO_VALID, NODE_NUMA_TOPO_INVALID = 0x40, 0x80, 0x100
 
@@ -53,7 +56,8 @@ CONFIG = np.dtype([
     ("la_score_according_prod_usage", "<i4"), ("la_has_aggregated", "<i4"),
     ("la_agg_usage_thresholds", RESOURCE_LIST), ("la_agg_usage_type", "<i4"), ("la_agg_score_type", "<i4"),
     ("la_agg_usage_duration_ns", "<i8"), ("la_agg_score_duration_ns", "<i8"),
-    ("weight_numa", "<i4"), ("numa_strategy", "<i4"), ("numa_hint_strategy", "<i4"), ("_pad1", "<i4"),
+    ("weight_numa", "<i4"), ("numa_strategy", "<i4"), ("numa_hint_strategy", "<i4"),
+    ("numa_default_cpu_bind_policy", "<i4"),
     ("numa_resource_weight", "<i8", (NUM_RES,)),
     ("device", "<i4"), ("place_chunk", "<i4"),
     ("weight_reservation", "<i4"), ("eq_check_parent_quota", "<i4"),
@@ -64,9 +68,11 @@ CONTAINER = np.dtype([("requests", RESOURCE_LIST), ("limits", RESOURCE_LIST)], a
 POD_SPEC = np.dtype([
     ("first_container", "<i4"), ("n_containers", "<i4"), ("first_init_container", "<i4"), ("n_init_containers", "<i4"),
     ("overhead", RESOURCE_LIST), ("has_priority", "<i4"), ("priority", "<i4"), ("label_priority_class", "<i4"),
-    ("label_qos", "<i4"), ("status_qos", "<i4"), ("is_daemonset", "<i4"), ("is_terminated", "<i4"), ("_pad", "<i4"),
+    ("label_qos", "<i4"), ("status_qos", "<i4"), ("is_daemonset", "<i4"), ("is_terminated", "<i4"),
+    ("cpu_bind_required", "<i4"),
     ("name_id", "<i8"),
     ("rsv_owner_class", "<i4"), ("rsv_affinity_class", "<i4"), ("quota", "<i4"), ("non_preemptible", "<i4"),
+    ("cpu_bind_preferred", "<i4"), ("cpu_exclusive", "<i4"),
 ], align=True)
 
 AGGREGATED_USAGE = np.dtype([("duration_ns", "<i8"), ("usage", RESOURCE_LIST, (NUM_AGG_TYPES,))], align=True)
@@ -91,12 +97,16 @@ NUMA_SPEC = np.dtype([
     ("zone_total", RESOURCE_LIST, (MAX_ZONES,)), ("zone_allocated", RESOURCE_LIST, (MAX_ZONES,)),
     ("cpu_amplification_ratio", "<f8"), ("cpu_topology_valid", "<i4"), ("cpuset_cpus", "<i4"),
     ("zone_cpuset_cpus", "<i4", (MAX_ZONES,)),
+    ("node_cpu_bind_policy", "<i4"), ("max_ref_count", "<i4"), ("first_cpu", "<i4"), ("n_cpus", "<i4"),
 ], align=True)
+
+CPU_INFO = np.dtype([("socket", "<i4"), ("node", "<i4"), ("core", "<i4"), ("refcount", "<i4"), ("exclusive", "<i4"),
+                     ("reserved", "<i4")], align=True)
 
 POD_ROW = np.dtype([
     ("request", "<i8", (NUM_RES,)), ("fit_score_request", "<i8", (NUM_RES,)), ("nonzero_request", "<i8", (2,)),
     ("la_estimate", "<i8", (2,)), ("request_present", "<u4"), ("flags", "<u4"),
-    ("numa_request", "<i8", (NUM_RES,)), ("numa_request_present", "<u4"), ("_pad", "<u4"),
+    ("numa_request", "<i8", (NUM_RES,)), ("numa_request_present", "<u4"), ("cpu_bind", "<u4"),
     ("rsv_owner_class", "<i4"), ("rsv_affinity_class", "<i4"), ("quota", "<i4"), ("_pad2", "<i4"),
 ], align=True)
 
@@ -108,6 +118,7 @@ NODE_ROW = np.dtype([
     ("zone_total", "<i8", (MAX_ZONES, 2)), ("zone_allocated", "<i8", (MAX_ZONES, 2)),
     ("zone_keys", "<u4"), ("zone_alloc_keys", "<u4"), ("cpu_amplification_ratio", "<f8"),
     ("cpuset_milli", "<i8"), ("cpuset_amp_milli", "<i8"), ("zone_cpuset_amp", "<i8", (MAX_ZONES,)),
+    ("node_cpu_bind", "<i4"), ("cpus_per_core", "<i4"), ("cpuset_full_free_cpus", "<i4"), ("cpuset_free_cores", "<i4"),
 ], align=True)
 
 RESERVATION = np.dtype([
@@ -126,7 +137,7 @@ RSV_RESTORED = np.dtype([
 ], align=True)
 
 STRUCT_IDS = [RESOURCE_LIST, CONFIG, CONTAINER, POD_SPEC, AGGREGATED_USAGE, POD_METRIC, ASSIGNED_POD, NODE_SPEC,
-              None, POD_ROW, NODE_ROW, None, NUMA_SPEC, RESERVATION, QUOTA, RSV_RESTORED]
+              None, POD_ROW, NODE_ROW, None, NUMA_SPEC, RESERVATION, QUOTA, RSV_RESTORED, CPU_INFO]
 
 
 class ClusterView(ctypes.Structure):
@@ -140,6 +151,7 @@ class ClusterView(ctypes.Structure):
         ("numa", ctypes.c_void_p), ("n_numa", ctypes.c_int32), ("_p6", ctypes.c_int32),
         ("reservations", ctypes.c_void_p), ("n_reservations", ctypes.c_int32), ("_p7", ctypes.c_int32),
         ("quotas", ctypes.c_void_p), ("n_quotas", ctypes.c_int32), ("_p8", ctypes.c_int32),
+        ("cpus", ctypes.c_void_p), ("n_cpus", ctypes.c_int32), ("_p9", ctypes.c_int32),
     ]
 
 
@@ -158,23 +170,25 @@ def ptr(a) -> ctypes.c_void_p:
 
 
 def make_view(pods, containers, nodes, aggregated, pod_metrics, assigned, numa=None, reservations=None,
-              quotas=None) -> ClusterView:
+              quotas=None, cpus=None) -> ClusterView:
     if numa is None:
         numa = np.zeros(0, dtype=NUMA_SPEC)
     if reservations is None:
         reservations = np.zeros(0, dtype=RESERVATION)
     if quotas is None:
         quotas = np.zeros(0, dtype=QUOTA)
+    if cpus is None:
+        cpus = np.zeros(0, dtype=CPU_INFO)
     v = ClusterView()
     for name, arr in (("pods", pods), ("containers", containers), ("nodes", nodes), ("aggregated", aggregated),
                       ("pod_metrics", pod_metrics), ("assigned", assigned), ("numa", numa),
-                      ("reservations", reservations), ("quotas", quotas)):
+                      ("reservations", reservations), ("quotas", quotas), ("cpus", cpus)):
         assert arr.flags["C_CONTIGUOUS"]
         setattr(v, name, arr.ctypes.data if len(arr) else 0)
     v.n_pods, v.n_containers, v.n_nodes = len(pods), len(containers), len(nodes)
     v.n_aggregated, v.n_pod_metrics, v.n_assigned = len(aggregated), len(pod_metrics), len(assigned)
-    v.n_numa, v.n_reservations, v.n_quotas = len(numa), len(reservations), len(quotas)
-    v._keep = (pods, containers, nodes, aggregated, pod_metrics, assigned, numa, reservations, quotas)
+    v.n_numa, v.n_reservations, v.n_quotas, v.n_cpus = len(numa), len(reservations), len(quotas), len(cpus)
+    v._keep = (pods, containers, nodes, aggregated, pod_metrics, assigned, numa, reservations, quotas, cpus)
     return v
 
 

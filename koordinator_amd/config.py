@@ -40,6 +40,7 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
                 aggregated: Optional[dict] = None,
                 weight_numa: int = 1, numa_strategy: str = "LeastAllocated",
                 numa_hint_strategy: str = "LeastAllocated", numa_resources: Optional[Dict[str, int]] = None,
+                numa_default_cpu_bind_policy: str = "FullPCPUs",
                 weight_reservation: int = 1, device: int = 0, place_chunk: int = 8) -> np.ndarray:
     c = np.zeros((), dtype=nat.CONFIG)
     c["abi_version"] = nat.ABI_VERSION
@@ -81,6 +82,10 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
     c["weight_numa"] = weight_numa
     c["numa_strategy"] = strategies[numa_strategy]
     c["numa_hint_strategy"] = strategies[numa_hint_strategy]
+    # NodeNUMAResourceArgs.DefaultCPUBindPolicy (v1beta2 defaults.go:50)
+    c["numa_default_cpu_bind_policy"] = {"": nat.CPU_BIND_UNSET, "FullPCPUs": nat.CPU_BIND_FULL_PCPUS,
+                                         "SpreadByPCPUs": nat.CPU_BIND_SPREAD_BY_PCPUS,
+                                         "ConstrainedBurst": nat.CPU_BIND_CONSTRAINED_BURST}[numa_default_cpu_bind_policy]
     for k, w in (numa_resources or {"cpu": 1, "memory": 1}).items():
         c["numa_resource_weight"][RES[k]] = w
     c["weight_reservation"] = weight_reservation  # profile weight (the shipped profile: 5000)

@@ -19,6 +19,7 @@
 // KGD_SLOW and take the exact int64 path (kg_pair_exact).  MostAllocated is the same with
 // F = RN(100*base/cap + 2^-42), q = min(q, 100).
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #include "../../include/koord_gpu.h"
@@ -66,7 +67,7 @@ struct kg_pod_dev {
     uint32_t fit_magic;          // ceil(2^31 / W) for W = Σ weight over fit_mask: s / W = umulhi(2s, magic)
     uint32_t fit_w;              // W
     uint32_t request_present;
-    uint32_t _pad;
+    uint32_t cpu_bind;           // kg_pod_row.cpu_bind: required | preferred << 4 | exclusive << 8
     int64_t nonzero[2];
     int64_t la_est_i[2];
     int64_t numa_req[KG_NUM_RES];// NodeNUMAResource PreFilter requests (PodRequestsAndLimits)
@@ -399,14 +400,15 @@ KG_HD uint32_t kg_numa_score_zones(const kg_consts &c, bool most, const int64_t 
 
 // the same over the node's Requested / Allocatable (policy None, or nothing allocated in zones)
 // `amplified`: scoreWithAmplifiedCPUs (scoring.go:99-116), the node's cpuset CPUs counted amplified
+// `pod_cpu` ≥ 0 replaces the pod's cpu request (a cpuset-bound pod's amplified request, plugin.go:458-462)
 KG_HD uint32_t kg_numa_score_node(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p,
-                                  bool amplified = false, const int64_t *requested = nullptr) {
+                                  bool amplified = false, const int64_t *requested = nullptr, int64_t pod_cpu = -1) {
     if (!requested) requested = row.requested;
     int64_t s = 0, w = 0;
     for (int r = 0; r < KG_NUM_RES; r++) {
         if (c.numa_w[r] <= 0) continue;
         const bool scalar = (KG_SCALAR_RES_MASK >> r) & 1u;
-        const int64_t pr = p.numa_req[r];
+        const int64_t pr = (r == KG_RES_CPU && pod_cpu >= 0) ? pod_cpu : p.numa_req[r];
         if (scalar && (pr == 0 || !((row.alloc_present >> r) & 1u))) continue;
         const int64_t a = row.alloc[r];
         if (a == 0) continue;
@@ -625,13 +627,28 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
     o.score = 0;
     o.n_alloc = 0;
     if (p.flags & KG_POD_NUMA_SKIP) return;
+    if (p.flags & KG_POD_NUMA_BIND_INVALID) {   // PreFilter: cpuset request not in whole cores
+        o.feasible = false;
+        return;
+    }
     const bool opts = (row.flags & KG_NODE_NUMA_OPTIONS) != 0;
     const int policy = opts ? row.numa_policy : KG_NUMA_NONE;
-    // filterAmplifiedCPUs (plugin.go:340-373) for a pod without cpuset binding
     const double ratio = opts ? row.cpu_amplification_ratio : 0.0;
     const int64_t pcpu = p.numa_req[KG_RES_CPU];
+    // requestCPUBind (util.go:105-122): the pod's own decision, or a node CPU bind policy for any cpu request
+    bool bind = (p.flags & KG_POD_NUMA_CPU_BIND) != 0;
+    const int node_bind = opts ? row.node_cpu_bind : KG_NODE_CPU_BIND_NONE;
+    if (!bind && pcpu != 0 && node_bind != KG_NODE_CPU_BIND_NONE) {
+        if (pcpu % 1000 != 0) {   // ErrInvalidRequestedCPUs
+            o.feasible = false;
+            return;
+        }
+        bind = true;
+    }
     const bool amplified = pcpu != 0 && ratio > 1.0;
-    if (amplified && !reserve) {
+    // a cpuset-bound pod's cpu request is amplified (plugin.go:354-356, getResourceOptions :458-462)
+    const int64_t pcpu_eff = bind && amplified ? (int64_t)ceil((double)pcpu * ratio) : pcpu;
+    if (amplified && !reserve) {   // filterAmplifiedCPUs (plugin.go:340-373)
         if (row.flags & KG_NODE_NUMA_TOPO_INVALID) {   // GetAvailableCPUs: invalid CPU topology
             o.feasible = false;
             return;
@@ -639,13 +656,43 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
         int64_t rq = requested[KG_RES_CPU];
         const int64_t am = row.cpuset_milli;
         if (rq >= am && am > 0) rq += row.cpuset_amp_milli - am;
-        if (pcpu > row.alloc[KG_RES_CPU] - rq) {
+        if (pcpu_eff > row.alloc[KG_RES_CPU] - rq) {
             o.feasible = false;
             return;
         }
     }
+    if (bind && !reserve) {   // Filter's cpuset branch (plugin.go:297-331)
+        if (!(row.flags & KG_NODE_NUMA_TOPO_VALID)) {   // ErrInvalidCPUTopology (nil or invalid)
+            o.feasible = false;
+            return;
+        }
+        const int own = (int)(p.cpu_bind & 15u);
+        int required = own;
+        if (node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) required = KG_CPU_BIND_FULL_PCPUS;
+        else if (node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) required = KG_CPU_BIND_SPREAD_BY_PCPUS;
+        const int64_t ncpus = pcpu / 1000;   // numCPUsNeeded
+        if ((own != KG_CPU_BIND_UNSET && own != required) ||   // ErrCPUBindPolicyConflict
+            (required == KG_CPU_BIND_FULL_PCPUS && (row.cpus_per_core <= 0 || ncpus % row.cpus_per_core != 0))) {
+            o.feasible = false;   // (or ErrSMTAlignmentError)
+            return;
+        }
+        // Allocate without a NUMA hint: available CPUs after the required policy's filter (whole free cores /
+        // one CPU per core), then takeCPUs, which succeeds whenever they are enough
+        if (required != KG_CPU_BIND_UNSET && policy == KG_NUMA_NONE) {
+            const int64_t avail = required == KG_CPU_BIND_FULL_PCPUS ? row.cpuset_full_free_cpus
+                                : required == KG_CPU_BIND_SPREAD_BY_PCPUS ? row.cpuset_free_cores : 0;
+            if (avail < ncpus) {
+                o.feasible = false;
+                return;
+            }
+        }
+    }
     if (policy == KG_NUMA_NONE) {
-        o.score = kg_numa_score_node(c, row, p, amplified, requested);
+        o.score = kg_numa_score_node(c, row, p, amplified, requested, pcpu_eff);
+        return;
+    }
+    if (bind) {   // a cpuset on a node with a NUMA topology policy: refused at kg_pods_set / upsert
+        o.feasible = false;
         return;
     }
     const int Z = row.n_zones;

@@ -1677,6 +1677,12 @@ struct kg_engine {
     // entry point but kg_snapshot_reset then fails with KG_ERR_STATE until the snapshot is reloaded
     uint64_t generation = 0;
     bool stale = false;
+    // cpuset binding (matrix mode on nodes without a NUMA topology policy): per-node facts of the host rows
+    // pushed by upsert, and whether the pod batch binds cpusets (KG_POD_NUMA_CPU_BIND)
+    std::vector<uint8_t> node_bind_facts;   // bit 0: NUMA topology policy; bit 1: node CPU bind policy;
+                                            // bit 2: valid CPU topology without CPU detail
+    int64_t n_numa_policy_nodes = 0, n_node_bind_nodes = 0, n_no_detail_nodes = 0;
+    bool batch_bind = false;
     bool profiling = false;
     // Reservation / ElasticQuota (config 5)
     void *rsv_mem = nullptr;            // slots | rfirst | rnode | E | O
@@ -2097,6 +2103,27 @@ RsvArgs rsv_args(const kg_engine *e) {
     return ra;
 }
 
+// Cpuset binding (NodeNUMAResource for LSE / LSR pods, or any cpu request on a node with a CPU bind policy)
+// is answered in matrix mode on nodes without a NUMA topology policy, where the Filter's Allocate reduces to
+// counts of free CPUs; the cpuset a Reserve takes (the CPU accumulator), cpusets on NUMA-policy nodes and
+// reservation-reserved cpusets are refused explicitly instead of being answered wrongly.
+kg_status bind_ready(kg_engine *e, bool placement) {
+    if (!(e->cfg.enabled_plugins & KG_PLUGIN_NUMA)) return KG_OK;
+    const bool any_bind = e->batch_bind || e->n_node_bind_nodes > 0;
+    if (placement && any_bind)
+        return set_err(e, KG_ERR_UNSUPPORTED,
+                       "cpuset allocation at Reserve (the CPU accumulator) is not on the engine path; evaluate "
+                       "cpuset-bound pods in matrix mode (kg_eval)");
+    if (e->batch_bind && (e->n_numa_policy_nodes > 0 || e->n_no_detail_nodes > 0))
+        return set_err(e, KG_ERR_UNSUPPORTED,
+                       "cpuset-bound pods need every node without a NUMA topology policy and with CPU detail "
+                       "(%lld NUMA-policy nodes, %lld without detail)",
+                       (long long)e->n_numa_policy_nodes, (long long)e->n_no_detail_nodes);
+    if (any_bind && (e->cfg.enabled_plugins & KG_PLUGIN_RESERVATION))
+        return set_err(e, KG_ERR_UNSUPPORTED, "cpuset binding with Reservation (reserved cpusets) is not on the engine path");
+    return KG_OK;
+}
+
 kg_status quota_ready(kg_engine *e) {
     if (!(e->consts.plugins & KG_PLUGIN_ELASTICQUOTA)) return KG_OK;
     if (e->max_pod_quota >= e->n_quota)
@@ -2250,6 +2277,8 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
     e->rsv_perm.clear();
     e->pl.cap = cap;
     e->n_nodes = n_nodes;
+    e->node_bind_facts.assign((size_t)n_nodes, 0);
+    e->n_numa_policy_nodes = e->n_node_bind_nodes = e->n_no_detail_nodes = 0;
     e->shard_begin = 0;
     e->shard_end = n_nodes;
     hipLaunchKernelGGL(k_finalize_range, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, e->stream, e->consts, e->pl,
@@ -2276,6 +2305,28 @@ kg_status kg_snapshot_upsert(kg_engine *e, const int32_t *node_index, const kg_n
     if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised (kg_snapshot_reset)");
     for (int32_t k = 0; k < n; k++)
         if (node_index[k] < 0 || node_index[k] >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "node index %d out of range", node_index[k]);
+    // cpuset-binding facts of the rows (bind_ready); a node CPU bind policy turns every cpu request into a
+    // cpuset request there, so it needs CPU detail and no NUMA topology policy
+    std::vector<uint8_t> facts((size_t)n);
+    for (int32_t k = 0; k < n; k++) {
+        const kg_node_row &r = rows[k];
+        const bool opts = (r.flags & KG_NODE_NUMA_OPTIONS) != 0;
+        uint8_t f = 0;
+        if (opts && r.numa_policy != KG_NUMA_NONE) f |= 1;
+        if (opts && r.node_cpu_bind != KG_NODE_CPU_BIND_NONE) f |= 2;
+        if ((r.flags & KG_NODE_NUMA_TOPO_VALID) && r.cpus_per_core <= 0) f |= 4;
+        if ((f & 2) && (f & 5))
+            return set_err(e, KG_ERR_UNSUPPORTED, "node %d: a CPU bind policy with a NUMA topology policy or without CPU detail",
+                           node_index[k]);
+        facts[k] = f;
+    }
+    for (int32_t k = 0; k < n; k++) {
+        uint8_t &old = e->node_bind_facts[node_index[k]];
+        e->n_numa_policy_nodes += (int)(facts[k] & 1) - (int)(old & 1);
+        e->n_node_bind_nodes += (int)((facts[k] >> 1) & 1) - (int)((old >> 1) & 1);
+        e->n_no_detail_nodes += (int)((facts[k] >> 2) & 1) - (int)((old >> 2) & 1);
+        old = facts[k];
+    }
     const size_t rb = sizeof(kg_node_row) * (size_t)n, ib = sizeof(int32_t) * (size_t)n;
     st = ensure_scratch(e, rb + ib + 256);
     if (st) return st;
@@ -2327,14 +2378,13 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     if (n < 0 || (n > 0 && !rows)) return set_err(e, KG_ERR_INVALID_ARG, "bad pod batch");
     std::vector<kg_pod_dev> dev((size_t)n);
     BatchMasks bm{0, 0};
-    bool la_prod = false, pow2 = true;
+    bool la_prod = false, pow2 = true, batch_bind = false;
     uint32_t need = 0;
     int32_t max_quota = -1;
     for (int32_t i = 0; i < n; i++) {
         if (!kg_pod_row_in_bounds(rows[i])) return set_err(e, KG_ERR_RANGE, "pod %d: request outside the engine bounds", i);
         if ((e->cfg.enabled_plugins & KG_PLUGIN_NUMA) && !(rows[i].flags & KG_POD_NUMA_SKIP)) {
-            if (rows[i].flags & KG_POD_NUMA_CPU_BIND)
-                return set_err(e, KG_ERR_UNSUPPORTED, "pod %d: NodeNUMAResource cpuset binding is not on the engine path", i);
+            if (rows[i].flags & KG_POD_NUMA_CPU_BIND) batch_bind = true;
             if (kg_numa_list_count(rows[i]) > KG_NUMA_MAX_LISTS)
                 return set_err(e, KG_ERR_UNSUPPORTED, "pod %d: more than %d NUMA hint lists", i, KG_NUMA_MAX_LISTS);
         }
@@ -2416,12 +2466,15 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     e->la_prod = la_prod;
     e->pow2 = pow2;
     e->pod_rows_h.assign(rows, rows + n);
+    e->batch_bind = batch_bind;
     cls_prepare(e);
     return KG_OK;
 }
 
 kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     kg_status st = check_engine(e);
+    if (st) return st;
+    st = bind_ready(e, false);
     if (st) return st;
     if (!out) return set_err(e, KG_ERR_INVALID_ARG, "null output");
     if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised");
@@ -2528,6 +2581,8 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
 kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev) {
     kg_status st = check_engine(e);
     if (st) return st;
+    st = bind_ready(e, true);
+    if (st) return st;
     if (pod_begin < 0 || n < 0 || pod_begin + (int64_t)n > e->n_pods || (n > 0 && !partial_dev))
         return set_err(e, KG_ERR_RANGE, "bad chunk");
     // the top-k kernel writes every slot of every tile of its shard; the NUMA kernel merges with atomics
@@ -2549,6 +2604,8 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
 kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, const uint32_t *partial_dev,
                                  int32_t *out_node_dev, int64_t *out_score_dev) {
     kg_status st = check_engine(e);
+    if (st) return st;
+    st = bind_ready(e, true);
     if (st) return st;
     if (pod_begin < 0 || n < 0 || n > KG_MAX_CHUNK || pod_begin + (int64_t)n > e->n_pods)
         return set_err(e, KG_ERR_RANGE, "bad chunk");
@@ -2733,6 +2790,8 @@ kg_status kg_commit(kg_engine *e, int32_t pod, int32_t node) {
     kg_status st = check_engine(e);
     if (st) return st;
     if (pod < 0 || pod >= e->n_pods || node < 0 || node >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "bad commit");
+    st = bind_ready(e, true);
+    if (st) return st;
     st = quota_ready(e);   // the pod's quota group must exist before its usage is committed
     if (st) return st;
     hipLaunchKernelGGL(k_commit_one, dim3(1), dim3(1), 0, e->stream, e->consts, e->pl, e->pods, pod, node, rsv_args(e));

@@ -335,6 +335,7 @@ int64_t kg_struct_size(int32_t sid) {
         case KG_SID_RESERVATION: return sizeof(kg_reservation);
         case KG_SID_QUOTA: return sizeof(kg_quota);
         case KG_SID_RSV_RESTORED: return sizeof(kg_rsv_restored);
+        case KG_SID_CPU_INFO: return sizeof(kg_cpu_info);
     }
     return -1;
 }
@@ -362,6 +363,7 @@ void kg_config_default(kg_config *c) {
     c->weight_numa = 1;
     c->numa_strategy = KG_STRATEGY_LEAST_ALLOCATED;
     c->numa_hint_strategy = KG_STRATEGY_LEAST_ALLOCATED;
+    c->numa_default_cpu_bind_policy = KG_CPU_BIND_FULL_PCPUS;   // v1beta2 defaults.go:50
     c->numa_resource_weight[KG_RES_CPU] = 1;
     c->numa_resource_weight[KG_RES_MEMORY] = 1;
     c->place_chunk = 8;
@@ -402,6 +404,10 @@ kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
     if ((c->enabled_plugins & KG_PLUGIN_NUMA) && nw == 0) return fail("NodeNUMAResource needs scoringStrategy resources");
     if (c->numa_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->numa_strategy != KG_STRATEGY_MOST_ALLOCATED)
         return fail("unsupported NodeNUMAResource scoring strategy");
+    if (c->numa_default_cpu_bind_policy != KG_CPU_BIND_UNSET && c->numa_default_cpu_bind_policy != KG_CPU_BIND_FULL_PCPUS &&
+        c->numa_default_cpu_bind_policy != KG_CPU_BIND_SPREAD_BY_PCPUS &&
+        c->numa_default_cpu_bind_policy != KG_CPU_BIND_CONSTRAINED_BURST)
+        return fail("unsupported NodeNUMAResource defaultCPUBindPolicy");
     if (c->numa_hint_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->numa_hint_strategy != KG_STRATEGY_MOST_ALLOCATED)
         return fail("unsupported NodeNUMAResource NUMA scoring strategy");
     if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && lw == 0) return fail("LoadAwareScheduling needs resourceWeights");
@@ -475,10 +481,30 @@ kg_status kg_build_pod_rows(const kg_config *cfg, const kg_cluster_view *view, c
             if (all_zero) row.flags |= KG_POD_NUMA_SKIP;
         }
         const int pc = priority_class_of(pv);
-        // AllowUseCPUSet (util.go:43-50): raw QoS label LSE/LSR and koord-prod; the default bind policy
-        // FullPCPUs (defaults.go:50) then asks for a cpuset whenever cpu is requested
-        if ((pv.p.label_qos == KG_QOS_LSE || pv.p.label_qos == KG_QOS_LSR) && pc == KG_PRIO_PROD && row.numa_request[KG_RES_CPU] > 0)
-            row.flags |= KG_POD_NUMA_CPU_BIND;
+        // PreFilter's cpuset decision (plugin.go:232-262) for AllowUseCPUSet pods (util.go:43-50: raw QoS
+        // label LSE / LSR and koord-prod): the preferred policy falls back to DefaultCPUBindPolicy when
+        // unset or Default, a required Default means DefaultCPUBindPolicy, and a required policy wins
+        if (!(row.flags & KG_POD_NUMA_SKIP) && (pv.p.label_qos == KG_QOS_LSE || pv.p.label_qos == KG_QOS_LSR) &&
+            pc == KG_PRIO_PROD) {
+            const int32_t dflt = cfg->numa_default_cpu_bind_policy;
+            int32_t bind = pv.p.cpu_bind_preferred;
+            if (bind == KG_CPU_BIND_UNSET || bind == KG_CPU_BIND_DEFAULT) bind = dflt;
+            int32_t required = pv.p.cpu_bind_required;
+            if (required == KG_CPU_BIND_DEFAULT) required = dflt;
+            if (required != KG_CPU_BIND_UNSET) bind = required;
+            if (required < 0 || required > KG_CPU_BIND_CONSTRAINED_BURST || bind < 0 || bind > KG_CPU_BIND_CONSTRAINED_BURST ||
+                pv.p.cpu_exclusive < 0 || pv.p.cpu_exclusive > KG_CPU_EXCL_NUMA_NODE_LEVEL)
+                return KG_ERR_INVALID_ARG;
+            const int64_t cpu = row.numa_request[KG_RES_CPU];
+            if (bind == KG_CPU_BIND_FULL_PCPUS || bind == KG_CPU_BIND_SPREAD_BY_PCPUS) {
+                if (cpu % 1000 != 0) {
+                    row.flags |= KG_POD_NUMA_BIND_INVALID;   // ErrInvalidRequestedCPUs
+                } else if (cpu > 0) {
+                    row.flags |= KG_POD_NUMA_CPU_BIND;
+                    row.cpu_bind = (uint32_t)required | (uint32_t)bind << 4 | (uint32_t)pv.p.cpu_exclusive << 8;
+                }
+            }
+        }
         if (pc == KG_PRIO_PROD) row.flags |= KG_POD_PROD;
         if (pc == KG_PRIO_PROD && cfg->la_score_according_prod_usage) row.flags |= KG_POD_LA_PROD_SCORE;
         if (pv.p.is_daemonset) row.flags |= KG_POD_DAEMONSET;
@@ -570,6 +596,40 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
                     return KG_ERR_INVALID_ARG;
                 row.zone_cpuset_amp[z] = amplify((int64_t)zc * 1000) - (int64_t)zc * 1000;
             }
+            // cpuset binding inputs: the node's CPU bind policy and, from the logical CPUs, the counts the
+            // Filter's Allocate reduces to on a node without a NUMA topology policy
+            if (nm.node_cpu_bind_policy < KG_NODE_CPU_BIND_NONE || nm.node_cpu_bind_policy > KG_NODE_CPU_BIND_SPREAD_BY_PCPUS ||
+                nm.n_cpus < 0 || nm.max_ref_count < 0)
+                return KG_ERR_INVALID_ARG;
+            row.node_cpu_bind = nm.node_cpu_bind_policy;
+            if (nm.n_cpus > 0) {
+                if (nm.first_cpu < 0 || nm.first_cpu + (int64_t)nm.n_cpus > view->n_cpus || !view->cpus) return KG_ERR_RANGE;
+                if (nm.n_cpus > KG_MAX_NODE_CPUS) return KG_ERR_UNSUPPORTED;
+                const kg_cpu_info *ci = view->cpus + nm.first_cpu;
+                const int32_t max_ref = nm.max_ref_count > 0 ? nm.max_ref_count : 1;
+                // compact core ids (cores are few; ids may be sparse, e.g. socket << 16 | core)
+                int32_t core_id[KG_MAX_NODE_CPUS], core_total[KG_MAX_NODE_CPUS], core_avail[KG_MAX_NODE_CPUS];
+                int32_t ncores = 0, nalloc = 0;
+                for (int32_t c = 0; c < nm.n_cpus; c++) {
+                    int32_t k = 0;
+                    while (k < ncores && core_id[k] != ci[c].core) k++;
+                    if (k == ncores) {
+                        core_id[ncores] = ci[c].core;
+                        core_total[ncores] = core_avail[ncores] = 0;
+                        ncores++;
+                    }
+                    core_total[k]++;
+                    // getAvailableCPUs (node_allocation.go:134-155): allocated = refcount ≥ maxRefCount; reserved out
+                    if (!(ci[c].refcount > 0 && ci[c].refcount >= max_ref) && !ci[c].reserved) core_avail[k]++;
+                    if (ci[c].refcount > 0) nalloc++;
+                }
+                row.cpus_per_core = nm.n_cpus / ncores;
+                for (int32_t k = 0; k < ncores; k++) {
+                    if (core_avail[k] == row.cpus_per_core) row.cpuset_full_free_cpus += core_avail[k];
+                    if (core_avail[k] > 0) row.cpuset_free_cores++;
+                }
+                if (nalloc != nm.cpuset_cpus) return KG_ERR_INVALID_ARG;   // the count fields must agree
+            }
             row.numa_policy = nm.policy;
             row.n_zones = nm.n_zones;
             row.cpu_amplification_ratio = nm.cpu_amplification_ratio;
@@ -593,8 +653,24 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
     return KG_OK;
 }
 
+// whether NodeNUMAResource binds a cpuset for the pair (requestCPUBind, util.go:105-122), and whether the
+// engine answers it (a node without a NUMA topology policy, with CPU detail when the topology is valid)
+static bool row_binds(const kg_config &cfg, const kg_node_row &node, const kg_pod_row &pod, bool &answered) {
+    answered = true;
+    if (!(cfg.enabled_plugins & KG_PLUGIN_NUMA) || (pod.flags & KG_POD_NUMA_SKIP)) return false;
+    const bool opts = (node.flags & KG_NODE_NUMA_OPTIONS) != 0;
+    const bool bind = (pod.flags & KG_POD_NUMA_CPU_BIND) ||
+                      (opts && node.node_cpu_bind != KG_NODE_CPU_BIND_NONE && pod.numa_request[KG_RES_CPU] != 0);
+    if (bind)
+        answered = !(opts && node.numa_policy != KG_NUMA_NONE) &&
+                   !((node.flags & KG_NODE_NUMA_TOPO_VALID) && node.cpus_per_core <= 0);
+    return bind;
+}
+
 kg_status kg_row_commit(const kg_config *cfg, kg_node_row *node, const kg_pod_row *pod) {
     if (!cfg || !node || !pod) return KG_ERR_INVALID_ARG;
+    bool answered;
+    if (row_binds(*cfg, *node, *pod, answered)) return KG_ERR_UNSUPPORTED;   // Reserve takes a cpuset
     kg_pod_dev pd;
     kg_pod_dev_from_row(*cfg, *pod, pd);
     kg_consts k;
@@ -607,6 +683,8 @@ kg_status kg_row_commit(const kg_config *cfg, kg_node_row *node, const kg_pod_ro
 kg_status kg_row_eval(const kg_config *cfg, const kg_node_row *node, const kg_pod_row *pod, int64_t now_ns,
                       int32_t *feasible, int32_t *fit_score, int32_t *la_score, int32_t *numa_score) {
     if (!cfg || !node || !pod || !feasible) return KG_ERR_INVALID_ARG;
+    bool answered;
+    if (row_binds(*cfg, *node, *pod, answered) && !answered) return KG_ERR_UNSUPPORTED;
     kg_consts k;
     kg_consts_from_config(*cfg, k);
     kg_pod_dev pd;
@@ -752,6 +830,7 @@ void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &
     d.la_est_i[1] = row.la_estimate[1];
     for (int r = 0; r < KG_NUM_RES; r++) d.numa_req[r] = row.numa_request[r];
     d.numa_present = row.numa_request_present;
+    d.cpu_bind = row.cpu_bind;
     d.rsv_owner = row.rsv_owner_class;
     d.rsv_aff = row.rsv_affinity_class;
     d.quota = (c.enabled_plugins & KG_PLUGIN_ELASTICQUOTA) ? row.quota : -1;

@@ -100,6 +100,10 @@ class Pod:
     priority: Optional[int] = None
     labels: Dict[str, str] = dataclasses.field(default_factory=dict)
     qos_status: str = ""
+    # annotation scheduling.koordinator.sh/resource-spec (ResourceSpec)
+    cpu_bind_required: str = ""
+    cpu_bind_preferred: str = ""
+    cpu_exclusive: str = ""
     daemonset: bool = False
     terminated: bool = False
     node_name: str = ""
@@ -129,13 +133,28 @@ class Node:
     cpu_topology_valid: bool = True          # CPUTopology.IsValid() of the NodeResourceTopology (nil without zones)
     cpuset_cpus: int = 0                     # CPUs held by cpuset pods (NodeAllocation.allocatedCPUs)
     zone_cpuset_cpus: Optional[Dict[int, int]] = None   # those CPUs by zone id
+    # cpuset binding: label node.koordinator.sh/cpu-bind-policy ("", "None", "FullPCPUsOnly", "SpreadByPCPUs"),
+    # the reported CPU topology as (socket, NUMA node, core) per cpu id, the node allocation's cpus
+    # {cpu: (refcount, exclusive policy)}, TopologyOptions.ReservedCPUs and MaxRefCount; with cpu_detail the
+    # counts above are derived from it
+    cpu_bind_policy: str = ""
+    cpu_detail: Optional[List[tuple]] = None
+    cpu_allocated: Optional[Dict[int, tuple]] = None
+    reserved_cpus: Sequence[int] = ()
+    max_ref_count: int = 1
 
 
 NUMA_POLICY = {"": nat.NUMA_NONE, "BestEffort": nat.NUMA_BEST_EFFORT, "Restricted": nat.NUMA_RESTRICTED,
                "SingleNUMANode": nat.NUMA_SINGLE_NUMA_NODE}
+CPU_BIND = {"": nat.CPU_BIND_UNSET, "Default": nat.CPU_BIND_DEFAULT, "FullPCPUs": nat.CPU_BIND_FULL_PCPUS,
+            "SpreadByPCPUs": nat.CPU_BIND_SPREAD_BY_PCPUS, "ConstrainedBurst": nat.CPU_BIND_CONSTRAINED_BURST}
+CPU_EXCLUSIVE = {"": nat.CPU_EXCL_UNSET, "None": nat.CPU_EXCL_NONE, "PCPULevel": nat.CPU_EXCL_PCPU_LEVEL,
+                 "NUMANodeLevel": nat.CPU_EXCL_NUMA_NODE_LEVEL}
+NODE_CPU_BIND = {"": nat.NODE_CPU_BIND_NONE, "None": nat.NODE_CPU_BIND_NONE,
+                 "FullPCPUsOnly": nat.NODE_CPU_BIND_FULL_PCPUS_ONLY, "SpreadByPCPUs": nat.NODE_CPU_BIND_SPREAD_BY_PCPUS}
 
 
-def numa_spec_record(n: "Node") -> np.ndarray:
+def numa_spec_record(n: "Node", cpus: Optional[list] = None) -> np.ndarray:
     rec = np.zeros((), dtype=nat.NUMA_SPEC)
     rec["policy"] = NUMA_POLICY[n.numa_policy]
     zones = n.numa_zones or []
@@ -148,10 +167,28 @@ def numa_spec_record(n: "Node") -> np.ndarray:
             rec["zone_allocated"][z] = resource_list(n.numa_allocated[zid])
     rec["cpu_amplification_ratio"] = n.cpu_amplification_ratio
     # no NodeResourceTopology (a node with only the amplification annotation): CPUTopology is nil
-    rec["cpu_topology_valid"] = -1 if n.numa_zones is None else int(n.cpu_topology_valid)
+    rec["cpu_topology_valid"] = -1 if n.numa_zones is None and n.cpu_detail is None else int(n.cpu_topology_valid)
     rec["cpuset_cpus"] = n.cpuset_cpus
     for z, zid in enumerate(ids):
         rec["zone_cpuset_cpus"][z] = (n.zone_cpuset_cpus or {}).get(zid, 0)
+    rec["node_cpu_bind_policy"] = NODE_CPU_BIND[n.cpu_bind_policy]
+    rec["max_ref_count"] = n.max_ref_count
+    if n.cpu_detail is not None and cpus is not None:
+        alloc = n.cpu_allocated or {}
+        rec["first_cpu"], rec["n_cpus"] = len(cpus), len(n.cpu_detail)
+        reserved = set(n.reserved_cpus)
+        for c, (sk, nd, co) in enumerate(n.cpu_detail):
+            ci = np.zeros((), dtype=nat.CPU_INFO)
+            ci["socket"], ci["node"], ci["core"] = sk, nd, co
+            ref, ex = alloc.get(c, (0, ""))
+            ci["refcount"], ci["exclusive"] = ref, CPU_EXCLUSIVE[ex] if ref > 0 else 0
+            ci["reserved"] = int(c in reserved)
+            cpus.append(ci)
+        # the node allocation's counts follow from the detail (allocatedCPUs, CPUsInNUMANodes)
+        held = [c for c in alloc if alloc[c][0] > 0]
+        rec["cpuset_cpus"] = len(held)
+        for z, zid in enumerate(ids):
+            rec["zone_cpuset_cpus"][z] = sum(1 for c in held if n.cpu_detail[c][1] == zid)
     return rec
 
 
@@ -298,9 +335,10 @@ class Cluster:
                 fv.assigned.append(rec)
             ns["n_assigned"] = len(self.assigned.get(n.name, []))
             ns["numa"] = -1
-            if n.numa_zones is not None or n.cpu_amplification_ratio > 1:
+            if (n.numa_zones is not None or n.cpu_amplification_ratio > 1 or n.cpu_detail is not None
+                    or NODE_CPU_BIND[n.cpu_bind_policy] != nat.NODE_CPU_BIND_NONE):
                 ns["numa"] = len(fv.numa)
-                fv.numa.append(numa_spec_record(n))
+                fv.numa.append(numa_spec_record(n, fv.cpus))
         fv.nodes = nodes
         return fv.finish()
 
@@ -335,6 +373,9 @@ def pod_spec_record(p: Pod, containers: list, name_id: int) -> np.ndarray:
     rec["status_qos"] = KUBE_QOS[p.qos_status]
     rec["is_daemonset"] = int(p.daemonset)
     rec["is_terminated"] = int(p.terminated)
+    rec["cpu_bind_required"] = CPU_BIND[p.cpu_bind_required]
+    rec["cpu_bind_preferred"] = CPU_BIND[p.cpu_bind_preferred]
+    rec["cpu_exclusive"] = CPU_EXCLUSIVE[p.cpu_exclusive]
     rec["name_id"] = name_id
     rec["rsv_owner_class"] = getattr(p, "rsv_owner_class", -1)
     rec["rsv_affinity_class"] = getattr(p, "rsv_affinity_class", -1)
@@ -371,6 +412,7 @@ class FlatView:
         self.pod_metrics: List[np.ndarray] = []
         self.assigned: List[np.ndarray] = []
         self.numa: List[np.ndarray] = []
+        self.cpus: List[np.ndarray] = []
         self.nodes = None
 
     def pod_index(self, p: Pod) -> int:
@@ -391,8 +433,9 @@ class FlatView:
         self.pod_metrics_arr = _stack(self.pod_metrics, nat.POD_METRIC)
         self.assigned_arr = _stack(self.assigned, nat.ASSIGNED_POD)
         self.numa_arr = _stack(self.numa, nat.NUMA_SPEC)
+        self.cpu_arr = _stack(self.cpus, nat.CPU_INFO)
         self.c_view = nat.make_view(self.pods, self.containers, self.nodes, self.aggregated_arr, self.pod_metrics_arr,
-                                    self.assigned_arr, self.numa_arr)
+                                    self.assigned_arr, self.numa_arr, cpus=self.cpu_arr)
         return self
 
     def add_pods(self, pods: Sequence[Pod]) -> List[int]:

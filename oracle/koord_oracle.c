@@ -917,6 +917,52 @@ static int numa_skip(const kg_resource_list *req) {
 
 /* Filter + Score of NodeNUMAResource for one pair (no cpuset binding).  `numa` may be NULL (no
  * topology options).  Returns feasibility; *score the plugin score; the best hint in *hint. */
+/* the CPU accumulator (oracle/cpu_accumulator.c; its own policy encodings: bind 1 FullPCPUs / 2 Spread,
+ * exclusive 0 none / 1 PCPU / 2 NUMA node) */
+typedef struct kgo_cpu_topo {
+    int32_t n_cpus;
+    const int32_t *socket, *node, *core;
+} kgo_cpu_topo;
+int kgo_take_preferred_cpus(const kgo_cpu_topo *topo, int max_ref, const uint8_t *available, const uint8_t *preferred,
+                            const int32_t *alloc_ref, const int8_t *alloc_excl, int need, int bind, int excl_policy,
+                            int strategy, uint8_t *result);
+void kgo_available_cpus(const kgo_cpu_topo *topo, int max_ref, const int32_t *alloc_ref, const uint8_t *reserved,
+                        const uint8_t *preferred, uint8_t *available, int32_t *ref_out);
+void kgo_filter_required_bind(const kgo_cpu_topo *topo, int bind, uint8_t *available);
+int kgo_satisfied_required_bind(const kgo_cpu_topo *topo, int bind, const uint8_t *cpus);
+
+static int acc_bind(int b) { return b == KG_CPU_BIND_FULL_PCPUS ? 1 : b == KG_CPU_BIND_SPREAD_BY_PCPUS ? 2 : 0; }
+static int acc_excl(int x) { return x == KG_CPU_EXCL_PCPU_LEVEL ? 1 : x == KG_CPU_EXCL_NUMA_NODE_LEVEL ? 2 : 0; }
+
+/* resourceManager.Allocate without a NUMA hint for a cpuset request (resource_manager.go:171-195, 296-375):
+ * available CPUs of the node allocation, filtered by the required bind policy, then takePreferredCPUs and the
+ * required-policy check.  1 ⇔ a cpuset was found. */
+static int numa_allocate_cpuset(const kg_cluster_view *v, const kg_numa_spec *numa, int need, int bind, int excl) {
+    const int n = numa->n_cpus;
+    if (n <= 0 || n > 1024 || numa->first_cpu < 0 || numa->first_cpu + n > v->n_cpus) return 0;
+    const kg_cpu_info *ci = v->cpus + numa->first_cpu;
+    int32_t sock[1024], node[1024], core[1024], ref[1024];
+    int8_t ex[1024];
+    uint8_t reserved[1024], avail[1024], got[1024];
+    for (int i = 0; i < n; i++) {
+        sock[i] = ci[i].socket, node[i] = ci[i].node, core[i] = ci[i].core;
+        ref[i] = ci[i].refcount;
+        ex[i] = (int8_t)(ci[i].refcount > 0 ? acc_excl(ci[i].exclusive) : 0);
+        reserved[i] = (uint8_t)(ci[i].reserved != 0);
+    }
+    const kgo_cpu_topo t = {n, sock, node, core};
+    const int max_ref = numa->max_ref_count > 0 ? numa->max_ref_count : 1;
+    kgo_available_cpus(&t, max_ref, ref, reserved, NULL, avail, NULL);
+    kgo_filter_required_bind(&t, acc_bind(bind), avail);   /* options.requiredCPUBindPolicy is true here */
+    int navail = 0;
+    for (int i = 0; i < n; i++) navail += avail[i];
+    if (navail < need) return 0;
+    /* the NUMA allocate strategy orders candidates only; whether a cpuset is found does not depend on it */
+    if (kgo_take_preferred_cpus(&t, max_ref, avail, NULL, ref, ex, need, acc_bind(bind), acc_excl(excl), 1, got) != 0)
+        return 0;
+    return kgo_satisfied_required_bind(&t, acc_bind(bind), got);
+}
+
 static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n,
                      const kg_numa_spec *numa, int64_t *score, numa_hint *hint) {
     kg_resource_list preq;
@@ -928,18 +974,66 @@ static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_
     hint->score = 0;
     if (numa_skip(&preq)) return 1;
     int policy = numa ? numa->policy : KG_NUMA_NONE;
-    /* filterAmplifiedCPUs (plugin.go:340-373); the pod binds no cpuset, the node's cpuset pods are
-     * NodeAllocation.allocatedCPUs (GetAvailableCPUs: nil topology ⇒ none, invalid ⇒ error) */
     double ratio = numa ? numa->cpu_amplification_ratio : 0.0;
     int64_t pcpu = get(&preq, KG_RES_CPU);
+    /* PreFilter's cpuset decision (plugin.go:232-262) for AllowUseCPUSet pods (util.go:43-50) */
+    int state_bind = 0, state_required = KG_CPU_BIND_UNSET, state_excl = KG_CPU_EXCL_UNSET;
+    if ((pod->label_qos == KG_QOS_LSE || pod->label_qos == KG_QOS_LSR) && kgo_priority_class(v, pod) == KG_PRIO_PROD) {
+        int bind = pod->cpu_bind_preferred;
+        if (bind == KG_CPU_BIND_UNSET || bind == KG_CPU_BIND_DEFAULT) bind = c->numa_default_cpu_bind_policy;
+        int required = pod->cpu_bind_required;
+        if (required == KG_CPU_BIND_DEFAULT) required = c->numa_default_cpu_bind_policy;
+        if (required != KG_CPU_BIND_UNSET) bind = required;
+        if (bind == KG_CPU_BIND_FULL_PCPUS || bind == KG_CPU_BIND_SPREAD_BY_PCPUS) {
+            if (pcpu % 1000 != 0) return 0;   /* ErrInvalidRequestedCPUs */
+            if (pcpu > 0) {
+                state_bind = 1;
+                state_required = required;
+                state_excl = pod->cpu_exclusive;
+            }
+        }
+    }
+    /* requestCPUBind (util.go:105-122): a node CPU bind policy binds any cpu request */
+    const int node_bind = numa ? numa->node_cpu_bind_policy : KG_NODE_CPU_BIND_NONE;
+    int bind = state_bind;
+    if (!bind && pcpu != 0 && node_bind != KG_NODE_CPU_BIND_NONE) {
+        if (pcpu % 1000 != 0) return 0;
+        bind = 1;
+    }
+    /* filterAmplifiedCPUs (plugin.go:340-373): a bound pod's request is amplified; the node's cpuset pods
+     * are NodeAllocation.allocatedCPUs (GetAvailableCPUs: nil topology ⇒ none, invalid ⇒ error) */
     int amplified = pcpu != 0 && ratio > 1.0;
+    const int64_t pod_cpu = bind && amplified ? amplify(pcpu, ratio) : pcpu;
     int64_t cs_milli = 0;
     if (amplified) {
         if (numa->cpu_topology_valid == 0) return 0;
         cs_milli = numa->cpu_topology_valid == 1 ? (int64_t)numa->cpuset_cpus * 1000 : 0;
         int64_t rq = get(&n->requested, KG_RES_CPU);
         if (rq >= cs_milli && cs_milli > 0) rq = rq - cs_milli + amplify(cs_milli, ratio);
-        if (pcpu > get(&n->allocatable, KG_RES_CPU) - rq) return 0;
+        if (pod_cpu > get(&n->allocatable, KG_RES_CPU) - rq) return 0;
+    }
+    if (bind) {   /* Filter's cpuset branch (plugin.go:297-331) */
+        if (!numa || numa->cpu_topology_valid != 1) return 0;   /* ErrInvalidCPUTopology */
+        int required = state_required;
+        if (node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) required = KG_CPU_BIND_FULL_PCPUS;
+        else if (node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) required = KG_CPU_BIND_SPREAD_BY_PCPUS;
+        if (state_required != KG_CPU_BIND_UNSET && state_required != required) return 0;   /* conflict */
+        const int need = (int)(pcpu / 1000);
+        if (required == KG_CPU_BIND_FULL_PCPUS) {   /* ErrSMTAlignmentError */
+            int ncore = 0, seen_core[1024];
+            const kg_cpu_info *ci = v->cpus + numa->first_cpu;
+            for (int i = 0; i < numa->n_cpus; i++) {
+                int k = 0;
+                while (k < ncore && seen_core[k] != ci[i].core) k++;
+                if (k == ncore) seen_core[ncore++] = ci[i].core;
+            }
+            const int cpc = ncore ? numa->n_cpus / ncore : 0;
+            if (cpc == 0 || need % cpc != 0) return 0;
+        }
+        if (required != KG_CPU_BIND_UNSET && policy == KG_NUMA_NONE &&
+            !numa_allocate_cpuset(v, numa, need, required, state_excl))
+            return 0;
+        if (policy != KG_NUMA_NONE) return 0;   /* FilterByNUMANode for cpusets: not restated (the engine refuses it) */
     }
     numa_zones z;
     if (policy != KG_NUMA_NONE) {
@@ -970,13 +1064,16 @@ static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_
         *score = numa_scorer(c, c->numa_strategy, &n->requested, &n->allocatable, &preq);
         return 1;
     }
-    /* policy none: scoreWithAmplifiedCPUs (scoring.go:99-116) */
+    /* policy none: scoreWithAmplifiedCPUs (scoring.go:99-116) with the bound pod's amplified request
+     * (getResourceOptions, plugin.go:458-462) */
     kg_resource_list rq = n->requested;
     if (amplified) {
         rq.v[KG_RES_CPU] = get(&rq, KG_RES_CPU) - cs_milli + amplify(cs_milli, ratio);
         rq.present |= 1u << KG_RES_CPU;
     }
-    *score = numa_scorer(c, c->numa_strategy, &rq, &n->allocatable, &preq);
+    kg_resource_list pr = preq;
+    pr.v[KG_RES_CPU] = pod_cpu;
+    *score = numa_scorer(c, c->numa_strategy, &rq, &n->allocatable, &pr);
     return 1;
 }
 

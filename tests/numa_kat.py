@@ -66,8 +66,9 @@ def _amp_node(name, cpu, memory, ratio, nrt, cpuset_cpus):
         zone = {"cpu": str(_amplify(16, ratio)), "memory": "20Gi"}
         node.numa_zones = [dict(zone), dict(zone)]
         node.cpu_topology_valid = True
-        node.cpuset_cpus = cpuset_cpus
-        node.zone_cpuset_cpus = {0: min(cpuset_cpus, 16), 1: max(cpuset_cpus - 16, 0)}
+        # the CPU detail of buildCPUTopologyForTest(2, 1, 8, 2): socket = NUMA node = cpu // 16, core = cpu // 2
+        node.cpu_detail = [(c // 16, c // 16, c // 2) for c in range(32)]
+        node.cpu_allocated = {c: (1, "PCPULevel") for c in range(cpuset_cpus)}
     return node
 
 

@@ -94,14 +94,8 @@ def test_kat_numa_node_score(case):
 
 @pytest.mark.parametrize("case", AMP["score_cases"], ids=lambda c: c["name"])
 def test_kat_amplified_score(case):
-    """TestScoreWithAmplifiedCPUs through kg_eval; a scheduled cpuset pod is rejected at kg_pods_set."""
+    """TestScoreWithAmplifiedCPUs through kg_eval, cpuset pods included (matrix mode)."""
     cfg, view, pi, cl = amplified_score_cluster(case)
-    if case["pod_cpuset"]:
-        with engine.Engine(cfg) as eng:
-            eng.load_snapshot(engine.build_node_rows(cfg, view))
-            with pytest.raises(engine.EngineError, match="cpuset"):
-                eng.set_pods(engine.build_pod_rows(cfg, view, [pi]))
-        return
     with _engine_for(cfg, view, [pi]) as eng:
         res = eng.eval(0)
     k = len(case["nodes"])
@@ -109,7 +103,7 @@ def test_kat_amplified_score(case):
     assert engine.unpack_mask(res["mask"], k).all()
 
 
-@pytest.mark.parametrize("case", [c for c in AMP["filter_cases"] if not c["pod_cpuset"]], ids=lambda c: c["name"])
+@pytest.mark.parametrize("case", AMP["filter_cases"], ids=lambda c: c["name"])
 def test_kat_amplified_filter(case):
     """TestFilterWithAmplifiedCPUs through kg_eval (NodeNUMAResource alone)."""
     cfg, view, pi, cl = amplified_filter_cluster(case)

@@ -42,7 +42,7 @@ def test_oracle_numa_score_kat(case):
     assert got == case["want"]
 
 
-@pytest.mark.parametrize("case", [c for c in AMP["score_cases"] if not c["pod_cpuset"]], ids=lambda c: c["name"])
+@pytest.mark.parametrize("case", AMP["score_cases"], ids=lambda c: c["name"])
 def test_oracle_amplified_score_kat(case):
     cfg, view, pi, cl = amplified_score_cluster(case)
     got = []
@@ -53,7 +53,7 @@ def test_oracle_amplified_score_kat(case):
     assert got == case["want"]
 
 
-@pytest.mark.parametrize("case", [c for c in AMP["filter_cases"] if not c["pod_cpuset"]], ids=lambda c: c["name"])
+@pytest.mark.parametrize("case", AMP["filter_cases"], ids=lambda c: c["name"])
 def test_oracle_amplified_filter_kat(case):
     cfg, view, pi, cl = amplified_filter_cluster(case)
     ok, _ = oracle.numa_eval(cfg, view, pi, 0)

@@ -101,15 +101,12 @@ def test_row_commit_numa_matches_sequential_oracle(seed):
 
 @pytest.mark.parametrize("case", AMP["score_cases"], ids=lambda c: c["name"])
 def test_row_eval_amplified_score_kat(case):
-    """TestScoreWithAmplifiedCPUs through the engine's per-pair code; a scheduled pod that binds a
-    cpuset (LSR prod, integer cpus) is flagged for rejection at kg_pods_set instead."""
+    """TestScoreWithAmplifiedCPUs through the engine's per-pair code, cpuset pods (LSR prod, integer cpus,
+    the default FullPCPUs policy: requestCPUBind) included."""
     cfg, view, pi, cl = amplified_score_cluster(case)
     nodes = engine.build_node_rows(cfg, view)
     pods = engine.build_pod_rows(cfg, view, [pi])
-    if case["pod_cpuset"]:
-        assert pods["flags"][0] & nat.POD_NUMA_CPU_BIND
-        return
-    assert not pods["flags"][0] & nat.POD_NUMA_CPU_BIND
+    assert bool(pods["flags"][0] & nat.POD_NUMA_CPU_BIND) == case["pod_cpuset"]
     got = [engine.row_eval(cfg, nodes[j:j + 1], pods, 0) for j in range(len(case["nodes"]))]
     assert all(g[0] for g in got)
     assert [g[3] for g in got] == case["want"]
@@ -120,9 +117,7 @@ def test_row_eval_amplified_filter_kat(case):
     cfg, view, pi, cl = amplified_filter_cluster(case)
     nodes = engine.build_node_rows(cfg, view)
     pods = engine.build_pod_rows(cfg, view, [pi])
-    if case["pod_cpuset"]:
-        assert pods["flags"][0] & nat.POD_NUMA_CPU_BIND
-        return
+    assert bool(pods["flags"][0] & nat.POD_NUMA_CPU_BIND) == case["pod_cpuset"]
     assert bool(engine.row_eval(cfg, nodes, pods, 0)[0]) == case["want"]
 
 
