@@ -42,6 +42,13 @@ AMPLIFICATION_RATIO = "node.koordinator.sh/resource-amplification-ratio"
 USAGE_THRESHOLDS = "scheduling.koordinator.sh/usage-thresholds"
 NUMA_POLICY_LABEL = "node.koordinator.sh/numa-topology-policy"
 CPU_TOPOLOGY = "node.koordinator.sh/cpu-topology"
+NODE_CPU_BIND_LABEL = "node.koordinator.sh/cpu-bind-policy"
+KUBELET_CPU_MANAGER_POLICY = "kubelet.koordinator.sh/cpu-manager-policy"
+POD_CPU_ALLOCS = "node.koordinator.sh/pod-cpu-allocs"
+RESOURCE_SPEC = "scheduling.koordinator.sh/resource-spec"
+RESOURCE_STATUS = "scheduling.koordinator.sh/resource-status"
+CPU_BIND_POLICIES = ("", "Default", "FullPCPUs", "SpreadByPCPUs", "ConstrainedBurst")
+CPU_EXCLUSIVE_POLICIES = ("", "None", "PCPULevel", "NUMANodeLevel")
 
 BATCH_CPU, BATCH_MEMORY = "kubernetes.io/batch-cpu", "kubernetes.io/batch-memory"
 # apis/extension/deprecated.go:48-60 (deprecated name → current name)
@@ -87,19 +94,23 @@ def replace_and_erase(rl: Resources, mapping: Dict[str, str]) -> bool:
     return done
 
 
-def cpuset_size(s: str) -> int:
-    """cpuset.Parse(s).Size() (pkg/util/cpuset): "0-3,8,10-11" → 7."""
-    n = 0
-    for part in filter(None, (p.strip() for p in s.split(","))):
+def parse_cpuset(s: str) -> List[int]:
+    """cpuset.Parse (pkg/util/cpuset): "0-3,8,10-11" → [0, 1, 2, 3, 8, 10, 11]."""
+    out = set()
+    for part in filter(None, (p.strip() for p in (s or "").split(","))):
         if "-" in part:
             a, b = (int(x) for x in part.split("-", 1))
             if b < a:
                 raise ValueError(f"bad cpuset {s!r}")
-            n += b - a + 1
+            out.update(range(a, b + 1))
         else:
-            int(part)
-            n += 1
-    return n
+            out.add(int(part))
+    return sorted(out)
+
+
+def cpuset_size(s: str) -> int:
+    """cpuset.Parse(s).Size()."""
+    return len(parse_cpuset(s))
 
 
 def node_reservation(annotations: dict) -> Optional[dict]:
@@ -210,15 +221,34 @@ def pod_from_object(pod: dict) -> ob.Pod:
         return out
 
     owners = meta.get("ownerReferences") or []
+    spec_ann = resource_spec((meta.get("annotations") or {}))
     return ob.Pod(
         namespace=meta.get("namespace", "default"), name=meta.get("name", ""),
         containers=containers("containers"), init_containers=containers("initContainers"),
         overhead=_engine_resources(resources(spec["overhead"]), name) if spec.get("overhead") else None,
         priority=spec.get("priority"), labels=dict(meta.get("labels") or {}),
         qos_status=status.get("qosClass", ""),
+        cpu_bind_required=spec_ann["requiredCPUBindPolicy"], cpu_bind_preferred=spec_ann["preferredCPUBindPolicy"],
+        cpu_exclusive=spec_ann["preferredCPUExclusivePolicy"],
         daemonset=any(o.get("kind") == "DaemonSet" and o.get("controller", False) for o in owners),
         terminated=status.get("phase") in ("Succeeded", "Failed"),
         node_name=spec.get("nodeName", ""))
+
+
+def resource_spec(annotations: dict) -> dict:
+    """GetResourceSpec (numa_aware.go:190-205); a policy the engine does not know binds no cpuset, as a
+    non-empty ConstrainedBurst does."""
+    d = {}
+    s = annotations.get(RESOURCE_SPEC)
+    if s:
+        d = json.loads(s)
+    out = {}
+    for k in ("requiredCPUBindPolicy", "preferredCPUBindPolicy"):
+        v = d.get(k, "")
+        out[k] = v if v in CPU_BIND_POLICIES else "ConstrainedBurst"
+    v = d.get("preferredCPUExclusivePolicy", "")
+    out["preferredCPUExclusivePolicy"] = v if v in CPU_EXCLUSIVE_POLICIES else "None"
+    return out
 
 
 def pod_fit_request(p: ob.Pod) -> Tuple[Dict[str, Fraction], Tuple[int, int]]:
@@ -345,6 +375,50 @@ def cpu_topology_valid(nrt: dict) -> bool:
     return len(detail) > 0
 
 
+def cpu_detail_from_nrt(nrt: dict) -> Optional[List[Tuple[int, int, int]]]:
+    """convertCPUTopology (topology_options.go:173-179): (socket, NUMA node, core) per cpu id; the engine
+    indexes CPUs by id, so the reported ids must be 0..n-1."""
+    s = (nrt.get("metadata", {}).get("annotations") or {}).get(CPU_TOPOLOGY, "")
+    if not s:
+        return None
+    detail = sorted(json.loads(s).get("detail") or [], key=lambda d: d["id"])
+    if [d["id"] for d in detail] != list(range(len(detail))):
+        raise UnsupportedResource("CPU ids of the reported topology are not 0..n-1")
+    return [(int(d["socket"]), int(d["node"]), int(d["core"])) for d in detail]
+
+
+def kubelet_cpu_policy(nrt: Optional[dict]) -> Optional[dict]:
+    s = ((nrt or {}).get("metadata", {}).get("annotations") or {}).get(KUBELET_CPU_MANAGER_POLICY)
+    return json.loads(s) if s else None
+
+
+def reserved_cpus_from_nrt(nrt: dict) -> List[int]:
+    """TopologyOptions.ReservedCPUs (topology_options.go:119-134): kubelet-managed pod cpusets, the kubelet
+    reserved CPUs and the node reservation's reservedCPUs."""
+    ann = nrt.get("metadata", {}).get("annotations") or {}
+    out = set()
+    for a in json.loads(ann.get(POD_CPU_ALLOCS, "[]") or "[]"):
+        if a.get("managedByKubelet") and a.get("uid") and a.get("cpuset"):
+            out.update(parse_cpuset(a["cpuset"]))
+    pol = kubelet_cpu_policy(nrt)
+    if pol and pol.get("reservedCPUs"):
+        out.update(parse_cpuset(pol["reservedCPUs"]))
+    rsv = node_reservation(ann)
+    if rsv and rsv.get("reservedCPUs"):
+        out.update(parse_cpuset(rsv["reservedCPUs"]))
+    return sorted(out)
+
+
+def node_cpu_bind_policy(labels: dict, nrt: Optional[dict]) -> str:
+    """GetNodeCPUBindPolicy (numa_aware.go:314-325)."""
+    v = labels.get(NODE_CPU_BIND_LABEL, "")
+    pol = kubelet_cpu_policy(nrt)
+    if v == "FullPCPUsOnly" or (pol and pol.get("policy") == "static" and
+                                (pol.get("options") or {}).get("full-pcpus-only") == "true"):
+        return "FullPCPUsOnly"
+    return "SpreadByPCPUs" if v == "SpreadByPCPUs" else "None"
+
+
 def amplification_ratios(annotations: Optional[dict]) -> Optional[Dict[str, float]]:
     s = (annotations or {}).get(AMPLIFICATION_RATIO)
     if s is None:
@@ -391,11 +465,16 @@ def node_from_object(node: dict, nrt: Optional[dict] = None) -> ob.Node:
         n.numa_zone_ids = [zid for zid, _ in zones]
         n.numa_policy = label_policy or nrt_policy(nrt)
         n.cpu_topology_valid = cpu_topology_valid(nrt)
+        if n.cpu_topology_valid:
+            n.cpu_detail = cpu_detail_from_nrt(nrt)
+            n.cpu_allocated = {}
+            n.reserved_cpus = reserved_cpus_from_nrt(nrt)
         if not ratios:
             nrt_ratios = amplification_ratios(nrt.get("metadata", {}).get("annotations")) or {}
             n.cpu_amplification_ratio = float(nrt_ratios.get("cpu", 0.0))
     elif label_policy:
         n.numa_policy = label_policy
+    n.cpu_bind_policy = node_cpu_bind_policy(labels, nrt)
     return n
 
 
@@ -406,11 +485,15 @@ def cluster_from_objects(nodes: Iterable[dict], pods: Iterable[dict] = (), node_
     by_nrt = {n.get("metadata", {}).get("name"): n for n in nrts}
     cl = ob.Cluster(now_ns)
     bound: Dict[str, List[ob.Pod]] = {}
+    status_of: Dict[int, dict] = {}
     for pj in pods:
         p = pod_from_object(pj)
         cl.add_lister_pod(p)
         if p.node_name and not p.terminated:
             bound.setdefault(p.node_name, []).append(p)
+            s = (pj.get("metadata", {}).get("annotations") or {}).get(RESOURCE_STATUS)
+            if s:
+                status_of[id(p)] = json.loads(s)
     for nj in nodes:
         n = node_from_object(nj, by_nrt.get(nj.get("metadata", {}).get("name")))
         req: Dict[str, Fraction] = {}
@@ -421,6 +504,24 @@ def cluster_from_objects(nodes: Iterable[dict], pods: Iterable[dict] = (), node_
                 req[k] = req.get(k, Fraction(0)) + v
             nz[0] += z[0]
             nz[1] += z[1]
+        # the plugin's NodeAllocation from the bound pods' resource status (pod_eventhandler.go:93-136;
+        # resourceManager.Update records nothing on an invalid topology)
+        if n.cpu_topology_valid and n.numa_zones is not None:
+            for p in bound.get(n.name, []):
+                st = status_of.get(id(p))
+                if not st:
+                    continue
+                for c in parse_cpuset(st.get("cpuset", "")):
+                    ref, _ = (n.cpu_allocated or {}).get(c, (0, ""))
+                    if n.cpu_allocated is not None:
+                        n.cpu_allocated[c] = (ref + 1, p.cpu_exclusive or "None")
+                for zr in st.get("numaNodeResources") or []:
+                    zid = int(zr["node"])
+                    acc = (n.numa_allocated or {}).get(zid, {})
+                    for k, v in resources(zr.get("resources")).items():
+                        if k in ob.RES:
+                            acc[k] = acc.get(k, Fraction(0)) + v
+                    n.numa_allocated = dict(n.numa_allocated or {}, **{zid: acc})
         cl.add_node(n, requested={k: v for k, v in req.items() if k in ob.RES},
                     nonzero_requested={"cpu": f"{nz[0]}m", "memory": str(nz[1])}, pod_count=len(bound.get(n.name, [])))
     for m in node_metrics:

@@ -249,3 +249,57 @@ def test_cluster_nodeinfo_from_bound_pods():
     assert int(ns["requested"]["v"][0]) == 2000 and int(ns["requested"]["v"][1]) == 2**30
     assert list(ns["nonzero_requested"]) == [2100, 2**30 + 200 * 2**20]
     assert isinstance(cl.nodes[0], Node)
+
+
+def _cpu_topology_ann(sockets, cores_per_socket, threads):
+    detail, cid = [], 0
+    for s in range(sockets):
+        for c in range(cores_per_socket):
+            for _ in range(threads):
+                detail.append({"id": cid, "core": s * cores_per_socket + c, "socket": s, "node": s})
+                cid += 1
+    return json.dumps({"detail": detail})
+
+
+def test_cpuset_inputs_from_objects():
+    """NodeResourceTopology CPU topology / kubelet policy / reserved CPUs, node reservation, bound pods'
+    resource-status cpusets and a pending pod's resource-spec → the engine's cpuset counts and verdicts,
+    the same as the oracle's literal Allocate."""
+    nrt = {"metadata": {"name": "n", "annotations": {
+        ingest.CPU_TOPOLOGY: _cpu_topology_ann(2, 4, 2),
+        ingest.KUBELET_CPU_MANAGER_POLICY: json.dumps({"policy": "static", "reservedCPUs": "0"}),
+        ingest.POD_CPU_ALLOCS: json.dumps([{"uid": "u1", "cpuset": "15", "managedByKubelet": True}])}},
+        "zones": [{"name": "node-0", "type": "Node", "resources": [{"name": "cpu", "allocatable": "8"}]},
+                  {"name": "node-1", "type": "Node", "resources": [{"name": "cpu", "allocatable": "8"}]}]}
+    node = _node({"cpu": "16", "memory": "64Gi", "pods": "110"}, name="n")
+    bound = {"metadata": {"name": "b", "annotations": {ingest.RESOURCE_STATUS: json.dumps({"cpuset": "2-5"}),
+                                                       ingest.RESOURCE_SPEC: json.dumps({"preferredCPUExclusivePolicy": "PCPULevel"})},
+                          "labels": {"koordinator.sh/qosClass": "LSR"}},
+             "spec": {"nodeName": "n", "priority": 9999,
+                      "containers": [{"resources": {"requests": {"cpu": "4"}, "limits": {"cpu": "4"}}}]}}
+    cl = ingest.cluster_from_objects([node], [bound], nrts=[nrt], now_ns=NOW_NS)
+    n = cl.nodes[0]
+    assert n.reserved_cpus == [0, 15] and n.cpu_allocated == {c: (1, "PCPULevel") for c in range(2, 6)}
+    assert n.cpu_bind_policy == "None"
+    pend = []
+    for name, spec, cpu in [("full", {"requiredCPUBindPolicy": "FullPCPUs"}, "6"),
+                            ("full-too-many", {"requiredCPUBindPolicy": "FullPCPUs"}, "10"),
+                            ("spread", {"requiredCPUBindPolicy": "SpreadByPCPUs"}, "5"),
+                            ("odd-full", {"requiredCPUBindPolicy": "FullPCPUs"}, "3"),
+                            ("preferred", {}, "8"), ("fractional", {}, "1500m")]:
+        pend.append(ingest.pod_from_object({"metadata": {"name": name, "labels": {"koordinator.sh/qosClass": "LSR"},
+                                                         "annotations": {ingest.RESOURCE_SPEC: json.dumps(spec)}},
+                                            "spec": {"priority": 9999, "containers": [{"resources": {
+                                                "requests": {"cpu": cpu}, "limits": {"cpu": cpu}}}]}}))
+    view = cl.view(extra_pods=pend)
+    cfg = make_config(plugins=("NodeNUMAResource",))
+    rows = engine.build_node_rows(cfg, view)
+    # free: cores {0,1}→cpus 1 (0 reserved); core 1 (2,3) held; core 2 (4,5) held; 6..14 free, 15 reserved
+    assert (rows[0]["cpus_per_core"], rows[0]["cpuset_full_free_cpus"], rows[0]["cpuset_free_cores"]) == (2, 8, 6)
+    want = {"full": True, "full-too-many": False, "spread": True, "odd-full": False, "preferred": True,
+            "fractional": False}
+    for p in pend:
+        pi = view.pod_index(p)
+        ok, _ = oracle.numa_eval(cfg, view, pi, 0)
+        got = engine.row_eval(cfg, rows[0:1], engine.build_pod_rows(cfg, view, [pi]), NOW_NS)
+        assert bool(ok) == bool(got[0]) == want[p.name], p.name
