@@ -51,3 +51,19 @@ def test_bind_placement_is_refused():
         with pytest.raises(engine.EngineError, match="cpuset"):
             eng.commit(0, 0)
         eng.eval(cl.now_ns)   # matrix mode still answers
+
+
+def test_numa_plugin_filter_kat_gpu():
+    """TestPlugin_Filter (plugin_test.go:552-899) through kg_eval; the SingleNUMANode cases are refused."""
+    from test_numa_plugin_filter_kat import DOC, _cluster
+    for case in DOC["cases"]:
+        cfg, view, pi = _cluster(case)
+        with engine.Engine(cfg) as eng:
+            eng.load_snapshot(engine.build_node_rows(cfg, view))
+            eng.set_pods(engine.build_pod_rows(cfg, view, [pi]))
+            if case.get("engine") == "unsupported":
+                with pytest.raises(engine.EngineError, match="cpuset"):
+                    eng.eval(0)
+                continue
+            res = eng.eval(0)
+        assert bool(engine.unpack_mask(res["mask"], 1)[0, 0]) == case["want"], case["name"]
