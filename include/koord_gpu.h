@@ -604,7 +604,7 @@ kg_status kg_place_chunk_resolve(kg_engine *eng, int64_t now_ns, int32_t pod_beg
  * KG_MAX_RSV_PER_NODE.  Nodes carrying slots are evaluated on the exact per-pair path with the
  * restore of transformer.go:49-291.  Matrix mode with reservations needs the unsharded engine.
  * kg_rsv_download returns the slots (allocated / n_assigned after placements) in kg_rsv_set order. */
-#define KG_MAX_RSV_PER_NODE 4
+#define KG_MAX_RSV_PER_NODE 16
 kg_status kg_rsv_set(kg_engine *eng, const kg_reservation *rsv, int32_t n);
 kg_status kg_rsv_download(kg_engine *eng, kg_reservation *out, int32_t n);
 /* ElasticQuota groups (KG_PLUGIN_ELASTICQUOTA); kg_pod_row.quota indexes them. */

@@ -28,7 +28,7 @@ STRATEGY_LEAST_ALLOCATED, STRATEGY_MOST_ALLOCATED = 0, 1
 PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_RESERVATION, PLUGIN_ELASTICQUOTA = 0x1, 0x2, 0x4, 0x8, 0x10
 RSV_POLICY_DEFAULT, RSV_POLICY_ALIGNED, RSV_POLICY_RESTRICTED = range(3)
 RSV_AVAILABLE, RSV_UNSCHEDULABLE, RSV_ALLOCATE_ONCE = 0x1, 0x2, 0x4
-MAX_RSV_PER_NODE = 4
+MAX_RSV_PER_NODE = 16
 NUMA_NONE, NUMA_BEST_EFFORT, NUMA_RESTRICTED, NUMA_SINGLE_NUMA_NODE = range(4)
 MAX_ZONES = 8
 

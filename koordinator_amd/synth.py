@@ -319,7 +319,8 @@ def make_numa_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS
 
 def make_rsv_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, rsv_node_frac: float = 0.10,
                      owner_classes: int = 16, n_quotas: int = 64, quota_ratio: float = 0.8,
-                     owned_frac: float = 0.8, affinity_frac: float = 0.1, non_preemptible_frac: float = 0.1) -> SynthView:
+                     owned_frac: float = 0.8, affinity_frac: float = 0.1, non_preemptible_frac: float = 0.1,
+                     max_rsv_per_node: int = 2) -> SynthView:
     """BASELINE config 5: colocation burst of batch pods (batch-cpu / batch-memory
     requests) with Reservations and ElasticQuota.  `rsv_node_frac` of the nodes carry 1–2
     reservations of batch resources (10–30 % of the node's batch allocatable; 95 % available, 5 %
@@ -331,7 +332,8 @@ def make_rsv_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS,
     group's total demand (min = half of it); `non_preemptible_frac` are non-preemptible."""
     rng = np.random.default_rng(seed + 555)
     nodes = make_nodes(n_nodes, seed, now_ns)
-    rsv = _reservations(nodes, rng, rsv_node_frac, owner_classes, (nat.RES_BATCH_CPU, nat.RES_BATCH_MEMORY))
+    rsv = _reservations(nodes, rng, rsv_node_frac, owner_classes, (nat.RES_BATCH_CPU, nat.RES_BATCH_MEMORY),
+                        max_rsv_per_node)
     pods, cont = make_pods(n_pods, seed)
     rq, lm = cont["requests"], cont["limits"]
     cpu_r = np.where(rq["present"] & (1 << nat.RES_CPU), rq["v"][:, nat.RES_CPU], rq["v"][:, nat.RES_BATCH_CPU])
@@ -347,12 +349,12 @@ def make_rsv_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS,
     return SynthView(pods, cont, nodes, now_ns, reservations=rsv, quotas=quotas)
 
 
-def _reservations(nodes, rng, rsv_node_frac, owner_classes, res):
-    """`rsv_node_frac` of the nodes carry 1–2 reservations of the two resources `res` (10–30 % of the
-    node's allocatable of them); the reserve pods and their assigned pods are pods of the node."""
+def _reservations(nodes, rng, rsv_node_frac, owner_classes, res, max_per_node=2):
+    """`rsv_node_frac` of the nodes carry 1–`max_per_node` reservations of the two resources `res` (10–30 %
+    of the node's allocatable of them); the reserve pods and their assigned pods are pods of the node."""
     n_nodes = len(nodes)
     rn = np.sort(rng.choice(n_nodes, int(round(rsv_node_frac * n_nodes)), replace=False))
-    node_of = np.repeat(rn, rng.integers(1, 3, len(rn)))
+    node_of = np.repeat(rn, rng.integers(1, max_per_node + 1, len(rn)))
     R = len(node_of)
     rsv = np.zeros(R, dtype=nat.RESERVATION)
     rsv["node"] = node_of

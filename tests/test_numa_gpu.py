@@ -154,8 +154,9 @@ def test_pods_set_rejects_numa_shapes_off_the_engine_path():
         bad = rows.copy()
         bad["flags"][1] |= nat.POD_NUMA_CPU_BIND
         bad["flags"][1] &= ~np.uint32(nat.POD_NUMA_SKIP)
+        eng.set_pods(bad)   # cpusets are answered only off NUMA-policy nodes: refused at evaluation
         with pytest.raises(engine.EngineError, match="cpuset"):
-            eng.set_pods(bad)
+            eng.eval(cl.now_ns)
         bad = rows.copy()
         bad["flags"][2] &= ~np.uint32(nat.POD_NUMA_SKIP)
         bad["numa_request_present"][2] = 0b111   # cpu, memory and a zero-valued ephemeral-storage key

@@ -37,6 +37,20 @@ def test_rows_match_oracle_matrix(seed):
     assert rsv.max() == 100 and m.any()
 
 
+def test_rows_match_oracle_many_reservations_per_node():
+    """Up to KG_MAX_RSV_PER_NODE (16) reservations on a node (the reservation cache is unbounded,
+    cache.go:60,252)."""
+    cl = rsv_cluster(300, 24, seed=77, rsv_node_frac=0.3, max_rsv_per_node=16)
+    counts = np.bincount(cl.rsv_arr["node"])
+    assert counts.max() > 8
+    cfg = shipped_profile(plugins=RSV)
+    idx = np.arange(24)
+    got = rows_matrix5(cfg, cl, idx, cl.now_ns)
+    want = oracle.eval_matrix5(cfg, cl, idx, cl.now_ns)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("seed", [54, 55])
 def test_rows_match_oracle_matrix_with_numa(seed):
     """Reservation + NodeNUMAResource (the shipped profile's filter set without ElasticQuota): the

@@ -190,3 +190,17 @@ def test_score_with_order_kat_gpu():
         res = eng.eval(view.now_ns)
     assert list(res["rsv_scores"][0, :4]) == RF["score_with_order"]["want"]
     assert engine.decode_top1(res["top1"])[0][0] == 3
+
+
+def test_rsv_many_per_node_matrix_and_placement():
+    """Up to 12 reservations per node: matrix planes and the sequential cycle vs the oracle."""
+    cl = rsv_cluster(1500, 200, seed=78, rsv_node_frac=0.3, max_rsv_per_node=12)
+    assert np.bincount(cl.rsv_arr["node"]).max() > 8
+    cfg = shipped_profile(plugins=RSV_EQ)
+    idx = np.arange(200)
+    _check_matrix(cfg, cl, idx)
+    with _engine(cfg, cl, idx) as eng:
+        nodes, scores = eng.place(cl.now_ns)
+    ref_nodes, ref_scores, _, _ = oracle.schedule2(cfg, cl, idx, cl.now_ns)
+    np.testing.assert_array_equal(nodes, ref_nodes)
+    np.testing.assert_array_equal(scores, ref_scores)
