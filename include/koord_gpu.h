@@ -218,7 +218,7 @@ typedef struct kg_config {
 
     /* engine knobs */
     int32_t device;            /* HIP device ordinal */
-    int32_t place_chunk;       /* pods per refresh in kg_place (0 ⇒ default 8; at most KG_PLACE_CHUNK_MAX) */
+    int32_t place_chunk;       /* pods per refresh in kg_place (0 ⇒ default 16; at most KG_PLACE_CHUNK_MAX) */
 
     /* Reservation (profile weight, config/manager/scheduler-config.yaml:82-91 ships 5000) */
     int32_t weight_reservation;
@@ -602,7 +602,11 @@ kg_status kg_place_chunk_resolve(kg_engine *eng, int64_t now_ns, int32_t pod_beg
 
 /* Reservation cache (KG_PLUGIN_RESERVATION): replaces every reservation slot; a node holds at most
  * KG_MAX_RSV_PER_NODE.  Nodes carrying slots are evaluated on the exact per-pair path with the
- * restore of transformer.go:49-291.  Matrix mode with reservations needs the unsharded engine.
+ * restore of transformer.go:49-291.  Under kg_set_shard every rank still evaluates every reservation
+ * node (the slots are replicated): the per-pod preferred-reservation choice and Reservation
+ * NormalizeScore's maximum (plugin.go Score / NormalizeScore) are global and identical on each rank,
+ * the planes cover the shard's columns only, and top1 includes every reservation node, so a max over
+ * the ranks' top1 keys equals the unsharded result.
  * kg_rsv_download returns the slots (allocated / n_assigned after placements) in kg_rsv_set order. */
 #define KG_MAX_RSV_PER_NODE 16
 kg_status kg_rsv_set(kg_engine *eng, const kg_reservation *rsv, int32_t n);

@@ -2523,9 +2523,9 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
         else rsvp = out->rsv_scores;
         if (numa_b) HIP_TRY(e, hipMemsetAsync(rsvp, 0, numa_b, e->stream));
     }
+    // reservation nodes are evaluated whole on every shard (replicated slots: the preferred reservation
+    // and NormalizeScore's max are global); planes are written for the shard's columns only
     const RsvArgs ra = rsv_args(e);
-    if (ra.rsv && (e->shard_begin != 0 || e->shard_end != e->n_nodes))
-        return set_err(e, KG_ERR_UNSUPPORTED, "Reservation matrix mode needs the whole snapshot (no shard)");
     st = quota_ready(e);
     if (st) return st;
     const bool gated = (ra.quota || ra.rsv) && P > 0;
@@ -2637,7 +2637,7 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
         return set_err(e, KG_ERR_STATE, "kg_place runs on the whole snapshot; use the chunk API for shards");
     const int32_t P = e->n_pods;
     if (P == 0) return KG_OK;
-    int32_t chunk = e->cfg.place_chunk > 0 ? e->cfg.place_chunk : 8;
+    int32_t chunk = e->cfg.place_chunk > 0 ? e->cfg.place_chunk : 16;
     if (chunk > KG_MAX_CHUNK) chunk = KG_MAX_CHUNK;
     const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS;
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };

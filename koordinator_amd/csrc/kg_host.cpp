@@ -366,7 +366,7 @@ void kg_config_default(kg_config *c) {
     c->numa_default_cpu_bind_policy = KG_CPU_BIND_FULL_PCPUS;   // v1beta2 defaults.go:50
     c->numa_resource_weight[KG_RES_CPU] = 1;
     c->numa_resource_weight[KG_RES_MEMORY] = 1;
-    c->place_chunk = 8;
+    c->place_chunk = 16;
 }
 
 void kg_config_shipped_profile(kg_config *c) {

@@ -66,14 +66,14 @@ def test_config_validation_rejects_bad_args():
     assert L.kg_config_validate(nat.ptr(bad), buf, 256) != 0
     for chunk, ok in ((-1, False), (0, True), (1, True), (1024, True), (1025, False)):
         c = good.copy()
-        c["place_chunk"] = chunk        # kg_place: 0 ⇒ default 8, at most KG_PLACE_CHUNK_MAX
+        c["place_chunk"] = chunk        # kg_place: 0 ⇒ default 16, at most KG_PLACE_CHUNK_MAX
         assert (L.kg_config_validate(nat.ptr(c), buf, 256) == 0) == ok, chunk
 
 
 def test_place_chunk_rule_matches_kg_place():
     from koordinator_amd import dist as kdist
     cfg = shipped_profile()
-    for chunk, want in ((0, 8), (1, 1), (64, 64), (1024, 1024), (5000, 1024)):
+    for chunk, want in ((0, 16), (1, 1), (64, 64), (1024, 1024), (5000, 1024)):
         cfg["place_chunk"] = chunk
         assert kdist.place_chunk_of(cfg) == want
     cfg["place_chunk"] = -3

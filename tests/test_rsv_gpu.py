@@ -192,6 +192,33 @@ def test_score_with_order_kat_gpu():
     assert engine.decode_top1(res["top1"])[0][0] == 3
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_rsv_matrix_sharded(world):
+    """Reservation matrix mode under node shards (the multi-GPU matrix path on one device): every shard
+    evaluates all reservation nodes, writes only its own columns, and the max over the shards' top1
+    keys (dist.merge_top1_) equals the unsharded result and the oracle's."""
+    from koordinator_amd.dist import shard_range
+    cl = synth.make_profile_cluster(2600, 48, seed=79, rsv_node_frac=0.3, n_quotas=6, quota_ratio=0.3)
+    cfg = shipped_profile(plugins=PROFILE, weight_numa=2)
+    N, idx = len(cl.nodes), np.arange(48)
+    m, fit, la, numa, rsv, top1 = oracle.eval_matrix5(cfg, cl, idx, cl.now_ns)
+    best = np.zeros(48, np.uint64)
+    with _engine(cfg, cl, idx) as eng:
+        for r in range(world):
+            b, e = shard_range(N, r, world)
+            eng.set_shard(b, e)
+            res = eng.eval(cl.now_ns)
+            W = e - b
+            np.testing.assert_array_equal(engine.unpack_mask(res["mask"], W), m[:, b:e])
+            np.testing.assert_array_equal(res["scores"][:, :W, 0], fit[:, b:e])
+            np.testing.assert_array_equal(res["scores"][:, :W, 1], la[:, b:e])
+            np.testing.assert_array_equal(res["numa_scores"][:, :W], numa[:, b:e])
+            np.testing.assert_array_equal(res["rsv_scores"][:, :W], rsv[:, b:e])
+            best = np.maximum(best, res["top1"].astype(np.uint64))
+    np.testing.assert_array_equal(best, top1)
+    assert rsv.max() == 100 and (top1 > 0).any()
+
+
 def test_rsv_many_per_node_matrix_and_placement():
     """Up to 12 reservations per node: matrix planes and the sequential cycle vs the oracle."""
     cl = rsv_cluster(1500, 200, seed=78, rsv_node_frac=0.3, max_rsv_per_node=12)
