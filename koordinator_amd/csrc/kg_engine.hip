@@ -686,25 +686,28 @@ __device__ __forceinline__ uint32_t sel_lanes(unsigned long long m, uint32_t v) 
 // lane select goes through M0 because a VOP3 may read only one SGPR)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"   // M0 is otherwise unused by these kernels (checked in the ISA)
-__device__ __forceinline__ void write_lanes(uint32_t (&mb)[4], uint32_t lane, unsigned long long b0,
-                                            unsigned long long b1) {
+__device__ __forceinline__ void write_lanes(uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3, uint32_t lane,
+                                            unsigned long long b0, unsigned long long b1) {
     asm("s_mov_b32 m0, %4\n\ts_nop 0\n\tv_writelane_b32 %0, %5, m0\n\tv_writelane_b32 %1, %6, m0\n\t"
         "v_writelane_b32 %2, %7, m0\n\tv_writelane_b32 %3, %8, m0"
-        : "+v"(mb[0]), "+v"(mb[1]), "+v"(mb[2]), "+v"(mb[3])
+        : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3)
         : "s"(lane), "s"((uint32_t)b0), "s"((uint32_t)(b0 >> 32)), "s"((uint32_t)b1), "s"((uint32_t)(b1 >> 32))
         : "m0");
 }
 #pragma clang diagnostic pop
 
-// Pods [p0, p1) of one class against the lane's two nodes; rows come from the LDS chunk buffer.
-// The feasibility ballots of the chunk are collected into lanes (p − p0) of four VGPRs and written
-// once per chunk; EDGE workgroups (the shard's last tile) check that a segment lies in the row.
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool STAGE, int CC, bool UNR>
-__device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> &n0,
-                                         const ClsNode<NC, NF> &n1, unsigned long long okm0, unsigned long long okm1,
-                                         const char *lrows, int p0, int p1, uint16_t *__restrict__ scores,
-                                         uint32_t scol, bool seg0, bool seg1, uint32_t kb0, uint32_t kb1,
-                                         uint32_t *kbuf, uint32_t (&mb)[4], uint16_t *sst) {
+// Pods [p0, p1) of one class against the lane's NPL nodes (columns 64·j + lane of the wave's segment);
+// rows come from the LDS chunk buffer.  The feasibility ballots of the chunk are collected into lanes
+// (p − p0) of 2·NPL VGPRs and written once per chunk; EDGE workgroups (the shard's last tile) check
+// that a segment lies in the row.
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool STAGE, int CC, bool UNR,
+          int NPL>
+__device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> (&n)[NPL],
+                                         const unsigned long long (&okm)[NPL], const char *lrows, int p0, int p1,
+                                         uint16_t *__restrict__ scores, uint32_t scol, const bool (&seg)[NPL],
+                                         const uint32_t (&kb)[NPL], uint32_t *kbuf, uint32_t (&mb)[2 * NPL],
+                                         uint16_t *sst) {
+    constexpr int BT = KG_TILE / NPL;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     // UNR: a whole chunk, unrolled, so every LDS address (pod row, key buffer, score staging) and
@@ -714,55 +717,45 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
     auto pod = [&](const int i) {
         const kg_pod_cls_t<NC, NF> pd =
             *reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(lrows + i * (int)sizeof(kg_pod_cls_t<NC, NF>));
-        const unsigned long long m0 = cls_ok_mask<NC, NF>(pd, n0, okm0);
-        const unsigned long long m1 = cls_ok_mask<NC, NF>(pd, n1, okm1);
+        unsigned long long m[NPL];
+#pragma unroll
+        for (int j = 0; j < NPL; j++) m[j] = cls_ok_mask<NC, NF>(pd, n[j], okm[j]);
+        uint32_t kmax = 0, s[NPL];
         if (FULL && W1) {
             // packed pair scores: key = dot2(H, {1024, 1024}) + kb = (fit + la) << 10 + kb in one
             // v_dot2_u32_u16; the staged u16 is the perm of H's low bytes (fit | la << 8)
-            const uint32_t h0 = cls_packed<NC, NF, MOST, FIT_ON, LA_ON>(pd, n0, shifts);
-            const uint32_t h1 = cls_packed<NC, NF, MOST, FIT_ON, LA_ON>(pd, n1, shifts);
             const kg_u16x2 kw = {(uint16_t)(1u << KG_TILE_SHIFT), (uint16_t)(1u << KG_TILE_SHIFT)};
-            const uint32_t k0 = sel_lanes(m0, __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h0), kw, kb0, false));
-            const uint32_t k1 = sel_lanes(m1, __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h1), kw, kb1, false));
-            kbuf[i * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
-            if (OUT) {
-                write_lanes(mb, (uint32_t)i, m0, m1);
-                const uint16_t s0 = (uint16_t)__builtin_amdgcn_perm(h0, h0, 0x0c0c0200u);
-                const uint16_t s1 = (uint16_t)__builtin_amdgcn_perm(h1, h1, 0x0c0c0200u);
-                if (STAGE) {
-                    sst[i * 128 + lane] = s0;
-                    sst[i * 128 + 64 + lane] = s1;
-                } else {
-                    uint16_t *srow = scores + pd.score_off;
-                    if (seg0) srow[scol] = s0;
-                    if (seg1) srow[scol + 64] = s1;
-                }
+#pragma unroll
+            for (int j = 0; j < NPL; j++) {
+                const uint32_t h = cls_packed<NC, NF, MOST, FIT_ON, LA_ON>(pd, n[j], shifts);
+                const uint32_t k = sel_lanes(m[j], __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h), kw, kb[j], false));
+                kmax = kmax > k ? kmax : k;
+                s[j] = __builtin_amdgcn_perm(h, h, 0x0c0c0200u);
             }
-            return;
-        }
-        uint32_t fit0, la0, fit1, la1;
-        cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n0, fit0, la0);
-        cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n1, fit1, la1);
-        uint32_t tot0, tot1;
-        if (W1) {
-            tot0 = fit0 + la0;
-            tot1 = fit1 + la1;
         } else {
-            tot0 = __umul24((uint32_t)c.weight_fit, fit0) + __umul24((uint32_t)c.weight_la, la0);
-            tot1 = __umul24((uint32_t)c.weight_fit, fit1) + __umul24((uint32_t)c.weight_la, la1);
+#pragma unroll
+            for (int j = 0; j < NPL; j++) {
+                uint32_t fit, la, tot;
+                cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n[j], fit, la);
+                tot = W1 ? fit + la : __umul24((uint32_t)c.weight_fit, fit) + __umul24((uint32_t)c.weight_la, la);
+                const uint32_t k = sel_lanes(m[j], (tot << KG_TILE_SHIFT) + kb[j]);
+                kmax = kmax > k ? kmax : k;
+                s[j] = fit | (la << 8);
+            }
         }
-        const uint32_t k0 = sel_lanes(m0, (tot0 << KG_TILE_SHIFT) + kb0);
-        const uint32_t k1 = sel_lanes(m1, (tot1 << KG_TILE_SHIFT) + kb1);
-        kbuf[i * KG_BLOCK + tid] = k0 > k1 ? k0 : k1;
+        kbuf[i * BT + tid] = kmax;
         if (OUT) {
-            write_lanes(mb, (uint32_t)i, m0, m1);
-            if (STAGE) {  // the wave's 128-column score segment of this pod, written out per chunk
-                sst[i * 128 + lane] = (uint16_t)(fit0 | (la0 << 8));
-                sst[i * 128 + 64 + lane] = (uint16_t)(fit1 | (la1 << 8));
+#pragma unroll
+            for (int j = 0; j < NPL; j += 2)
+                write_lanes(mb[2 * j], mb[2 * j + 1], mb[2 * j + 2], mb[2 * j + 3], (uint32_t)i, m[j], m[j + 1]);
+            if (STAGE) {  // the wave's 64·NPL-column score segment of this pod, written out per chunk
+#pragma unroll
+                for (int j = 0; j < NPL; j++) sst[i * (64 * NPL) + 64 * j + lane] = (uint16_t)s[j];
             } else {
                 uint16_t *srow = scores + pd.score_off;
-                if (seg0) srow[scol] = (uint16_t)(fit0 | (la0 << 8));
-                if (seg1) srow[scol + 64] = (uint16_t)(fit1 | (la1 << 8));
+#pragma unroll
+                for (int j = 0; j < NPL; j++)
+                    if (seg[j]) srow[scol + 64 * j] = (uint16_t)s[j];
             }
         }
     };
@@ -774,34 +767,45 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
     }
 }
 
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE>
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE, int NPL>
 __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
                                           const kg_cls_work &w, const char *__restrict__ rows_base,
                                           uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
                                           uint32_t *__restrict__ partials, uint32_t *kbuf, char *lrows,
                                           uint16_t *sstage) {
+    constexpr int BT = KG_TILE / NPL;                     // threads of the workgroup
     constexpr int RB = (int)sizeof(kg_pod_cls_t<NC, NF>);
-    constexpr int CHUNK_DW = CC * RB / 4;                 // dwords of one chunk of rows (≤ KG_BLOCK)
-    constexpr int G = KG_BLOCK / CC;                      // threads reducing one pod's keys
+    constexpr int CHUNK_DW = CC * RB / 4;                 // dwords of one chunk of rows (≤ BT)
+    constexpr int G = BT / CC;                            // threads reducing one pod's keys
+    constexpr int SEGW = 64 * NPL;                        // score columns of one wave
+    static_assert(NPL == 2 || NPL == 4, "two or four nodes per lane");
     static_assert(G == 32 || G == 64, "key reduction groups are half or whole waves");
-    static_assert(CHUNK_DW <= KG_BLOCK, "one dword per thread stages a chunk");
+    static_assert(CHUNK_DW <= BT, "one dword per thread stages a chunk");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tile = a.tile_begin + blockIdx.x;
-    const int64_t wave_base = (int64_t)tile * KG_TILE + wave * 128;
-    ClsNode<NC, NF> n0, n1;
-    load_cls_node<NC, NF, FIT_ON, LA_ON>(c, pl, d, wave_base + lane, a.node_end, a.now_ns, n0);
-    load_cls_node<NC, NF, FIT_ON, LA_ON>(c, pl, d, wave_base + 64 + lane, a.node_end, a.now_ns, n1);
-    const unsigned long long okm0 = __builtin_amdgcn_ballot_w64(n0.ok), okm1 = __builtin_amdgcn_ballot_w64(n1.ok);
-    const uint32_t W = 1u << d.fit_shift;
-    const bool full = !FIT_ON || __all((n0.w == W || wave_base + lane >= a.node_end) &&
-                                       (n1.w == W || wave_base + 64 + lane >= a.node_end));
+    const int64_t wave_base = (int64_t)tile * KG_TILE + wave * SEGW;
+    ClsNode<NC, NF> n[NPL];
+    unsigned long long okm[NPL];
+    bool full_l = true;
+#pragma unroll
+    for (int j = 0; j < NPL; j++) {
+        load_cls_node<NC, NF, FIT_ON, LA_ON>(c, pl, d, wave_base + 64 * j + lane, a.node_end, a.now_ns, n[j]);
+        okm[j] = __builtin_amdgcn_ballot_w64(n[j].ok);
+        full_l = full_l && (n[j].w == (1u << d.fit_shift) || wave_base + 64 * j + lane >= a.node_end);
+    }
+    const bool full = !FIT_ON || __all(full_l);
     const int64_t col0 = wave_base - a.col_begin;
-    const bool seg0 = col0 < a.score_stride, seg1 = col0 + 64 < a.score_stride;
-    const uint32_t scol = (uint32_t)col0 + (uint32_t)lane;        // score column of n0
-    const uint32_t local0 = (uint32_t)(wave * 128 + lane);
-    const uint32_t kb0 = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0, kb1 = kb0 - 64;
+    bool seg[NPL];
+    uint32_t kb[NPL];
+    const uint32_t local0 = (uint32_t)(wave * SEGW + lane);
+#pragma unroll
+    for (int j = 0; j < NPL; j++) {
+        seg[j] = col0 + 64 * j < a.score_stride;
+        kb[j] = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0 - 64u * j;
+    }
+    const uint32_t scol = (uint32_t)col0 + (uint32_t)lane;        // score column of n[0]
     // pod rows are staged chunk by chunk into LDS (double buffer); the next chunk's global load is
     // in flight while the current chunk is evaluated, so no pod pays a memory round trip
     const uint32_t *gsrc = reinterpret_cast<const uint32_t *>(rows_base + d.rows_offset);
@@ -816,7 +820,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __syncthreads();
     const int rj = tid / G, rg = tid % G;
-    uint16_t *sst = sstage + wave * (CC * 128);
+    uint16_t *sst = sstage + wave * (CC * SEGW);
     int buf = 0;
     for (int p0 = w.begin; p0 < w.end; p0 += CC) {
         const int p1 = min(p0 + CC, w.end);
@@ -827,40 +831,48 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
             staged = gsrc[src < last_dw ? src : last_dw];
         }
         const char *cur = lrows + buf * (CC * RB);
-        uint32_t mb[4] = {0u, 0u, 0u, 0u};
+        uint32_t mb[2 * NPL];
+#pragma unroll
+        for (int j = 0; j < 2 * NPL; j++) mb[j] = 0u;
 #define KG_CLS_PODS(FULL_, UNR_)                                                                                    \
-    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, STAGE, CC, UNR_>(c, d, n0, n1, okm0, okm1, cur, p0, p1, scores, \
-                                                                          scol, seg0, seg1, kb0, kb1, kbuf, mb, sst)
+    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, STAGE, CC, UNR_, NPL>(c, d, n, okm, cur, p0, p1, scores, scol, \
+                                                                               seg, kb, kbuf, mb, sst)
         if (full && p1 - p0 == CC) KG_CLS_PODS(true, true);
         else if (full) KG_CLS_PODS(true, false);
         else KG_CLS_PODS(false, false);
 #undef KG_CLS_PODS
         if (OUT && STAGE) {
-            // 16 lanes × 16 B cover one pod's 128 columns: four pods per wave-wide 1 KiB store.  The
+            // LP lanes × 16 B cover one pod's SEGW columns: 64 / LP pods per wave-wide 1 KiB store.  The
             // reads see the other lanes' ds_writes: a wave's LDS operations complete in order.
+            constexpr int LP = SEGW / 8, PPS = 64 / LP;
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
-            const int np = p1 - p0, s8 = lane & 15;
-            const bool segs = s8 < 8 ? seg0 : seg1;
-            for (int it = 0; it * 4 < np; it++) {
-                const int pp = it * 4 + (lane >> 4);
+            const int np = p1 - p0, s8 = lane % LP, sj = s8 / 8;
+            bool segs = seg[0];
+#pragma unroll
+            for (int j = 1; j < NPL; j++)
+                if (sj == j) segs = seg[j];
+            for (int it = 0; it * PPS < np; it++) {
+                const int pp = it * PPS + lane / LP;
                 if (pp < np && segs) {
-                    const uint4 v = *reinterpret_cast<const uint4 *>(sst + pp * 128 + s8 * 8);
+                    const uint4 v = *reinterpret_cast<const uint4 *>(sst + pp * SEGW + s8 * 8);
                     const int64_t off = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[pp].score_off;
                     *reinterpret_cast<uint4 *>(scores + off + col0 + s8 * 8) = v;
                 }
             }
         }
-        if (OUT && lane < p1 - p0 && seg0) {
-            // lane l writes the two feasibility words of pod p0 + l
+        if (OUT && lane < p1 - p0 && seg[0]) {
+            // lane l writes the NPL feasibility words of pod p0 + l
             const kg_pod_cls_t<NC, NF> &pr = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[lane];
             uint64_t *mw = mask + pr.mask_off + (col0 >> 6);
             mw[0] = (uint64_t)mb[0] | ((uint64_t)mb[1] << 32);
-            if (seg1) mw[1] = (uint64_t)mb[2] | ((uint64_t)mb[3] << 32);
+#pragma unroll
+            for (int j = 1; j < NPL; j++)
+                if (seg[j]) mw[j] = (uint64_t)mb[2 * j] | ((uint64_t)mb[2 * j + 1] << 32);
         }
         if (more && tid < CHUNK_DW) lbuf[(buf ^ 1) * (CC * RB / 4) + tid] = staged;
         __syncthreads();
-        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * KG_BLOCK + rg * CC);
+        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * BT + rg * CC);
         uint32_t mx = 0;
 #pragma unroll
         for (int k = 0; k < CC / 4; k++) {
@@ -885,24 +897,24 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
 }
 
 // One launch per class kind (the work table is grouped by kind): each kernel is register-allocated for
-// its own kind, so the common 2-compare / 2-score kind runs at 6 waves per SIMD (≤ 80 VGPRs, LDS
-// ≤ 53 KiB per workgroup) instead of inheriting the 4-resource kinds' budget.
-template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE, int KIND>
-__global__ __launch_bounds__(KG_BLOCK) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? 6 : KIND == 2 ? 5 : 4))) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
+// its own kind.  NPL nodes per lane: a 1024-node tile is KG_TILE / NPL threads.
+template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE, int KIND, int NPL>
+__global__ __launch_bounds__(KG_TILE / NPL) __attribute__((amdgpu_waves_per_eu(NPL == 4 ? 4 : KIND == 0 ? 6 : KIND == 2 ? 5 : 4))) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_cls_desc *__restrict__ descs,
                                                     const kg_cls_work *__restrict__ work,
                                                     const char *__restrict__ rows, uint64_t *__restrict__ mask,
                                                     uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
-    __shared__ __attribute__((aligned(16))) uint32_t kbuf[CC * KG_BLOCK];
+    constexpr int BT = KG_TILE / NPL;
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[CC * BT];
     __shared__ __attribute__((aligned(64))) char lrows[2 * CC * 128];
-    __shared__ __attribute__((aligned(16))) uint16_t sstage[STAGE ? (KG_BLOCK / 64) * CC * 128 : 8];
+    __shared__ __attribute__((aligned(16))) uint16_t sstage[STAGE ? (BT / 64) * CC * 64 * NPL : 8];
     const kg_cls_work w = work[blockIdx.y];
     const kg_cls_desc d = descs[w.cls];
 #define KG_CLS_ARGS c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows, sstage
-    if constexpr (KIND == 0) cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS);
-    else if constexpr (KIND == 1) cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS);
-    else if constexpr (KIND == 2) cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS);
-    else cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE>(KG_CLS_ARGS);
+    if constexpr (KIND == 0) cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, NPL>(KG_CLS_ARGS);
+    else if constexpr (KIND == 1) cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, NPL>(KG_CLS_ARGS);
+    else if constexpr (KIND == 2) cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, NPL>(KG_CLS_ARGS);
+    else cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, NPL>(KG_CLS_ARGS);
 #undef KG_CLS_ARGS
 }
 
@@ -1955,11 +1967,12 @@ void launch_cls_kind(kg_engine *e, dim3 grid, const HotArgs &a, const kg_cls_des
     if (count == 0) return;
     grid.y = (unsigned)count;
     // matrix mode: 8-pod chunks, score segments staged in LDS and written as 1 KiB wave stores
+    // two nodes per lane (four: 92 VGPRs, 5 waves per SIMD, 1.98 vs 0.88 ms per config-2 pass)
     if (mask)
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, 8, true, KIND>), grid, dim3(KG_BLOCK), 0, e->stream,
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, 8, true, KIND, 2>), grid, dim3(KG_TILE / 2), 0, e->stream,
                            e->consts, e->pl, a, descs, work + first, rows, mask, scores, partials);
     else
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, 16, false, KIND>), grid, dim3(KG_BLOCK), 0, e->stream,
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, 16, false, KIND, 2>), grid, dim3(KG_TILE / 2), 0, e->stream,
                            e->consts, e->pl, a, descs, work + first, rows, mask, scores, partials);
 }
 

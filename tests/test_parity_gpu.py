@@ -185,7 +185,7 @@ def test_snapshot_generation_counts_mutations():
     """kg_snapshot_generation: reset, upsert / remove, commit and each placement resolve
     advance it; evaluations do not."""
     cl = synth.make_cluster(1_500, 16, seed=9)
-    cfg = shipped_profile()
+    cfg = shipped_profile(place_chunk=8)
     idx = np.arange(16)
     with engine.Engine(cfg) as eng:
         assert eng.generation() == 0
