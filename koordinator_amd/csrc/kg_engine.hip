@@ -899,11 +899,10 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
 // One launch per class kind (the work table is grouped by kind): each kernel is register-allocated for
 // its own kind.  NPL nodes per lane: a 1024-node tile is KG_TILE / NPL threads.
 template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE, int KIND, int NPL>
-__global__ __launch_bounds__(KG_TILE / NPL) __attribute__((amdgpu_waves_per_eu(NPL == 4 ? 4 : KIND == 0 ? 6 : KIND == 2 ? 5 : 4))) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
-                                                    const kg_cls_desc *__restrict__ descs,
-                                                    const kg_cls_work *__restrict__ work,
-                                                    const char *__restrict__ rows, uint64_t *__restrict__ mask,
-                                                    uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
+__device__ __forceinline__ void k_eval3_body(const kg_consts &c, const kg_planes &pl, const HotArgs &a,
+                                             const kg_cls_desc *__restrict__ descs, const kg_cls_work *__restrict__ work,
+                                             const char *__restrict__ rows, uint64_t *__restrict__ mask,
+                                             uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
     constexpr int BT = KG_TILE / NPL;
     __shared__ __attribute__((aligned(16))) uint32_t kbuf[CC * BT];
     __shared__ __attribute__((aligned(64))) char lrows[2 * CC * 128];
@@ -918,6 +917,16 @@ __global__ __launch_bounds__(KG_TILE / NPL) __attribute__((amdgpu_waves_per_eu(N
 #undef KG_CLS_ARGS
 }
 
+// One launch per class kind (the work table is grouped by kind): each kernel is register-allocated for
+// its own kind.  NPL nodes per lane: a 1024-node tile is KG_TILE / NPL threads.
+template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE, int KIND, int NPL>
+__global__ __launch_bounds__(KG_TILE / NPL) __attribute__((amdgpu_waves_per_eu(NPL == 4 ? 4 : KIND == 0 ? 6 : KIND == 2 ? 5 : 4))) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
+                                                    const kg_cls_desc *__restrict__ descs,
+                                                    const kg_cls_work *__restrict__ work,
+                                                    const char *__restrict__ rows, uint64_t *__restrict__ mask,
+                                                    uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
+    k_eval3_body<MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, KIND, NPL>(c, pl, a, descs, work, rows, mask, scores, partials);
+}
 // Slow nodes (outside the fp64 exactness bounds) come out of k_eval2 as infeasible with
 // zero scores; k_slow_list collects them and k_fix_slow re-evaluates those pairs exactly.
 __global__ void k_slow_list(const uint32_t *__restrict__ dflags, int64_t begin, int64_t end, int32_t *__restrict__ list,
