@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 5
+#define KG_ABI_VERSION 6
 
 /* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
 #define KG_PLACE_CHUNK_MAX 1024
@@ -196,7 +196,9 @@ typedef struct kg_config {
     int32_t la_filter_expired_node_metrics;   /* *FilterExpiredNodeMetrics (nil ⇒ 0) */
     int32_t la_has_expiration;                /* NodeMetricExpirationSeconds != nil  */
     int64_t la_expiration_seconds;
-    int64_t la_resource_weight[KG_NUM_RES];   /* ResourceWeights (0 ⇔ absent) */
+    int64_t la_resource_weight[KG_NUM_RES];   /* ResourceWeights (0 ⇔ absent).  Weights on resources other than
+                                                 cpu / memory take the exact int64 pair path on every node
+                                                 (correct, not the fp64 fast kernels) */
     int64_t la_scaling_factor[KG_NUM_RES];    /* EstimatedScalingFactors (missing key ⇒ 0) */
     kg_resource_list la_usage_thresholds;     /* UsageThresholds */
     kg_resource_list la_prod_usage_thresholds;/* ProdUsageThresholds */
@@ -419,6 +421,7 @@ typedef struct kg_pod_row {
     int32_t rsv_affinity_class;         /* kg_pod_spec.rsv_affinity_class */
     int32_t quota;                      /* kg_pod_spec.quota */
     int32_t _pad2;
+    int64_t la_estimate_x[KG_NUM_RES - 2]; /* EstimatePod(pod)[r] for r = 2..7 (0 unless resourceWeights name r) */
 } kg_pod_row;
 
 #define KG_NODE_VALID 0x1u
@@ -464,6 +467,10 @@ typedef struct kg_node_row {
     int32_t cpus_per_core;              /* CPUTopology.CPUsPerCore() (0 ⇔ no CPU detail) */
     int32_t cpuset_full_free_cpus;      /* CPUs of the cores whose every CPU is available (getAvailableCPUs) */
     int32_t cpuset_free_cores;          /* cores with at least one available CPU */
+    /* LoadAwareScheduling resourceWeights beyond cpu / memory (resources 2..7; zero unless weighted):
+       EstimateNode(node)[r] and the [nonProd, prod] node terms of r */
+    int64_t la_alloc_x[KG_NUM_RES - 2];
+    int64_t la_used_x[2][KG_NUM_RES - 2];
 } kg_node_row;
 
 /* ------------------------------------------------------------------ */

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 NUM_RES = 8
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
  RES_EXTENDED) = range(8)
@@ -108,6 +108,7 @@ POD_ROW = np.dtype([
     ("la_estimate", "<i8", (2,)), ("request_present", "<u4"), ("flags", "<u4"),
     ("numa_request", "<i8", (NUM_RES,)), ("numa_request_present", "<u4"), ("cpu_bind", "<u4"),
     ("rsv_owner_class", "<i4"), ("rsv_affinity_class", "<i4"), ("quota", "<i4"), ("_pad2", "<i4"),
+    ("la_estimate_x", "<i8", (NUM_RES - 2,)),
 ], align=True)
 
 NODE_ROW = np.dtype([
@@ -119,6 +120,7 @@ NODE_ROW = np.dtype([
     ("zone_keys", "<u4"), ("zone_alloc_keys", "<u4"), ("cpu_amplification_ratio", "<f8"),
     ("cpuset_milli", "<i8"), ("cpuset_amp_milli", "<i8"), ("zone_cpuset_amp", "<i8", (MAX_ZONES,)),
     ("node_cpu_bind", "<i4"), ("cpus_per_core", "<i4"), ("cpuset_full_free_cpus", "<i4"), ("cpuset_free_cores", "<i4"),
+    ("la_alloc_x", "<i8", (NUM_RES - 2,)), ("la_used_x", "<i8", (2, NUM_RES - 2)),
 ], align=True)
 
 RESERVATION = np.dtype([

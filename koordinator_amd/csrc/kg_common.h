@@ -76,6 +76,7 @@ struct kg_pod_dev {
     int32_t rsv_aff;             // required reservation-affinity class (−1 none)
     int32_t quota;               // ElasticQuota group (−1 none)
     uint32_t _pad2;
+    int64_t la_est_x[KG_NUM_RES - 2]; // EstimatePod of resources 2..7 (LoadAware weights beyond cpu / memory)
 };
 
 // config-derived constants passed by value to every kernel
@@ -97,6 +98,8 @@ struct kg_consts {
     int32_t numa_hint_most;      // NUMAScoringStrategy MostAllocated
     int32_t numa_w[KG_NUM_RES];  // ScoringStrategy.Resources weights
     int32_t weight_rsv;          // Reservation profile weight
+    int32_t la_extra;            // LoadAware weights beyond cpu / memory: every node takes kg_pair_exact
+    int32_t la_wx[KG_NUM_RES - 2]; // their weights (resources 2..7; included in la_wsum)
     int32_t _pad;
 };
 
@@ -250,7 +253,7 @@ KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, in
                           double *F0_out = nullptr, double *F1_out = nullptr) {
     const kg_node_row &row = pl.rows[i];
     const int64_t cap = pl.cap;
-    bool slow = false;
+    bool slow = c.la_extra != 0;   // weights beyond cpu / memory: the fp64 planes cover only cpu / memory
     int64_t a = row.la_alloc[r];
     double R = 0.0, F0 = 0.0, F1 = 0.0;
     if (a != 0) {
@@ -323,6 +326,10 @@ KG_HD void kg_apply_commit(kg_node_row &row, const kg_pod_dev &p) {
     if (p.flags & KG_POD_PROD) {
         row.la_used[1][0] += p.la_est_i[0];
         row.la_used[1][1] += p.la_est_i[1];
+    }
+    for (int r = 0; r < KG_NUM_RES - 2; r++) {   // zero unless LoadAware weights name the resource
+        row.la_used_x[0][r] += p.la_est_x[r];
+        if (p.flags & KG_POD_PROD) row.la_used_x[1][r] += p.la_est_x[r];
     }
 }
 
@@ -921,6 +928,14 @@ KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_
             int64_t req = p.la_est_i[r] + row.la_used[v][r];
             int64_t q = (a == 0 || req > a) ? 0 : (a - req) * 100 / a;
             s += q * c.la_w[r];
+        }
+        if (c.la_extra) {
+            for (int r = 0; r < KG_NUM_RES - 2; r++) {
+                if (c.la_wx[r] == 0) continue;
+                const int64_t a = row.la_alloc_x[r];
+                const int64_t req = p.la_est_x[r] + row.la_used_x[v][r];
+                s += ((a == 0 || req > a) ? 0 : kg_qdiv((a - req) * 100, a)) * c.la_wx[r];
+            }
         }
         la = c.la_wsum ? (uint32_t)(s / c.la_wsum) : 0;
     }

@@ -960,6 +960,35 @@ __global__ void k_fix_slow(kg_consts c, kg_planes pl, const kg_pod_dev *__restri
     }
 }
 
+// Matrix mode when every node takes the exact int64 pair path (LoadAware resourceWeights beyond cpu /
+// memory, which the fp64 planes do not carry): one thread per (pod, node); a wave covers 64 columns
+// of one pod row, so the feasibility word is its ballot.  Reservation nodes are left to k_rsv_eval.
+__global__ __launch_bounds__(256) void k_eval_exact(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods,
+                                                    int32_t n_pods, int64_t begin, int64_t end, int32_t mask_words,
+                                                    int64_t score_stride, int32_t tiles_total, int64_t now_ns,
+                                                    unsigned long long *mask, uint16_t *scores, uint32_t *partials) {
+    const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t node = begin + col;
+    const bool in = node < end;
+    const uint32_t df = in ? pl.dflags[node] : 0u;
+    const bool own = in && !(df & KGD_RSV);
+    for (int p = blockIdx.y; p < n_pods; p += gridDim.y) {
+        bool feas = false;
+        uint32_t fit = 0, la = 0;
+        if (own) kg_pair_exact(c, pl.rows[node], df, pods[p], now_ns, feas, fit, la);
+        if (own && scores) scores[(int64_t)p * score_stride + col] = (uint16_t)(fit | (la << 8));
+        const unsigned long long word = __builtin_amdgcn_ballot_w64(feas);
+        if (mask && (threadIdx.x & 63) == 0 && (col >> 6) < mask_words && in) mask[(int64_t)p * mask_words + (col >> 6)] = word;
+        uint32_t key = 0;
+        if (feas) {
+            const uint32_t tot = (uint32_t)c.weight_fit * fit + (uint32_t)c.weight_la * la;
+            key = ((tot + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - (node % KG_TILE));
+        }
+        key = wave_max_u32(key);
+        if ((threadIdx.x & 63) == 0 && key) atomicMax(&partials[(int64_t)p * tiles_total + node / KG_TILE], key);
+    }
+}
+
 // NodeNUMAResource enabled (config 3; matrix mode and placement chunks), pod per lane: a wave holds 64 pods and walks 256 nodes of a tile one
 // node at a time, so every node-side value (derived planes, canonical row with its zones) is
 // wave-uniform (one cache line per load, served to all 64 pods) and the NUMA hint enumeration runs
@@ -1590,6 +1619,12 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             const int r = tid - 64 - KG_NUM_RES;
             row.la_used[0][r] += pd.la_est_i[r];
             if (pd.flags & KG_POD_PROD) row.la_used[1][r] += pd.la_est_i[r];
+            if (r == 0 && c.la_extra) {   // LoadAware weights beyond cpu / memory
+                for (int x = 0; x < KG_NUM_RES - 2; x++) {
+                    row.la_used_x[0][x] += pd.la_est_x[x];
+                    if (pd.flags & KG_POD_PROD) row.la_used_x[1][x] += pd.la_est_x[x];
+                }
+            }
             double R, F0, F1;
             fin[KG_NUM_RES + r] = kg_finalize_la(c, pl, node, r, &R, &F0, &F1) ? 1u : 0u;
             if (ce) {
@@ -2072,6 +2107,20 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
                                e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials,
                                e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr);
         }
+        HIP_TRY(e, hipGetLastError());
+        if (e->profiling) {
+            HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
+            e->ev_count++;
+        }
+        return KG_OK;
+    }
+    if (e->consts.la_extra && !topk) {   // every node is on the exact path: no fast kernel, no slow list
+        if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
+        const int64_t width = e->shard_end - e->shard_begin;
+        dim3 grid((unsigned)((width + 255) / 256), (unsigned)(n < 65535 ? n : 65535));
+        hipLaunchKernelGGL(k_eval_exact, grid, dim3(256), 0, e->stream, e->consts, e->pl, e->pods + pod_begin, n,
+                           e->shard_begin, e->shard_end, a.mask_words, a.score_stride, a.tiles_total, now_ns,
+                           (unsigned long long *)mask, scores, partials);
         HIP_TRY(e, hipGetLastError());
         if (e->profiling) {
             HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));

@@ -135,12 +135,12 @@ int translate_resource(int pc, int r) {  // -1 ⇔ "" (no such resource)
     return -1;
 }
 
-// EstimatePod for the two engine resources (cpu, memory)
-void estimate_pod(const kg_config &cfg, const PodView &pv, int64_t out[2]) {
+// EstimatePod (default_estimator.go:57-70): every resource resourceWeights names (0 elsewhere)
+void estimate_pod(const kg_config &cfg, const PodView &pv, int64_t out[KG_NUM_RES]) {
     kg_resource_list req, lim;
     requests_and_limits(pv, req, lim);
     const int pc = priority_class_of(pv);
-    for (int r = 0; r < 2; r++) {
+    for (int r = 0; r < KG_NUM_RES; r++) {
         out[r] = 0;
         if (cfg.la_resource_weight[r] == 0) continue;
         const int real = translate_resource(pc, r);
@@ -260,14 +260,15 @@ MetricIndex pod_metric_map(const kg_cluster_view &v, const kg_node_spec &n, bool
 }
 
 // node-side sum of LoadAware.Score for one variant (0 = non-prod, 1 = prod usage)
-void loadaware_node_term(const kg_config &c, const kg_cluster_view &v, const kg_node_spec &n, int variant, int64_t out[2]) {
+void loadaware_node_term(const kg_config &c, const kg_cluster_view &v, const kg_node_spec &n, int variant,
+                         int64_t out[KG_NUM_RES]) {
     const bool prod = variant == 1;
     const MetricIndex pm = pod_metric_map(v, n, prod);
     const bool score_agg = c.la_has_aggregated && c.la_agg_score_type != KG_AGG_UNSET;
     const kg_resource_list *agg = score_agg ? aggregated_usage(v, n, c.la_agg_score_duration_ns, c.la_agg_score_type) : nullptr;
     const int64_t upd = n.has_update_time ? n.update_time_ns : INT64_MIN;
     const int64_t interval = (n.has_report_interval ? n.report_interval_seconds : 60) * 1000000000LL;
-    out[0] = out[1] = 0;
+    for (int r = 0; r < KG_NUM_RES; r++) out[r] = 0;
     std::unordered_set<int64_t> estimated;
     for (int i = 0; i < n.n_assigned; i++) {
         const kg_assigned_pod &a = v.assigned[n.first_assigned + i];
@@ -277,9 +278,9 @@ void loadaware_node_term(const kg_config &c, const kg_cluster_view &v, const kg_
         const kg_resource_list *usage = it == pm.usage.end() ? nullptr : it->second;
         const bool recent = a.timestamp_ns > upd || (a.timestamp_ns < upd && upd - a.timestamp_ns < interval);
         if (usage == nullptr || nkeys(*usage) == 0 || recent || (score_agg && agg == nullptr)) {
-            int64_t est[2];
+            int64_t est[KG_NUM_RES];
             estimate_pod(c, ap, est);
-            for (int r = 0; r < 2; r++) {
+            for (int r = 0; r < KG_NUM_RES; r++) {
                 if (c.la_resource_weight[r] == 0) continue;
                 int64_t x = est[r];
                 if (usage && bit(usage->present, r) && usage->v[r] > x) x = usage->v[r];
@@ -288,20 +289,18 @@ void loadaware_node_term(const kg_config &c, const kg_cluster_view &v, const kg_
             estimated.insert(ap.p.name_id);
         }
     }
-    int64_t actual[2] = {0, 0}, est_actual[2] = {0, 0};
+    int64_t actual[KG_NUM_RES] = {}, est_actual[KG_NUM_RES] = {};
     for (int64_t name : pm.order) {
         const kg_resource_list *u = pm.usage.at(name);
         int64_t *dst = estimated.count(name) ? est_actual : actual;
-        dst[0] += val(*u, 0);
-        dst[1] += val(*u, 1);
+        for (int r = 0; r < KG_NUM_RES; r++) dst[r] += val(*u, r);
     }
     if (prod) {
-        out[0] += actual[0];
-        out[1] += actual[1];
+        for (int r = 0; r < KG_NUM_RES; r++) out[r] += actual[r];
     } else if (n.has_node_metric_info) {
         const kg_resource_list *nu = score_agg ? agg : &n.node_usage;
         if (nu) {
-            for (int r = 0; r < 2; r++) {
+            for (int r = 0; r < KG_NUM_RES; r++) {
                 if (!bit(nu->present, r)) continue;
                 int64_t q = nu->v[r];
                 if (est_actual[r] != 0 && q >= est_actual[r]) q -= est_actual[r];
@@ -397,8 +396,6 @@ kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
         fw += c->fit_resource_weight[r];
         lw += c->la_resource_weight[r];
         nw += c->numa_resource_weight[r];
-        if (r >= 2 && c->la_resource_weight[r] != 0)
-            return fail("LoadAwareScheduling resourceWeights beyond cpu/memory are not supported by the engine");
     }
     if (fw > 600 || lw > 600 || nw > 600) return fail("resource weight sum too large (max 600)");
     if ((c->enabled_plugins & KG_PLUGIN_NUMA) && nw == 0) return fail("NodeNUMAResource needs scoringStrategy resources");
@@ -467,7 +464,13 @@ kg_status kg_build_pod_rows(const kg_config *cfg, const kg_cluster_view *view, c
             row.fit_score_request[r] = s;
             if (r < 2) row.nonzero_request[r] = nz;
         }
-        estimate_pod(*cfg, pv, row.la_estimate);
+        {
+            int64_t est[KG_NUM_RES];
+            estimate_pod(*cfg, pv, est);
+            row.la_estimate[0] = est[KG_RES_CPU];
+            row.la_estimate[1] = est[KG_RES_MEMORY];
+            for (int r = 2; r < KG_NUM_RES; r++) row.la_estimate_x[r - 2] = est[r];
+        }
         // NodeNUMAResource PreFilter (plugin.go:219-269): PodRequestsAndLimits requests; skip when all zero
         {
             kg_resource_list nreq, nlim;
@@ -540,6 +543,7 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
         estimate_node(ns, est);
         row.la_alloc[0] = val(est, KG_RES_CPU);
         row.la_alloc[1] = val(est, KG_RES_MEMORY);
+        for (int r = 2; r < KG_NUM_RES; r++) row.la_alloc_x[r - 2] = val(est, r);
         if (ns.has_node_metric) {
             row.flags |= KG_NODE_HAS_METRIC;
             if (ns.has_update_time) {
@@ -570,8 +574,13 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
             }
             if (pass_np) row.flags |= KG_NODE_LA_PASS_NONPROD;
             if (pass_p) row.flags |= KG_NODE_LA_PASS_PROD;
-            loadaware_node_term(*cfg, *view, ns, 0, row.la_used[0]);
-            loadaware_node_term(*cfg, *view, ns, 1, row.la_used[1]);
+            for (int v = 0; v < 2; v++) {
+                int64_t used[KG_NUM_RES];
+                loadaware_node_term(*cfg, *view, ns, v, used);
+                row.la_used[v][0] = used[KG_RES_CPU];
+                row.la_used[v][1] = used[KG_RES_MEMORY];
+                for (int r = 2; r < KG_NUM_RES; r++) row.la_used_x[v][r - 2] = used[r];
+            }
         }
         // NodeNUMAResource topology options (topology_options.go) with amplified zone cpu
         // (util.go:62-85 amplifyNUMANodeResources) and the plugin's zone allocations
@@ -781,6 +790,11 @@ void kg_consts_from_config(const kg_config &c, kg_consts &k) {
     k.la_w[0] = (int32_t)c.la_resource_weight[0];
     k.la_w[1] = (int32_t)c.la_resource_weight[1];
     k.la_wsum = k.la_w[0] + k.la_w[1];
+    for (int r = 2; r < KG_NUM_RES; r++) {
+        k.la_wx[r - 2] = (int32_t)c.la_resource_weight[r];
+        k.la_wsum += k.la_wx[r - 2];
+        if (k.la_wx[r - 2] != 0) k.la_extra = 1;
+    }
     k.la_magic = k.la_wsum ? (uint32_t)((0x80000000ULL + (uint64_t)k.la_wsum - 1) / (uint64_t)k.la_wsum) : 0;
     k.la_shift = 0xFF;
     if (k.la_wsum > 0 && (k.la_wsum & (k.la_wsum - 1)) == 0) k.la_shift = __builtin_ctz((unsigned)k.la_wsum);
@@ -828,6 +842,7 @@ void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &
     d.nonzero[1] = row.nonzero_request[1];
     d.la_est_i[0] = row.la_estimate[0];
     d.la_est_i[1] = row.la_estimate[1];
+    for (int r = 0; r < KG_NUM_RES - 2; r++) d.la_est_x[r] = row.la_estimate_x[r];
     for (int r = 0; r < KG_NUM_RES; r++) d.numa_req[r] = row.numa_request[r];
     d.numa_present = row.numa_request_present;
     d.cpu_bind = row.cpu_bind;

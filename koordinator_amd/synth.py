@@ -454,3 +454,46 @@ CONFIGS = {
     2: dict(n_nodes=100_000, n_pods=10_000, seed=2),
     4: dict(n_nodes=1_000_000, n_pods=10_000, seed=4),
 }
+
+
+def make_la_extra_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS) -> SynthView:
+    """A config-2 cluster whose LoadAware inputs also carry the resources beyond cpu / memory that
+    resourceWeights may name: ephemeral-storage and an extended resource in allocatable (some nodes
+    without them), node usage of ephemeral-storage / batch-cpu / batch-memory / the extended resource,
+    pod requests and limits of ephemeral-storage and the extended resource, and those resources in the
+    assigned pods' PodsMetric."""
+    base = make_cluster(n_nodes, n_pods, seed, now_ns)
+    rng = np.random.default_rng(seed + 4242)
+    nodes = base.nodes.copy()
+    n = len(nodes)
+    eph = rng.integers(50, 500, n) * GI
+    gpu = rng.integers(0, 9, n)
+    has_eph, has_gpu = rng.random(n) < 0.85, rng.random(n) < 0.5
+    _rl_fill(nodes["allocatable"], nat.RES_EPHEMERAL_STORAGE, eph, has_eph)
+    _rl_fill(nodes["allocatable"], nat.RES_EXTENDED, gpu, has_gpu)
+    _rl_fill(nodes["requested"], nat.RES_EXTENDED, (gpu * rng.integers(0, 3, n)) // 4, has_gpu)
+    usage = nodes["node_usage"]
+    live = usage["present"] != 0
+    _rl_fill(usage, nat.RES_EPHEMERAL_STORAGE, (eph // 100) * rng.integers(0, 101, n), live & has_eph)
+    ba = nodes["allocatable"]["v"]
+    _rl_fill(usage, nat.RES_BATCH_CPU, (ba[:, nat.RES_BATCH_CPU] * rng.integers(0, 91, n)) // 100, live)
+    _rl_fill(usage, nat.RES_BATCH_MEMORY, (ba[:, nat.RES_BATCH_MEMORY] // 100) * rng.integers(0, 91, n), live)
+    _rl_fill(usage, nat.RES_EXTENDED, (gpu * rng.integers(0, 5, n)) // 4, live & has_gpu)
+    cont = base.containers.copy()
+    c = len(cont)
+    rq, lm = cont["requests"], cont["limits"]
+    e_req = rng.integers(1, 40, c) * GI
+    want_eph, want_gpu = rng.random(c) < 0.6, rng.random(c) < 0.25
+    _rl_fill(rq, nat.RES_EPHEMERAL_STORAGE, e_req, want_eph)
+    _rl_fill(lm, nat.RES_EPHEMERAL_STORAGE, e_req * rng.integers(1, 3, c), want_eph & (rng.random(c) < 0.5))
+    g_req = rng.integers(1, 3, c)
+    _rl_fill(rq, nat.RES_EXTENDED, g_req, want_gpu)
+    _rl_fill(lm, nat.RES_EXTENDED, g_req, want_gpu)
+    pm = base.pod_metrics_arr.copy()
+    m = len(pm)
+    if m:
+        _rl_fill(pm["usage"], nat.RES_EPHEMERAL_STORAGE, rng.integers(0, 30, m) * GI, rng.random(m) < 0.7)
+        _rl_fill(pm["usage"], nat.RES_BATCH_CPU, rng.integers(0, 4000, m), rng.random(m) < 0.4)
+        _rl_fill(pm["usage"], nat.RES_EXTENDED, rng.integers(0, 3, m), rng.random(m) < 0.2)
+    return SynthView(base.pods, cont, nodes, now_ns, aggregated=base.aggregated_arr, pod_metrics=pm,
+                     assigned=base.assigned_arr)

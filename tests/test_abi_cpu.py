@@ -61,9 +61,9 @@ def test_config_validation_rejects_bad_args():
     bad["weight_fit"] = 30000
     bad["weight_loadaware"] = 30000     # totals would overflow the 32-bit tile keys
     assert L.kg_config_validate(nat.ptr(bad), buf, 256) != 0
-    bad = good.copy()
-    bad["la_resource_weight"][3] = 1    # LoadAware weights beyond cpu/memory are unsupported
-    assert L.kg_config_validate(nat.ptr(bad), buf, 256) != 0
+    extra = good.copy()
+    extra["la_resource_weight"][3] = 1  # LoadAware weights beyond cpu/memory: the exact pair path
+    assert L.kg_config_validate(nat.ptr(extra), buf, 256) == 0
     for chunk, ok in ((-1, False), (0, True), (1, True), (1024, True), (1025, False)):
         c = good.copy()
         c["place_chunk"] = chunk        # kg_place: 0 ⇒ default 16, at most KG_PLACE_CHUNK_MAX
