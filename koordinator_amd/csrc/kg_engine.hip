@@ -841,6 +841,10 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         else if (full) KG_CLS_PODS(true, false);
         else KG_CLS_PODS(false, false);
 #undef KG_CLS_PODS
+        // the next chunk's rows go to the other LDS buffer before this chunk's global stores are issued:
+        // waiting for the row load (vmcnt) after the stores would wait for the stores too (vmcnt counts
+        // both), stalling every chunk on the HBM write latency
+        if (more && tid < CHUNK_DW) lbuf[(buf ^ 1) * (CC * RB / 4) + tid] = staged;
         if (OUT && STAGE) {
             // LP lanes × 16 B cover one pod's SEGW columns: 64 / LP pods per wave-wide 1 KiB store.  The
             // reads see the other lanes' ds_writes: a wave's LDS operations complete in order.
@@ -870,7 +874,6 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
             for (int j = 1; j < NPL; j++)
                 if (seg[j]) mw[j] = (uint64_t)mb[2 * j] | ((uint64_t)mb[2 * j + 1] << 32);
         }
-        if (more && tid < CHUNK_DW) lbuf[(buf ^ 1) * (CC * RB / 4) + tid] = staged;
         __syncthreads();
         const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * BT + rg * CC);
         uint32_t mx = 0;
