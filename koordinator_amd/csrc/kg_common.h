@@ -222,9 +222,9 @@ KG_HD double kg_scaled_ratio(int64_t num, int64_t den) {
 //   kg_finalize_la(r)   LoadAware planes of resource r (r < 2)             → slow
 //   kg_finalize_flags   dflags / fit_mask / metric from the parts' results
 // (free / R / F out: optional copies of the written plane values, for the resolve kernel's node cache)
-KG_HD uint32_t kg_finalize_fit(const kg_consts &c, const kg_planes &pl, int64_t i, int r, int64_t *free_out = nullptr,
-                               double *R_out = nullptr, double *F_out = nullptr) {
-    const kg_node_row &row = pl.rows[i];
+// (the _r forms take the canonical row by reference: the placement resolve passes its LDS copy)
+KG_HD uint32_t kg_finalize_fit_r(const kg_consts &c, const kg_planes &pl, int64_t i, const kg_node_row &row, int r,
+                                 int64_t *free_out = nullptr, double *R_out = nullptr, double *F_out = nullptr) {
     const int64_t cap = pl.cap;
     uint32_t out = 0;
     const int64_t fr = row.alloc[r] - row.requested[r];
@@ -249,9 +249,12 @@ KG_HD uint32_t kg_finalize_fit(const kg_consts &c, const kg_planes &pl, int64_t 
     if (F_out) *F_out = F;
     return out;
 }
-KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, int r, double *R_out = nullptr,
-                          double *F0_out = nullptr, double *F1_out = nullptr) {
-    const kg_node_row &row = pl.rows[i];
+KG_HD uint32_t kg_finalize_fit(const kg_consts &c, const kg_planes &pl, int64_t i, int r, int64_t *free_out = nullptr,
+                               double *R_out = nullptr, double *F_out = nullptr) {
+    return kg_finalize_fit_r(c, pl, i, pl.rows[i], r, free_out, R_out, F_out);
+}
+KG_HD bool kg_finalize_la_r(const kg_consts &c, const kg_planes &pl, int64_t i, const kg_node_row &row, int r,
+                            double *R_out = nullptr, double *F0_out = nullptr, double *F1_out = nullptr) {
     const int64_t cap = pl.cap;
     bool slow = c.la_extra != 0;   // weights beyond cpu / memory: the fp64 planes cover only cpu / memory
     int64_t a = row.la_alloc[r];
@@ -275,6 +278,10 @@ KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, in
         *F1_out = F1;
     }
     return slow;
+}
+KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, int r, double *R_out = nullptr,
+                          double *F0_out = nullptr, double *F1_out = nullptr) {
+    return kg_finalize_la_r(c, pl, i, pl.rows[i], r, R_out, F0_out, F1_out);
 }
 // the bits of dflags a Reserve can change, from the committed row values
 #define KGD_DYNAMIC (KGD_PODS_FULL | KGD_OVER_CPU | KGD_OVER_MEM | KGD_OVER_EPH | KGD_SLOW)
@@ -885,14 +892,28 @@ KG_HD void kg_numa_commit(const kg_consts &c, kg_node_row &row, const kg_pod_dev
 KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_t *requested, const int64_t *nonzero,
                         int64_t pod_count, uint32_t df, const kg_pod_dev &p, int64_t now_ns, bool &feasible,
                         uint32_t &fit, uint32_t &la) {
+    // every row field first, as independent loads (on the device the row is in global memory: loads
+    // interleaved with the compares below would each wait for the previous one)
+    int64_t al[KG_NUM_RES], rq[KG_NUM_RES];
+#pragma unroll
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        al[r] = row.alloc[r];
+        rq[r] = requested[r];
+    }
+    const int64_t nz[2] = {nonzero[0], nonzero[1]};
+    const int v = (p.flags & KG_POD_LA_PROD_SCORE) ? 1 : 0;
+    const int64_t la_a[2] = {row.la_alloc[0], row.la_alloc[1]};
+    const int64_t la_u[2] = {row.la_used[v][0], row.la_used[v][1]};
+    const uint32_t rflags = row.flags, apresent = row.alloc_present;
+    const int64_t allowed = (int64_t)row.allowed_pods;
     bool expired = kg_metric_expired(c, df, row.metric_update_ns, now_ns);
-    bool ok = (row.flags & KG_NODE_VALID) != 0;
+    bool ok = (rflags & KG_NODE_VALID) != 0;
     if (c.plugins & KG_PLUGIN_FIT) {
-        if (pod_count + 1 > (int64_t)row.allowed_pods) ok = false;
+        if (pod_count + 1 > allowed) ok = false;
         if (p.flags & KG_POD_HAS_REQUEST) {
             for (int r = 0; r < KG_NUM_RES; r++) {
                 bool chk = r < 3 || ((p.request_present >> r) & 1u);
-                if (chk && p.req[r] > row.alloc[r] - requested[r]) ok = false;
+                if (chk && p.req[r] > al[r] - rq[r]) ok = false;
             }
         }
     }
@@ -906,10 +927,10 @@ KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_
         int64_t s = 0, w = 0;
         for (int r = 0; r < KG_NUM_RES; r++) {
             if (!((p.fit_mask >> r) & 1u)) continue;
-            bool present = r < 3 || ((row.alloc_present >> r) & 1u);
-            int64_t a = row.alloc[r];
+            bool present = r < 3 || ((apresent >> r) & 1u);
+            int64_t a = al[r];
             if (!present || a == 0) continue;
-            int64_t base = r < 2 ? nonzero[r] : requested[r];
+            int64_t base = r < 2 ? nz[r] : rq[r];
             int64_t req = base + p.fit_pr_i[r];
             int64_t q;
             if (c.fit_most) q = (req > a ? a : req) * 100 / a;
@@ -920,12 +941,11 @@ KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_
         fit = w ? (uint32_t)(s / w) : 0;
     }
     if ((c.plugins & KG_PLUGIN_LOADAWARE) && kg_la_valid(c, df, expired)) {
-        int v = (p.flags & KG_POD_LA_PROD_SCORE) ? 1 : 0;
         int64_t s = 0;
         for (int r = 0; r < 2; r++) {
             if (c.la_w[r] == 0) continue;
-            int64_t a = row.la_alloc[r];
-            int64_t req = p.la_est_i[r] + row.la_used[v][r];
+            int64_t a = la_a[r];
+            int64_t req = p.la_est_i[r] + la_u[r];
             int64_t q = (a == 0 || req > a) ? 0 : (a - req) * 100 / a;
             s += q * c.la_w[r];
         }

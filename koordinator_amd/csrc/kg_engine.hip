@@ -1422,6 +1422,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     constexpr int POD_DW = (int)(sizeof(kg_pod_dev) / 4);
     static_assert(sizeof(kg_pod_dev) % 4 == 0 && POD_DW <= KG_RESOLVE_THREADS, "pod rows are staged one dword per thread");
     __shared__ int32_t touched[KG_MAX_CHUNK];
+    __shared__ uint8_t ttile[KG_MAX_TILES];   // the tile holds a touched node (the key lists of others are exact)
     __shared__ int32_t rescan[KG_MAX_TILES];
     __shared__ unsigned long long red[KG_RESOLVE_THREADS / 64];
     __shared__ int64_t redo[KG_RESOLVE_THREADS / 64];
@@ -1468,6 +1469,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         n_rescan[0] = n_rescan[1] = 0;
         n_slow = *slow_count;
     }
+    for (int t = tid; t < tiles_total; t += KG_RESOLVE_THREADS) ttile[t] = 0;
     if (tid < POD_DW && n > 0) reinterpret_cast<uint32_t *>(&lpod[0])[tid] = reinterpret_cast<const uint32_t *>(pods + pod_begin)[tid];
     load_keys(0, kcur);
     __syncthreads();
@@ -1501,7 +1503,8 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 if (!k) continue;
                 const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
                 bool hit = false;
-                for (int q = 0; q < nt; q++) hit |= touched[q] == node;
+                if (ttile[t])
+                    for (int q = 0; q < nt; q++) hit |= touched[q] == node;
                 if (hit) rescan[atomicAdd(&n_rescan[par], 1)] = t;
                 else best = best > k ? best : k;
                 continue;
@@ -1511,6 +1514,11 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             // (fully unrolled: the list stays in registers)
             unsigned long long cand = 0;
             bool found = false, ended = false;
+            if (!ttile[t]) {   // no touched node in the tile: its best key stands
+                cand = decode_partial(kcur[0], t);
+                best = best > cand ? best : cand;
+                continue;
+            }
 #pragma unroll
             for (int s = 0; s < KG_TOPK; s++) {
                 const unsigned long long k = decode_partial(kcur[s], t);
@@ -1583,11 +1591,17 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         }
         // Reserve.  The Reservation nomination (restore) and NodeNUMAResource's zone commit (its
         // amplified-cpu filter) read the pre-Reserve node, so they go first when enabled.
+        // the node's canonical row, staged into LDS by one wave (a single coalesced round trip): the
+        // Reserve parts below update and re-derive from this copy and store their fields back
         kg_node_row &srow = nrow[KG_NCACHE];
-        if (numa_on) {   // stage the node's row for the zone commit
-            if (tid < ROW_U4) reinterpret_cast<uint4 *>(&srow)[tid] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
-            __syncthreads();
+        uint32_t old_df = 0;
+        int64_t old_metric = 0;
+        if (tid == 0) {   // the planes tid 0 needs, in flight with the row
+            old_df = pl.dflags[node];
+            old_metric = pl.metric_ns[node];
         }
+        if (tid < ROW_U4) reinterpret_cast<uint4 *>(&srow)[tid] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
+        __syncthreads();
         if ((ra.rsv && ra.n_rn > 0) || numa_on) {
             if (tid == 0) {
                 rsv_commit(pl, ra, pd, node);
@@ -1606,13 +1620,18 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         kg_node_row &row = pl.rows[node];
         if (tid >= 64 && tid < 64 + KG_NUM_RES) {
             const int r = tid - 64;
-            const int64_t req = row.requested[r] + pd.req[r];
+            const int64_t req = srow.requested[r] + pd.req[r];
+            srow.requested[r] = req;
             row.requested[r] = req;
-            if (r < 2) row.nonzero_requested[r] += pd.nonzero[r];
-            if (r < 3) fl_over[r] = row.alloc[r] - req < 0 ? 1u : 0u;
+            if (r < 2) {
+                const int64_t nz = srow.nonzero_requested[r] + pd.nonzero[r];
+                srow.nonzero_requested[r] = nz;
+                row.nonzero_requested[r] = nz;
+            }
+            if (r < 3) fl_over[r] = srow.alloc[r] - req < 0 ? 1u : 0u;
             int64_t fr;
             double R, F;
-            fin[r] = kg_finalize_fit(c, pl, node, r, &fr, &R, &F);
+            fin[r] = kg_finalize_fit_r(c, pl, node, srow, r, &fr, &R, &F);
             if (ce) {
                 ce->n.free_[r] = fr;
                 ce->n.fit_R[r] = R;
@@ -1620,16 +1639,24 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             }
         } else if (tid >= 64 + KG_NUM_RES && tid < 64 + KG_NUM_RES + 2) {
             const int r = tid - 64 - KG_NUM_RES;
-            row.la_used[0][r] += pd.la_est_i[r];
-            if (pd.flags & KG_POD_PROD) row.la_used[1][r] += pd.la_est_i[r];
+            srow.la_used[0][r] += pd.la_est_i[r];
+            row.la_used[0][r] = srow.la_used[0][r];
+            if (pd.flags & KG_POD_PROD) {
+                srow.la_used[1][r] += pd.la_est_i[r];
+                row.la_used[1][r] = srow.la_used[1][r];
+            }
             if (r == 0 && c.la_extra) {   // LoadAware weights beyond cpu / memory
                 for (int x = 0; x < KG_NUM_RES - 2; x++) {
-                    row.la_used_x[0][x] += pd.la_est_x[x];
-                    if (pd.flags & KG_POD_PROD) row.la_used_x[1][x] += pd.la_est_x[x];
+                    srow.la_used_x[0][x] += pd.la_est_x[x];
+                    row.la_used_x[0][x] = srow.la_used_x[0][x];
+                    if (pd.flags & KG_POD_PROD) {
+                        srow.la_used_x[1][x] += pd.la_est_x[x];
+                        row.la_used_x[1][x] = srow.la_used_x[1][x];
+                    }
                 }
             }
             double R, F0, F1;
-            fin[KG_NUM_RES + r] = kg_finalize_la(c, pl, node, r, &R, &F0, &F1) ? 1u : 0u;
+            fin[KG_NUM_RES + r] = kg_finalize_la_r(c, pl, node, srow, r, &R, &F0, &F1) ? 1u : 0u;
             if (ce) {
                 ce->n.la_R[r] = R;
                 ce->n.la_F0[r] = F0;
@@ -1642,18 +1669,22 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             if (zi == 0) row.zone_alloc_keys = srow.zone_alloc_keys;
         } else if (tid == 0) {
             if (ra.quota && pd.quota >= 0) kg_quota_commit(ra.quota[pd.quota], pd);
-            const int32_t pc = row.pod_count + 1;
+            const int32_t pc = srow.pod_count + 1;
+            srow.pod_count = pc;
             row.pod_count = pc;
-            fl_pods_full = (int64_t)pc + 1 > (int64_t)row.allowed_pods ? 1 : 0;
-            fl_old_df = pl.dflags[node];
-            if (ce) ce->metric_ns = pl.metric_ns[node];
-            if (slot == nt) touched[n_touched++] = node;
+            fl_pods_full = (int64_t)pc + 1 > (int64_t)srow.allowed_pods ? 1 : 0;
+            fl_old_df = old_df;
+            if (ce) ce->metric_ns = old_metric;
+            if (slot == nt) {
+                touched[n_touched++] = node;
+                ttile[node / KG_TILE] = 1;
+            }
             out_node[j] = node;
             out_score[j] = (int64_t)(w >> 32) - 1;
         }
         __syncthreads();
         if (numa_on && ce && tid >= 128 && tid < 128 + ROW_U4)   // the committed row into the node cache
-            reinterpret_cast<uint4 *>(&nrow[slot])[tid - 128] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid - 128];
+            reinterpret_cast<uint4 *>(&nrow[slot])[tid - 128] = reinterpret_cast<const uint4 *>(&srow)[tid - 128];
         if (tid == 0) {   // kg_finalize_flags from the parts (metric and the static bits are unchanged)
             bool slow = false;
             uint32_t fmask = 0;
