@@ -188,3 +188,59 @@ def test_sharded_placement_reservation_quota_two_ranks_one_gpu():
     for rank, placed_ok, some_rejected in res:
         assert placed_ok, f"rank {rank}: sharded placement differs from the sequential oracle"
         assert some_rejected
+
+
+def _gpu_more_worker(rank, world, port, q, case):
+    from oracle import oracle
+
+    _init(rank, world, port)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        if case == "numa":
+            # config 3 (NodeNUMAResource) through the node-sharded placement: zone commits in the resolve
+            cl = synth.make_numa_cluster(3_000, 120, seed=73)
+            cfg = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "NodeNUMAResource"))
+            idx = np.arange(120)
+            nodes = engine.build_node_rows(cfg, cl)
+            pods = engine.build_pod_rows(cfg, cl, idx)
+            got_n, got_s = kdist.place(cfg, nodes, pods, cl.now_ns, device=dev)
+            ref_n, ref_s = oracle.schedule(cfg, cl, idx, cl.now_ns)
+            ok = np.array_equal(got_n, ref_n) and np.array_equal(got_s, ref_s)
+        else:
+            # Reservation + ElasticQuota matrix mode on each rank's shard, top-1 merged over the ranks
+            cl = synth.make_rsv_cluster(3_000, 64, seed=74, rsv_node_frac=0.3, n_quotas=6, quota_ratio=0.4)
+            cfg = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "Reservation", "ElasticQuota"))
+            idx = np.arange(64)
+            nodes = engine.build_node_rows(cfg, cl)
+            pods = engine.build_pod_rows(cfg, cl, idx)
+            eng = kdist.sharded_engine(cfg, nodes, pods, dev, reservations=cl.rsv_arr, quotas=cl.quota_arr)
+            with torch.cuda.stream(eng.torch_stream):
+                top1 = torch.zeros(len(idx), dtype=torch.int64, device=dev)
+                eng.eval_device(cl.now_ns, 0, 0, top1.data_ptr())
+                kdist.merge_top1_(top1)
+                torch.cuda.synchronize(dev)
+            eng.close()
+            ref = oracle.eval_matrix5(cfg, cl, idx, cl.now_ns)[5]
+            ok = np.array_equal(top1.cpu().numpy().view(np.uint64), ref) and bool((ref > 0).any())
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["numa", "rsv_matrix"])
+def test_sharded_more_two_ranks_one_gpu(case):
+    """NodeNUMAResource placement and Reservation matrix mode through the two-rank sharded paths."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_more_worker, args=(r, 2, port, q, case)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=110) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, ok in res:
+        assert ok, f"rank {rank}: {case} differs from the oracle"
