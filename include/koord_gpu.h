@@ -471,6 +471,15 @@ typedef struct kg_node_row {
        EstimateNode(node)[r] and the [nonProd, prod] node terms of r */
     int64_t la_alloc_x[KG_NUM_RES - 2];
     int64_t la_used_x[2][KG_NUM_RES - 2];
+    /* cpusets on a node with a NUMA topology policy (trimNUMANodeResources, allocateCPUSet): the node's
+       available CPUs, and per zone its available CPUs, the CPUs of its wholly available cores and its
+       cores with an available CPU */
+    int32_t cpuset_avail_cpus;
+    int32_t _pad_cpu;
+    int16_t zone_cpus_avail[KG_MAX_ZONES];
+    int16_t zone_cpus_full[KG_MAX_ZONES];
+    int16_t zone_cores_free[KG_MAX_ZONES];
+    int64_t _pad_row;
 } kg_node_row;
 
 /* ------------------------------------------------------------------ */

@@ -121,6 +121,8 @@ NODE_ROW = np.dtype([
     ("cpuset_milli", "<i8"), ("cpuset_amp_milli", "<i8"), ("zone_cpuset_amp", "<i8", (MAX_ZONES,)),
     ("node_cpu_bind", "<i4"), ("cpus_per_core", "<i4"), ("cpuset_full_free_cpus", "<i4"), ("cpuset_free_cores", "<i4"),
     ("la_alloc_x", "<i8", (NUM_RES - 2,)), ("la_used_x", "<i8", (2, NUM_RES - 2)),
+    ("cpuset_avail_cpus", "<i4"), ("_pad_cpu", "<i4"), ("zone_cpus_avail", "<i2", (MAX_ZONES,)),
+    ("zone_cpus_full", "<i2", (MAX_ZONES,)), ("zone_cores_free", "<i2", (MAX_ZONES,)), ("_pad_row", "<i8"),
 ], align=True)
 
 RESERVATION = np.dtype([

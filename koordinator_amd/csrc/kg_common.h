@@ -401,11 +401,11 @@ KG_HD int64_t kg_mr_i(int64_t req, int64_t cap) { return cap == 0 ? 0 : kg_qdiv(
 // resourceAllocationScorer.score (scoring.go:187-226) where only cpu / memory can be allocatable
 // (zone sums): every other resource is either native with allocatable 0 or a missing scalar key.
 KG_HD uint32_t kg_numa_score_zones(const kg_consts &c, bool most, const int64_t used[2], const int64_t total[2],
-                                   const kg_pod_dev &p) {
+                                   const kg_pod_dev &p, int64_t pod_cpu = -1) {
     int64_t s = 0, w = 0;
     for (int r = 0; r < 2; r++) {
         if (c.numa_w[r] <= 0 || total[r] == 0) continue;
-        const int64_t rq = used[r] + p.numa_req[r];
+        const int64_t rq = used[r] + ((r == KG_RES_CPU && pod_cpu >= 0) ? pod_cpu : p.numa_req[r]);
         s += (most ? kg_mr_i(rq, total[r]) : kg_lr_i(rq, total[r])) * c.numa_w[r];
         w += c.numa_w[r];
     }
@@ -612,22 +612,62 @@ KG_HD void kg_numa_fold(kg_numa_best &b, uint64_t m, bool pref, uint32_t score) 
 
 // score of a hint mask (generateResourceHints: the NUMA scorer over requested = total − available)
 template <class ZS>
-KG_HD uint32_t kg_hint_score(const kg_consts &c, const ZS &zs, const kg_pod_dev &p, uint32_t m) {
+KG_HD uint32_t kg_hint_score(const kg_consts &c, const ZS &zs, const kg_pod_dev &p, uint32_t m, int64_t pod_cpu) {
     int64_t tot[2], av[2];
     zs.sums(m, tot, av);
     const int64_t used[2] = {tot[0] - av[0], tot[1] - av[1]};
-    return kg_numa_score_zones(c, c.numa_hint_most != 0, used, tot, p);
+    return kg_numa_score_zones(c, c.numa_hint_most != 0, used, tot, p, pod_cpu);
 }
 
 // one permutation (masks a, b in index space; `full` stands for a nil hint of an empty list)
 template <class ZS>
 KG_HD void kg_numa_visit(const kg_consts &c, const ZS &zs, const kg_pod_dev &p, kg_numa_best &best,
-                         uint32_t a, bool a_hint, uint32_t b, bool b_hint, bool pref) {
+                         uint32_t a, bool a_hint, uint32_t b, bool b_hint, bool pref, int64_t pod_cpu) {
     const uint32_t m = a & b;
     if (m == 0) return;
     const bool member = (a_hint && a == m) || (b_hint && b == m);
-    kg_numa_fold(best, zs.idmask(m), pref, member ? kg_hint_score(c, zs, p, m) : 0u);
+    kg_numa_fold(best, zs.idmask(m), pref, member ? kg_hint_score(c, zs, p, m, pod_cpu) : 0u);
 }
+
+// a cpuset request on a node with a NUMA topology policy (plugin.go:297-331 → FilterByNUMANode → Allocate)
+struct kg_numa_bind {
+    int64_t need;        // numCPUsNeeded
+    int required;        // the effective required bind policy (kg_cpu_bind_policy; UNSET ⇔ not required)
+};
+
+// trimNUMANodeResources (resource_manager.go:141-169) for a required bind policy: a zone's available cpu
+// is capped by its available CPUs — after the policy's filter (whole available cores / one CPU per core)
+// when those are at least the quantity — in milli-CPUs.  Hint totals are untouched.
+struct kg_zone_trim {
+    const kg_node_row &row;
+    int64_t cap[KG_MAX_ZONES];
+    KG_HD kg_zone_trim(const kg_node_row &r, int required) : row(r) {
+        for (int i = 0; i < KG_MAX_ZONES; i++) {
+            int64_t q = i < r.n_zones ? kg_zone_avail(r, i, KG_RES_CPU) : 0;
+            if (q != 0 && required != KG_CPU_BIND_UNSET) {
+                int64_t n = r.zone_cpus_avail[i];
+                if (n * 1000 >= q)
+                    n = required == KG_CPU_BIND_FULL_PCPUS ? r.zone_cpus_full[i]
+                      : required == KG_CPU_BIND_SPREAD_BY_PCPUS ? r.zone_cores_free[i] : n;
+                if (n * 1000 < q) q = n * 1000;
+            }
+            cap[i] = q;
+        }
+    }
+    KG_HD void sums(uint32_t m, int64_t tot[2], int64_t av[2]) const {
+        kg_mask_sums(row, m, tot, av);
+        av[0] = 0;
+        for (int i = 0; i < KG_MAX_ZONES; i++)
+            if ((m >> i) & 1u) av[0] += cap[i];
+    }
+    KG_HD uint64_t idmask(uint32_t m) const { return kg_id_mask(row, m); }
+    KG_HD uint32_t next(uint32_t m, int Z) const { return kg_combo_next(m, Z); }
+    KG_HD int min_k(int r, int64_t q, int Z) const { return kg_zone_calc{row}.min_k(r, q, Z); }
+};
+
+template <class ZS>
+KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
+                         const ZS &zs, const int64_t *requested, int policy, int64_t pcpu, const kg_numa_bind *bd);
 
 // Filter + Score of NodeNUMAResource for one pair; o.zone / o.alloc are what Reserve records.
 // `requested`: NodeInfo.Requested the plugin sees (default the row's; the Reservation restore's view on a
@@ -705,10 +745,27 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
         o.score = kg_numa_score_node(c, row, p, amplified, requested, pcpu_eff);
         return;
     }
-    if (bind) {   // a cpuset on a node with a NUMA topology policy: refused at kg_pods_set / upsert
+    if (bind && reserve) {   // the Reserve of a cpuset (choosing the CPUs) is not on the engine
         o.feasible = false;
         return;
     }
+    if (bind) {   // FilterByNUMANode with the cpuset options: trimmed hints, then the zone-wise take
+        const int own = (int)(p.cpu_bind & 15u);
+        int required = own;
+        if (node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) required = KG_CPU_BIND_FULL_PCPUS;
+        else if (node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) required = KG_CPU_BIND_SPREAD_BY_PCPUS;
+        const kg_numa_bind bd{pcpu / 1000, required};
+        kg_numa_zoned(c, row, p, o, kg_zone_trim(row, required), requested, policy, pcpu_eff, &bd);
+        return;
+    }
+    kg_numa_zoned(c, row, p, o, zs, requested, policy, pcpu, (const kg_numa_bind *)nullptr);
+}
+
+// hint generation, merge, Admit, allocateResourcesByHint and the zone score (the part of Filter / Score
+// that depends on the zone provider); `pcpu`: the cpu request (a cpuset-bound pod's amplified one)
+template <class ZS>
+KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
+                         const ZS &zs, const int64_t *requested, int policy, int64_t pcpu, const kg_numa_bind *bd) {
     const int Z = row.n_zones;
     if (Z <= 0) {
         o.feasible = false;
@@ -723,7 +780,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
     for (int j = 0; j < KG_NUM_RES; j++) {
         const int r = sorted[j];
         if (!((p.numa_present >> r) & 1u)) continue;
-        const int64_t q = p.numa_req[r];
+        const int64_t q = r == KG_RES_CPU ? pcpu : p.numa_req[r];
         kg_numa_list l{r, Z, false, q};
         bool keyed = false;   // some zone's total has the resource (totalResourceNames)
         if (r <= KG_RES_MEMORY) {
@@ -756,7 +813,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
             for (uint32_t a = (1u << L[0].k) - 1u; a; a = zs.next(a, Z)) {
                 if (!kg_list_fits(zs, L[0], a)) continue;
                 if (nl == 1) {
-                    kg_numa_visit(c, zs, p, best, a, true, full, false, true);
+                    kg_numa_visit(c, zs, p, best, a, true, full, false, true, pcpu);
                     continue;
                 }
                 if (L[0].k == 1) {
@@ -769,13 +826,13 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
                         for (uint32_t b = (1u << L[1].k) - 1u; b && !hit; b = zs.next(b, Z))
                             hit = (a & b) && kg_list_fits(zs, L[1], b);
                     }
-                    if (hit) kg_numa_visit(c, zs, p, best, a, true, a, true, true);
+                    if (hit) kg_numa_visit(c, zs, p, best, a, true, a, true, true, pcpu);
                     continue;
                 }
                 // a permutation with a & b == 0 is skipped by kg_numa_visit: test that before the
                 // (zone-sum) fit of b, so disjoint hints cost a bit test, not a zone sum
                 for (uint32_t b = (1u << L[1].k) - 1u; b; b = zs.next(b, Z))
-                    if ((a & b) && kg_list_fits(zs, L[1], b)) kg_numa_visit(c, zs, p, best, a, true, b, true, true);
+                    if ((a & b) && kg_list_fits(zs, L[1], b)) kg_numa_visit(c, zs, p, best, a, true, b, true, true, pcpu);
             }
         }
         if (!best.pref && policy == KG_NUMA_BEST_EFFORT) {
@@ -786,7 +843,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
                     if (ka && !kg_list_fits(zs, L[0], a)) continue;
                     const bool pa = ka == L[0].k;
                     if (nl == 1) {
-                        kg_numa_visit(c, zs, p, best, a, ka != 0, full, false, pa && ka != 0);
+                        kg_numa_visit(c, zs, p, best, a, ka != 0, full, false, pa && ka != 0, pcpu);
                         continue;
                     }
                     const int kb0 = L[1].any ? 1 : 0, kb1 = L[1].any ? Z : 0;
@@ -794,7 +851,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
                         for (uint32_t b = kb ? (1u << kb) - 1u : full; b; b = kb ? zs.next(b, Z) : 0u) {
                             if (!(a & b) || (kb && !kg_list_fits(zs, L[1], b))) continue;
                             const bool pb = kb == L[1].k;
-                            kg_numa_visit(c, zs, p, best, a, ka != 0, b, kb != 0, pa && ka != 0 && pb && kb != 0);
+                            kg_numa_visit(c, zs, p, best, a, ka != 0, b, kb != 0, pa && ka != 0 && pb && kb != 0, pcpu);
                         }
                     }
                 }
@@ -808,6 +865,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
     }
     if (!(single && best.mask == dflt)) {   // SingleNUMANode: the all-zones hint is nil
         // allocateResourcesByHint: zones of the hint in ascending affinity id, greedily
+        // allocateResourcesByHint takes a cpuset request's original (unamplified) requests
         int64_t req[2] = {p.numa_req[0], p.numa_req[1]};
         bool want[2] = {(p.numa_present & 1u) != 0, ((p.numa_present >> 1) & 1u) != 0};
         bool inter[2] = {false, false};
@@ -840,8 +898,37 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
             return;
         }
     }
+    if (bd) {
+        // allocateCPUSet (resource_manager.go:273-360): the available CPUs (filtered by a required policy)
+        // must cover the request; each allocated zone gives min(its available CPUs, its cpu / 1000), which
+        // takeCPUs always finds, and those must add up to the request exactly; a required FullPCPUs
+        // policy needs whole cores from every zone (satisfiedRequiredCPUBindPolicy)
+        const int req_pol = bd->required;
+        const int64_t node_av = req_pol == KG_CPU_BIND_FULL_PCPUS ? row.cpuset_full_free_cpus
+                              : req_pol == KG_CPU_BIND_SPREAD_BY_PCPUS ? row.cpuset_free_cores : row.cpuset_avail_cpus;
+        bool ok = node_av >= bd->need;
+        if (ok && o.n_alloc > 0) {
+            int64_t sum = 0;
+            for (int j = 0; j < o.n_alloc; j++) {
+                const int zi = o.zone[j];
+                const int64_t zav = req_pol == KG_CPU_BIND_FULL_PCPUS ? row.zone_cpus_full[zi]
+                                  : req_pol == KG_CPU_BIND_SPREAD_BY_PCPUS ? row.zone_cores_free[zi] : row.zone_cpus_avail[zi];
+                int64_t n = o.alloc[j][0] / 1000;
+                if (zav < n) n = zav;
+                if (req_pol == KG_CPU_BIND_FULL_PCPUS && (row.cpus_per_core <= 0 || n % row.cpus_per_core != 0)) ok = false;
+                sum += n;
+            }
+            ok = ok && sum == bd->need;
+        }
+        if (!ok) {
+            o.feasible = false;
+            o.n_alloc = 0;
+            return;
+        }
+    }
     if (o.n_alloc > 0) {
-        // calculateAllocatableAndRequested (scoring.go:118-164) over the allocated zones
+        // calculateAllocatableAndRequested (scoring.go:118-164) over the allocated zones; with a cpuset the
+        // requested cpu is the node's amplified cpuset CPUs
         int64_t tot[2] = {0, 0}, used[2] = {0, 0};
         for (int j = 0; j < o.n_alloc; j++) {
             const int zi = o.zone[j];
@@ -851,7 +938,13 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
                 used[r] += u > 0 ? u : 0;
             }
         }
-        o.score = kg_numa_score_zones(c, c.numa_most != 0, used, tot, p);
+        if (bd) used[KG_RES_CPU] = row.cpuset_amp_milli;
+        o.score = kg_numa_score_zones(c, c.numa_most != 0, used, tot, p, pcpu);
+    } else if (bd) {
+        int64_t rq[KG_NUM_RES];
+        for (int r = 0; r < KG_NUM_RES; r++) rq[r] = requested[r];
+        rq[KG_RES_CPU] = row.cpuset_amp_milli;
+        o.score = kg_numa_score_node(c, row, p, false, rq, pcpu);
     } else {
         o.score = kg_numa_score_node(c, row, p, false, requested);
     }

@@ -2209,9 +2209,10 @@ RsvArgs rsv_args(const kg_engine *e) {
 }
 
 // Cpuset binding (NodeNUMAResource for LSE / LSR pods, or any cpu request on a node with a CPU bind policy)
-// is answered in matrix mode on nodes without a NUMA topology policy, where the Filter's Allocate reduces to
-// counts of free CPUs; the cpuset a Reserve takes (the CPU accumulator), cpusets on NUMA-policy nodes and
-// reservation-reserved cpusets are refused explicitly instead of being answered wrongly.
+// is answered in matrix mode, where the Filter's Allocate reduces to counts of free CPUs (node-wide without a
+// NUMA topology policy, per allocated zone with one); the cpuset a Reserve takes (the CPU accumulator), nodes
+// whose valid topology lacks CPU detail and reservation-reserved cpusets are refused explicitly instead of
+// being answered wrongly.
 kg_status bind_ready(kg_engine *e, bool placement) {
     if (!(e->cfg.enabled_plugins & KG_PLUGIN_NUMA)) return KG_OK;
     const bool any_bind = e->batch_bind || e->n_node_bind_nodes > 0;
@@ -2219,11 +2220,10 @@ kg_status bind_ready(kg_engine *e, bool placement) {
         return set_err(e, KG_ERR_UNSUPPORTED,
                        "cpuset allocation at Reserve (the CPU accumulator) is not on the engine path; evaluate "
                        "cpuset-bound pods in matrix mode (kg_eval)");
-    if (e->batch_bind && (e->n_numa_policy_nodes > 0 || e->n_no_detail_nodes > 0))
+    if (e->batch_bind && e->n_no_detail_nodes > 0)
         return set_err(e, KG_ERR_UNSUPPORTED,
-                       "cpuset-bound pods need every node without a NUMA topology policy and with CPU detail "
-                       "(%lld NUMA-policy nodes, %lld without detail)",
-                       (long long)e->n_numa_policy_nodes, (long long)e->n_no_detail_nodes);
+                       "cpuset-bound pods need CPU detail on every node with a valid CPU topology (%lld without)",
+                       (long long)e->n_no_detail_nodes);
     if (any_bind && (e->cfg.enabled_plugins & KG_PLUGIN_RESERVATION))
         return set_err(e, KG_ERR_UNSUPPORTED, "cpuset binding with Reservation (reserved cpusets) is not on the engine path");
     return KG_OK;
@@ -2411,7 +2411,7 @@ kg_status kg_snapshot_upsert(kg_engine *e, const int32_t *node_index, const kg_n
     for (int32_t k = 0; k < n; k++)
         if (node_index[k] < 0 || node_index[k] >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "node index %d out of range", node_index[k]);
     // cpuset-binding facts of the rows (bind_ready); a node CPU bind policy turns every cpu request into a
-    // cpuset request there, so it needs CPU detail and no NUMA topology policy
+    // cpuset request there, so it needs CPU detail
     std::vector<uint8_t> facts((size_t)n);
     for (int32_t k = 0; k < n; k++) {
         const kg_node_row &r = rows[k];
@@ -2420,9 +2420,8 @@ kg_status kg_snapshot_upsert(kg_engine *e, const int32_t *node_index, const kg_n
         if (opts && r.numa_policy != KG_NUMA_NONE) f |= 1;
         if (opts && r.node_cpu_bind != KG_NODE_CPU_BIND_NONE) f |= 2;
         if ((r.flags & KG_NODE_NUMA_TOPO_VALID) && r.cpus_per_core <= 0) f |= 4;
-        if ((f & 2) && (f & 5))
-            return set_err(e, KG_ERR_UNSUPPORTED, "node %d: a CPU bind policy with a NUMA topology policy or without CPU detail",
-                           node_index[k]);
+        if ((f & 2) && (f & 4))
+            return set_err(e, KG_ERR_UNSUPPORTED, "node %d: a CPU bind policy without CPU detail", node_index[k]);
         facts[k] = f;
     }
     for (int32_t k = 0; k < n; k++) {

@@ -633,9 +633,25 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
                     if (ci[c].refcount > 0) nalloc++;
                 }
                 row.cpus_per_core = nm.n_cpus / ncores;
+                // the zone of each core (its CPUs' NUMA node); −1 ⇔ a NUMA node without a zone
+                int32_t core_zone[KG_MAX_NODE_CPUS];
+                for (int32_t k = 0; k < ncores; k++) core_zone[k] = -1;
+                for (int32_t c = 0; c < nm.n_cpus; c++) {
+                    int32_t k = 0;
+                    while (core_id[k] != ci[c].core) k++;
+                    for (int z = 0; z < nm.n_zones && z < KG_MAX_ZONES; z++)
+                        if (nm.zone_id[z] == ci[c].node) core_zone[k] = z;
+                }
                 for (int32_t k = 0; k < ncores; k++) {
-                    if (core_avail[k] == row.cpus_per_core) row.cpuset_full_free_cpus += core_avail[k];
+                    const bool full = core_avail[k] == row.cpus_per_core;
+                    if (full) row.cpuset_full_free_cpus += core_avail[k];
                     if (core_avail[k] > 0) row.cpuset_free_cores++;
+                    row.cpuset_avail_cpus += core_avail[k];
+                    const int32_t z = core_zone[k];
+                    if (z < 0) continue;
+                    row.zone_cpus_avail[z] = (int16_t)(row.zone_cpus_avail[z] + core_avail[k]);
+                    if (full) row.zone_cpus_full[z] = (int16_t)(row.zone_cpus_full[z] + core_avail[k]);
+                    if (core_avail[k] > 0) row.zone_cores_free[z]++;
                 }
                 if (nalloc != nm.cpuset_cpus) return KG_ERR_INVALID_ARG;   // the count fields must agree
             }
@@ -663,16 +679,14 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
 }
 
 // whether NodeNUMAResource binds a cpuset for the pair (requestCPUBind, util.go:105-122), and whether the
-// engine answers it (a node without a NUMA topology policy, with CPU detail when the topology is valid)
+// engine answers it (with CPU detail when the topology is valid)
 static bool row_binds(const kg_config &cfg, const kg_node_row &node, const kg_pod_row &pod, bool &answered) {
     answered = true;
     if (!(cfg.enabled_plugins & KG_PLUGIN_NUMA) || (pod.flags & KG_POD_NUMA_SKIP)) return false;
     const bool opts = (node.flags & KG_NODE_NUMA_OPTIONS) != 0;
     const bool bind = (pod.flags & KG_POD_NUMA_CPU_BIND) ||
                       (opts && node.node_cpu_bind != KG_NODE_CPU_BIND_NONE && pod.numa_request[KG_RES_CPU] != 0);
-    if (bind)
-        answered = !(opts && node.numa_policy != KG_NUMA_NONE) &&
-                   !((node.flags & KG_NODE_NUMA_TOPO_VALID) && node.cpus_per_core <= 0);
+    if (bind) answered = !((node.flags & KG_NODE_NUMA_TOPO_VALID) && node.cpus_per_core <= 0);
     return bind;
 }
 

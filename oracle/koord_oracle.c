@@ -963,6 +963,119 @@ static int numa_allocate_cpuset(const kg_cluster_view *v, const kg_numa_spec *nu
     return kgo_satisfied_required_bind(&t, acc_bind(bind), got);
 }
 
+/* FilterByNUMANode + Score for a cpuset request on a node with a NUMA topology policy: the options of
+ * getResourceOptions (plugin.go:481-527: cpu request amplified), GetTopologyHints with
+ * trimNUMANodeResources for a required policy (resource_manager.go:122-169), Admit, then Allocate with
+ * the hint — allocateResourcesByHint on the untrimmed availability and allocateCPUSet (:273-360) through
+ * the CPU accumulator — and the score over calculateAllocatableAndRequested (scoring.go:118-164). */
+static int numa_pair_cpuset(const kg_config *c, const kg_cluster_view *v, const kg_node_spec *n,
+                            const kg_numa_spec *numa, int policy, const kg_resource_list *preq, int64_t pod_cpu,
+                            int need, int required, int take_policy, int excl, int64_t *score, numa_hint *hint) {
+    const int ncpu = numa->n_cpus;
+    if (ncpu <= 0 || ncpu > 1024 || numa->first_cpu < 0 || numa->first_cpu + ncpu > v->n_cpus) return 0;
+    const kg_cpu_info *ci = v->cpus + numa->first_cpu;
+    int32_t sock[1024], node[1024], core[1024], ref[1024];
+    int8_t ex[1024];
+    uint8_t reserved[1024], avail[1024], zav[1024], got[1024], result[1024];
+    for (int i = 0; i < ncpu; i++) {
+        sock[i] = ci[i].socket, node[i] = ci[i].node, core[i] = ci[i].core;
+        ref[i] = ci[i].refcount;
+        ex[i] = (int8_t)(ci[i].refcount > 0 ? acc_excl(ci[i].exclusive) : 0);
+        reserved[i] = (uint8_t)(ci[i].reserved != 0);
+    }
+    const kgo_cpu_topo t = {ncpu, sock, node, core};
+    const int max_ref = numa->max_ref_count > 0 ? numa->max_ref_count : 1;
+    kgo_available_cpus(&t, max_ref, ref, reserved, NULL, avail, NULL);
+    kg_resource_list pr = *preq;
+    pr.v[KG_RES_CPU] = pod_cpu;
+    numa_zones z, zt;
+    numa_zones_of(numa, &z);
+    zt = z;
+    if (required != KG_CPU_BIND_UNSET) {   /* trimNUMANodeResources */
+        for (int i = 0; i < zt.n; i++) {
+            const int64_t q = get(&zt.avail[i], KG_RES_CPU);
+            if (q == 0) continue;
+            int raw = 0;
+            for (int k = 0; k < ncpu; k++) {
+                zav[k] = (uint8_t)(avail[k] && node[k] == zt.id[i]);
+                raw += zav[k];
+            }
+            int cnt = raw;
+            if ((int64_t)raw * 1000 >= q) {
+                kgo_filter_required_bind(&t, acc_bind(required), zav);
+                cnt = 0;
+                for (int k = 0; k < ncpu; k++) cnt += zav[k];
+            }
+            if ((int64_t)cnt * 1000 < q) zt.avail[i].v[KG_RES_CPU] = (int64_t)cnt * 1000;
+        }
+    }
+    if (!numa_admit(c, &zt, policy, &pr, hint)) return 0;
+    kg_resource_list zg[KG_MAX_ZONES];
+    int ng, gz[KG_MAX_ZONES];
+    /* allocateResourcesByHint takes options.originalRequests for a cpuset request */
+    if (numa_allocate(&z, hint, preq, zg, &ng, gz) != 0) return 0;
+    /* allocateCPUSet */
+    if (required != KG_CPU_BIND_UNSET) kgo_filter_required_bind(&t, acc_bind(required), avail);
+    int navail = 0;
+    for (int k = 0; k < ncpu; k++) navail += avail[k];
+    if (navail < need) return 0;
+    memset(result, 0, sizeof(result));
+    int left = need;
+    if (ng > 0) {
+        int taken = 0;
+        for (int j = 0; j < ng; j++) {
+            int cnt = 0;
+            for (int k = 0; k < ncpu; k++) {
+                zav[k] = (uint8_t)(avail[k] && node[k] == z.id[gz[j]]);
+                cnt += zav[k];
+            }
+            int want = (int)(get(&zg[j], KG_RES_CPU) / 1000);
+            if (want < cnt) cnt = want;
+            if (kgo_take_preferred_cpus(&t, max_ref, zav, NULL, ref, ex, cnt, acc_bind(take_policy), acc_excl(excl), 1,
+                                        got) != 0)
+                return 0;
+            for (int k = 0; k < ncpu; k++)
+                if (got[k] && !result[k]) { result[k] = 1; taken++; }
+        }
+        left -= taken;
+        if (left != 0) return 0;
+    }
+    if (left > 0) {
+        for (int k = 0; k < ncpu; k++) zav[k] = (uint8_t)(avail[k] && !result[k]);
+        if (kgo_take_preferred_cpus(&t, max_ref, zav, NULL, ref, ex, left, acc_bind(take_policy), acc_excl(excl), 1,
+                                    got) != 0)
+            return 0;
+        for (int k = 0; k < ncpu; k++) result[k] |= got[k];
+    }
+    if (required != KG_CPU_BIND_UNSET && !kgo_satisfied_required_bind(&t, acc_bind(required), result)) return 0;
+    /* Score: the node's cpuset CPUs (amplified) as the requested cpu */
+    const int64_t cs = amplify((int64_t)numa->cpuset_cpus * 1000, numa->cpu_amplification_ratio);
+    if (ng > 0) {
+        kg_resource_list alloc, req;
+        memset(&alloc, 0, sizeof(alloc));
+        memset(&req, 0, sizeof(req));
+        for (int i = 0; i < ng; i++) {
+            int zi = gz[i];
+            if (z.has_alloc[zi]) {
+                kg_resource_list none, a;
+                memset(&none, 0, sizeof(none));
+                rl_sub_nonneg(&z.allocated[zi], &none, &a);
+                rl_add(&req, &a);
+            }
+            rl_add(&alloc, &z.total[zi]);
+        }
+        req.v[KG_RES_CPU] = cs;
+        req.present |= 1u << KG_RES_CPU;
+        *score = numa_scorer(c, c->numa_strategy, &req, &alloc, &pr);
+        return 1;
+    }
+    kg_resource_list rq = n->requested;
+    rq.v[KG_RES_CPU] = cs;
+    rq.present |= 1u << KG_RES_CPU;
+    *score = numa_scorer(c, c->numa_strategy, &rq, &n->allocatable, &pr);
+    return 1;
+}
+
 static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n,
                      const kg_numa_spec *numa, int64_t *score, numa_hint *hint) {
     kg_resource_list preq;
@@ -977,7 +1090,7 @@ static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_
     double ratio = numa ? numa->cpu_amplification_ratio : 0.0;
     int64_t pcpu = get(&preq, KG_RES_CPU);
     /* PreFilter's cpuset decision (plugin.go:232-262) for AllowUseCPUSet pods (util.go:43-50) */
-    int state_bind = 0, state_required = KG_CPU_BIND_UNSET, state_excl = KG_CPU_EXCL_UNSET;
+    int state_bind = 0, state_required = KG_CPU_BIND_UNSET, state_excl = KG_CPU_EXCL_UNSET, state_policy = KG_CPU_BIND_UNSET;
     if ((pod->label_qos == KG_QOS_LSE || pod->label_qos == KG_QOS_LSR) && kgo_priority_class(v, pod) == KG_PRIO_PROD) {
         int bind = pod->cpu_bind_preferred;
         if (bind == KG_CPU_BIND_UNSET || bind == KG_CPU_BIND_DEFAULT) bind = c->numa_default_cpu_bind_policy;
@@ -990,6 +1103,7 @@ static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_
                 state_bind = 1;
                 state_required = required;
                 state_excl = pod->cpu_exclusive;
+                state_policy = bind;
             }
         }
     }
@@ -1033,7 +1147,13 @@ static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_
         if (required != KG_CPU_BIND_UNSET && policy == KG_NUMA_NONE &&
             !numa_allocate_cpuset(v, numa, need, required, state_excl))
             return 0;
-        if (policy != KG_NUMA_NONE) return 0;   /* FilterByNUMANode for cpusets: not restated (the engine refuses it) */
+        if (policy != KG_NUMA_NONE) {
+            if (numa->n_zones == 0) return 0;   /* node(s) missing NUMA resources */
+            /* getCPUBindPolicy (util.go:85-103): the required policy, else the preferred one */
+            const int take_policy = required != KG_CPU_BIND_UNSET ? required : state_policy;
+            return numa_pair_cpuset(c, v, n, numa, policy, &preq, pod_cpu, need, required, take_policy, state_excl,
+                                    score, hint);
+        }
     }
     numa_zones z;
     if (policy != KG_NUMA_NONE) {

@@ -1,6 +1,7 @@
-"""Seeded clusters for NodeNUMAResource cpuset binding on nodes without a NUMA topology policy: nodes with
+"""Seeded clusters for NodeNUMAResource cpuset binding: nodes with
 reported CPU topologies (1–2 sockets, 1–2 NUMA nodes per socket, 2–8 cores per NUMA node, 1–2 threads
-per core; some with sparse core ids socket << 16 | core), node allocations (refcounts up to MaxRefCount,
+per core; some with sparse core ids socket << 16 | core), a NUMA topology policy on some of them (one zone
+per NUMA node, zone allocations), node allocations (refcounts up to MaxRefCount,
 exclusive policies), reserved CPUs, node CPU bind policies, cpu amplification ratios, invalid / missing
 topologies; pods that bind cpusets (LSE / LSR prod, required / preferred / default / exclusive policies,
 whole and fractional cpu requests) and pods that a node's CPU bind policy binds."""
@@ -28,7 +29,7 @@ def _topology(rng):
     return out
 
 
-def make_bind_cluster(n_nodes: int, n_pods: int, seed: int):
+def make_bind_cluster(n_nodes: int, n_pods: int, seed: int, numa_frac: float = 0.35):
     rng = np.random.default_rng(seed)
     cl = Cluster()
     for j in range(n_nodes):
@@ -51,6 +52,16 @@ def make_bind_cluster(n_nodes: int, n_pods: int, seed: int):
             held = len(alloc)
             node.reserved_cpus = [int(c) for c in rng.choice(ncpu, size=int(rng.integers(0, 3)), replace=False)]
             node.cpu_bind_policy = str(rng.choice(NODE_BIND))
+            if rng.random() < numa_frac:   # a NUMA topology policy: one zone per NUMA node of the detail
+                node.numa_policy = str(rng.choice(["BestEffort", "Restricted", "SingleNUMANode"]))
+                ids = sorted({nd for _, nd, _ in detail})
+                per = {i: sum(1 for _, nd, _ in detail if nd == i) for i in ids}
+                node.numa_zones = [{"cpu": f"{per[i]}", "memory": f"{per[i] * 4}Gi"} for i in ids]
+                node.numa_zone_ids = ids
+                zheld = {i: sum(1 for c in alloc if detail[c][1] == i) for i in ids}
+                node.numa_allocated = {i: {"cpu": f"{zheld[i] * 1000 + int(rng.integers(0, 2)) * 500}m",
+                                           "memory": f"{int(rng.integers(0, per[i] * 3))}Gi"}
+                                       for i in ids if rng.random() < 0.8}
         elif kind < 0.93:  # reported but invalid topology
             node.numa_zones = []
             node.cpu_topology_valid = False

@@ -1,7 +1,7 @@
-"""NodeNUMAResource cpuset binding through kg_eval on the GPU (matrix mode, nodes without a NUMA topology
-policy) against the oracle's literal Allocate (CPU accumulator pinned by cpu_accumulator_test.go), with
-NodeResourcesFit and LoadAwareScheduling in the profile; the paths the engine does not take (Reserve of a
-cpuset, cpusets on NUMA-policy nodes) are refused, not answered."""
+"""NodeNUMAResource cpuset binding through kg_eval on the GPU (matrix mode; nodes with and without a NUMA
+topology policy) against the oracle's literal Allocate (CPU accumulator pinned by cpu_accumulator_test.go),
+with NodeResourcesFit and LoadAwareScheduling in the profile; the path the engine does not take (the Reserve
+of a cpuset) is refused, not answered."""
 import numpy as np
 import pytest
 
@@ -20,9 +20,10 @@ def _cfg(**kw):
     return cfg
 
 
-@pytest.mark.parametrize("seed,n_nodes,n_pods", [(1, 300, 96), (2, 1100, 70), (3, 64, 200)])
-def test_bind_matrix_matches_oracle(seed, n_nodes, n_pods):
-    cl, view, idx = make_bind_cluster(n_nodes, n_pods, seed)
+@pytest.mark.parametrize("seed,n_nodes,n_pods,numa_frac", [(1, 300, 96, 0.35), (2, 1100, 70, 0.35), (3, 64, 200, 0.35),
+                                                            (5, 700, 90, 1.0)])
+def test_bind_matrix_matches_oracle(seed, n_nodes, n_pods, numa_frac):
+    cl, view, idx = make_bind_cluster(n_nodes, n_pods, seed, numa_frac=numa_frac)
     cfg = _cfg()
     with engine.Engine(cfg) as eng:
         eng.load_snapshot(engine.build_node_rows(cfg, view))
@@ -54,16 +55,12 @@ def test_bind_placement_is_refused():
 
 
 def test_numa_plugin_filter_kat_gpu():
-    """TestPlugin_Filter (plugin_test.go:552-899) through kg_eval; the SingleNUMANode cases are refused."""
+    """TestPlugin_Filter (plugin_test.go:552-899) through kg_eval, the SingleNUMANode cpuset cases included."""
     from test_numa_plugin_filter_kat import DOC, _cluster
     for case in DOC["cases"]:
         cfg, view, pi = _cluster(case)
         with engine.Engine(cfg) as eng:
             eng.load_snapshot(engine.build_node_rows(cfg, view))
             eng.set_pods(engine.build_pod_rows(cfg, view, [pi]))
-            if case.get("engine") == "unsupported":
-                with pytest.raises(engine.EngineError, match="cpuset"):
-                    eng.eval(0)
-                continue
             res = eng.eval(0)
         assert bool(engine.unpack_mask(res["mask"], 1)[0, 0]) == case["want"], case["name"]

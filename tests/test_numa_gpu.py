@@ -154,7 +154,7 @@ def test_pods_set_rejects_numa_shapes_off_the_engine_path():
         bad = rows.copy()
         bad["flags"][1] |= nat.POD_NUMA_CPU_BIND
         bad["flags"][1] &= ~np.uint32(nat.POD_NUMA_SKIP)
-        eng.set_pods(bad)   # cpusets are answered only off NUMA-policy nodes: refused at evaluation
+        eng.set_pods(bad)   # cpusets need the nodes' CPU detail (these zoned nodes have none): refused at evaluation
         with pytest.raises(engine.EngineError, match="cpuset"):
             eng.eval(cl.now_ns)
         bad = rows.copy()

@@ -1,6 +1,6 @@
 """NodeNUMAResource Filter known answers with cpuset binding (TestPlugin_Filter, plugin_test.go:552-899;
-tests/golden/numa_plugin_filter_kat.json) through the oracle and the engine's per-pair code (kg_row_eval);
-the two cases on a SingleNUMANode node (FilterByNUMANode for a cpuset) are refused by the engine."""
+tests/golden/numa_plugin_filter_kat.json) through the oracle and the engine's per-pair code (kg_row_eval),
+including the two cases on a SingleNUMANode node (FilterByNUMANode for a cpuset)."""
 import pytest
 
 from kat import load
@@ -37,12 +37,7 @@ def _cluster(case):
 @pytest.mark.parametrize("case", DOC["cases"], ids=lambda c: c["name"])
 def test_numa_plugin_filter_kat(case):
     cfg, view, pi = _cluster(case)
-    if case.get("engine") != "unsupported":
-        assert bool(oracle.numa_eval(cfg, view, pi, 0)[0]) == case["want"]
+    assert bool(oracle.numa_eval(cfg, view, pi, 0)[0]) == case["want"]
     rows = engine.build_node_rows(cfg, view)
     prow = engine.build_pod_rows(cfg, view, [pi])
-    if case.get("engine") == "unsupported":
-        with pytest.raises(engine.EngineError):
-            engine.row_eval(cfg, rows, prow, 0)
-        return
     assert bool(engine.row_eval(cfg, rows, prow, 0)[0]) == case["want"]
