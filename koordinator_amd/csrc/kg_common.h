@@ -669,11 +669,26 @@ template <class ZS>
 KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                          const ZS &zs, const int64_t *requested, int policy, int64_t pcpu, const kg_numa_bind *bd);
 
+// the cpuset path with its own (trimmed) zone provider, out of line on the device: the hint enumeration
+// of k_eval_numa2 keeps its register budget for the common, unbound pods
+#if defined(__HIPCC__)
+static __host__ __device__ __noinline__
+#else
+inline
+#endif
+void kg_numa_bind_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
+                        const int64_t *requested, int policy, int64_t pcpu_eff, int required) {
+    const kg_numa_bind bd{p.numa_req[KG_RES_CPU] / 1000, required};
+    kg_numa_zoned(c, row, p, o, kg_zone_trim(row, required), requested, policy, pcpu_eff, &bd);
+}
+
 // Filter + Score of NodeNUMAResource for one pair; o.zone / o.alloc are what Reserve records.
 // `requested`: NodeInfo.Requested the plugin sees (default the row's; the Reservation restore's view on a
 // node with reservations, transformer.go:49-291 restores the snapshot NodeInfo every plugin reads).
 // `reserve`: the Reserve path (Allocate on the stored hint, plugin.go:406-416) — no Filter-only checks.
-template <class ZS>
+// BZ: answer cpusets on NUMA-policy nodes here (host, k_numa_bind_fix); the hot device kernels pass false
+// and leave those pairs infeasible for the fix-up kernel, so they carry no call into the cpuset path
+template <class ZS, bool BZ = true>
 KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                           const ZS &zs, const int64_t *requested = nullptr, bool reserve = false) {
     if (!requested) requested = row.requested;
@@ -754,8 +769,8 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
         int required = own;
         if (node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) required = KG_CPU_BIND_FULL_PCPUS;
         else if (node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) required = KG_CPU_BIND_SPREAD_BY_PCPUS;
-        const kg_numa_bind bd{pcpu / 1000, required};
-        kg_numa_zoned(c, row, p, o, kg_zone_trim(row, required), requested, policy, pcpu_eff, &bd);
+        if constexpr (BZ) kg_numa_bind_zoned(c, row, p, o, requested, policy, pcpu_eff, required);
+        else o.feasible = false;   // the caller re-evaluates these pairs (k_numa_bind_fix)
         return;
     }
     kg_numa_zoned(c, row, p, o, zs, requested, policy, pcpu, (const kg_numa_bind *)nullptr);
@@ -959,7 +974,11 @@ inline
 #endif
 void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                   const int64_t *requested = nullptr, bool reserve = false) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    kg_numa_pair_z<kg_zone_calc, false>(c, row, p, o, kg_zone_calc{row}, requested, reserve);
+#else
     kg_numa_pair_z(c, row, p, o, kg_zone_calc{row}, requested, reserve);
+#endif
 }
 
 // Reserve of NodeNUMAResource (plugin.go:375-419): record the zone allocations of the chosen node

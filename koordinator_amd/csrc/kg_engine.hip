@@ -992,6 +992,44 @@ __global__ __launch_bounds__(256) void k_eval_exact(kg_consts c, kg_planes pl, c
     }
 }
 
+// NodeNUMAResource pairs that bind a cpuset on a node with a NUMA topology policy (the trimmed-hint and
+// zone-wise-take path): k_eval_numa2 leaves them infeasible; one thread per (pod, node) re-evaluates them in
+// full and patches the mask bit, the score planes and the tile key.  Launched only when the batch or the
+// snapshot can bind cpusets and the snapshot has NUMA-policy nodes.
+__global__ __launch_bounds__(256) void k_numa_bind_fix(kg_consts c, kg_planes pl, HotArgs a, const kg_pod_dev *__restrict__ pods,
+                                                       unsigned long long *mask, uint16_t *scores, uint8_t *numa_scores,
+                                                       uint32_t *partials) {
+    const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t node = a.col_begin + col;
+    if (node >= a.node_end) return;
+    const kg_node_row &row = pl.rows[node];
+    if (!(row.flags & KG_NODE_NUMA_OPTIONS) || row.numa_policy == KG_NUMA_NONE || row.n_zones <= 0 ||
+        !(row.flags & KG_NODE_NUMA_TOPO_VALID))
+        return;
+    const BatchMasks bm{0xFFu, 0xFFu};
+    for (int p = blockIdx.y; p < a.n_pods; p += gridDim.y) {
+        const kg_pod_dev &pd = pods[p];
+        if (pd.flags & (KG_POD_NUMA_SKIP | KG_POD_NUMA_BIND_INVALID)) continue;
+        const bool bind = (pd.flags & KG_POD_NUMA_CPU_BIND) ||
+                          (row.node_cpu_bind != KG_NODE_CPU_BIND_NONE && pd.numa_req[KG_RES_CPU] != 0);
+        if (!bind) continue;
+        NodeRegs n;
+        load_node(c, pl, node, true, bm, a.now_ns, n);
+        uint32_t fit = 0, la = 0;
+        bool ok = eval_pair(c, pl, pd, n, node, a.now_ns, fit, la);
+        kg_numa_out o;
+        kg_numa_pair_z<kg_zone_calc, true>(c, row, pd, o, kg_zone_calc{row});
+        ok = ok && o.feasible;
+        if (scores) scores[(int64_t)p * a.score_stride + col] = (uint16_t)(fit | (la << 8));
+        if (numa_scores) numa_scores[(int64_t)p * a.score_stride + col] = (uint8_t)o.score;
+        if (ok) {
+            if (mask) atomicOr(&mask[(int64_t)p * a.mask_words + (col >> 6)], 1ull << (col & 63));
+            const uint32_t key = ((total_of(c, fit, la, o.score) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - (node % KG_TILE));
+            atomicMax(&partials[(int64_t)p * a.tiles_total + node / KG_TILE], key);
+        }
+    }
+}
+
 // NodeNUMAResource enabled (config 3; matrix mode and placement chunks), pod per lane: a wave holds 64 pods and walks 256 nodes of a tile one
 // node at a time, so every node-side value (derived planes, canonical row with its zones) is
 // wave-uniform (one cache line per load, served to all 64 pods) and the NUMA hint enumeration runs
@@ -1058,7 +1096,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                 asm volatile("" ::: "memory");
             }
             kg_numa_out o;   // a node without zones returns before the hint enumeration reads the table
-            kg_numa_pair_z(c, row, pd, o, kg_zone_tab{zt});
+            kg_numa_pair_z<kg_zone_tab, false>(c, row, pd, o, kg_zone_tab{zt});
             ok = ok && o.feasible;
             nsc = o.score;
         }
@@ -2142,6 +2180,13 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
                                e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr);
         }
         HIP_TRY(e, hipGetLastError());
+        if (!topk && e->n_numa_policy_nodes > 0 && (e->batch_bind || e->n_node_bind_nodes > 0)) {
+            const int64_t width = e->shard_end - e->shard_begin;
+            dim3 grid((unsigned)((width + 255) / 256), (unsigned)(n < 65535 ? n : 65535));
+            hipLaunchKernelGGL(k_numa_bind_fix, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
+                               (unsigned long long *)mask, scores, numa_scores, partials);
+            HIP_TRY(e, hipGetLastError());
+        }
         if (e->profiling) {
             HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
             e->ev_count++;
