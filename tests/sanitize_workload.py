@@ -105,4 +105,23 @@ for a, b in zip(got, ref):
 cfg_all = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "Reservation", "NodeNUMAResource",
                                    "ElasticQuota"), weight_numa=2)
 oracle.schedule2(cfg_all, cl, np.arange(16), cl.now_ns)
+# cpuset binding, with and without NUMA topology policies (the oracle's accumulator and zone-wise take)
+from bind_cases import bind_config, make_bind_cluster  # noqa: E402
+cl, view, idx = make_bind_cluster(14, 18, 5, numa_frac=0.5)
+cfg = bind_config()
+nodes = engine.build_node_rows(cfg, view)
+pods = engine.build_pod_rows(cfg, view, idx)
+for i, pi in enumerate(idx):
+    for j in range(len(nodes)):
+        ok, score = oracle.numa_eval(cfg, view, pi, j)
+        got = engine.row_eval(cfg, nodes[j:j + 1], pods[i:i + 1], 0)
+        assert (bool(got[0]), got[3] if got[0] else 0) == (bool(ok), score if ok else 0)
+
+# LoadAware resourceWeights beyond cpu / memory (the exact pair path)
+cl = synth.make_la_extra_cluster(40, 12, seed=6)
+cfg = make_config(plugins=("NodeResourcesFit", "LoadAwareScheduling"),
+                  resource_weights={"cpu": 1, "memory": 1, "ephemeral-storage": 1, "example.com/gpu": 2})
+got = pairs(cfg, cl, 12, 40)
+m, f, la = oracle.eval_matrix(cfg, cl, np.arange(12), cl.now_ns)
+assert (got[0].astype(bool) == m).all() and (got[1] == f).all() and (got[2] == la).all()
 print("sanitize workload ok")
