@@ -53,7 +53,8 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 6
+#define KG_ABI_VERSION 7
+#define KG_QUOTA_MAX_DEPTH 64 /* longest kg_quota parent chain (cycles are rejected) */
 
 /* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
 #define KG_PLACE_CHUNK_MAX 1024
@@ -224,7 +225,8 @@ typedef struct kg_config {
 
     /* Reservation (profile weight, config/manager/scheduler-config.yaml:82-91 ships 5000) */
     int32_t weight_reservation;
-    /* ElasticQuotaArgs.EnableCheckParentQuota (must be 0: parent recursion is not modelled) */
+    /* ElasticQuotaArgs.EnableCheckParentQuota: PreFilter also checks every ancestor group below the root
+     * (plugin.go:250-252, plugin_helper.go:281-297 checkQuotaRecursive) */
     int32_t eq_check_parent_quota;
 } kg_config;
 
@@ -375,6 +377,11 @@ typedef struct kg_quota {
     kg_resource_list used;                 /* Used */
     kg_resource_list min;                  /* CalculateInfo.Min (non-preemptible gate) */
     kg_resource_list non_preemptible_used; /* NonPreemptibleUsed */
+    /* ParentName as an index into the same list; -1 ⇔ the parent is the root quota (or is not tracked).
+     * Reserve adds the pod's requests to the group and every ancestor (group_quota_manager.go:227-238,
+     * :334-354); kg_quota_set rejects indices out of range and chains deeper than KG_QUOTA_MAX_DEPTH. */
+    int32_t parent;
+    int32_t _pad;
 } kg_quota;
 
 typedef struct kg_cluster_view {

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 NUM_RES = 8
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
  RES_EXTENDED) = range(8)
@@ -132,7 +132,7 @@ RESERVATION = np.dtype([
 
 QUOTA = np.dtype([
     ("used_limit", RESOURCE_LIST), ("used", RESOURCE_LIST), ("min", RESOURCE_LIST),
-    ("non_preemptible_used", RESOURCE_LIST),
+    ("non_preemptible_used", RESOURCE_LIST), ("parent", "<i4"), ("_pad", "<i4"),
 ], align=True)
 
 RSV_RESTORED = np.dtype([

@@ -41,7 +41,8 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
                 weight_numa: int = 1, numa_strategy: str = "LeastAllocated",
                 numa_hint_strategy: str = "LeastAllocated", numa_resources: Optional[Dict[str, int]] = None,
                 numa_default_cpu_bind_policy: str = "FullPCPUs",
-                weight_reservation: int = 1, device: int = 0, place_chunk: int = 16) -> np.ndarray:
+                weight_reservation: int = 1, eq_check_parent_quota: int = 0, device: int = 0,
+                place_chunk: int = 16) -> np.ndarray:
     c = np.zeros((), dtype=nat.CONFIG)
     c["abi_version"] = nat.ABI_VERSION
     bits = 0
@@ -91,6 +92,7 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
     c["weight_reservation"] = weight_reservation  # profile weight (the shipped profile: 5000)
     c["device"] = device
     c["place_chunk"] = place_chunk
+    c["eq_check_parent_quota"] = eq_check_parent_quota  # ElasticQuotaArgs.EnableCheckParentQuota
     return c
 
 

@@ -1304,9 +1304,15 @@ KG_HD bool kg_quota_leq(const kg_pod_dev &p, const kg_resource_list &used, const
             return false;
     return true;
 }
-KG_HD bool kg_quota_pass(const kg_quota &q, const kg_pod_dev &p) {
+// the pod's group g; with EnableCheckParentQuota also checkQuotaRecursive (plugin_helper.go:281-297):
+// every ancestor below the root passes used + request ≤ usedLimit (kg_quota_set bounds the chains)
+KG_HD bool kg_quota_pass(const kg_quota *qs, int32_t g, const kg_pod_dev &p, bool check_parent) {
+    const kg_quota &q = qs[g];
     if (!kg_quota_leq(p, q.used, q.used_limit)) return false;
     if ((p.flags & KG_POD_NON_PREEMPTIBLE) && !kg_quota_leq(p, q.non_preemptible_used, q.min)) return false;
+    if (check_parent)
+        for (int32_t a = q.parent, d = 0; a >= 0 && d < KG_QUOTA_MAX_DEPTH; a = qs[a].parent, d++)
+            if (!kg_quota_leq(p, qs[a].used, qs[a].used_limit)) return false;
     return true;
 }
 KG_HD void kg_rl_add_pod(kg_resource_list &l, const kg_pod_dev &p) {
@@ -1314,7 +1320,10 @@ KG_HD void kg_rl_add_pod(kg_resource_list &l, const kg_pod_dev &p) {
         if ((p.numa_present >> q) & 1u) l.v[q] = kg_rl_get(l, q) + p.numa_req[q];
     l.present |= p.numa_present;
 }
-KG_HD void kg_quota_commit(kg_quota &q, const kg_pod_dev &p) {
-    kg_rl_add_pod(q.used, p);
-    if (p.flags & KG_POD_NON_PREEMPTIBLE) kg_rl_add_pod(q.non_preemptible_used, p);
+// ReservePod → updateGroupDeltaUsedNoLock: the group and all its ancestors (group_quota_manager.go:227-238)
+KG_HD void kg_quota_commit(kg_quota *qs, int32_t g, const kg_pod_dev &p) {
+    for (int32_t a = g, d = 0; a >= 0 && d <= KG_QUOTA_MAX_DEPTH; a = qs[a].parent, d++) {
+        kg_rl_add_pod(qs[a].used, p);
+        if (p.flags & KG_POD_NON_PREEMPTIBLE) kg_rl_add_pod(qs[a].non_preemptible_used, p);
+    }
 }

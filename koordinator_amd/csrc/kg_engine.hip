@@ -1235,7 +1235,7 @@ struct RsvArgs {
     const int32_t *rfirst;      // [n_rn + 1] first slot of each reservation node
     const int32_t *rnode;       // [n_rn] node of each reservation node (ascending)
     int32_t n_rn;
-    int32_t _pad;
+    int32_t quota_parent;       // ElasticQuotaArgs.EnableCheckParentQuota
     unsigned long long *E;      // [pods][n_rn]
     int64_t *O;                 // [pods][n_rn]
     kg_quota *quota;            // ElasticQuota groups (nullptr: ElasticQuota off)
@@ -1375,11 +1375,11 @@ __global__ __launch_bounds__(256) void k_rsv_reduce(kg_consts c, RsvArgs ra, int
 
 // ElasticQuota PreFilter of pods [0, P) against the current quota state
 // gate[p]: ElasticQuota PreFilter; gate[P + p]: the plain (reservation-less) nodes are open to the pod
-__global__ void k_pod_gate(const kg_quota *__restrict__ quota, const kg_pod_dev *__restrict__ pods, int32_t P,
-                           uint8_t *__restrict__ gate) {
+__global__ void k_pod_gate(const kg_quota *__restrict__ quota, int32_t check_parent, const kg_pod_dev *__restrict__ pods,
+                           int32_t P, uint8_t *__restrict__ gate) {
     const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
-    const bool q = !quota || pods[p].quota < 0 || kg_quota_pass(quota[pods[p].quota], pods[p]);
+    const bool q = !quota || pods[p].quota < 0 || kg_quota_pass(quota, pods[p].quota, pods[p], check_parent != 0);
     gate[p] = q ? 1 : 0;
     gate[P + p] = (q && !(pods[p].flags & KGP_RSV_REQUIRED)) ? 1 : 0;
 }
@@ -1415,7 +1415,7 @@ __device__ __forceinline__ void rsv_commit(const kg_planes &pl, const RsvArgs &r
 __device__ __forceinline__ void rsv_quota_commit(const kg_planes &pl, const RsvArgs &ra, const kg_pod_dev &p,
                                                  int32_t node) {
     rsv_commit(pl, ra, p, node);
-    if (ra.quota && p.quota >= 0) kg_quota_commit(ra.quota[p.quota], p);
+    if (ra.quota && p.quota >= 0) kg_quota_commit(ra.quota, p.quota, p);
 }
 
 // Sequential commit of pods [pod_begin, pod_begin + n) given their per-tile partial keys.
@@ -1515,7 +1515,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         const int par = j & 1;
         const kg_pod_dev &pd = lpod[par];
         if (tid == 0)  // ElasticQuota PreFilter on the quota state after every earlier Reserve (read after the sync below)
-            gate_ok[par] = !ra.quota || pd.quota < 0 || kg_quota_pass(ra.quota[pd.quota], pd);
+            gate_ok[par] = !ra.quota || pd.quota < 0 || kg_quota_pass(ra.quota, pd.quota, pd, ra.quota_parent != 0);
         // prefetch pod j + 1 (its slot's last reader, pod j − 1, is past this pod's first barrier... see the
         // note above: a barrier-free pod j − 1 reads its row only before its own second barrier)
         if (j + 1 < n && tid >= KG_RESOLVE_THREADS - POD_DW)
@@ -1706,7 +1706,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             row.zone_allocated[zi][1] = srow.zone_allocated[zi][1];
             if (zi == 0) row.zone_alloc_keys = srow.zone_alloc_keys;
         } else if (tid == 0) {
-            if (ra.quota && pd.quota >= 0) kg_quota_commit(ra.quota[pd.quota], pd);
+            if (ra.quota && pd.quota >= 0) kg_quota_commit(ra.quota, pd.quota, pd);
             const int32_t pc = srow.pod_count + 1;
             srow.pod_count = pc;
             row.pod_count = pc;
@@ -2250,6 +2250,7 @@ RsvArgs rsv_args(const kg_engine *e) {
         ra.O = e->rsv_o;
     }
     if (e->consts.plugins & KG_PLUGIN_ELASTICQUOTA) ra.quota = e->quota;
+    ra.quota_parent = e->cfg.eq_check_parent_quota != 0;
     return ra;
 }
 
@@ -2679,7 +2680,7 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     if (st) return st;
     const bool gated = (ra.quota || ra.rsv) && P > 0;
     if (gated) {
-        hipLaunchKernelGGL(k_pod_gate, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, e->stream, ra.quota, e->pods, P,
+        hipLaunchKernelGGL(k_pod_gate, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, e->stream, ra.quota, ra.quota_parent, e->pods, P,
                            e->gate);
         HIP_TRY(e, hipGetLastError());
     }
@@ -2915,6 +2916,13 @@ kg_status kg_quota_set(kg_engine *e, const kg_quota *q, int32_t n) {
     if (st) return st;
     if (!(e->consts.plugins & KG_PLUGIN_ELASTICQUOTA)) return set_err(e, KG_ERR_STATE, "ElasticQuota plugin not enabled");
     if (n < 0 || (n > 0 && !q)) return set_err(e, KG_ERR_INVALID_ARG, "bad quota list");
+    for (int32_t g = 0; g < n; g++) {  // parent chains end at the root within KG_QUOTA_MAX_DEPTH steps (no cycles)
+        int32_t a = q[g].parent, d = 0;
+        for (; a >= 0 && a < n && d < KG_QUOTA_MAX_DEPTH; a = q[a].parent) d++;
+        if (a < -1 || a >= n) return set_err(e, KG_ERR_INVALID_ARG, "quota %d: parent index %d out of range", g, a);
+        if (a >= 0) return set_err(e, KG_ERR_INVALID_ARG, "quota %d: parent chain cyclic or deeper than %d", g,
+                                   KG_QUOTA_MAX_DEPTH);
+    }
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     if (e->quota) HIP_TRY(e, hipFree(e->quota));
     e->quota = nullptr;

@@ -388,7 +388,7 @@ kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
     if (c->enabled_plugins &
         ~(KG_PLUGIN_FIT | KG_PLUGIN_LOADAWARE | KG_PLUGIN_NUMA | KG_PLUGIN_RESERVATION | KG_PLUGIN_ELASTICQUOTA))
         return fail("unsupported plugin bit");
-    if (c->eq_check_parent_quota) return fail("ElasticQuota EnableCheckParentQuota is not supported by the engine");
+    if (c->eq_check_parent_quota != 0 && c->eq_check_parent_quota != 1) return fail("eq_check_parent_quota must be 0 or 1");
     int64_t fw = 0, lw = 0, nw = 0;
     for (int r = 0; r < KG_NUM_RES; r++) {
         if (c->fit_resource_weight[r] < 0 || c->la_resource_weight[r] < 0 || c->numa_resource_weight[r] < 0)

@@ -320,7 +320,7 @@ def make_numa_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS
 def make_rsv_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, rsv_node_frac: float = 0.10,
                      owner_classes: int = 16, n_quotas: int = 64, quota_ratio: float = 0.8,
                      owned_frac: float = 0.8, affinity_frac: float = 0.1, non_preemptible_frac: float = 0.1,
-                     max_rsv_per_node: int = 2) -> SynthView:
+                     max_rsv_per_node: int = 2, quota_tree: bool = False) -> SynthView:
     """BASELINE config 5: colocation burst of batch pods (batch-cpu / batch-memory
     requests) with Reservations and ElasticQuota.  `rsv_node_frac` of the nodes carry 1–2
     reservations of batch resources (10–30 % of the node's batch allocatable; 95 % available, 5 %
@@ -345,7 +345,7 @@ def make_rsv_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS,
         _rl_fill(arr, nat.RES_BATCH_CPU, cpu_r)
         _rl_fill(arr, nat.RES_BATCH_MEMORY, mem_r)
     quotas = _owners_and_quotas(pods, cont, seed, owner_classes, n_quotas, quota_ratio, owned_frac, affinity_frac,
-                                non_preemptible_frac)
+                                non_preemptible_frac, quota_tree)
     return SynthView(pods, cont, nodes, now_ns, reservations=rsv, quotas=quotas)
 
 
@@ -403,10 +403,11 @@ def _reservations(nodes, rng, rsv_node_frac, owner_classes, res, max_per_node=2)
 
 
 def _owners_and_quotas(pods, cont, seed, owner_classes, n_quotas, quota_ratio, owned_frac, affinity_frac,
-                       non_preemptible_frac):
+                       non_preemptible_frac, quota_tree=False):
     """Reservation owner / affinity classes, quota groups and non-preemptible flags of the pods; each
     group's runtime (used limit) is `quota_ratio` of its total demand of every requested resource
-    (min = half of it)."""
+    (min = half of it).  quota_tree: the groups form a binary heap (group g's parent is (g - 1) // 2,
+    group 0's the root) and a group's limit is `quota_ratio` of its whole subtree's demand."""
     n_pods = len(pods)
     prng = np.random.default_rng(seed + 4242)
     owned = prng.random(n_pods) < owned_frac
@@ -417,12 +418,17 @@ def _owners_and_quotas(pods, cont, seed, owner_classes, n_quotas, quota_ratio, o
     pods["quota"] = q
     pods["non_preemptible"] = prng.random(n_pods) < non_preemptible_frac
     quotas = np.zeros(n_quotas, dtype=nat.QUOTA)
+    g = np.arange(n_quotas)
+    quotas["parent"] = np.where(quota_tree & (g > 0), (g - 1) // 2, -1)
     rq = cont["requests"]
     for r in (nat.RES_CPU, nat.RES_MEMORY, nat.RES_BATCH_CPU, nat.RES_BATCH_MEMORY):
         has = (rq["present"] & np.uint32(1 << r)) != 0
         if not has.any():
             continue
         d = np.bincount(q, weights=np.where(has, rq["v"][:, r], 0), minlength=n_quotas).astype(np.int64)
+        if quota_tree:
+            for k in range(n_quotas - 1, 0, -1):
+                d[(k - 1) // 2] += d[k]
         lim = (d * int(quota_ratio * 100)) // 100 if r in (nat.RES_CPU, nat.RES_BATCH_CPU) else \
             (d // 100) * int(quota_ratio * 100)
         _rl_fill(quotas["used_limit"], r, lim)
@@ -433,7 +439,7 @@ def _owners_and_quotas(pods, cont, seed, owner_classes, n_quotas, quota_ratio, o
 def make_profile_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, rsv_node_frac: float = 0.1,
                          owner_classes: int = 16, n_quotas: int = 32, quota_ratio: float = 0.8,
                          owned_frac: float = 0.6, affinity_frac: float = 0.1, non_preemptible_frac: float = 0.1,
-                         zones=(2, 4, 8)) -> SynthView:
+                         zones=(2, 4, 8), quota_tree: bool = False) -> SynthView:
     """The shipped profile with every engine plugin (Fit, LoadAware, NodeNUMAResource, Reservation,
     ElasticQuota): config-3 nodes (NUMA zones, policy mix) and LS / batch pods, with reservations of
     cpu / memory on `rsv_node_frac` of the nodes (so the restored NodeInfo moves NodeNUMAResource's
@@ -444,7 +450,7 @@ def make_profile_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW
     rsv = _reservations(nodes, rng, rsv_node_frac, owner_classes, (nat.RES_CPU, nat.RES_MEMORY))
     pods, cont = cl.pods, cl.containers
     quotas = _owners_and_quotas(pods, cont, seed, owner_classes, n_quotas, quota_ratio, owned_frac, affinity_frac,
-                                non_preemptible_frac)
+                                non_preemptible_frac, quota_tree)
     return SynthView(pods, cont, nodes, now_ns, numa=cl.numa_arr, reservations=rsv, quotas=quotas)
 
 

@@ -1415,17 +1415,26 @@ static int quota_leq(const kg_resource_list *preq, const kg_resource_list *used,
         if (has(limit, q) && has(preq, q) && preq->v[q] + get(used, q) > limit->v[q]) return 0;
     return 1;
 }
-static int quota_prefilter(const kg_pod_spec *pod, const kg_resource_list *preq, const kg_quota *qs) {
+static int quota_prefilter(const kg_config *c, const kg_pod_spec *pod, const kg_resource_list *preq,
+                           const kg_quota *qs) {
     if (pod->quota < 0) return 1;
     const kg_quota *q = &qs[pod->quota];
     if (!quota_leq(preq, &q->used, &q->used_limit)) return 0;
     if (pod->non_preemptible && !quota_leq(preq, &q->non_preemptible_used, &q->min)) return 0;
+    /* EnableCheckParentQuota: checkQuotaRecursive (plugin_helper.go:281-297) re-checks the group, then walks
+     * ParentName until the root; the leaf re-check is the first test above */
+    if (c->eq_check_parent_quota)
+        for (int32_t a = q->parent, d = 0; a >= 0 && d < KG_QUOTA_MAX_DEPTH; a = qs[a].parent, d++)
+            if (!quota_leq(preq, &qs[a].used, &qs[a].used_limit)) return 0;
     return 1;
 }
+/* ReservePod → updateGroupDeltaUsedNoLock over getCurToAllParentGroupQuotaInfoNoLock (group_quota_manager.go:
+ * 227-238, 334-354): the group and every ancestor */
 static void quota_reserve(const kg_pod_spec *pod, const kg_resource_list *preq, kg_quota *qs) {
-    if (pod->quota < 0) return;
-    rl_add(&qs[pod->quota].used, preq);
-    if (pod->non_preemptible) rl_add(&qs[pod->quota].non_preemptible_used, preq);
+    for (int32_t a = pod->quota, d = 0; a >= 0 && d <= KG_QUOTA_MAX_DEPTH; a = qs[a].parent, d++) {
+        rl_add(&qs[a].used, preq);
+        if (pod->non_preemptible) rl_add(&qs[a].non_preemptible_used, preq);
+    }
 }
 
 /* ---------------------------------------------------------------- */
@@ -1522,7 +1531,7 @@ static int32_t oracle_pod(const kg_config *c, kg_cluster_view *vv, node_state *s
     const int rsv_on = (c->enabled_plugins & KG_PLUGIN_RESERVATION) != 0;
     kg_resource_list preq;
     numa_pod_requests(vv, pod, &preq);
-    const int gate = !(c->enabled_plugins & KG_PLUGIN_ELASTICQUOTA) || quota_prefilter(pod, &preq, quotas);
+    const int gate = !(c->enabled_plugins & KG_PLUGIN_ELASTICQUOTA) || quota_prefilter(c, pod, &preq, quotas);
     int64_t *base = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
     int64_t *raw = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
     int64_t *ord = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));

@@ -18,6 +18,11 @@ def doc():
         return json.load(f)
 
 
+def quota_config(case):
+    from koordinator_amd.config import make_config
+    return make_config(plugins=("NodeResourcesFit", "ElasticQuota"), eq_check_parent_quota=int(case.get("check_parent", 0)))
+
+
 def _rl(d):
     out = np.zeros((), dtype=nat.RESOURCE_LIST)
     for k, v in (d or {}).items():
@@ -41,9 +46,15 @@ def quota_view(case):
     pods["non_preemptible"] = 1 if case.get("non_preemptible") else 0
     cont = np.zeros(1, dtype=nat.CONTAINER)
     cont[0]["requests"] = _rl(case["pod"])
-    q = np.zeros(1, dtype=nat.QUOTA)
+    chain = case.get("parents", [])
+    q = np.zeros(1 + len(chain), dtype=nat.QUOTA)
     q[0]["used_limit"] = _rl(case["used_limit"])
     q[0]["used"] = _rl(case.get("used"))
     q[0]["min"] = _rl(case.get("min"))
     q[0]["non_preemptible_used"] = _rl(case.get("non_preemptible_used"))
+    for i, a in enumerate(chain):  # group i's parent is group i + 1; the last one's parent is the root
+        q[i + 1]["used_limit"] = _rl(a["used_limit"])
+        q[i + 1]["used"] = _rl(a.get("used"))
+    q["parent"] = np.arange(1, len(q) + 1)
+    q["parent"][-1] = -1
     return synth.SynthView(pods, cont, nodes, synth.NOW_NS, quotas=q)

@@ -80,3 +80,27 @@ def test_oracle_quota_gate_and_reserve():
             assert quota["used"]["v"][g, r] <= cl.quota_arr["used_limit"]["v"][g, r]
     # every placement on a node with a nominated reservation added to that reservation
     assert (rsv["n_assigned"] >= cl.rsv_arr["n_assigned"]).all()
+
+
+@pytest.mark.parametrize("check_parent", [0, 1])
+def test_oracle_quota_tree_reserve_and_parent_gate(check_parent):
+    """ElasticQuota over a quota tree: Reserve adds the pod's requests to its group and every ancestor
+    (updateGroupDeltaUsedNoLock); with EnableCheckParentQuota every ancestor's used stays within its
+    limit, without it only the pod's own group's does."""
+    cl = rsv_cluster(400, 300, seed=54, n_quotas=7, quota_ratio=0.5, quota_tree=True)
+    assert list(cl.quota_arr["parent"]) == [-1, 0, 0, 1, 1, 2, 2]
+    cfg = shipped_profile(plugins=RSV + ("ElasticQuota",), eq_check_parent_quota=check_parent)
+    nodes, _, _, quota = oracle.schedule2(cfg, cl, np.arange(300), cl.now_ns)
+    req = cl.containers["requests"]["v"]
+    sub = {g: {g} for g in range(7)}
+    for g in range(6, 0, -1):
+        sub[(g - 1) // 2] |= sub[g]
+    over = False
+    for g in range(7):
+        placed = (nodes >= 0) & np.isin(cl.pods["quota"], sorted(sub[g]))
+        own = (nodes >= 0) & (cl.pods["quota"] == g)
+        for r in (3, 4):
+            assert quota["used"]["v"][g, r] == req[placed, r].sum()
+            assert req[own, r].sum() <= cl.quota_arr["used_limit"]["v"][g, r]
+            over |= quota["used"]["v"][g, r] > cl.quota_arr["used_limit"]["v"][g, r]
+    assert over == (not check_parent)

@@ -231,3 +231,49 @@ def test_rsv_many_per_node_matrix_and_placement():
     ref_nodes, ref_scores, _, _ = oracle.schedule2(cfg, cl, idx, cl.now_ns)
     np.testing.assert_array_equal(nodes, ref_nodes)
     np.testing.assert_array_equal(scores, ref_scores)
+
+
+@pytest.mark.parametrize("check_parent", [0, 1])
+@pytest.mark.parametrize("chunk", [1, 16])
+def test_quota_tree_placement_matches_sequential_cycle(check_parent, chunk):
+    """A quota tree (binary heap of 15 groups): Reserve walks the ancestors, EnableCheckParentQuota gates
+    on them (k_resolve's gate and commit); quota states after the cycle equal the oracle's."""
+    cl = rsv_cluster(2000, 400, seed=67, n_quotas=15, quota_ratio=0.5, quota_tree=True)
+    cfg = shipped_profile(plugins=RSV_EQ, place_chunk=chunk, eq_check_parent_quota=check_parent)
+    idx = np.arange(400)
+    with _engine(cfg, cl, idx) as eng:
+        nodes, scores = eng.place(cl.now_ns)
+        q_after = eng.download_quotas()
+    ref_nodes, ref_scores, _, ref_q = oracle.schedule2(cfg, cl, idx, cl.now_ns)
+    assert (ref_nodes == -1).any() and (ref_nodes >= 0).any()
+    np.testing.assert_array_equal(nodes, ref_nodes)
+    np.testing.assert_array_equal(scores, ref_scores)
+    np.testing.assert_array_equal(q_after["used"]["v"], ref_q["used"]["v"])
+    np.testing.assert_array_equal(q_after["non_preemptible_used"]["v"], ref_q["non_preemptible_used"]["v"])
+    np.testing.assert_array_equal(q_after["parent"], cl.quota_arr["parent"])
+
+
+def test_quota_tree_matrix_parent_gate():
+    """Matrix mode (k_pod_gate) with ancestors already near their limits: the parent check closes pods
+    whose own group has room."""
+    cl = rsv_cluster(1500, 120, seed=68, n_quotas=7, quota_ratio=0.6, quota_tree=True)
+    q = cl.quota_arr
+    q["used"] = q["used_limit"]
+    q["used"]["v"][1:] = 0
+    q["used"]["v"][0] = np.maximum(q["used_limit"]["v"][0] - 1, 0)   # the root-most group is full
+    off = _check_matrix(shipped_profile(plugins=RSV_EQ), cl, np.arange(120))[0]
+    on = _check_matrix(shipped_profile(plugins=RSV_EQ, eq_check_parent_quota=1), cl, np.arange(120))[0]
+    closed = off.any(axis=1) & ~on.any(axis=1)
+    assert closed.any() and not (on & ~off).any()
+
+
+def test_quota_set_rejects_cyclic_tree():
+    cl = rsv_cluster(64, 4, seed=69, n_quotas=3, quota_tree=True)
+    q = cl.quota_arr.copy()
+    q["parent"] = [1, 2, 0]
+    with engine.Engine(shipped_profile(plugins=RSV_EQ)) as eng:
+        with pytest.raises(RuntimeError, match="cyclic"):
+            eng.set_quotas(q)
+        q["parent"] = [-1, 5, 0]
+        with pytest.raises(RuntimeError, match="out of range"):
+            eng.set_quotas(q)
