@@ -105,6 +105,12 @@ for a, b in zip(got, ref):
 cfg_all = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "Reservation", "NodeNUMAResource",
                                    "ElasticQuota"), weight_numa=2)
 oracle.schedule2(cfg_all, cl, np.arange(16), cl.now_ns)
+# ElasticQuota tree with EnableCheckParentQuota (the oracle's ancestor walks)
+cl = synth.make_rsv_cluster(40, 30, seed=10, n_quotas=7, quota_ratio=0.4, quota_tree=True)
+cfg_tree = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "Reservation", "ElasticQuota"),
+                           eq_check_parent_quota=1)
+assert L.kg_config_validate(nat.ptr(cfg_tree), buf, 256) == 0
+oracle.schedule2(cfg_tree, cl, np.arange(30), cl.now_ns)
 # cpuset binding, with and without NUMA topology policies (the oracle's accumulator and zone-wise take)
 from bind_cases import bind_config, make_bind_cluster  # noqa: E402
 cl, view, idx = make_bind_cluster(14, 18, 5, numa_frac=0.5)
