@@ -158,8 +158,9 @@ def _gpu_rsv_worker(rank, world, port, q):
     try:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        cl = synth.make_rsv_cluster(5_000, 300, seed=72, n_quotas=8, quota_ratio=0.6)
-        cfg = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "Reservation", "ElasticQuota"))
+        cl = synth.make_rsv_cluster(5_000, 300, seed=72, n_quotas=15, quota_ratio=0.6, quota_tree=True)
+        cfg = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "Reservation", "ElasticQuota"),
+                              eq_check_parent_quota=1)
         idx = np.arange(300)
         nodes = engine.build_node_rows(cfg, cl)
         pods = engine.build_pod_rows(cfg, cl, idx)
@@ -173,8 +174,8 @@ def _gpu_rsv_worker(rank, world, port, q):
 
 @pytest.mark.gpu
 def test_sharded_placement_reservation_quota_two_ranks_one_gpu():
-    """Config 5 through the node-sharded placement: replicated reservation / quota state, per-tile
-    partial keys merged over the ranks, identical resolves."""
+    """Config 5 through the node-sharded placement: replicated reservation / quota state (a quota tree
+    with EnableCheckParentQuota), per-tile partial keys merged over the ranks, identical resolves."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
