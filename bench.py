@@ -278,8 +278,52 @@ def bench_config5(args, engine, synth, shipped_profile, dev, stream, cpu_model):
     return out
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawned_rank(rank: int, world: int, port: int) -> None:
+    """Entry of one rank started by `launch` (a fresh interpreter: nothing GPU-side is inherited)."""
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    main()
+
+
+def launch(args) -> int:
+    """`python bench.py --gpus N` without a launcher: start N ranks, one process per GPU, before this
+    process touches the GPU (torch.cuda.device_count() does not initialise it), and return the worst
+    exit code.  Under torchrun (WORLD_SIZE set) --gpus must equal WORLD_SIZE."""
+    import torch
+    import torch.multiprocessing as mp
+
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and args.gpus > ndev:
+        print(f"bench.py: --gpus {args.gpus} with backend nccl needs {args.gpus} GPUs, this node has {ndev} "
+              "(use --backend gloo to rehearse more ranks than GPUs)", file=sys.stderr)
+        return 2
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_spawned_rank, args=(r, args.gpus, port)) for r in range(args.gpus)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join()
+    codes = [p.exitcode for p in procs]
+    bad = [c for c in codes if c != 0]
+    return 0 if not bad else (bad[0] if bad[0] and bad[0] > 0 else 1)
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch(args))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}; they must agree", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
@@ -466,6 +510,9 @@ def main():
                          "traffic": None if traffic is None else int(traffic), "traffic_unit": "bytes per launch (PMC)",
                          "traffic_source": traffic_src,
                          "kernel": "k_eval3", "kernel_ms": round(k_ms, 4),
+                         "kernel_ms_source": "HIP events on the engine stream around the k_eval3 launches of each "
+                                             "timed step (kg_set_profiling), this run; rocprofv3 summaries of the "
+                                             "same command are under profiles/",
                          "algorithmic_bytes_per_launch": int(algo_bytes)},
             "cpu_baseline": cpu_baseline,
             "placement": placement,
