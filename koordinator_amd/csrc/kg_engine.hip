@@ -930,6 +930,235 @@ __global__ __launch_bounds__(KG_TILE / NPL) __attribute__((amdgpu_waves_per_eu(N
                                                     uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
     k_eval3_body<MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, KIND, NPL>(c, pl, a, descs, work, rows, mask, scores, partials);
 }
+// ---------------------------------------------------------------------------------------
+// k_mat: matrix mode WITH planes (the bench's hot launch), class-specialised like k_eval3 (same class
+// rows, same work table) but laid out for the store stream instead of the LDS:
+//   * lane l of wave w holds the ADJACENT nodes 2l, 2l+1 of the wave's 128-node segment, so one dword
+//     per lane and pod ({fit, la} of both nodes) is the pod's whole 256-B score segment: the scores go
+//     from registers straight to HBM, one global_store_dword per pod and wave, no LDS staging;
+//   * the pod row is wave-uniform: scalar loads, one pod ahead (no LDS round trip per pod);
+//   * feasibility: per pod the two ballots (even nodes, odd nodes) are parked in lane (pod mod 64) of
+//     four VGPRs by v_writelane; every 64 pods each lane bit-interleaves its pod's ballots into the two
+//     u64 mask words of the segment and stores them;
+//   * per-(pod, tile) keys: the lane's max of its two keys goes to the wave's own LDS slice; every 16
+//     pods the wave reduces them (a quad of lanes per pod) and ds_max's the result into the workgroup's
+//     per-pod key slots — no workgroup barrier inside the pod loop; the partials are written once per
+//     work item.
+// Grid: x = shard tiles padded to a multiple of the XCD count, so under the round-robin block→XCD
+// dispatch a tile always lands on the same XCD and its node planes are re-read from that XCD's L2 (a
+// placement assumption for speed only; any placement is correct).
+#define KG_MAT_KC 16                       // pods per wave-local key reduction
+#define KG_MAT_ITEM_MAX 1024               // pods per work item (the workgroup's key slots)
+#define KG_MAT_XCDS 8
+
+// the per-pod fields of a class row the pod loop reads (scalar loads: only these dwords)
+template <int NC, int NF>
+struct MatRow {
+    int64_t req[NC];
+    double pr[NF];
+    double la[2];
+    int64_t score_off;
+};
+template <int NC, int NF>
+__device__ __forceinline__ MatRow<NC, NF> load_mat_row(const kg_pod_cls_t<NC, NF> *__restrict__ p) {
+    MatRow<NC, NF> r;
+#pragma unroll
+    for (int k = 0; k < NC; k++) r.req[k] = p->req[k];
+#pragma unroll
+    for (int f = 0; f < NF; f++) r.pr[f] = p->pr[f];
+    r.la[0] = p->la[0];
+    r.la[1] = p->la[1];
+    r.score_off = p->score_off;
+    return r;
+}
+
+// spread the 16 bits of x to the even bit positions of a 32-bit word
+__device__ __forceinline__ uint32_t spread16(uint32_t x) {
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+// the 64-bit mask word of 64 consecutive nodes from the even-node and odd-node ballot halves
+__device__ __forceinline__ uint64_t interleave32(uint32_t even, uint32_t odd) {
+    const uint32_t lo = spread16(even) | (spread16(odd) << 1);
+    const uint32_t hi = spread16(even >> 16) | (spread16(odd >> 16) << 1);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// FAST: every node of the wave has all the class's scored resources (the Fit sum is a shift), unit weights
+// and the wave's whole 128-column segment inside the output rows; otherwise the generic per-node form
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool W1, bool FAST>
+__device__ __forceinline__ void mat_pods(const kg_consts &c, const kg_cls_desc &d, const kg_cls_work &w,
+                                         const kg_pod_cls_t<NC, NF> *__restrict__ rows, const ClsNode<NC, NF> (&n)[2],
+                                         const unsigned long long (&okm)[2], int64_t col0, bool in_row, bool mseg0,
+                                         bool mseg1, uint32_t kb0, uint64_t *__restrict__ mask,
+                                         uint32_t *__restrict__ scores32, uint32_t *kws, uint32_t *wkey) {
+    const int lane = threadIdx.x & 63;
+    const kg_u16x2 shifts = {(uint16_t)d.fit_shift, (uint16_t)c.la_shift};
+    const kg_u16x2 kw2 = {(uint16_t)(1u << KG_TILE_SHIFT), (uint16_t)(1u << KG_TILE_SHIFT)};
+    constexpr bool FULL = FAST;
+    MatRow<NC, NF> nxt = load_mat_row<NC, NF>(rows + w.begin);
+    // one pod: i = index in the 64-pod mask chunk, slot = index in the 16-pod key chunk
+    auto pod = [&](const int p, const uint32_t i, const int slot, uint32_t (&mb)[4]) {
+        const MatRow<NC, NF> pd = nxt;
+        nxt = load_mat_row<NC, NF>(rows + p + 1);   // one row past the class's end is padding (cls_layout)
+        unsigned long long m[2];
+        uint32_t k[2], s;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            m[j] = okm[j];
+#pragma unroll
+            for (int q = 0; q < NC; q++) m[j] &= __builtin_amdgcn_ballot_w64(pd.req[q] <= n[j].fr[q]);
+        }
+        if (FAST && W1) {
+            uint32_t h[2];
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                uint32_t sf = 0, sl = 0;
+                if (FIT_ON) {
+#pragma unroll
+                    for (int f = 0; f < NF; f++) {
+                        uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n[j].R[f], n[j].F[f]));
+                        if (MOST) q = q < 100u ? q : 100u;
+                        sf += q;
+                    }
+                }
+                if (LA_ON) {
+                    const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la[0], n[j].laR[0], n[j].laF[0]));
+                    const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la[1], n[j].laR[1], n[j].laF[1]));
+                    sl = (q0 + q1) << 16;
+                }
+                h[j] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(kg_u16x2, sf + sl) >> shifts);
+                k[j] = sel_lanes(m[j], __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h[j]), kw2, kb0 - j, false));
+            }
+            s = __builtin_amdgcn_perm(h[1], h[0], 0x06040200u);   // fit0 | la0 << 8 | fit1 << 16 | la1 << 24
+        } else {
+            uint32_t fit[2], la[2];
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                kg_pod_cls_t<NC, NF> pr;
+#pragma unroll
+                for (int f = 0; f < NF; f++) pr.pr[f] = pd.pr[f];
+                pr.la[0] = pd.la[0];
+                pr.la[1] = pd.la[1];
+                cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pr, n[j], fit[j], la[j]);
+                const uint32_t tot = W1 ? fit[j] + la[j]
+                                        : __umul24((uint32_t)c.weight_fit, fit[j]) + __umul24((uint32_t)c.weight_la, la[j]);
+                k[j] = sel_lanes(m[j], (tot << KG_TILE_SHIFT) + kb0 - j);
+            }
+            s = fit[0] | (la[0] << 8) | (fit[1] << 16) | (la[1] << 24);
+        }
+        uint32_t *dst = scores32 + ((uint64_t)(pd.score_off + col0) >> 1);
+        if (FAST || in_row) dst[lane] = s;
+        kws[slot * 64 + lane] = k[0] > k[1] ? k[0] : k[1];
+        write_lanes(mb[0], mb[1], mb[2], mb[3], i, m[0], m[1]);
+    };
+    for (int c0 = w.begin; c0 < w.end; c0 += 64) {
+        const int c1 = min(c0 + 64, w.end);
+        uint32_t mb[4] = {0u, 0u, 0u, 0u};   // ballots of pod c0 + l in lane l: even lo, even hi, odd lo, odd hi
+        for (int k0 = c0; k0 < c1; k0 += KG_MAT_KC) {
+            const int k1 = min(k0 + KG_MAT_KC, c1);
+            if (k1 - k0 == KG_MAT_KC) {
+#pragma unroll
+                for (int t = 0; t < KG_MAT_KC; t++) pod(k0 + t, (uint32_t)(k0 - c0 + t), t, mb);
+            } else {
+                for (int t = 0; t < k1 - k0; t++) pod(k0 + t, (uint32_t)(k0 - c0 + t), t, mb);
+            }
+            // the wave's keys of these pods: lane l reduces pod l / 4's quarter (l % 4) of the 64 lane keys;
+            // a wave's LDS operations complete in order, so the reads see this wave's writes
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const uint4 *src = reinterpret_cast<const uint4 *>(kws + (lane >> 2) * 64 + (lane & 3) * 16);
+            uint32_t mx = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint4 v = src[q];
+                const uint32_t a0 = v.x > v.y ? v.x : v.y, a1 = v.z > v.w ? v.z : v.w;
+                const uint32_t a2 = a0 > a1 ? a0 : a1;
+                mx = mx > a2 ? mx : a2;
+            }
+            uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+            mx = mx > o ? mx : o;
+            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x4E, 0xf, 0xf, false);            // quad_perm [2,3,0,1]
+            mx = mx > o ? mx : o;
+            if ((lane & 3) == 0 && (lane >> 2) < k1 - k0 && mx) atomicMax(&wkey[k0 - w.begin + (lane >> 2)], mx);
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+        }
+        // mask words of pods c0 .. c1−1: lane l writes pod c0 + l's two words of this segment
+        if (lane < c1 - c0) {
+            const int32_t moff = rows[c0 + lane].mask_off;
+            uint64_t *mw = mask + moff + (col0 >> 6);
+            if (mseg0) mw[0] = interleave32(mb[0], mb[2]);
+            if (mseg1) mw[1] = interleave32(mb[1], mb[3]);
+        }
+    }
+}
+
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool W1>
+__device__ __forceinline__ void mat_block(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
+                                          const kg_cls_work &w, int tile, const char *__restrict__ rows_base,
+                                          uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
+                                          uint32_t *__restrict__ partials, uint32_t *kw, uint32_t *wkey) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t wave_base = (int64_t)tile * KG_TILE + wave * 128;
+    const kg_pod_cls_t<NC, NF> *rows = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(rows_base + d.rows_offset);
+    const int np = w.end - w.begin;
+    for (int i = tid; i < np; i += KG_TILE / 2) wkey[i] = 0u;
+    ClsNode<NC, NF> n[2];
+    unsigned long long okm[2];
+    bool full_l = true;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int64_t node = wave_base + 2 * lane + j;
+        load_cls_node<NC, NF, FIT_ON, LA_ON>(c, pl, d, node, a.node_end, a.now_ns, n[j]);
+        okm[j] = __builtin_amdgcn_ballot_w64(n[j].ok);
+        full_l = full_l && (n[j].w == (1u << d.fit_shift) || node >= a.node_end);
+    }
+    const int64_t col0 = wave_base - a.col_begin;
+    const bool in_row = col0 + 2 * lane < a.score_stride;
+    const bool fast = W1 && (!FIT_ON || __all(full_l)) && __all(in_row);
+    const bool mseg0 = col0 < a.score_stride, mseg1 = col0 + 64 < a.score_stride;
+    const uint32_t kb0 = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - (uint32_t)(wave * 128 + 2 * lane);
+    uint32_t *kws = kw + wave * (KG_MAT_KC * 64);
+    uint32_t *scores32 = reinterpret_cast<uint32_t *>(scores);
+    __syncthreads();   // key slots zeroed
+    if (fast)
+        mat_pods<NC, NF, MOST, FIT_ON, LA_ON, W1, true>(c, d, w, rows, n, okm, col0, in_row, mseg0, mseg1, kb0, mask,
+                                                        scores32, kws, wkey);
+    else
+        mat_pods<NC, NF, MOST, FIT_ON, LA_ON, W1, false>(c, d, w, rows, n, okm, col0, in_row, mseg0, mseg1, kb0, mask,
+                                                         scores32, kws, wkey);
+    __syncthreads();
+    for (int i = tid; i < np; i += KG_TILE / 2)
+        partials[(int64_t)rows[w.begin + i].row * a.tiles_total + tile] = wkey[i];
+}
+
+template <bool MOST, bool FIT_ON, bool LA_ON, bool W1, int KIND>
+__global__ __launch_bounds__(KG_TILE / 2) void k_mat(kg_consts c, kg_planes pl, HotArgs a,
+                                                     const kg_cls_desc *__restrict__ descs,
+                                                     const kg_cls_work *__restrict__ work, const char *__restrict__ rows,
+                                                     uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
+                                                     uint32_t *__restrict__ partials, int32_t shard_tiles) {
+    __shared__ __attribute__((aligned(16))) uint32_t kw[(KG_TILE / 128) * KG_MAT_KC * 64];
+    __shared__ uint32_t wkey[KG_MAT_ITEM_MAX];
+    if ((int)blockIdx.x >= shard_tiles) return;   // XCD padding of the grid (whole workgroup)
+    const int tile = a.tile_begin + blockIdx.x;
+    const kg_cls_work w = work[blockIdx.y];
+    const kg_cls_desc d = descs[w.cls];
+#define KG_MAT_ARGS c, pl, a, d, w, tile, rows, mask, scores, partials, kw, wkey
+    if constexpr (KIND == 0) mat_block<2, 2, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);
+    else if constexpr (KIND == 1) mat_block<2, 4, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);
+    else if constexpr (KIND == 2) mat_block<4, 2, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);
+    else mat_block<4, 4, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);
+#undef KG_MAT_ARGS
+}
+
 // Slow nodes (outside the fp64 exactness bounds) come out of k_eval2 as infeasible with
 // zero scores; k_slow_list collects them and k_fix_slow re-evaluates those pairs exactly.
 __global__ void k_slow_list(const uint32_t *__restrict__ dflags, int64_t begin, int64_t end, int32_t *__restrict__ list,
@@ -1812,6 +2041,7 @@ struct kg_engine {
     int64_t n_numa_policy_nodes = 0, n_node_bind_nodes = 0, n_no_detail_nodes = 0;
     bool batch_bind = false;
     bool profiling = false;
+    bool mat_kernel = false;            // matrix mode with planes through k_mat (else k_eval3); KG_MATRIX_KERNEL
     // Reservation / ElasticQuota (config 5)
     void *rsv_mem = nullptr;            // slots | rfirst | rnode | E | O
     kg_reservation *rsv = nullptr;      // slots grouped by node (stable)
@@ -1869,7 +2099,7 @@ int pods_per_block_for(int64_t n_pods, int64_t tiles) {
     int64_t ppb = (n_pods * tiles + target_blocks - 1) / target_blocks;
     ppb = (ppb + KG_POD_CHUNK - 1) / KG_POD_CHUNK * KG_POD_CHUNK;
     if (ppb < KG_POD_CHUNK) ppb = KG_POD_CHUNK;
-    if (ppb > 4096) ppb = 4096;
+    if (ppb > KG_MAT_ITEM_MAX) ppb = KG_MAT_ITEM_MAX;   // k_mat's per-workgroup key slots
     return (int)ppb;
 }
 
@@ -2039,7 +2269,7 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
         }
         e->cls_kind_work[kind][1] = (int32_t)work.size() - e->cls_kind_work[kind][0];
     }
-    std::vector<char> rows(rows_bytes ? rows_bytes : 64, 0);
+    std::vector<char> rows(rows_bytes + 256, 0);   // + padding: k_mat prefetches one row past a class's end
     for (size_t c = 0; c < descs.size(); c++) {
         const kg_cls_desc &d = descs[c];
         for (int32_t j = 0; j < d.count; j++) {
@@ -2082,6 +2312,13 @@ void launch_cls_kind(kg_engine *e, dim3 grid, const HotArgs &a, const kg_cls_des
     const int32_t first = e->cls_kind_work[KIND][0], count = e->cls_kind_work[KIND][1];
     if (count == 0) return;
     grid.y = (unsigned)count;
+    if (mask && e->mat_kernel) {
+        const int32_t shard_tiles = (int32_t)grid.x;
+        grid.x = (unsigned)((shard_tiles + KG_MAT_XCDS - 1) / KG_MAT_XCDS * KG_MAT_XCDS);
+        hipLaunchKernelGGL((k_mat<MOST, FIT_ON, LA_ON, W1, KIND>), grid, dim3(KG_TILE / 2), 0, e->stream, e->consts, e->pl,
+                           a, descs, work + first, rows, mask, scores, partials, shard_tiles);
+        return;
+    }
     // matrix mode: 8-pod chunks, score segments staged in LDS and written as 1 KiB wave stores
     // two nodes per lane (four: 92 VGPRs, 5 waves per SIMD, 1.98 vs 0.88 ms per config-2 pass)
     if (mask)
@@ -2333,6 +2570,9 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
         return KG_ERR_HIP;
     }
     e->own_stream = true;
+    // measurement switch: KG_MATRIX_KERNEL=eval3 | mat selects the matrix-mode kernel with planes
+    const char *mk = getenv("KG_MATRIX_KERNEL");
+    e->mat_kernel = mk && strcmp(mk, "mat") == 0;
     *out = e;
     return KG_OK;
 }
@@ -2917,6 +3157,9 @@ kg_status kg_quota_set(kg_engine *e, const kg_quota *q, int32_t n) {
     if (!(e->consts.plugins & KG_PLUGIN_ELASTICQUOTA)) return set_err(e, KG_ERR_STATE, "ElasticQuota plugin not enabled");
     if (n < 0 || (n > 0 && !q)) return set_err(e, KG_ERR_INVALID_ARG, "bad quota list");
     for (int32_t g = 0; g < n; g++) {  // parent chains end at the root within KG_QUOTA_MAX_DEPTH steps (no cycles)
+        if (q[g].parent == g)   // the usual cause: a zero-filled record (the root is parent = -1, not 0)
+            return set_err(e, KG_ERR_INVALID_ARG,
+                           "quota %d is its own parent: a group directly under the root has parent = -1", g);
         int32_t a = q[g].parent, d = 0;
         for (; a >= 0 && a < n && d < KG_QUOTA_MAX_DEPTH; a = q[a].parent) d++;
         if (a < -1 || a >= n) return set_err(e, KG_ERR_INVALID_ARG, "quota %d: parent index %d out of range", g, a);

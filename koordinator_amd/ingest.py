@@ -45,6 +45,7 @@ CPU_TOPOLOGY = "node.koordinator.sh/cpu-topology"
 NODE_CPU_BIND_LABEL = "node.koordinator.sh/cpu-bind-policy"
 KUBELET_CPU_MANAGER_POLICY = "kubelet.koordinator.sh/cpu-manager-policy"
 POD_CPU_ALLOCS = "node.koordinator.sh/pod-cpu-allocs"
+SYSTEM_QOS_RESOURCE = "node.koordinator.sh/system-qos-resource"
 RESOURCE_SPEC = "scheduling.koordinator.sh/resource-spec"
 RESOURCE_STATUS = "scheduling.koordinator.sh/resource-status"
 CPU_BIND_POLICIES = ("", "Default", "FullPCPUs", "SpreadByPCPUs", "ConstrainedBurst")
@@ -392,9 +393,29 @@ def kubelet_cpu_policy(nrt: Optional[dict]) -> Optional[dict]:
     return json.loads(s) if s else None
 
 
+def system_qos_cpus(annotations: dict) -> List[int]:
+    """The exclusive system-QoS cpuset of GetSystemQOSResource (apis/extension/system_qos.go:35-55): the
+    cpuset of node.koordinator.sh/system-qos-resource when cpusetExclusive is absent or true; nothing for
+    a missing annotation, unparsable JSON or an unparsable cpuset (the reference logs and skips those,
+    topology_options.go:124-134)."""
+    s = (annotations or {}).get(SYSTEM_QOS_RESOURCE)
+    if s is None:
+        return []
+    try:
+        res = json.loads(s)
+    except ValueError:
+        return []
+    if not isinstance(res, dict) or res.get("cpusetExclusive", True) is False:
+        return []
+    try:
+        return parse_cpuset(res.get("cpuset") or "")
+    except ValueError:
+        return []
+
+
 def reserved_cpus_from_nrt(nrt: dict) -> List[int]:
     """TopologyOptions.ReservedCPUs (topology_options.go:119-134): kubelet-managed pod cpusets, the kubelet
-    reserved CPUs and the node reservation's reservedCPUs."""
+    reserved CPUs, the node reservation's reservedCPUs and the exclusive system-QoS cpuset."""
     ann = nrt.get("metadata", {}).get("annotations") or {}
     out = set()
     for a in json.loads(ann.get(POD_CPU_ALLOCS, "[]") or "[]"):
@@ -406,6 +427,7 @@ def reserved_cpus_from_nrt(nrt: dict) -> List[int]:
     rsv = node_reservation(ann)
     if rsv and rsv.get("reservedCPUs"):
         out.update(parse_cpuset(rsv["reservedCPUs"]))
+    out.update(system_qos_cpus(ann))
     return sorted(out)
 
 

@@ -1437,6 +1437,25 @@ static void quota_reserve(const kg_pod_spec *pod, const kg_resource_list *preq, 
     }
 }
 
+/* The quota inputs a run reads, checked once before it starts with kg_quota_set's rule: every parent
+ * in [-1, n) and not the group itself, every chain reaching the root within KG_QUOTA_MAX_DEPTH steps (so
+ * no cycle), every pod's group < n.  0 ok, -2 invalid (the walks above then never leave the array). */
+static int quota_inputs_valid(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P) {
+    if (!(c->enabled_plugins & KG_PLUGIN_ELASTICQUOTA)) return 0;
+    const int32_t n = v->n_quotas;
+    for (int32_t g = 0; g < n; g++) {
+        int32_t a = g, d = 0;
+        while (a >= 0) {
+            const int32_t up = v->quotas[a].parent;
+            if (up < -1 || up >= n || up == a || ++d > KG_QUOTA_MAX_DEPTH) return -2;
+            a = up;
+        }
+    }
+    for (int32_t p = 0; p < P; p++)
+        if (v->pods[pod_index[p]].quota >= n) return -2;
+    return 0;
+}
+
 /* ---------------------------------------------------------------- */
 /* combined per-pair evaluation and the sequential reference cycle    */
 /* ---------------------------------------------------------------- */
@@ -1668,6 +1687,7 @@ int kgo_rsv_restore(const kg_config *c, const kg_cluster_view *v, int32_t pod_i,
 int kgo_eval_matrix5(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
                      uint8_t *mask, uint8_t *fit, uint8_t *la, uint8_t *numa, uint8_t *rsv, uint64_t *top1) {
     const int32_t N = v->n_nodes;
+    if (quota_inputs_valid(c, v, pod_index, P) != 0) return -2;
     kg_cluster_view vv = *v;
     node_state *st = states_build(v, N);
     rsv_index ri;
@@ -1746,6 +1766,7 @@ static void reserve_pod(const kg_config *c, kg_cluster_view *vv, const kg_cluste
 int kgo_schedule2(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
                   int32_t *out_node, int64_t *out_score, kg_reservation *out_rsv, kg_quota *out_quota) {
     int32_t N = v->n_nodes;
+    if (quota_inputs_valid(c, v, pod_index, P) != 0) return -2;
     node_state *st = states_build(v, N);
     kg_cluster_view vv = *v;
     rsv_index ri;

@@ -58,3 +58,45 @@ def quota_view(case):
     q["parent"] = np.arange(1, len(q) + 1)
     q["parent"][-1] = -1
     return synth.SynthView(pods, cont, nodes, synth.NOW_NS, quotas=q)
+
+
+def used_tree_doc():
+    with open(os.path.join(HERE, "golden", "elasticquota_used_tree_kat.json")) as f:
+        return json.load(f)
+
+
+def used_tree_view(case):
+    """A one-node cluster with the case's groups (usedLimit / min far above every request) and its pods."""
+    names = [g["name"] for g in case["groups"]]
+    nodes = np.zeros(1, dtype=nat.NODE_SPEC)
+    nodes["numa"] = -1
+    nodes[0]["allocatable"] = _rl({"cpu": 1 << 40, "memory": 1 << 50})
+    nodes[0]["allowed_pods"] = 110
+    P = len(case["pods"])
+    pods = np.zeros(P, dtype=nat.POD_SPEC)
+    pods["n_containers"] = 1
+    pods["first_container"] = np.arange(P)
+    pods["label_priority_class"] = -1
+    pods["label_qos"] = -1
+    pods["rsv_owner_class"] = -1
+    pods["rsv_affinity_class"] = -1
+    cont = np.zeros(P, dtype=nat.CONTAINER)
+    for i, p in enumerate(case["pods"]):
+        pods[i]["quota"] = names.index(p["group"])
+        pods[i]["non_preemptible"] = 1 if p["non_preemptible"] else 0
+        cont[i]["requests"] = _rl({"cpu": p["cpu"], "memory": p["memory"]})
+    q = np.zeros(len(names), dtype=nat.QUOTA)
+    for i, g in enumerate(case["groups"]):
+        q[i]["used_limit"] = _rl({"cpu": 1 << 40, "memory": 1 << 50})
+        q[i]["min"] = _rl({"cpu": 1 << 40, "memory": 1 << 50})
+        q[i]["parent"] = -1 if g["parent"] is None else names.index(g["parent"])
+    return synth.SynthView(pods, cont, nodes, synth.NOW_NS, quotas=q), names
+
+
+def used_tree_want(case, names):
+    """want[group] → (used, nonPreemptibleUsed) as [NUM_RES] arrays."""
+    out = []
+    for name in names:
+        w = case["want"].get(name, {"used": {}, "non_preemptible_used": {}})
+        out.append((_rl(w["used"])["v"].copy(), _rl(w["non_preemptible_used"])["v"].copy()))
+    return out

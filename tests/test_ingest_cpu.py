@@ -303,3 +303,42 @@ def test_cpuset_inputs_from_objects():
         ok, _ = oracle.numa_eval(cfg, view, pi, 0)
         got = engine.row_eval(cfg, rows[0:1], engine.build_pod_rows(cfg, view, [pi]), NOW_NS)
         assert bool(ok) == bool(got[0]) == want[p.name], p.name
+
+
+@pytest.mark.parametrize("ann, reserved", [
+    (None, [0, 15]),
+    (json.dumps({"cpuset": "6-9"}), [0, 6, 7, 8, 9, 15]),                        # cpusetExclusive defaults to true
+    (json.dumps({"cpuset": "6-9", "cpusetExclusive": True}), [0, 6, 7, 8, 9, 15]),
+    (json.dumps({"cpuset": "6-9", "cpusetExclusive": False}), [0, 15]),
+    ("bad-format-str", [0, 15]),                                                 # GetSystemQOSResource error
+    (json.dumps({"cpuset": "9-6"}), [0, 15]),                                    # cpuset.Parse error
+])
+def test_system_qos_exclusive_cpuset_is_reserved(ann, reserved):
+    """NewTopologyOptions (topology_options.go:119-134) unions the exclusive system-QoS cpuset of
+    node.koordinator.sh/system-qos-resource into ReservedCPUs (system_qos.go:35-38: exclusive unless
+    cpusetExclusive is false; TestGetSystemQOSResource's "bad-format-str" is skipped); a FullPCPUs pod that
+    needs the reserved cores then fails on the engine exactly as in the oracle's literal Allocate."""
+    anns = {ingest.CPU_TOPOLOGY: _cpu_topology_ann(2, 4, 2),
+            ingest.KUBELET_CPU_MANAGER_POLICY: json.dumps({"policy": "static", "reservedCPUs": "0"}),
+            ingest.POD_CPU_ALLOCS: json.dumps([{"uid": "u1", "cpuset": "15", "managedByKubelet": True}])}
+    if ann is not None:
+        anns[ingest.SYSTEM_QOS_RESOURCE] = ann
+    nrt = {"metadata": {"name": "n", "annotations": anns},
+           "zones": [{"name": "node-0", "type": "Node", "resources": [{"name": "cpu", "allocatable": "8"}]},
+                     {"name": "node-1", "type": "Node", "resources": [{"name": "cpu", "allocatable": "8"}]}]}
+    node = _node({"cpu": "16", "memory": "64Gi", "pods": "110"}, name="n")
+    cl = ingest.cluster_from_objects([node], [], nrts=[nrt], now_ns=NOW_NS)
+    assert cl.nodes[0].reserved_cpus == reserved
+    pend = ingest.pod_from_object({"metadata": {"name": "full8", "labels": {"koordinator.sh/qosClass": "LSR"},
+                                                "annotations": {ingest.RESOURCE_SPEC: json.dumps(
+                                                    {"requiredCPUBindPolicy": "FullPCPUs"})}},
+                                   "spec": {"priority": 9999, "containers": [{"resources": {
+                                       "requests": {"cpu": "10"}, "limits": {"cpu": "10"}}}]}})
+    view = cl.view(extra_pods=[pend])
+    cfg = make_config(plugins=("NodeNUMAResource",))
+    rows = engine.build_node_rows(cfg, view)
+    pi = view.pod_index(pend)
+    ok, _ = oracle.numa_eval(cfg, view, pi, 0)
+    got = engine.row_eval(cfg, rows[0:1], engine.build_pod_rows(cfg, view, [pi]), NOW_NS)
+    # 16 CPUs, 2 per core: the whole free cores hold 12 CPUs with 0 and 15 reserved, 8 with 6-9 too
+    assert bool(ok) == bool(got[0]) == (len(reserved) == 2)

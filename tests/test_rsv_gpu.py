@@ -277,3 +277,6 @@ def test_quota_set_rejects_cyclic_tree():
         q["parent"] = [-1, 5, 0]
         with pytest.raises(RuntimeError, match="out of range"):
             eng.set_quotas(q)
+        q["parent"] = 0          # a zero-filled record: group 0 its own parent
+        with pytest.raises(RuntimeError, match="its own parent"):
+            eng.set_quotas(q)
