@@ -501,15 +501,20 @@ def node_from_object(node: dict, nrt: Optional[dict] = None) -> ob.Node:
 
 
 def cluster_from_objects(nodes: Iterable[dict], pods: Iterable[dict] = (), node_metrics: Iterable[dict] = (),
-                         nrts: Iterable[dict] = (), now_ns: int = 1_700_000_000 * 10**9) -> ob.Cluster:
+                         nrts: Iterable[dict] = (), now_ns: int = 1_700_000_000 * 10**9,
+                         assign_cache: Optional[Dict[str, Dict[str, int]]] = None) -> ob.Cluster:
     """A scheduler snapshot: nodes with the NodeInfo of their bound, non-terminated pods, NodeMetrics and
-    NodeResourceTopologies by node name; every pod also goes to the pod lister (PodsMetric lookups)."""
+    NodeResourceTopologies by node name; every pod also goes to the pod lister (PodsMetric lookups).
+    assign_cache: LoadAware's podAssignCache, node name → pod UID → assign timestamp (ns) of pods among
+    `pods` (feeders.SnapshotFeeder keeps it event by event); None leaves it empty."""
     by_nrt = {n.get("metadata", {}).get("name"): n for n in nrts}
     cl = ob.Cluster(now_ns)
     bound: Dict[str, List[ob.Pod]] = {}
     status_of: Dict[int, dict] = {}
+    by_uid: Dict[str, ob.Pod] = {}
     for pj in pods:
         p = pod_from_object(pj)
+        by_uid[(pj.get("metadata") or {}).get("uid", "")] = p
         cl.add_lister_pod(p)
         if p.node_name and not p.terminated:
             bound.setdefault(p.node_name, []).append(p)
@@ -548,4 +553,7 @@ def cluster_from_objects(nodes: Iterable[dict], pods: Iterable[dict] = (), node_
                     nonzero_requested={"cpu": f"{nz[0]}m", "memory": str(nz[1])}, pod_count=len(bound.get(n.name, [])))
     for m in node_metrics:
         cl.set_metric(m.get("metadata", {}).get("name"), node_metric_from_object(m, now_ns))
+    for node_name, items in (assign_cache or {}).items():
+        for uid, ts in sorted(items.items(), key=lambda kv: kv[1]):
+            cl.assign_at(node_name, by_uid[uid], ts)
     return cl

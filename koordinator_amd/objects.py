@@ -245,7 +245,11 @@ class Cluster:
 
     def assign(self, node_name: str, pod: Pod, age_s: float) -> "Cluster":
         """podAssignCache entry with timestamp now − age_s."""
-        self.assigned.setdefault(node_name, []).append((pod, age_s))
+        return self.assign_at(node_name, pod, self.now_ns - int(round(age_s * 10**9)))
+
+    def assign_at(self, node_name: str, pod: Pod, timestamp_ns: int) -> "Cluster":
+        """podAssignCache entry with an absolute timestamp (pod_assign_cache.go:53-68 timeNowFn())."""
+        self.assigned.setdefault(node_name, []).append((pod, int(timestamp_ns)))
         return self
 
     def name_id(self, key: str) -> int:
@@ -328,10 +332,10 @@ class Cluster:
                     fv.pod_metrics.append(rec)
                 ns["n_pod_metric"] = len(m.pods_metric)
             ns["first_assigned"] = len(fv.assigned)
-            for pod, age in self.assigned.get(n.name, []):
+            for pod, ts in self.assigned.get(n.name, []):
                 rec = np.zeros((), dtype=nat.ASSIGNED_POD)
                 rec["pod"] = fv.pod_index(pod)
-                rec["timestamp_ns"] = self.now_ns - int(round(age * 10**9))
+                rec["timestamp_ns"] = ts
                 fv.assigned.append(rec)
             ns["n_assigned"] = len(self.assigned.get(n.name, []))
             ns["numa"] = -1
