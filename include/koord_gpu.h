@@ -75,6 +75,7 @@ typedef int32_t kg_status;
 #define KG_ERR_UNSUPPORTED (-3)
 #define KG_ERR_RANGE (-4)
 #define KG_ERR_STATE (-5)
+#define KG_NOT_FOUND 1       /* a search found nothing (kg_cpuset_take: no cpuset satisfies the request) */
 
 /* upstream framework.Code values used in filter results */
 #define KG_CODE_SUCCESS 0
@@ -597,6 +598,16 @@ kg_status kg_snapshot_download(kg_engine *eng, int32_t first, int32_t n, kg_node
  * the generation reached), every other entry point fails with KG_ERR_STATE, and the caller falls back to
  * the CPU plugins until kg_snapshot_reset + upsert reload the snapshot. */
 kg_status kg_snapshot_generation(kg_engine *eng, uint64_t *out);
+
+/* NodeNUMAResource's CPU accumulator on one node's logical CPUs: the cpuset a Reserve takes
+ * (takeCPUs, nodenumaresource/cpu_accumulator.go:87-822) from `available` (per cpu id), with the node's
+ * allocated CPUs' RefCount / ExclusivePolicy from `cpus`.  bind_policy / exclusive_policy:
+ * kg_cpu_bind_policy / kg_cpu_exclusive_policy; numa_strategy: kg_scoring_strategy (NUMAAllocateStrategy).
+ * KG_OK ⇔ `need` CPUs marked in result[n_cpus]; KG_NOT_FOUND ⇔ the accumulator fails.  The engine runs the
+ * same code at Reserve in kg_place / kg_commit; exposed for host tools and tests. */
+kg_status kg_cpuset_take(const kg_cpu_info *cpus, int32_t n_cpus, int32_t max_ref_count, const uint8_t *available,
+                         int32_t need, int32_t bind_policy, int32_t exclusive_policy, int32_t numa_strategy,
+                         uint8_t *result);
 /* Restrict kg_eval/kg_place evaluation to nodes [begin, end) (node sharding across GPUs);
  * node indices stay global.  begin must be a multiple of 1024 unless the shard is empty. */
 kg_status kg_set_shard(kg_engine *eng, int32_t begin, int32_t end);

@@ -203,7 +203,7 @@ EXPORTED = [
     "kg_snapshot_download", "kg_set_shard", "kg_pods_set", "kg_eval", "kg_place", "kg_num_tiles",
     "kg_place_chunk_eval", "kg_place_chunk_resolve", "kg_commit", "kg_set_profiling", "kg_eval_kernel_times",
     "kg_rsv_set", "kg_rsv_download", "kg_quota_set", "kg_quota_download", "kg_row_eval_rsv", "kg_row_rsv_restore",
-    "kg_snapshot_generation",
+    "kg_snapshot_generation", "kg_cpuset_take",
 ]
 
 _lib = None
@@ -217,7 +217,8 @@ def lib() -> ctypes.CDLL:
     # test hook (tests/test_sanitizers_cpu.py): a sanitizer build of the host code alone; the engine
     # entry points are absent from it, so any GPU call fails
     host_only = os.environ.get("KG_SANITIZED_HOST_SO")
-    so = host_only or ENGINE_SO
+    # measurement builds of the engine (tools/ablate_mat.sh): an alternative in-tree library
+    so = host_only or os.environ.get("KG_ENGINE_SO") or ENGINE_SO
     if not os.path.exists(so):
         raise RuntimeError(f"{so} is missing: build it with `python koordinator_amd/build.py` "
                            "(there is no CPU fallback for the engine)")
@@ -245,6 +246,7 @@ def lib() -> ctypes.CDLL:
         "kg_row_eval_rsv": (i32, [vp, vp, vp, i32, vp, i64, vp, vp, vp, vp, vp, vp, vp]),
         "kg_row_rsv_restore": (i32, [vp, vp, vp, i32, vp, vp]),
         "kg_snapshot_generation": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
+        "kg_cpuset_take": (i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp]),
     }
     for name, (res, args) in sig.items():
         if host_only and not hasattr(L, name):

@@ -35,7 +35,7 @@ def _newer(target: str, sources: list[str]) -> bool:
 
 
 def engine_sources() -> list[str]:
-    names = ["kg_engine.hip", "kg_host.cpp", "kg_common.h", "kg_host.h"]
+    names = ["kg_engine.hip", "kg_host.cpp", "kg_cpuset.cpp", "kg_common.h", "kg_host.h"]
     return [os.path.join(CSRC, n) for n in names] + [os.path.join(ROOT, "include", "koord_gpu.h")]
 
 
@@ -49,10 +49,12 @@ def build_engine(force: bool = False) -> str:
     common = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
     host_obj = os.path.join(obj_dir, "kg_host.o")
     _run(["g++", *common, "-c", os.path.join(CSRC, "kg_host.cpp"), "-o", host_obj])
+    cpuset_obj = os.path.join(obj_dir, "kg_cpuset.o")
+    _run(["g++", *common, "-c", os.path.join(CSRC, "kg_cpuset.cpp"), "-o", cpuset_obj])
     dev_obj = os.path.join(obj_dir, "kg_engine.o")
     _run([hipcc, *common, f"--offload-arch={ARCH}", "-c", os.path.join(CSRC, "kg_engine.hip"), "-o", dev_obj])
     tmp = ENGINE_SO + ".tmp"
-    _run([hipcc, "-shared", f"--offload-arch={ARCH}", dev_obj, host_obj, "-o", tmp])
+    _run([hipcc, "-shared", f"--offload-arch={ARCH}", dev_obj, host_obj, cpuset_obj, "-o", tmp])
     os.replace(tmp, ENGINE_SO)
     return ENGINE_SO
 
@@ -85,9 +87,9 @@ SAN_FLAGS = ["-O1", "-g", "-fPIC", "-shared", "-ffp-contract=off", "-fno-omit-fr
 def build_sanitized(force: bool = False) -> tuple[str, str]:
     os.makedirs(SAN_DIR, exist_ok=True)
     inc = ["-I", os.path.join(ROOT, "include")]
-    host_src = os.path.join(CSRC, "kg_host.cpp")
+    host_src = [os.path.join(CSRC, "kg_host.cpp"), os.path.join(CSRC, "kg_cpuset.cpp")]
     if force or _newer(SAN_HOST_SO, engine_sources()):
-        _run(["g++", "-std=c++17", *SAN_FLAGS, *inc, host_src, "-o", SAN_HOST_SO + ".tmp"])
+        _run(["g++", "-std=c++17", *SAN_FLAGS, *inc, *host_src, "-o", SAN_HOST_SO + ".tmp"])
         os.replace(SAN_HOST_SO + ".tmp", SAN_HOST_SO)
     srcs = oracle_sources()
     if force or _newer(SAN_ORACLE_SO, [*srcs, os.path.join(ROOT, "include", "koord_gpu.h")]):

@@ -682,6 +682,16 @@ __device__ __forceinline__ uint32_t sel_lanes(unsigned long long m, uint32_t v) 
     return r;
 }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is also a release of global memory, so it waits
+// for every outstanding vector-memory operation of the wave (s_waitcnt vmcnt(0)) — including the score
+// stores, which then stall each chunk for the HBM write latency.  The pod loops share only LDS between
+// waves, so their barriers wait for lgkmcnt alone.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // v_writelane_b32 ×4: lane `lane` of mb[0..3] := the wave-uniform words (no exec change; the
 // lane select goes through M0 because a VOP3 may read only one SGPR)
 #pragma clang diagnostic push
@@ -696,6 +706,9 @@ __device__ __forceinline__ void write_lanes(uint32_t &w0, uint32_t &w1, uint32_t
 }
 #pragma clang diagnostic pop
 
+#ifndef KG_EVAL3_NT
+#define KG_EVAL3_NT 1   // non-temporal staged score stores of k_eval3 (a write-once stream)
+#endif
 // Pods [p0, p1) of one class against the lane's NPL nodes (columns 64·j + lane of the wave's segment);
 // rows come from the LDS chunk buffer.  The feasibility ballots of the chunk are collected into lanes
 // (p − p0) of 2·NPL VGPRs and written once per chunk; EDGE workgroups (the shard's last tile) check
@@ -861,7 +874,12 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
                 if (pp < np && segs) {
                     const uint4 v = *reinterpret_cast<const uint4 *>(sst + pp * SEGW + s8 * 8);
                     const int64_t off = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[pp].score_off;
+#if KG_EVAL3_NT
+                    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(scores + off + col0 + s8 * 8));
+#else
                     *reinterpret_cast<uint4 *>(scores + off + col0 + s8 * 8) = v;
+#endif
                 }
             }
         }
@@ -874,7 +892,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
             for (int j = 1; j < NPL; j++)
                 if (seg[j]) mw[j] = (uint64_t)mb[2 * j] | ((uint64_t)mb[2 * j + 1] << 32);
         }
-        __syncthreads();
+        lds_barrier();
         const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * BT + rg * CC);
         uint32_t mx = 0;
 #pragma unroll
@@ -894,7 +912,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
             const int32_t row = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[rj].row;
             partials[(int64_t)row * a.tiles_total + tile] = mx;
         }
-        __syncthreads();
+        lds_barrier();
         buf ^= 1;
     }
 }
@@ -936,9 +954,12 @@ __global__ __launch_bounds__(KG_TILE / NPL) __attribute__((amdgpu_waves_per_eu(N
 //   * lane l of wave w holds the ADJACENT nodes 2l, 2l+1 of the wave's 128-node segment, so one dword
 //     per lane and pod ({fit, la} of both nodes) is the pod's whole 256-B score segment: the scores go
 //     from registers straight to HBM, one global_store_dword per pod and wave, no LDS staging;
-//   * the pod row is wave-uniform: scalar loads, one pod ahead (no LDS round trip per pod);
+//   * class rows are staged through LDS 16 pods (a group) at a time: the next group's global load is in
+//     flight while the current group is evaluated and lands in LDS right after the group's score stores
+//     (an in-order vmcnt wait that skips the stores); the group barrier orders LDS only (lds_barrier), so
+//     no wave ever waits for its own score stores to reach HBM;
 //   * feasibility: per pod the two ballots (even nodes, odd nodes) are parked in lane (pod mod 64) of
-//     four VGPRs by v_writelane; every 64 pods each lane bit-interleaves its pod's ballots into the two
+//     four VGPRs by v_writelane; every 64 pods (four groups) each lane bit-interleaves its pod's ballots into the two
 //     u64 mask words of the segment and stores them;
 //   * per-(pod, tile) keys: the lane's max of its two keys goes to the wave's own LDS slice; every 16
 //     pods the wave reduces them (a quad of lanes per pod) and ds_max's the result into the workgroup's
@@ -950,27 +971,9 @@ __global__ __launch_bounds__(KG_TILE / NPL) __attribute__((amdgpu_waves_per_eu(N
 #define KG_MAT_KC 16                       // pods per wave-local key reduction
 #define KG_MAT_ITEM_MAX 1024               // pods per work item (the workgroup's key slots)
 #define KG_MAT_XCDS 8
-
-// the per-pod fields of a class row the pod loop reads (scalar loads: only these dwords)
-template <int NC, int NF>
-struct MatRow {
-    int64_t req[NC];
-    double pr[NF];
-    double la[2];
-    int64_t score_off;
-};
-template <int NC, int NF>
-__device__ __forceinline__ MatRow<NC, NF> load_mat_row(const kg_pod_cls_t<NC, NF> *__restrict__ p) {
-    MatRow<NC, NF> r;
-#pragma unroll
-    for (int k = 0; k < NC; k++) r.req[k] = p->req[k];
-#pragma unroll
-    for (int f = 0; f < NF; f++) r.pr[f] = p->pr[f];
-    r.la[0] = p->la[0];
-    r.la[1] = p->la[1];
-    r.score_off = p->score_off;
-    return r;
-}
+#ifndef KG_MAT_NT
+#define KG_MAT_NT 1                        // non-temporal score stores (a write-once stream)
+#endif
 
 // spread the 16 bits of x to the even bit positions of a 32-bit word
 __device__ __forceinline__ uint32_t spread16(uint32_t x) {
@@ -989,22 +992,27 @@ __device__ __forceinline__ uint64_t interleave32(uint32_t even, uint32_t odd) {
 }
 
 // FAST: every node of the wave has all the class's scored resources (the Fit sum is a shift), unit weights
-// and the wave's whole 128-column segment inside the output rows; otherwise the generic per-node form
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool W1, bool FAST>
-__device__ __forceinline__ void mat_pods(const kg_consts &c, const kg_cls_desc &d, const kg_cls_work &w,
-                                         const kg_pod_cls_t<NC, NF> *__restrict__ rows, const ClsNode<NC, NF> (&n)[2],
-                                         const unsigned long long (&okm)[2], int64_t col0, bool in_row, bool mseg0,
-                                         bool mseg1, uint32_t kb0, uint64_t *__restrict__ mask,
-                                         uint32_t *__restrict__ scores32, uint32_t *kws, uint32_t *wkey) {
+// and the wave's whole 128-column segment inside the output rows; otherwise the generic per-node form.
+// FULLG: a whole group of KG_MAT_KC pods (the pod loop unrolled).
+// Pods [g0, g1) of one group (rows in LDS at `lr`, row g0 first), the group's pods at ballot lanes
+// win·16 + t.  The next group's staged row dword is written to LDS right after this group's score stores:
+// the stores were issued after its global load and vector memory completes in issue order, so on the
+// unrolled path the wait is vmcnt(stores of the group) — the load only, never the stores' HBM latency.
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool W1, bool FAST, bool FULLG>
+__device__ __forceinline__ void mat_group(const kg_consts &c, const kg_cls_desc &d, int item0, int g0, int g1,
+                                          const kg_pod_cls_t<NC, NF> *lr, const ClsNode<NC, NF> (&n)[2],
+                                          const unsigned long long (&okm)[2], int64_t col0, bool in_row, uint32_t kb0,
+                                          uint32_t *__restrict__ scores32, uint32_t *kws, uint32_t *wkey,
+                                          uint32_t (&mb)[4], int win, bool stage, uint32_t staged, uint32_t *stage_dst,
+                                          int64_t stride) {
+    using Row = kg_pod_cls_t<NC, NF>;
+    constexpr bool FULL = FAST;
     const int lane = threadIdx.x & 63;
     const kg_u16x2 shifts = {(uint16_t)d.fit_shift, (uint16_t)c.la_shift};
     const kg_u16x2 kw2 = {(uint16_t)(1u << KG_TILE_SHIFT), (uint16_t)(1u << KG_TILE_SHIFT)};
-    constexpr bool FULL = FAST;
-    MatRow<NC, NF> nxt = load_mat_row<NC, NF>(rows + w.begin);
-    // one pod: i = index in the 64-pod mask chunk, slot = index in the 16-pod key chunk
-    auto pod = [&](const int p, const uint32_t i, const int slot, uint32_t (&mb)[4]) {
-        const MatRow<NC, NF> pd = nxt;
-        nxt = load_mat_row<NC, NF>(rows + p + 1);   // one row past the class's end is padding (cls_layout)
+    // one pod: t = index in the group
+    auto pod = [&](const int t) {
+        const Row pd = lr[t];   // the whole row into registers (broadcast ds_read_b128s), read once
         unsigned long long m[2];
         uint32_t k[2], s;
 #pragma unroll
@@ -1013,24 +1021,40 @@ __device__ __forceinline__ void mat_pods(const kg_consts &c, const kg_cls_desc &
 #pragma unroll
             for (int q = 0; q < NC; q++) m[j] &= __builtin_amdgcn_ballot_w64(pd.req[q] <= n[j].fr[q]);
         }
+#ifdef KG_MAT_ABLATE
+        if (KG_MAT_ABLATE & 16) {   // no evaluation: the stores alone
+            s = pd.req[0] ^ lane;
+            k[0] = k[1] = 0u;
+        } else
+#endif
         if (FAST && W1) {
             uint32_t h[2];
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 uint32_t sf = 0, sl = 0;
-                if (FIT_ON) {
+#ifdef KG_MAT_ABLATE
+                if (KG_MAT_ABLATE & 8) {   // Fit terms only
+                    uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.pr[0], n[j].R[0], n[j].F[0]));
+                    uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.pr[1], n[j].R[1], n[j].F[1]));
+                    sf = q0 + q1;
+                } else
+#endif
+                {
+                    if (FIT_ON) {
 #pragma unroll
-                    for (int f = 0; f < NF; f++) {
-                        uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n[j].R[f], n[j].F[f]));
-                        if (MOST) q = q < 100u ? q : 100u;
-                        sf += q;
+                        for (int f = 0; f < NF; f++) {
+                            uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n[j].R[f], n[j].F[f]));
+                            if (MOST) q = q < 100u ? q : 100u;
+                            sf += q;
+                        }
+                    }
+                    if (LA_ON) {
+                        const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la[0], n[j].laR[0], n[j].laF[0]));
+                        const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la[1], n[j].laR[1], n[j].laF[1]));
+                        sl = (q0 + q1) << 16;
                     }
                 }
-                if (LA_ON) {
-                    const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la[0], n[j].laR[0], n[j].laF[0]));
-                    const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la[1], n[j].laR[1], n[j].laF[1]));
-                    sl = (q0 + q1) << 16;
-                }
+                // v_dot2_u32_u16 of the packed {fit, la} with the tile weights: the key's total
                 h[j] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(kg_u16x2, sf + sl) >> shifts);
                 k[j] = sel_lanes(m[j], __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h[j]), kw2, kb0 - j, false));
             }
@@ -1039,77 +1063,87 @@ __device__ __forceinline__ void mat_pods(const kg_consts &c, const kg_cls_desc &
             uint32_t fit[2], la[2];
 #pragma unroll
             for (int j = 0; j < 2; j++) {
-                kg_pod_cls_t<NC, NF> pr;
-#pragma unroll
-                for (int f = 0; f < NF; f++) pr.pr[f] = pd.pr[f];
-                pr.la[0] = pd.la[0];
-                pr.la[1] = pd.la[1];
-                cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pr, n[j], fit[j], la[j]);
+                cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n[j], fit[j], la[j]);
                 const uint32_t tot = W1 ? fit[j] + la[j]
                                         : __umul24((uint32_t)c.weight_fit, fit[j]) + __umul24((uint32_t)c.weight_la, la[j]);
                 k[j] = sel_lanes(m[j], (tot << KG_TILE_SHIFT) + kb0 - j);
             }
             s = fit[0] | (la[0] << 8) | (fit[1] << 16) | (la[1] << 24);
         }
-        uint32_t *dst = scores32 + ((uint64_t)(pd.score_off + col0) >> 1);
+        // the output row is wave-uniform: one readfirstlane, the row × stride address in SALU, so the
+        // store is saddr + the lane's offset (score_off = row × stride, kg_cls_row)
+        const int64_t orow = __builtin_amdgcn_readfirstlane(pd.row);
+        uint32_t *dst = scores32 + ((orow * stride + col0) >> 1);
+#ifdef KG_MAT_ABLATE   // measurement builds only (tools/ablate_mat.sh): drop parts of the pod body
+        if (KG_MAT_ABLATE & 1) asm volatile("" ::"v"(s)); else
+#endif
+#if KG_MAT_NT
+        if (FAST || in_row) __builtin_nontemporal_store(s, dst + lane);
+#else
         if (FAST || in_row) dst[lane] = s;
-        kws[slot * 64 + lane] = k[0] > k[1] ? k[0] : k[1];
-        write_lanes(mb[0], mb[1], mb[2], mb[3], i, m[0], m[1]);
+#endif
+#ifdef KG_MAT_ABLATE
+        if (KG_MAT_ABLATE & 2) asm volatile("" ::"v"(k[0] > k[1] ? k[0] : k[1])); else
+#endif
+        kws[t * 64 + lane] = k[0] > k[1] ? k[0] : k[1];
+#ifdef KG_MAT_ABLATE
+        if (KG_MAT_ABLATE & 4) asm volatile("" ::"s"(m[0]), "s"(m[1])); else
+#endif
+        write_lanes(mb[0], mb[1], mb[2], mb[3], (uint32_t)(win * KG_MAT_KC + t), m[0], m[1]);
     };
-    for (int c0 = w.begin; c0 < w.end; c0 += 64) {
-        const int c1 = min(c0 + 64, w.end);
-        uint32_t mb[4] = {0u, 0u, 0u, 0u};   // ballots of pod c0 + l in lane l: even lo, even hi, odd lo, odd hi
-        for (int k0 = c0; k0 < c1; k0 += KG_MAT_KC) {
-            const int k1 = min(k0 + KG_MAT_KC, c1);
-            if (k1 - k0 == KG_MAT_KC) {
+    if (FULLG) {
 #pragma unroll
-                for (int t = 0; t < KG_MAT_KC; t++) pod(k0 + t, (uint32_t)(k0 - c0 + t), t, mb);
-            } else {
-                for (int t = 0; t < k1 - k0; t++) pod(k0 + t, (uint32_t)(k0 - c0 + t), t, mb);
-            }
-            // the wave's keys of these pods: lane l reduces pod l / 4's quarter (l % 4) of the 64 lane keys;
-            // a wave's LDS operations complete in order, so the reads see this wave's writes
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("" ::: "memory");
-            const uint4 *src = reinterpret_cast<const uint4 *>(kws + (lane >> 2) * 64 + (lane & 3) * 16);
-            uint32_t mx = 0;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint4 v = src[q];
-                const uint32_t a0 = v.x > v.y ? v.x : v.y, a1 = v.z > v.w ? v.z : v.w;
-                const uint32_t a2 = a0 > a1 ? a0 : a1;
-                mx = mx > a2 ? mx : a2;
-            }
-            uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
-            mx = mx > o ? mx : o;
-            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x4E, 0xf, 0xf, false);            // quad_perm [2,3,0,1]
-            mx = mx > o ? mx : o;
-            if ((lane & 3) == 0 && (lane >> 2) < k1 - k0 && mx) atomicMax(&wkey[k0 - w.begin + (lane >> 2)], mx);
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("" ::: "memory");
-        }
-        // mask words of pods c0 .. c1−1: lane l writes pod c0 + l's two words of this segment
-        if (lane < c1 - c0) {
-            const int32_t moff = rows[c0 + lane].mask_off;
-            uint64_t *mw = mask + moff + (col0 >> 6);
-            if (mseg0) mw[0] = interleave32(mb[0], mb[2]);
-            if (mseg1) mw[1] = interleave32(mb[1], mb[3]);
-        }
+        for (int t = 0; t < KG_MAT_KC; t++) pod(t);
+    } else {
+        for (int t = 0; t < g1 - g0; t++) pod(t);
     }
+    if (stage) *stage_dst = staged;
+    // the wave's keys of these pods: lane l reduces pod l / 4's quarter (l % 4) of the 64 lane keys;
+    // a wave's LDS operations complete in order, so the reads see this wave's writes
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const uint4 *src = reinterpret_cast<const uint4 *>(kws + (lane >> 2) * 64 + (lane & 3) * 16);
+    uint32_t mx = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint4 v = src[q];
+        const uint32_t a0 = v.x > v.y ? v.x : v.y, a1 = v.z > v.w ? v.z : v.w;
+        const uint32_t a2 = a0 > a1 ? a0 : a1;
+        mx = mx > a2 ? mx : a2;
+    }
+    uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    mx = mx > o ? mx : o;
+    o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x4E, 0xf, 0xf, false);            // quad_perm [2,3,0,1]
+    mx = mx > o ? mx : o;
+    if ((lane & 3) == 0 && (lane >> 2) < g1 - g0 && mx) atomicMax(&wkey[g0 - item0 + (lane >> 2)], mx);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
 }
 
 template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool W1>
 __device__ __forceinline__ void mat_block(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
                                           const kg_cls_work &w, int tile, const char *__restrict__ rows_base,
                                           uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
-                                          uint32_t *__restrict__ partials, uint32_t *kw, uint32_t *wkey) {
+                                          uint32_t *__restrict__ partials, uint32_t *kw, uint32_t *wkey, char *lrows) {
+    using Row = kg_pod_cls_t<NC, NF>;
+    constexpr int RB = (int)sizeof(Row);
+    constexpr int BT = KG_TILE / 2;                     // threads
+    constexpr int G_DW = KG_MAT_KC * RB / 4;            // dwords of one group's rows (one per staging thread)
+    static_assert((KG_MAT_KC * RB) % 4 == 0 && G_DW <= BT, "a group's rows are one dword per thread");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t wave_base = (int64_t)tile * KG_TILE + wave * 128;
-    const kg_pod_cls_t<NC, NF> *rows = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(rows_base + d.rows_offset);
+    const Row *rows = reinterpret_cast<const Row *>(rows_base + d.rows_offset);
+    const uint32_t *gsrc = reinterpret_cast<const uint32_t *>(rows);
+    const int64_t last_dw = (int64_t)w.end * (RB / 4) - 1;     // stay inside the class's rows
+    uint32_t *lbuf = reinterpret_cast<uint32_t *>(lrows);
     const int np = w.end - w.begin;
-    for (int i = tid; i < np; i += KG_TILE / 2) wkey[i] = 0u;
+    for (int i = tid; i < np; i += BT) wkey[i] = 0u;
+    if (tid < G_DW) {   // group 0 → buffer 0
+        const int64_t src = (int64_t)w.begin * (RB / 4) + tid;
+        lbuf[tid] = gsrc[src < last_dw ? src : last_dw];
+    }
     ClsNode<NC, NF> n[2];
     unsigned long long okm[2];
     bool full_l = true;
@@ -1127,31 +1161,70 @@ __device__ __forceinline__ void mat_block(const kg_consts &c, const kg_planes &p
     const uint32_t kb0 = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - (uint32_t)(wave * 128 + 2 * lane);
     uint32_t *kws = kw + wave * (KG_MAT_KC * 64);
     uint32_t *scores32 = reinterpret_cast<uint32_t *>(scores);
-    __syncthreads();   // key slots zeroed
-    if (fast)
-        mat_pods<NC, NF, MOST, FIT_ON, LA_ON, W1, true>(c, d, w, rows, n, okm, col0, in_row, mseg0, mseg1, kb0, mask,
-                                                        scores32, kws, wkey);
-    else
-        mat_pods<NC, NF, MOST, FIT_ON, LA_ON, W1, false>(c, d, w, rows, n, okm, col0, in_row, mseg0, mseg1, kb0, mask,
-                                                         scores32, kws, wkey);
-    __syncthreads();
-    for (int i = tid; i < np; i += KG_TILE / 2)
-        partials[(int64_t)rows[w.begin + i].row * a.tiles_total + tile] = wkey[i];
+    // every node-plane load lands before the pod loop, so inside it the only vector-memory operations in
+    // flight are the score stores and the next group's row load (the waits there count the stores)
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    __syncthreads();   // key slots zeroed, group 0 staged (no score store issued yet)
+    uint32_t mb[4] = {0u, 0u, 0u, 0u};   // ballots of the window's pod l in lane l: even lo, even hi, odd lo, odd hi
+    for (int g0 = w.begin, gi = 0; g0 < w.end; g0 += KG_MAT_KC, gi++) {
+        const int g1 = min(g0 + KG_MAT_KC, w.end);
+        const int win = gi & 3;   // the group's quarter of the 64-pod mask window
+        const bool more = g1 < w.end;
+        const bool stage = more && tid < G_DW;
+        uint32_t staged = 0;
+        if (stage) {   // the next group's rows are in flight while this group is evaluated
+            const int64_t src = (int64_t)g1 * (RB / 4) + tid;
+            staged = gsrc[src < last_dw ? src : last_dw];
+        }
+        // LDS ring of 8 group slots: the window being evaluated (4 slots, kept for its mask offsets) and
+        // the next window's first group, staged while this group is evaluated
+        const Row *lr = reinterpret_cast<const Row *>(lrows + (gi & 7) * (KG_MAT_KC * RB));
+        uint32_t *stage_dst = lbuf + ((gi + 1) & 7) * G_DW + tid;
+#define KG_MAT_GROUP(F, G)                                                                                             \
+    mat_group<NC, NF, MOST, FIT_ON, LA_ON, W1, F, G>(c, d, w.begin, g0, g1, lr, n, okm, col0, in_row, kb0, scores32, kws, \
+                                                    wkey, mb, win, stage, staged, stage_dst, a.score_stride)
+        if (fast && g1 - g0 == KG_MAT_KC) KG_MAT_GROUP(true, true);
+        else if (fast) KG_MAT_GROUP(true, false);
+        else KG_MAT_GROUP(false, false);
+#undef KG_MAT_GROUP
+        if (win == 3 || !more) {
+            // mask words of the window's pods: lane l writes pod l's two words of this segment
+            const int wn = g1 - (g0 - win * KG_MAT_KC);
+            if (lane < wn) {
+                const Row *wr = reinterpret_cast<const Row *>(lrows + (gi & 4) * (KG_MAT_KC * RB));
+                uint64_t *mw = mask + wr[lane].mask_off + (col0 >> 6);
+                if (mseg0) mw[0] = interleave32(mb[0], mb[2]);
+                if (mseg1) mw[1] = interleave32(mb[1], mb[3]);
+            }
+            mb[0] = mb[1] = mb[2] = mb[3] = 0u;
+        }
+        lds_barrier();
+    }
+    for (int i = tid; i < np; i += BT) partials[(int64_t)rows[w.begin + i].row * a.tiles_total + tile] = wkey[i];
 }
 
+#ifndef KG_MAT_WPE0
+#define KG_MAT_WPE0 5   // waves per SIMD the register allocation of k_mat kind 0 targets (others: KG_MAT_WPE1)
+#endif
+#ifndef KG_MAT_WPE1
+#define KG_MAT_WPE1 4
+#endif
 template <bool MOST, bool FIT_ON, bool LA_ON, bool W1, int KIND>
-__global__ __launch_bounds__(KG_TILE / 2) void k_mat(kg_consts c, kg_planes pl, HotArgs a,
+__global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? KG_MAT_WPE0 : KG_MAT_WPE1))) void k_mat(kg_consts c, kg_planes pl, HotArgs a,
                                                      const kg_cls_desc *__restrict__ descs,
                                                      const kg_cls_work *__restrict__ work, const char *__restrict__ rows,
                                                      uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
                                                      uint32_t *__restrict__ partials, int32_t shard_tiles) {
     __shared__ __attribute__((aligned(16))) uint32_t kw[(KG_TILE / 128) * KG_MAT_KC * 64];
     __shared__ uint32_t wkey[KG_MAT_ITEM_MAX];
+    constexpr int RB = KIND == 0 ? (int)sizeof(kg_pod_cls_t<2, 2>) : KIND == 1 ? (int)sizeof(kg_pod_cls_t<2, 4>)
+                     : KIND == 2 ? (int)sizeof(kg_pod_cls_t<4, 2>) : (int)sizeof(kg_pod_cls_t<4, 4>);
+    __shared__ __attribute__((aligned(64))) char lrows[8 * KG_MAT_KC * RB];
     if ((int)blockIdx.x >= shard_tiles) return;   // XCD padding of the grid (whole workgroup)
     const int tile = a.tile_begin + blockIdx.x;
     const kg_cls_work w = work[blockIdx.y];
     const kg_cls_desc d = descs[w.cls];
-#define KG_MAT_ARGS c, pl, a, d, w, tile, rows, mask, scores, partials, kw, wkey
+#define KG_MAT_ARGS c, pl, a, d, w, tile, rows, mask, scores, partials, kw, wkey, lrows
     if constexpr (KIND == 0) mat_block<2, 2, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);
     else if constexpr (KIND == 1) mat_block<2, 4, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);
     else if constexpr (KIND == 2) mat_block<4, 2, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);

@@ -10,3 +10,10 @@ int kg_numa_list_count(const kg_pod_row &row);   // NodeNUMAResource hint lists 
 // need a slot (compared or scored), so the caller can check the profile covers them.
 template <int S>
 uint32_t kg_pod_hot_from_row(const kg_config &c, const kg_pod_row &row, const int32_t *slot_res, kg_pod_hot_t<S> &h);
+
+// kg_cpuset.cpp — the CPU accumulator (cpuset take at Reserve) and NodeAllocation's available CPUs
+int kg_cpuset_take_cpus(const kg_cpu_info *cpus, int32_t n_cpus, int32_t max_ref, const uint8_t *available, int32_t need,
+                        int32_t bind, int32_t exclusive, int32_t strategy, uint8_t *result);
+void kg_cpuset_available(const kg_cpu_info *cpus, int32_t n_cpus, int32_t max_ref, uint8_t *available);
+void kg_cpuset_filter_required(const kg_cpu_info *cpus, int32_t n_cpus, int32_t bind, uint8_t *available);
+bool kg_cpuset_satisfies_required(const kg_cpu_info *cpus, int32_t n_cpus, int32_t bind, const uint8_t *taken);

@@ -239,3 +239,14 @@ class SnapshotFeeder:
         if len(idx):
             eng.upsert(idx, rows)
         return len(idx)
+
+    def cluster(self) -> "ingest.ob.Cluster":
+        """The whole cache state as an objects.Cluster, nodes in row-index order (indices must be dense:
+        a deleted node's slot refilled), for evaluation by the host tools and the oracle."""
+        names = sorted(self.nodes, key=lambda n: self.index[n])
+        if [self.index[n] for n in names] != list(range(len(names))):
+            raise ValueError("row indices have holes (a deleted node's slot not refilled)")
+        return ingest.cluster_from_objects(
+            [self.nodes[n] for n in names], list(self.pods.values()), [self.metrics[n] for n in names if n in self.metrics],
+            [self.nrts[n] for n in names if n in self.nrts], now_ns=int(self.now_fn()),
+            assign_cache={n: self.assign_cache[n] for n in names if n in self.assign_cache})
