@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 7
+#define KG_ABI_VERSION 8
 #define KG_QUOTA_MAX_DEPTH 64 /* longest kg_quota parent chain (cycles are rejected) */
 
 /* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
@@ -149,7 +149,7 @@ enum kg_scoring_strategy {
 
 #define KG_PLUGIN_FIT 0x1u       /* NodeResourcesFit       */
 #define KG_PLUGIN_LOADAWARE 0x2u /* LoadAwareScheduling    */
-#define KG_PLUGIN_NUMA 0x4u      /* NodeNUMAResource (zone fit + score; no cpuset binding) */
+#define KG_PLUGIN_NUMA 0x4u      /* NodeNUMAResource (zone fit + score, cpuset binding) */
 #define KG_PLUGIN_RESERVATION 0x8u  /* Reservation (restore, Filter, Score + NormalizeScore, Reserve) */
 #define KG_PLUGIN_ELASTICQUOTA 0x10u /* ElasticQuota (PreFilter quota gate, Reserve used accounting) */
 
@@ -169,6 +169,12 @@ enum kg_cpu_exclusive_policy {     /* ResourceSpec.PreferredCPUExclusivePolicy /
 enum kg_node_cpu_bind_policy {     /* GetNodeCPUBindPolicy: label node.koordinator.sh/cpu-bind-policy, or the
                                       kubelet static policy with full-pcpus-only (numa_aware.go:314-325) */
     KG_NODE_CPU_BIND_NONE = 0, KG_NODE_CPU_BIND_FULL_PCPUS_ONLY = 1, KG_NODE_CPU_BIND_SPREAD_BY_PCPUS = 2,
+};
+
+enum kg_numa_allocate_strategy {   /* label node.koordinator.sh/numa-allocate-strategy (numa_aware.go:52-53, util.go:35-41) */
+    KG_NUMA_ALLOC_DEFAULT = 0,     /* label absent: the plugin default (NUMAMostAllocated iff NUMAScoringStrategy.Type is
+                                      MostAllocated, util.go:27-33) */
+    KG_NUMA_ALLOC_MOST = 1, KG_NUMA_ALLOC_LEAST = 2, KG_NUMA_ALLOC_DISTRIBUTE_EVENLY = 3
 };
 
 enum kg_numa_policy {
@@ -341,6 +347,8 @@ typedef struct kg_numa_spec {
     int32_t node_cpu_bind_policy;                    /* kg_node_cpu_bind_policy */
     int32_t max_ref_count;                           /* ≥ 1 */
     int32_t first_cpu, n_cpus;
+    int32_t numa_allocate_strategy;                  /* kg_numa_allocate_strategy: which CPUs a Reserve takes */
+    int32_t _pad_s;
 } kg_numa_spec;
 
 /* One logical CPU of a node (CPUInfo of cpu_topology.go + the node allocation's view of it). */
@@ -551,6 +559,18 @@ kg_status kg_row_commit(const kg_config *cfg, kg_node_row *node, const kg_pod_ro
  * Scores are the plugin scores (0..100) of the enabled plugins, 0 otherwise. */
 kg_status kg_row_eval(const kg_config *cfg, const kg_node_row *node, const kg_pod_row *pod, int64_t now_ns,
                       int32_t *feasible, int32_t *fit_score, int32_t *la_score, int32_t *numa_score);
+/* Reserve of a pod that may bind a cpuset, on host rows (NodeNUMAResource.Reserve, plugin.go:375-419):
+ * requestCPUBind on the node (util.go:105-122), then resourceManager.Allocate (resource_manager.go:171-195) —
+ * allocateResourcesByHint on the Filter's hint with the original requests and allocateCPUSet (:273-360), the
+ * CPU accumulator zone by zone — and Update (node_allocation.go:57-100): the taken CPUs' RefCount + 1 and
+ * ExclusivePolicy, the zone allocations, AssumePod / LoadAware deltas, and the row's cpuset counts re-derived
+ * from `cpus` (the node's logical CPUs as kg_cluster_view.cpus holds them; updated in place).
+ * numa_allocate_strategy: kg_numa_allocate_strategy of the node (DEFAULT ⇒ the plugin default from cfg).
+ * KG_OK: reserved, taken[n_cpus] marks the cpuset (all zero when the pod binds none);
+ * KG_NOT_FOUND: Allocate fails ("not enough cpus available to satisfy request" or a required policy that the
+ * take cannot satisfy) — the Reserve fails and nothing is changed (Unreserve + ForgetPod). */
+kg_status kg_row_reserve(const kg_config *cfg, kg_node_row *node, const kg_pod_row *pod, kg_cpu_info *cpus,
+                         int32_t n_cpus, int32_t max_ref_count, int32_t numa_allocate_strategy, uint8_t *taken);
 
 /* Reservation-aware Filter + Score of one (pod, node) pair on host rows through the kernels' per-pair
  * code (kg_rsv_pair): the node's reservation slots `rsv` (≤ KG_MAX_RSV_PER_NODE, in cache order) are
@@ -608,6 +628,14 @@ kg_status kg_snapshot_generation(kg_engine *eng, uint64_t *out);
 kg_status kg_cpuset_take(const kg_cpu_info *cpus, int32_t n_cpus, int32_t max_ref_count, const uint8_t *available,
                          int32_t need, int32_t bind_policy, int32_t exclusive_policy, int32_t numa_strategy,
                          uint8_t *result);
+/* The logical CPUs of snapshot nodes (NodeNUMAResource's NodeAllocation.allocatedCPUs + CPUTopology +
+ * ReservedCPUs, with MaxRefCount and the node's NUMA allocate strategy): snapshot node k gets the CPU detail
+ * of view node node_index[k] (node_index NULL ⇔ k itself; n nodes).  Replaces every table; kg_snapshot_reset
+ * drops them, kg_snapshot_remove drops the node's.  kg_place / kg_commit take cpusets from these tables at
+ * Reserve (the host runs the CPU accumulator for the chosen node between device chunks) and write the
+ * node's cpuset counts back to its row.  kg_cpus_download reads one node's table (n = its CPU count). */
+kg_status kg_cpus_set(kg_engine *eng, const kg_cluster_view *view, const int32_t *node_index, int32_t n);
+kg_status kg_cpus_download(kg_engine *eng, int32_t node, kg_cpu_info *out, int32_t n);
 /* Restrict kg_eval/kg_place evaluation to nodes [begin, end) (node sharding across GPUs);
  * node indices stay global.  begin must be a multiple of 1024 unless the shard is empty. */
 kg_status kg_set_shard(kg_engine *eng, int32_t begin, int32_t end);
@@ -621,10 +649,13 @@ kg_status kg_eval(kg_engine *eng, int64_t now_ns, const kg_eval_out *out);
 /* Placement mode: schedule the uploaded batch in queue order exactly like the sequential
  * cycle (Filter all nodes → Score → argmax, lowest index on ties → Reserve), committing
  * each placement to the snapshot.  out_node[p] = node or −1, out_score[p] = total score
- * (−1 when unschedulable). */
+ * (−1 when unschedulable, or when its Reserve fails: a cpuset the CPU accumulator cannot take).
+ * Pods that may bind a cpuset end their device chunk; their Reserve takes the CPUs on the host
+ * (kg_cpus_set tables) before the next chunk is evaluated. */
 kg_status kg_place(kg_engine *eng, int64_t now_ns, int32_t *out_node, int64_t *out_score);
 
-/* Multi-GPU building blocks of kg_place (see koordinator_amd/dist.py):
+/* Multi-GPU building blocks of kg_place (see koordinator_amd/dist.py); pods that bind cpusets are refused
+ * here (KG_ERR_UNSUPPORTED: the sharded resolve has no host Reserve step):
  * chunk_eval writes per-(pod, 1024-node tile) partial keys of the shard for pods
  * [pod_begin, pod_begin+n) into partial_dev ([n][tiles_total][KG_PARTIAL_SLOTS] uint32, tile index
  * global; the caller zeroes nothing, chunk_eval clears the buffer's n rows itself);
@@ -649,7 +680,8 @@ kg_status kg_rsv_download(kg_engine *eng, kg_reservation *out, int32_t n);
 kg_status kg_quota_set(kg_engine *eng, const kg_quota *q, int32_t n);
 kg_status kg_quota_download(kg_engine *eng, kg_quota *out, int32_t n);
 
-/* Single Reserve on the device snapshot (pod = index in the uploaded batch). */
+/* Single Reserve on the device snapshot (pod = index in the uploaded batch); a cpuset pod takes its CPUs
+ * from the node's kg_cpus_set table.  KG_NOT_FOUND ⇔ its Allocate fails (nothing changed). */
 kg_status kg_commit(kg_engine *eng, int32_t pod, int32_t node);
 
 /* Measurement: when on, every k_eval launch (kg_eval, kg_place_chunk_eval) is bracketed by a

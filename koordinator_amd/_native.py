@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 NUM_RES = 8
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
  RES_EXTENDED) = range(8)
@@ -37,6 +37,8 @@ POD_NUMA_SKIP, POD_NUMA_CPU_BIND, POD_NON_PREEMPTIBLE, POD_NUMA_BIND_INVALID = 0
 CPU_BIND_UNSET, CPU_BIND_DEFAULT, CPU_BIND_FULL_PCPUS, CPU_BIND_SPREAD_BY_PCPUS, CPU_BIND_CONSTRAINED_BURST = range(5)
 CPU_EXCL_UNSET, CPU_EXCL_NONE, CPU_EXCL_PCPU_LEVEL, CPU_EXCL_NUMA_NODE_LEVEL = range(4)
 NODE_CPU_BIND_NONE, NODE_CPU_BIND_FULL_PCPUS_ONLY, NODE_CPU_BIND_SPREAD_BY_PCPUS = range(3)
+NUMA_ALLOC_DEFAULT, NUMA_ALLOC_MOST, NUMA_ALLOC_LEAST, NUMA_ALLOC_DISTRIBUTE_EVENLY = range(4)
+NOT_FOUND = 1   # KG_NOT_FOUND
 NODE_VALID, NODE_HAS_METRIC, NODE_HAS_UPDATE_TIME, NODE_LA_PASS_NONPROD, NODE_LA_PASS_PROD = 0x1, 0x2, 0x4, 0x8, 0x10
 NODE_NUMA_OPTIONS, NODE_NUMA_TOPO_VALID, NODE_NUMA_TOPO_INVALID = 0x40, 0x80, 0x100
 
@@ -98,6 +100,7 @@ NUMA_SPEC = np.dtype([
     ("cpu_amplification_ratio", "<f8"), ("cpu_topology_valid", "<i4"), ("cpuset_cpus", "<i4"),
     ("zone_cpuset_cpus", "<i4", (MAX_ZONES,)),
     ("node_cpu_bind_policy", "<i4"), ("max_ref_count", "<i4"), ("first_cpu", "<i4"), ("n_cpus", "<i4"),
+    ("numa_allocate_strategy", "<i4"), ("_pad_s", "<i4"),
 ], align=True)
 
 CPU_INFO = np.dtype([("socket", "<i4"), ("node", "<i4"), ("core", "<i4"), ("refcount", "<i4"), ("exclusive", "<i4"),
@@ -203,7 +206,7 @@ EXPORTED = [
     "kg_snapshot_download", "kg_set_shard", "kg_pods_set", "kg_eval", "kg_place", "kg_num_tiles",
     "kg_place_chunk_eval", "kg_place_chunk_resolve", "kg_commit", "kg_set_profiling", "kg_eval_kernel_times",
     "kg_rsv_set", "kg_rsv_download", "kg_quota_set", "kg_quota_download", "kg_row_eval_rsv", "kg_row_rsv_restore",
-    "kg_snapshot_generation", "kg_cpuset_take",
+    "kg_snapshot_generation", "kg_cpuset_take", "kg_row_reserve", "kg_cpus_set", "kg_cpus_download",
 ]
 
 _lib = None
@@ -247,6 +250,8 @@ def lib() -> ctypes.CDLL:
         "kg_row_rsv_restore": (i32, [vp, vp, vp, i32, vp, vp]),
         "kg_snapshot_generation": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
         "kg_cpuset_take": (i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp]),
+        "kg_row_reserve": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
+        "kg_cpus_set": (i32, [vp, vp, vp, i32]), "kg_cpus_download": (i32, [vp, i32, vp, i32]),
     }
     for name, (res, args) in sig.items():
         if host_only and not hasattr(L, name):

@@ -760,10 +760,6 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
         o.score = kg_numa_score_node(c, row, p, amplified, requested, pcpu_eff);
         return;
     }
-    if (bind && reserve) {   // the Reserve of a cpuset (choosing the CPUs) is not on the engine
-        o.feasible = false;
-        return;
-    }
     if (bind) {   // FilterByNUMANode with the cpuset options: trimmed hints, then the zone-wise take
         const int own = (int)(p.cpu_bind & 15u);
         int required = own;
@@ -981,13 +977,47 @@ void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &
 #endif
 }
 
-// Reserve of NodeNUMAResource (plugin.go:375-419): record the zone allocations of the chosen node
+// Reserve's cpuset decision for a pair (plugin.go:375-404): requestCPUBind (util.go:105-122) and
+// getCPUBindPolicy (util.go:85-103) — *required: the required bind policy (the pod's own, else the node's CPU
+// bind policy; UNSET ⇔ none), *take: the policy the accumulator takes with (required, else the pod's
+// preferred).  A pod skipped by PreFilter or with an invalid cpu request never reaches Reserve.
+KG_HD bool kg_numa_binds(const kg_node_row &row, const kg_pod_dev &p, int &required, int &take) {
+    required = take = KG_CPU_BIND_UNSET;
+    if (p.flags & (KG_POD_NUMA_SKIP | KG_POD_NUMA_BIND_INVALID)) return false;
+    const bool opts = (row.flags & KG_NODE_NUMA_OPTIONS) != 0;
+    const int node_bind = opts ? row.node_cpu_bind : KG_NODE_CPU_BIND_NONE;
+    const int64_t pcpu = p.numa_req[KG_RES_CPU];
+    const bool own = (p.flags & KG_POD_NUMA_CPU_BIND) != 0;
+    if (!own && (pcpu == 0 || node_bind == KG_NODE_CPU_BIND_NONE || pcpu % 1000 != 0)) return false;
+    required = own ? (int)(p.cpu_bind & 15u) : KG_CPU_BIND_UNSET;
+    if (required == KG_CPU_BIND_UNSET) {
+        if (node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) required = KG_CPU_BIND_FULL_PCPUS;
+        else if (node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) required = KG_CPU_BIND_SPREAD_BY_PCPUS;
+    }
+    take = required != KG_CPU_BIND_UNSET ? required : (int)((p.cpu_bind >> 4) & 15u);
+    return true;
+}
+
+// Reserve of NodeNUMAResource (plugin.go:375-419): record the zone allocations of the chosen node — the
+// hint of its Filter (for a cpuset, the trimmed hint of FilterByNUMANode with the cpuset options) and
+// allocateResourcesByHint on the original requests.  The cpuset itself is taken on the host (kg_cpuset.cpp).
 KG_HD void kg_numa_commit(const kg_consts &c, kg_node_row &row, const kg_pod_dev &p) {
     if (!(c.plugins & KG_PLUGIN_NUMA) || !(row.flags & KG_NODE_NUMA_OPTIONS) || row.numa_policy == KG_NUMA_NONE ||
         !(row.flags & KG_NODE_NUMA_TOPO_VALID))
         return;
     kg_numa_out o;
-    kg_numa_pair(c, row, p, o, nullptr, true);
+    int required, take;
+    if (kg_numa_binds(row, p, required, take)) {
+        const int64_t pcpu = p.numa_req[KG_RES_CPU];
+        const double ratio = row.cpu_amplification_ratio;
+        const int64_t pcpu_eff = pcpu != 0 && ratio > 1.0 ? (int64_t)ceil((double)pcpu * ratio) : pcpu;
+        o.feasible = true;
+        o.score = 0;
+        o.n_alloc = 0;
+        kg_numa_bind_zoned(c, row, p, o, row.requested, row.numa_policy, pcpu_eff, required);
+    } else {
+        kg_numa_pair(c, row, p, o, nullptr, true);
+    }
     if (!o.feasible) return;
     for (int j = 0; j < o.n_alloc; j++) {
         const int zi = o.zone[j];

@@ -11,6 +11,7 @@
 // Every ordering the reference sorts with a total order is a std::sort with that comparator; the two
 // sorts without a tie-break (cpu_accumulator.go:142, :161: socket groups by length, which Go's pdqsort
 // insertion-sorts at these sizes, i.e. stably) are std::stable_sort.
+#include <math.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -398,6 +399,139 @@ bool kg_cpuset_satisfies_required(const kg_cpu_info *cpus, int32_t n_cpus, int32
     if (bind == kBindFull) return ncore * t.per_core == ncpu;
     if (bind == kBindSpread) return ncore == ncpu;
     return true;
+}
+
+// The row's cpuset facts from the node's logical CPUs (what kg_build_node_rows derives from the view, and what
+// a Reserve re-derives after it took CPUs): CPUsPerCore, the available CPUs (getAvailableCPUs: allocated once
+// RefCount ≥ maxRefCount, reserved CPUs out) node-wide and per zone — all of them, those of wholly available
+// cores, cores with one — and the cpuset pods' CPUs (allocatedCPUs, RefCount > 0) with their amplified
+// terms.  Returns the allocated CPU count.
+int32_t kg_cpuset_row_fields(kg_node_row &row, const kg_cpu_info *ci, int32_t n, int32_t max_ref) {
+    if (max_ref < 1) max_ref = 1;
+    std::vector<int32_t> core_id, core_total, core_avail, core_zone;
+    int32_t nalloc = 0, zone_alloc[KG_MAX_ZONES] = {};
+    for (int32_t c = 0; c < n; c++) {
+        size_t k = 0;
+        while (k < core_id.size() && core_id[k] != ci[c].core) k++;
+        if (k == core_id.size()) {
+            core_id.push_back(ci[c].core);
+            core_total.push_back(0);
+            core_avail.push_back(0);
+            core_zone.push_back(-1);
+        }
+        core_total[k]++;
+        if (!(ci[c].refcount > 0 && ci[c].refcount >= max_ref) && !ci[c].reserved) core_avail[k]++;
+        for (int z = 0; z < row.n_zones && z < KG_MAX_ZONES; z++)
+            if (row.zone_id[z] == ci[c].node) {
+                core_zone[k] = z;   // the zone of each core (its CPUs' NUMA node); −1 ⇔ no zone
+                if (ci[c].refcount > 0) zone_alloc[z]++;
+            }
+        if (ci[c].refcount > 0) nalloc++;
+    }
+    const int32_t ncores = (int32_t)core_id.size();
+    row.cpus_per_core = ncores ? n / ncores : 0;
+    row.cpuset_full_free_cpus = row.cpuset_free_cores = row.cpuset_avail_cpus = 0;
+    for (int z = 0; z < KG_MAX_ZONES; z++) row.zone_cpus_avail[z] = row.zone_cpus_full[z] = row.zone_cores_free[z] = 0;
+    for (int32_t k = 0; k < ncores; k++) {
+        const bool full = core_avail[k] == row.cpus_per_core;
+        if (full) row.cpuset_full_free_cpus += core_avail[k];
+        if (core_avail[k] > 0) row.cpuset_free_cores++;
+        row.cpuset_avail_cpus += core_avail[k];
+        const int32_t z = core_zone[k];
+        if (z < 0) continue;
+        row.zone_cpus_avail[z] = (int16_t)(row.zone_cpus_avail[z] + core_avail[k]);
+        if (full) row.zone_cpus_full[z] = (int16_t)(row.zone_cpus_full[z] + core_avail[k]);
+        if (core_avail[k] > 0) row.zone_cores_free[z]++;
+    }
+    // the amplified-CPU terms of filterAmplifiedCPUs / scoreWithAmplifiedCPUs / getAvailableNUMANodeResources
+    const double ratio = row.cpu_amplification_ratio;
+    const auto amplify = [ratio](int64_t x) { return ratio > 1.0 ? (int64_t)ceil((double)x * ratio) : x; };
+    row.cpuset_milli = (int64_t)nalloc * 1000;
+    row.cpuset_amp_milli = amplify(row.cpuset_milli);
+    for (int z = 0; z < KG_MAX_ZONES; z++)
+        row.zone_cpuset_amp[z] = amplify((int64_t)zone_alloc[z] * 1000) - (int64_t)zone_alloc[z] * 1000;
+    return nalloc;
+}
+
+// resourceManager.Allocate's cpuset part for a pod that binds on the node (resource_manager.go:171-195,
+// 273-360): the zones of the Filter's hint (allocateResourcesByHint on the original requests, through the same
+// per-pair code the kernels run) and allocateCPUSet — available CPUs, the required policy's filter, per
+// allocated zone min(its available CPUs, its cpu / 1000) through the accumulator, the rest node-wide, and
+// satisfiedRequiredCPUBindPolicy.  0 ⇔ a cpuset was taken into taken[n]; −1 ⇔ Allocate fails.
+int kg_cpuset_allocate(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, int required, int take,
+                       const kg_cpu_info *cpus, int32_t n, int32_t max_ref, int32_t strategy, uint8_t *taken) {
+    if (max_ref < 1) max_ref = 1;
+    memset(taken, 0, (size_t)n);
+    if (!(row.flags & KG_NODE_NUMA_TOPO_VALID) || n <= 0) return -1;   // ErrInvalidCPUTopology
+    const int64_t pcpu = p.numa_req[KG_RES_CPU];
+    const int need_all = (int)(pcpu / 1000);   // numCPUsNeeded
+    // PodAllocation.CPUExclusivePolicy = the pod's preferredCPUExclusivePolicy (set by its own PreFilter only)
+    const int excl = (p.flags & KG_POD_NUMA_CPU_BIND) ? (int)((p.cpu_bind >> 8) & 15u) : KG_CPU_EXCL_UNSET;
+    kg_numa_out o;
+    o.feasible = true;
+    o.score = 0;
+    o.n_alloc = 0;
+    const bool opts = (row.flags & KG_NODE_NUMA_OPTIONS) != 0;
+    if (opts && row.numa_policy != KG_NUMA_NONE) {   // a hint exists only where the Filter admitted one
+        const double ratio = row.cpu_amplification_ratio;
+        const int64_t pcpu_eff = pcpu != 0 && ratio > 1.0 ? (int64_t)ceil((double)pcpu * ratio) : pcpu;
+        kg_numa_bind_zoned(c, row, p, o, row.requested, row.numa_policy, pcpu_eff, required);
+        if (!o.feasible) return -1;
+    }
+    std::vector<uint8_t> avail((size_t)n), zav((size_t)n), got((size_t)n);
+    kg_cpuset_available(cpus, n, max_ref, avail.data());
+    if (required != KG_CPU_BIND_UNSET) kg_cpuset_filter_required(cpus, n, required, avail.data());
+    int navail = 0;
+    for (int32_t k = 0; k < n; k++) navail += avail[k];
+    if (navail < need_all) return -1;   // "not enough cpus available to satisfy request"
+    int need = need_all;
+    if (o.n_alloc > 0) {
+        int taken_n = 0;
+        for (int j = 0; j < o.n_alloc; j++) {   // allocatedNUMANodes in ascending affinity id
+            const int32_t zid = row.zone_id[o.zone[j]];
+            int cnt = 0;
+            for (int32_t k = 0; k < n; k++) {
+                zav[k] = (uint8_t)(avail[k] && cpus[k].node == zid);
+                cnt += zav[k];
+            }
+            const int64_t want = o.alloc[j][KG_RES_CPU] / 1000;
+            if (want < cnt) cnt = (int)want;
+            if (kg_cpuset_take_cpus(cpus, n, max_ref, zav.data(), cnt, take, excl, strategy, got.data()) != 0) return -1;
+            for (int32_t k = 0; k < n; k++)
+                if (got[k] && !taken[k]) {
+                    taken[k] = 1;
+                    taken_n++;
+                }
+        }
+        need -= taken_n;
+        if (need != 0) return -1;
+    }
+    if (need > 0) {
+        for (int32_t k = 0; k < n; k++) zav[k] = (uint8_t)(avail[k] && !taken[k]);
+        if (kg_cpuset_take_cpus(cpus, n, max_ref, zav.data(), need, take, excl, strategy, got.data()) != 0) return -1;
+        for (int32_t k = 0; k < n; k++) taken[k] |= got[k];
+    }
+    if (required != KG_CPU_BIND_UNSET && !kg_cpuset_satisfies_required(cpus, n, required, taken)) return -1;
+    return 0;
+}
+
+// NodeAllocation.addPodAllocation (node_allocation.go:72-100) for the cpuset: RefCount + 1 and the pod's
+// exclusive policy on every taken CPU
+void kg_cpuset_apply(const kg_pod_dev &p, kg_cpu_info *cpus, int32_t n, const uint8_t *taken) {
+    const int excl = (p.flags & KG_POD_NUMA_CPU_BIND) ? (int)((p.cpu_bind >> 8) & 15u) : KG_CPU_EXCL_UNSET;
+    for (int32_t k = 0; k < n; k++)
+        if (taken[k]) {
+            cpus[k].refcount++;
+            cpus[k].exclusive = excl;
+        }
+}
+
+// the accumulator's strategy for a node: its label, else the plugin default (util.go:27-41); only
+// NUMAMostAllocated changes the orderings (cpu_accumulator.go:434-733)
+int32_t kg_cpuset_strategy(const kg_config &cfg, int32_t label) {
+    if (label == KG_NUMA_ALLOC_MOST) return KG_STRATEGY_MOST_ALLOCATED;
+    if (label == KG_NUMA_ALLOC_LEAST || label == KG_NUMA_ALLOC_DISTRIBUTE_EVENLY) return KG_STRATEGY_LEAST_ALLOCATED;
+    return cfg.numa_hint_strategy == KG_STRATEGY_MOST_ALLOCATED ? KG_STRATEGY_MOST_ALLOCATED : KG_STRATEGY_LEAST_ALLOCATED;
 }
 
 extern "C" kg_status kg_cpuset_take(const kg_cpu_info *cpus, int32_t n_cpus, int32_t max_ref_count,

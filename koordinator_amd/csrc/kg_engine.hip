@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <map>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -1758,7 +1759,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                                                                 int64_t n_nodes, int64_t now_ns, int32_t *out_node,
                                                                 int64_t *out_score, RsvArgs ra, int32_t kslots,
                                                                 int32_t *slow_list, int32_t *slow_count,
-                                                                int32_t rescore_slow) {
+                                                                int32_t rescore_slow, int32_t defer_last) {
     constexpr int POD_DW = (int)(sizeof(kg_pod_dev) / 4);
     static_assert(sizeof(kg_pod_dev) % 4 == 0 && POD_DW <= KG_RESOLVE_THREADS, "pod rows are staged one dword per thread");
     __shared__ int32_t touched[KG_MAX_CHUNK];
@@ -1922,10 +1923,12 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         }
         const unsigned long long w = gate_ok[par] ? wb : 0ull;   // a pod failing the quota gate is unschedulable
         const int32_t node = w ? (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull)) : -1;
-        if (!w) {
+        if (!w || (defer_last && j == n - 1)) {
+            // no feasible node; or the chunk's last pod may bind a cpuset: it is selected here and reserved by
+            // the host (the CPU accumulator) after the launch
             if (tid == 0) {
-                out_node[j] = -1;
-                out_score[j] = -1;
+                out_node[j] = node;
+                out_score[j] = w ? (int64_t)(w >> 32) - 1 : -1;
             }
             continue;   // nothing changed: the next pod's first barrier orders the outputs
         }
@@ -2113,6 +2116,14 @@ struct kg_engine {
                                             // bit 2: valid CPU topology without CPU detail
     int64_t n_numa_policy_nodes = 0, n_node_bind_nodes = 0, n_no_detail_nodes = 0;
     bool batch_bind = false;
+    // cpuset Reserve (kg_cpus_set): each node's logical CPUs as NodeAllocation holds them, its MaxRefCount and
+    // accumulator strategy; pods that may bind a cpuset end their placement chunk (pod_may_bind)
+    struct CpuTable {
+        int32_t max_ref = 1, strategy = KG_STRATEGY_LEAST_ALLOCATED;
+        std::vector<kg_cpu_info> cpus;
+    };
+    std::unordered_map<int32_t, CpuTable> cpu_tab;
+    std::vector<uint8_t> pod_may_bind;   // bit 0: binds by its own PreFilter; bit 1: a cpu request (node policy)
     bool profiling = false;
     bool mat_kernel = false;            // matrix mode with planes through k_mat (else k_eval3); KG_MATRIX_KERNEL
     // Reservation / ElasticQuota (config 5)
@@ -2564,18 +2575,23 @@ RsvArgs rsv_args(const kg_engine *e) {
     return ra;
 }
 
-// Cpuset binding (NodeNUMAResource for LSE / LSR pods, or any cpu request on a node with a CPU bind policy)
-// is answered in matrix mode, where the Filter's Allocate reduces to counts of free CPUs (node-wide without a
-// NUMA topology policy, per allocated zone with one); the cpuset a Reserve takes (the CPU accumulator), nodes
-// whose valid topology lacks CPU detail and reservation-reserved cpusets are refused explicitly instead of
-// being answered wrongly.
-kg_status bind_ready(kg_engine *e, bool placement) {
+// Cpuset binding (NodeNUMAResource for LSE / LSR pods, or any cpu request on a node with a CPU bind policy):
+// the Filter's Allocate reduces to counts of free CPUs (node-wide without a NUMA topology policy, per allocated
+// zone with one), which the rows carry; the Reserve takes the CPUs on the host from the kg_cpus_set tables
+// (kg_place, kg_commit).  The sharded chunk API (no host Reserve step), nodes whose valid topology lacks CPU
+// detail and reservation-reserved cpusets are refused explicitly instead of being answered wrongly.
+kg_status bind_ready(kg_engine *e, bool placement, bool host_reserve = false) {
     if (!(e->cfg.enabled_plugins & KG_PLUGIN_NUMA)) return KG_OK;
     const bool any_bind = e->batch_bind || e->n_node_bind_nodes > 0;
-    if (placement && any_bind)
+    if (placement && any_bind && !host_reserve)
         return set_err(e, KG_ERR_UNSUPPORTED,
-                       "cpuset allocation at Reserve (the CPU accumulator) is not on the engine path; evaluate "
-                       "cpuset-bound pods in matrix mode (kg_eval)");
+                       "cpuset Reserve runs in kg_place / kg_commit (the host takes the CPUs between chunks); the "
+                       "chunk API does not bind cpusets");
+    if (placement && any_bind) {   // every node a cpuset can land on needs its CPU table
+        for (size_t i = 0; i < e->node_bind_facts.size(); i++)
+            if ((e->node_bind_facts[i] & 8) && !e->cpu_tab.count((int32_t)i))
+                return set_err(e, KG_ERR_STATE, "node %zu: cpuset Reserve needs the node's CPUs (kg_cpus_set)", i);
+    }
     if (e->batch_bind && e->n_no_detail_nodes > 0)
         return set_err(e, KG_ERR_UNSUPPORTED,
                        "cpuset-bound pods need CPU detail on every node with a valid CPU topology (%lld without)",
@@ -2742,6 +2758,7 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
     e->pl.cap = cap;
     e->n_nodes = n_nodes;
     e->node_bind_facts.assign((size_t)n_nodes, 0);
+    e->cpu_tab.clear();   // CPU tables refer to node indices: dropped with the snapshot
     e->n_numa_policy_nodes = e->n_node_bind_nodes = e->n_no_detail_nodes = 0;
     e->shard_begin = 0;
     e->shard_end = n_nodes;
@@ -2779,6 +2796,7 @@ kg_status kg_snapshot_upsert(kg_engine *e, const int32_t *node_index, const kg_n
         if (opts && r.numa_policy != KG_NUMA_NONE) f |= 1;
         if (opts && r.node_cpu_bind != KG_NODE_CPU_BIND_NONE) f |= 2;
         if ((r.flags & KG_NODE_NUMA_TOPO_VALID) && r.cpus_per_core <= 0) f |= 4;
+        if ((r.flags & KG_NODE_NUMA_TOPO_VALID) && r.cpus_per_core > 0) f |= 8;   // CPU detail: a cpuset can land
         if ((f & 2) && (f & 4))
             return set_err(e, KG_ERR_UNSUPPORTED, "node %d: a CPU bind policy without CPU detail", node_index[k]);
         facts[k] = f;
@@ -2811,6 +2829,7 @@ kg_status kg_snapshot_remove(kg_engine *e, int32_t node_index) {
     if (node_index < 0 || node_index >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "node index out of range");
     kg_node_row row;
     memset(&row, 0, sizeof(row));  // flags = 0 → invalid, never feasible
+    e->cpu_tab.erase(node_index);
     return kg_snapshot_upsert(e, &node_index, &row, 1);
 }
 
@@ -2930,6 +2949,13 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     e->pow2 = pow2;
     e->pod_rows_h.assign(rows, rows + n);
     e->batch_bind = batch_bind;
+    e->pod_may_bind.assign((size_t)n, 0);
+    if (e->cfg.enabled_plugins & KG_PLUGIN_NUMA)
+        for (int32_t i = 0; i < n; i++) {
+            if (rows[i].flags & (KG_POD_NUMA_SKIP | KG_POD_NUMA_BIND_INVALID)) continue;
+            e->pod_may_bind[i] = (uint8_t)(((rows[i].flags & KG_POD_NUMA_CPU_BIND) ? 1 : 0) |
+                                           (rows[i].numa_request[KG_RES_CPU] != 0 && rows[i].numa_request[KG_RES_CPU] % 1000 == 0 ? 2 : 0));
+        }
     cls_prepare(e);
     return KG_OK;
 }
@@ -3041,11 +3067,11 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     return KG_OK;
 }
 
-kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev) {
-    kg_status st = check_engine(e);
-    if (st) return st;
-    st = bind_ready(e, true);
-    if (st) return st;
+}  // extern "C"
+
+namespace {
+
+kg_status chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev) {
     if (pod_begin < 0 || n < 0 || pod_begin + (int64_t)n > e->n_pods || (n > 0 && !partial_dev))
         return set_err(e, KG_ERR_RANGE, "bad chunk");
     // the top-k kernel writes every slot of every tile of its shard; the NUMA kernel merges with atomics
@@ -3053,7 +3079,7 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
     const bool whole = e->shard_begin == 0 && e->shard_end == e->n_nodes;
     if (((e->consts.plugins & KG_PLUGIN_NUMA) && n > KG_NUMA_CHUNK_PODS) || !whole)
         HIP_TRY(e, hipMemsetAsync(partial_dev, 0, (size_t)n * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS, e->stream));
-    st = launch_eval(e, now_ns, pod_begin, n, nullptr, nullptr, partial_dev, false, nullptr, true);
+    kg_status st = launch_eval(e, now_ns, pod_begin, n, nullptr, nullptr, partial_dev, false, nullptr, true);
     if (st) return st;
     // reservation nodes: entries of every reservation node (the snapshot is replicated across
     // ranks in the multi-GPU placement, so each rank holds all of them), rows 0..n of E / O
@@ -3064,16 +3090,13 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
     return KG_OK;
 }
 
-kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, const uint32_t *partial_dev,
-                                 int32_t *out_node_dev, int64_t *out_score_dev) {
-    kg_status st = check_engine(e);
-    if (st) return st;
-    st = bind_ready(e, true);
-    if (st) return st;
+// defer_last: the chunk's last pod is only selected (out_node / out_score); its Reserve is host_reserve's
+kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, const uint32_t *partial_dev,
+                        int32_t *out_node_dev, int64_t *out_score_dev, bool defer_last) {
     if (pod_begin < 0 || n < 0 || n > KG_MAX_CHUNK || pod_begin + (int64_t)n > e->n_pods)
         return set_err(e, KG_ERR_RANGE, "bad chunk");
     if (n == 0) return KG_OK;
-    st = quota_ready(e);
+    kg_status st = quota_ready(e);
     if (st) return st;
     RsvArgs ra = rsv_args(e);
     if (ra.rsv) {  // this chunk's entries were written by kg_place_chunk_eval from row 0
@@ -3085,10 +3108,87 @@ kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream, e->consts, e->pl, e->pods, pod_begin, n,
                        partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev, ra,
                        numa && n > KG_NUMA_CHUNK_PODS ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count,
-                       numa ? 0 : 1);   // the NUMA chunk kernels list slow nodes themselves (exact pair path)
+                       numa ? 0 : 1,   // the NUMA chunk kernels list slow nodes themselves (exact pair path)
+                       defer_last ? 1 : 0);
     HIP_TRY(e, hipGetLastError());
     e->generation++;   // the resolve commits the chunk's winners to the snapshot
     return KG_OK;
+}
+
+// Reserve of `pod` on `node` with the cpuset part on the host (NodeNUMAResource.Reserve, plugin.go:375-419):
+// when the pod binds a cpuset there, resourceManager.Allocate runs on the pre-Reserve row and the node's CPU
+// table (kg_cpuset_allocate — the hint's zones through the kernels' own per-pair code, then the CPU
+// accumulator); if it fails the Reserve fails and nothing changes (*failed = true; the scheduler's Unreserve
+// + ForgetPod).  Otherwise the device commits every plugin's Reserve (k_commit_one: zone allocations of the
+// same hint, AssumePod, LoadAware, ElasticQuota) and the host writes the taken CPUs into the table and the
+// node's cpuset counts into its row.
+kg_status host_reserve(kg_engine *e, int32_t pod, int32_t node, bool *failed) {
+    *failed = false;
+    kg_node_row row;
+    HIP_TRY(e, hipMemcpyAsync(&row, e->pl.rows + node, sizeof(row), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    kg_pod_dev pd;
+    kg_pod_dev_from_row(e->cfg, e->pod_rows_h[(size_t)pod], pd);
+    int required, take;
+    const bool bind = (e->consts.plugins & KG_PLUGIN_NUMA) && kg_numa_binds(row, pd, required, take);
+    std::vector<uint8_t> taken;
+    kg_engine::CpuTable *tab = nullptr;
+    if (bind) {
+        auto it = e->cpu_tab.find(node);
+        if (it == e->cpu_tab.end())
+            return set_err(e, KG_ERR_STATE, "node %d: cpuset Reserve needs the node's CPUs (kg_cpus_set)", node);
+        tab = &it->second;
+        const int32_t nc = (int32_t)tab->cpus.size();
+        taken.assign((size_t)nc, 0);
+        if (kg_cpuset_allocate(e->consts, row, pd, required, take, tab->cpus.data(), nc, tab->max_ref, tab->strategy,
+                               taken.data()) != 0) {
+            *failed = true;
+            return KG_OK;
+        }
+    }
+    hipLaunchKernelGGL(k_commit_one, dim3(1), dim3(1), 0, e->stream, e->consts, e->pl, e->pods, pod, node, rsv_args(e));
+    HIP_TRY(e, hipGetLastError());
+    if (bind) {
+        const int32_t nc = (int32_t)tab->cpus.size();
+        kg_cpuset_apply(pd, tab->cpus.data(), nc, taken.data());
+        HIP_TRY(e, hipMemcpyAsync(&row, e->pl.rows + node, sizeof(row), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+        kg_cpuset_row_fields(row, tab->cpus.data(), nc, tab->max_ref);
+        // the row back, its planes re-derived (k_upsert)
+        kg_status st = ensure_scratch(e, sizeof(row) + 512);
+        if (st) return st;
+        char *sc = (char *)e->scratch;
+        HIP_TRY(e, hipMemcpyAsync(sc, &row, sizeof(row), hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(e, hipMemcpyAsync(sc + (sizeof(row) + 255) / 256 * 256, &node, 4, hipMemcpyHostToDevice, e->stream));
+        hipLaunchKernelGGL(k_upsert, dim3(1), dim3(256), 0, e->stream, e->consts, e->pl, (const kg_node_row *)sc,
+                           (const int32_t *)(sc + (sizeof(row) + 255) / 256 * 256), 1);
+        HIP_TRY(e, hipGetLastError());
+    }
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->slow_valid = false;   // the commit may move the node off (or onto) the fast paths
+    e->generation++;
+    return KG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    st = bind_ready(e, true);
+    if (st) return st;
+    return chunk_eval(e, now_ns, pod_begin, n, partial_dev);
+}
+
+kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, const uint32_t *partial_dev,
+                                 int32_t *out_node_dev, int64_t *out_score_dev) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    st = bind_ready(e, true);
+    if (st) return st;
+    return chunk_resolve(e, now_ns, pod_begin, n, partial_dev, out_node_dev, out_score_dev, false);
 }
 
 kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score) {
@@ -3098,28 +3198,101 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
     if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised");
     if (e->shard_begin != 0 || e->shard_end != e->n_nodes)
         return set_err(e, KG_ERR_STATE, "kg_place runs on the whole snapshot; use the chunk API for shards");
+    st = bind_ready(e, true, true);
+    if (st) return st;
     const int32_t P = e->n_pods;
     if (P == 0) return KG_OK;
     int32_t chunk = e->cfg.place_chunk > 0 ? e->cfg.place_chunk : 16;
     if (chunk > KG_MAX_CHUNK) chunk = KG_MAX_CHUNK;
     const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS;
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
-    st = ensure_scratch(e, up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + 256);
+    // the host Reserve's row upload reuses the head of the scratch buffer: the partials live after it
+    const size_t head = 1024;
+    st = ensure_scratch(e, head + up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + 256);
     if (st) return st;
-    char *s = (char *)e->scratch;
+    char *s = (char *)e->scratch + head;
     uint32_t *part = (uint32_t *)s;
     int32_t *dnode = (int32_t *)(s + up(part_b));
     int64_t *dscore = (int64_t *)(s + up(part_b) + up((size_t)P * 4));
-    for (int32_t b = 0; b < P; b += chunk) {
-        const int32_t n = P - b < chunk ? P - b : chunk;
-        st = kg_place_chunk_eval(e, now_ns, b, n, part);
+    // a pod that may bind a cpuset (its own PreFilter decision, or a cpu request where nodes have a CPU bind
+    // policy) ends its chunk, and its Reserve runs on the host before the next chunk is evaluated
+    const bool bind_mode = (e->consts.plugins & KG_PLUGIN_NUMA) && (e->batch_bind || e->n_node_bind_nodes > 0);
+    const uint8_t may_mask = e->n_node_bind_nodes > 0 ? 3 : 1;
+    for (int32_t b = 0; b < P;) {
+        int32_t n = P - b < chunk ? P - b : chunk;
+        bool defer = false;
+        if (bind_mode)
+            for (int32_t k = 0; k < n; k++)
+                if (e->pod_may_bind[(size_t)(b + k)] & may_mask) {
+                    n = k + 1;
+                    defer = true;
+                    break;
+                }
+        st = chunk_eval(e, now_ns, b, n, part);
         if (st) return st;
-        st = kg_place_chunk_resolve(e, now_ns, b, n, part, dnode + b, dscore + b);
+        st = chunk_resolve(e, now_ns, b, n, part, dnode + b, dscore + b, defer);
         if (st) return st;
+        if (defer) {
+            const int32_t j = b + n - 1;
+            int32_t node = -1;
+            HIP_TRY(e, hipMemcpyAsync(&node, dnode + j, 4, hipMemcpyDeviceToHost, e->stream));
+            HIP_TRY(e, hipStreamSynchronize(e->stream));
+            if (node >= 0) {
+                bool failed = false;
+                st = host_reserve(e, j, node, &failed);
+                if (st) return st;
+                if (failed) {   // the Reserve failed: the pod is not placed
+                    const int32_t no = -1;
+                    const int64_t ns = -1;
+                    HIP_TRY(e, hipMemcpyAsync(dnode + j, &no, 4, hipMemcpyHostToDevice, e->stream));
+                    HIP_TRY(e, hipMemcpyAsync(dscore + j, &ns, 8, hipMemcpyHostToDevice, e->stream));
+                    HIP_TRY(e, hipStreamSynchronize(e->stream));
+                }
+            }
+        }
+        b += n;
     }
     HIP_TRY(e, hipMemcpyAsync(out_node, dnode, (size_t)P * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipMemcpyAsync(out_score, dscore, (size_t)P * 8, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return KG_OK;
+}
+
+kg_status kg_cpus_set(kg_engine *e, const kg_cluster_view *view, const int32_t *node_index, int32_t n) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (!view || n < 0 || (!node_index && n > view->n_nodes)) return set_err(e, KG_ERR_INVALID_ARG, "bad CPU table arguments");
+    if (n > e->n_nodes) return set_err(e, KG_ERR_RANGE, "%d CPU tables for %lld nodes", n, (long long)e->n_nodes);
+    std::unordered_map<int32_t, kg_engine::CpuTable> tab;
+    for (int32_t k = 0; k < n; k++) {
+        const int32_t vi = node_index ? node_index[k] : k;
+        if (vi < 0 || vi >= view->n_nodes) return set_err(e, KG_ERR_RANGE, "view node %d out of range", vi);
+        const kg_node_spec &ns = view->nodes[vi];
+        if (ns.numa < 0) continue;
+        if (ns.numa >= view->n_numa || !view->numa) return set_err(e, KG_ERR_RANGE, "node %d: bad NUMA spec index", vi);
+        const kg_numa_spec &nm = view->numa[ns.numa];
+        if (nm.n_cpus <= 0) continue;
+        if (nm.n_cpus > KG_MAX_NODE_CPUS || nm.first_cpu < 0 || nm.first_cpu + (int64_t)nm.n_cpus > view->n_cpus || !view->cpus)
+            return set_err(e, KG_ERR_RANGE, "node %d: bad CPU range", vi);
+        if (nm.numa_allocate_strategy < KG_NUMA_ALLOC_DEFAULT || nm.numa_allocate_strategy > KG_NUMA_ALLOC_DISTRIBUTE_EVENLY)
+            return set_err(e, KG_ERR_INVALID_ARG, "node %d: bad NUMA allocate strategy", vi);
+        kg_engine::CpuTable &t = tab[k];
+        t.max_ref = nm.max_ref_count > 0 ? nm.max_ref_count : 1;
+        t.strategy = kg_cpuset_strategy(e->cfg, nm.numa_allocate_strategy);
+        t.cpus.assign(view->cpus + nm.first_cpu, view->cpus + nm.first_cpu + nm.n_cpus);
+    }
+    e->cpu_tab.swap(tab);
+    return KG_OK;
+}
+
+kg_status kg_cpus_download(kg_engine *e, int32_t node, kg_cpu_info *out, int32_t n) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    auto it = e->cpu_tab.find(node);
+    if (it == e->cpu_tab.end()) return set_err(e, KG_ERR_RANGE, "node %d has no CPU table", node);
+    if (n != (int32_t)it->second.cpus.size() || (n > 0 && !out))
+        return set_err(e, KG_ERR_RANGE, "node %d has %zu CPUs, asked for %d", node, it->second.cpus.size(), n);
+    memcpy(out, it->second.cpus.data(), sizeof(kg_cpu_info) * (size_t)n);
     return KG_OK;
 }
 
@@ -3263,15 +3436,14 @@ kg_status kg_commit(kg_engine *e, int32_t pod, int32_t node) {
     kg_status st = check_engine(e);
     if (st) return st;
     if (pod < 0 || pod >= e->n_pods || node < 0 || node >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "bad commit");
-    st = bind_ready(e, true);
+    st = bind_ready(e, true, true);
     if (st) return st;
     st = quota_ready(e);   // the pod's quota group must exist before its usage is committed
     if (st) return st;
-    hipLaunchKernelGGL(k_commit_one, dim3(1), dim3(1), 0, e->stream, e->consts, e->pl, e->pods, pod, node, rsv_args(e));
-    e->slow_valid = false;
-    HIP_TRY(e, hipGetLastError());
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
-    e->generation++;
+    bool failed = false;
+    st = host_reserve(e, pod, node, &failed);
+    if (st) return st;
+    if (failed) return set_err(e, KG_NOT_FOUND, "pod %d on node %d: not enough cpus available to satisfy request", pod, node);
     return KG_OK;
 }
 

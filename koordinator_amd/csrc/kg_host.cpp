@@ -611,50 +611,8 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
                 nm.n_cpus < 0 || nm.max_ref_count < 0)
                 return KG_ERR_INVALID_ARG;
             row.node_cpu_bind = nm.node_cpu_bind_policy;
-            if (nm.n_cpus > 0) {
-                if (nm.first_cpu < 0 || nm.first_cpu + (int64_t)nm.n_cpus > view->n_cpus || !view->cpus) return KG_ERR_RANGE;
-                if (nm.n_cpus > KG_MAX_NODE_CPUS) return KG_ERR_UNSUPPORTED;
-                const kg_cpu_info *ci = view->cpus + nm.first_cpu;
-                const int32_t max_ref = nm.max_ref_count > 0 ? nm.max_ref_count : 1;
-                // compact core ids (cores are few; ids may be sparse, e.g. socket << 16 | core)
-                int32_t core_id[KG_MAX_NODE_CPUS], core_total[KG_MAX_NODE_CPUS], core_avail[KG_MAX_NODE_CPUS];
-                int32_t ncores = 0, nalloc = 0;
-                for (int32_t c = 0; c < nm.n_cpus; c++) {
-                    int32_t k = 0;
-                    while (k < ncores && core_id[k] != ci[c].core) k++;
-                    if (k == ncores) {
-                        core_id[ncores] = ci[c].core;
-                        core_total[ncores] = core_avail[ncores] = 0;
-                        ncores++;
-                    }
-                    core_total[k]++;
-                    // getAvailableCPUs (node_allocation.go:134-155): allocated = refcount ≥ maxRefCount; reserved out
-                    if (!(ci[c].refcount > 0 && ci[c].refcount >= max_ref) && !ci[c].reserved) core_avail[k]++;
-                    if (ci[c].refcount > 0) nalloc++;
-                }
-                row.cpus_per_core = nm.n_cpus / ncores;
-                // the zone of each core (its CPUs' NUMA node); −1 ⇔ a NUMA node without a zone
-                int32_t core_zone[KG_MAX_NODE_CPUS];
-                for (int32_t k = 0; k < ncores; k++) core_zone[k] = -1;
-                for (int32_t c = 0; c < nm.n_cpus; c++) {
-                    int32_t k = 0;
-                    while (core_id[k] != ci[c].core) k++;
-                    for (int z = 0; z < nm.n_zones && z < KG_MAX_ZONES; z++)
-                        if (nm.zone_id[z] == ci[c].node) core_zone[k] = z;
-                }
-                for (int32_t k = 0; k < ncores; k++) {
-                    const bool full = core_avail[k] == row.cpus_per_core;
-                    if (full) row.cpuset_full_free_cpus += core_avail[k];
-                    if (core_avail[k] > 0) row.cpuset_free_cores++;
-                    row.cpuset_avail_cpus += core_avail[k];
-                    const int32_t z = core_zone[k];
-                    if (z < 0) continue;
-                    row.zone_cpus_avail[z] = (int16_t)(row.zone_cpus_avail[z] + core_avail[k]);
-                    if (full) row.zone_cpus_full[z] = (int16_t)(row.zone_cpus_full[z] + core_avail[k]);
-                    if (core_avail[k] > 0) row.zone_cores_free[z]++;
-                }
-                if (nalloc != nm.cpuset_cpus) return KG_ERR_INVALID_ARG;   // the count fields must agree
-            }
+            if (nm.numa_allocate_strategy < KG_NUMA_ALLOC_DEFAULT || nm.numa_allocate_strategy > KG_NUMA_ALLOC_DISTRIBUTE_EVENLY)
+                return KG_ERR_INVALID_ARG;
             row.numa_policy = nm.policy;
             row.n_zones = nm.n_zones;
             row.cpu_amplification_ratio = nm.cpu_amplification_ratio;
@@ -672,6 +630,15 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
                     if (bit(nm.zone_total[z].present, r)) row.zone_keys |= 1u << (2 * z + r);
                     if (bit(nm.zone_allocated[z].present, r)) row.zone_alloc_keys |= 1u << (2 * z + r);
                 }
+            }
+            // the CPU detail's counts (kg_cpuset_row_fields, the derivation a cpuset Reserve repeats); the
+            // count fields of the spec must agree with it
+            if (nm.n_cpus > 0) {
+                if (nm.first_cpu < 0 || nm.first_cpu + (int64_t)nm.n_cpus > view->n_cpus || !view->cpus) return KG_ERR_RANGE;
+                if (nm.n_cpus > KG_MAX_NODE_CPUS) return KG_ERR_UNSUPPORTED;
+                const int32_t max_ref = nm.max_ref_count > 0 ? nm.max_ref_count : 1;
+                if (kg_cpuset_row_fields(row, view->cpus + nm.first_cpu, nm.n_cpus, max_ref) != nm.cpuset_cpus)
+                    return KG_ERR_INVALID_ARG;
             }
         }
     }
@@ -693,13 +660,41 @@ static bool row_binds(const kg_config &cfg, const kg_node_row &node, const kg_po
 kg_status kg_row_commit(const kg_config *cfg, kg_node_row *node, const kg_pod_row *pod) {
     if (!cfg || !node || !pod) return KG_ERR_INVALID_ARG;
     bool answered;
-    if (row_binds(*cfg, *node, *pod, answered)) return KG_ERR_UNSUPPORTED;   // Reserve takes a cpuset
+    if (row_binds(*cfg, *node, *pod, answered)) return KG_ERR_UNSUPPORTED;   // Reserve takes a cpuset: kg_row_reserve
     kg_pod_dev pd;
     kg_pod_dev_from_row(*cfg, *pod, pd);
     kg_consts k;
     kg_consts_from_config(*cfg, k);
     kg_numa_commit(k, *node, pd);   // zone allocations first: they see the pre-Reserve node
     kg_apply_commit(*node, pd);
+    return KG_OK;
+}
+
+kg_status kg_row_reserve(const kg_config *cfg, kg_node_row *node, const kg_pod_row *pod, kg_cpu_info *cpus,
+                         int32_t n_cpus, int32_t max_ref_count, int32_t numa_allocate_strategy, uint8_t *taken) {
+    if (!cfg || !node || !pod || n_cpus < 0 || n_cpus > KG_MAX_NODE_CPUS || (n_cpus > 0 && (!cpus || !taken)) ||
+        numa_allocate_strategy < KG_NUMA_ALLOC_DEFAULT || numa_allocate_strategy > KG_NUMA_ALLOC_DISTRIBUTE_EVENLY)
+        return KG_ERR_INVALID_ARG;
+    kg_pod_dev pd;
+    kg_pod_dev_from_row(*cfg, *pod, pd);
+    kg_consts k;
+    kg_consts_from_config(*cfg, k);
+    if (n_cpus > 0) memset(taken, 0, (size_t)n_cpus);
+    int required, take;
+    const bool bind = (k.plugins & KG_PLUGIN_NUMA) && kg_numa_binds(*node, pd, required, take);
+    if (bind) {   // NodeNUMAResource.Reserve → Allocate: the cpuset comes first, a failure changes nothing
+        if (!(node->flags & KG_NODE_NUMA_TOPO_VALID)) return KG_NOT_FOUND;   // ErrInvalidCPUTopology
+        if (n_cpus == 0) return KG_ERR_UNSUPPORTED;   // a valid topology without CPU detail
+        if (kg_cpuset_allocate(k, *node, pd, required, take, cpus, n_cpus, max_ref_count,
+                               kg_cpuset_strategy(*cfg, numa_allocate_strategy), taken) != 0)
+            return KG_NOT_FOUND;
+    }
+    kg_numa_commit(k, *node, pd);   // zone allocations first: they see the pre-Reserve node
+    kg_apply_commit(*node, pd);
+    if (bind) {   // Update: the cpuset into the node allocation, and the row's counts from it
+        kg_cpuset_apply(pd, cpus, n_cpus, taken);
+        kg_cpuset_row_fields(*node, cpus, n_cpus, max_ref_count);
+    }
     return KG_OK;
 }
 

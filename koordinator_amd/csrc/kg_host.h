@@ -17,3 +17,8 @@ int kg_cpuset_take_cpus(const kg_cpu_info *cpus, int32_t n_cpus, int32_t max_ref
 void kg_cpuset_available(const kg_cpu_info *cpus, int32_t n_cpus, int32_t max_ref, uint8_t *available);
 void kg_cpuset_filter_required(const kg_cpu_info *cpus, int32_t n_cpus, int32_t bind, uint8_t *available);
 bool kg_cpuset_satisfies_required(const kg_cpu_info *cpus, int32_t n_cpus, int32_t bind, const uint8_t *taken);
+int32_t kg_cpuset_row_fields(kg_node_row &row, const kg_cpu_info *cpus, int32_t n, int32_t max_ref);
+int kg_cpuset_allocate(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, int required, int take,
+                       const kg_cpu_info *cpus, int32_t n, int32_t max_ref, int32_t strategy, uint8_t *taken);
+void kg_cpuset_apply(const kg_pod_dev &p, kg_cpu_info *cpus, int32_t n, const uint8_t *taken);
+int32_t kg_cpuset_strategy(const kg_config &cfg, int32_t label);

@@ -40,6 +40,20 @@ def row_commit(cfg: np.ndarray, node_row: np.ndarray, pod_row: np.ndarray) -> No
     _check(nat.lib().kg_row_commit(nat.ptr(cfg), nat.ptr(node_row), nat.ptr(pod_row)), what="kg_row_commit")
 
 
+def row_reserve(cfg: np.ndarray, node_row: np.ndarray, pod_row: np.ndarray, cpus: np.ndarray, max_ref_count: int = 1,
+                numa_allocate_strategy: int = 0):
+    """kg_row_reserve: the Reserve of one pair on a host row and the node's CPU_INFO array (both updated in
+    place).  Returns the taken cpuset (bool per cpu), or None when the Reserve fails (KG_NOT_FOUND)."""
+    taken = np.zeros(len(cpus), dtype=np.uint8)
+    st = nat.lib().kg_row_reserve(nat.ptr(cfg), nat.ptr(node_row), nat.ptr(pod_row), nat.ptr(cpus) if len(cpus) else None,
+                                  len(cpus), int(max_ref_count), int(numa_allocate_strategy),
+                                  nat.ptr(taken) if len(cpus) else None)
+    if st == nat.NOT_FOUND:
+        return None
+    _check(st, what="kg_row_reserve")
+    return taken.astype(bool)
+
+
 def row_eval(cfg: np.ndarray, node_row: np.ndarray, pod_row: np.ndarray, now_ns: int):
     """(feasible, fit, la, numa) of one pair on host rows (the kernels' per-pair code, run on the CPU)."""
     f, a, b, c = (ctypes.c_int32() for _ in range(4))
@@ -116,6 +130,19 @@ class Engine:
         idx = np.ascontiguousarray(idx, dtype=np.int32)
         rows = np.ascontiguousarray(rows, dtype=nat.NODE_ROW)
         _check(nat.lib().kg_snapshot_upsert(self._h, nat.ptr(idx), nat.ptr(rows), len(idx)), self, "kg_snapshot_upsert")
+
+    def set_cpus(self, view, node_index: Optional[Sequence[int]] = None) -> None:
+        """kg_cpus_set: snapshot node k takes the CPU detail of view node node_index[k] (default k)."""
+        if node_index is None:
+            _check(nat.lib().kg_cpus_set(self._h, ctypes.byref(view.c_view), None, len(view.nodes)), self, "kg_cpus_set")
+            return
+        idx = np.ascontiguousarray(node_index, dtype=np.int32)
+        _check(nat.lib().kg_cpus_set(self._h, ctypes.byref(view.c_view), nat.ptr(idx), len(idx)), self, "kg_cpus_set")
+
+    def download_cpus(self, node: int, n_cpus: int) -> np.ndarray:
+        out = np.zeros(n_cpus, dtype=nat.CPU_INFO)
+        _check(nat.lib().kg_cpus_download(self._h, int(node), nat.ptr(out), n_cpus), self, "kg_cpus_download")
+        return out
 
     def remove(self, i: int) -> None:
         _check(nat.lib().kg_snapshot_remove(self._h, int(i)), self, "kg_snapshot_remove")
@@ -223,8 +250,13 @@ class Engine:
                                                 ctypes.c_void_p(node_ptr), ctypes.c_void_p(score_ptr)), self,
                "kg_place_chunk_resolve")
 
-    def commit(self, pod: int, node: int) -> None:
-        _check(nat.lib().kg_commit(self._h, pod, node), self, "kg_commit")
+    def commit(self, pod: int, node: int) -> bool:
+        """kg_commit; False ⇔ the Reserve failed (a cpuset the accumulator cannot take; nothing changed)."""
+        st = nat.lib().kg_commit(self._h, pod, node)
+        if st == nat.NOT_FOUND:
+            return False
+        _check(st, self, "kg_commit")
+        return True
 
     # Reservation / ElasticQuota -----------------------------------------------------------
     def set_reservations(self, rsv: np.ndarray) -> None:

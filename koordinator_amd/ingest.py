@@ -43,6 +43,7 @@ USAGE_THRESHOLDS = "scheduling.koordinator.sh/usage-thresholds"
 NUMA_POLICY_LABEL = "node.koordinator.sh/numa-topology-policy"
 CPU_TOPOLOGY = "node.koordinator.sh/cpu-topology"
 NODE_CPU_BIND_LABEL = "node.koordinator.sh/cpu-bind-policy"
+NUMA_ALLOCATE_STRATEGY_LABEL = "node.koordinator.sh/numa-allocate-strategy"   # numa_aware.go:52-53
 KUBELET_CPU_MANAGER_POLICY = "kubelet.koordinator.sh/cpu-manager-policy"
 POD_CPU_ALLOCS = "node.koordinator.sh/pod-cpu-allocs"
 SYSTEM_QOS_RESOURCE = "node.koordinator.sh/system-qos-resource"
@@ -497,6 +498,10 @@ def node_from_object(node: dict, nrt: Optional[dict] = None) -> ob.Node:
     elif label_policy:
         n.numa_policy = label_policy
     n.cpu_bind_policy = node_cpu_bind_policy(labels, nrt)
+    # GetNUMAAllocateStrategy (util.go:35-41): any non-empty label value replaces the plugin default; the CPU
+    # accumulator only tells NUMAMostAllocated from the rest
+    v = labels.get(NUMA_ALLOCATE_STRATEGY_LABEL, "")
+    n.numa_allocate_strategy = v if v in ob.NUMA_ALLOCATE else ("LeastAllocated" if v else "")
     return n
 
 

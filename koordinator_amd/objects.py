@@ -142,6 +142,7 @@ class Node:
     cpu_allocated: Optional[Dict[int, tuple]] = None
     reserved_cpus: Sequence[int] = ()
     max_ref_count: int = 1
+    numa_allocate_strategy: str = ""         # label node.koordinator.sh/numa-allocate-strategy
 
 
 NUMA_POLICY = {"": nat.NUMA_NONE, "BestEffort": nat.NUMA_BEST_EFFORT, "Restricted": nat.NUMA_RESTRICTED,
@@ -150,6 +151,8 @@ CPU_BIND = {"": nat.CPU_BIND_UNSET, "Default": nat.CPU_BIND_DEFAULT, "FullPCPUs"
             "SpreadByPCPUs": nat.CPU_BIND_SPREAD_BY_PCPUS, "ConstrainedBurst": nat.CPU_BIND_CONSTRAINED_BURST}
 CPU_EXCLUSIVE = {"": nat.CPU_EXCL_UNSET, "None": nat.CPU_EXCL_NONE, "PCPULevel": nat.CPU_EXCL_PCPU_LEVEL,
                  "NUMANodeLevel": nat.CPU_EXCL_NUMA_NODE_LEVEL}
+NUMA_ALLOCATE = {"": nat.NUMA_ALLOC_DEFAULT, "MostAllocated": nat.NUMA_ALLOC_MOST,
+                 "LeastAllocated": nat.NUMA_ALLOC_LEAST, "DistributeEvenly": nat.NUMA_ALLOC_DISTRIBUTE_EVENLY}
 NODE_CPU_BIND = {"": nat.NODE_CPU_BIND_NONE, "None": nat.NODE_CPU_BIND_NONE,
                  "FullPCPUsOnly": nat.NODE_CPU_BIND_FULL_PCPUS_ONLY, "SpreadByPCPUs": nat.NODE_CPU_BIND_SPREAD_BY_PCPUS}
 
@@ -173,6 +176,7 @@ def numa_spec_record(n: "Node", cpus: Optional[list] = None) -> np.ndarray:
         rec["zone_cpuset_cpus"][z] = (n.zone_cpuset_cpus or {}).get(zid, 0)
     rec["node_cpu_bind_policy"] = NODE_CPU_BIND[n.cpu_bind_policy]
     rec["max_ref_count"] = n.max_ref_count
+    rec["numa_allocate_strategy"] = NUMA_ALLOCATE[n.numa_allocate_strategy]
     if n.cpu_detail is not None and cpus is not None:
         alloc = n.cpu_allocated or {}
         rec["first_cpu"], rec["n_cpus"] = len(cpus), len(n.cpu_detail)

@@ -937,7 +937,18 @@ static int acc_excl(int x) { return x == KG_CPU_EXCL_PCPU_LEVEL ? 1 : x == KG_CP
 /* resourceManager.Allocate without a NUMA hint for a cpuset request (resource_manager.go:171-195, 296-375):
  * available CPUs of the node allocation, filtered by the required bind policy, then takePreferredCPUs and the
  * required-policy check.  1 ⇔ a cpuset was found. */
+static int numa_allocate_cpuset2(const kg_cluster_view *v, const kg_numa_spec *numa, int need, int required, int take,
+                                 int excl, int strategy, uint8_t *out);
 static int numa_allocate_cpuset(const kg_cluster_view *v, const kg_numa_spec *numa, int need, int bind, int excl) {
+    /* the NUMA allocate strategy orders candidates only; whether a cpuset is found does not depend on it */
+    return numa_allocate_cpuset2(v, numa, need, bind, bind, excl, 1, NULL);
+}
+
+/* allocateCPUSet without allocated NUMA nodes (resource_manager.go:296-375): `required` filters the available
+ * CPUs and is checked at the end (UNSET ⇔ not required); the accumulator takes with `take`; `out` (may be NULL)
+ * receives the cpuset. */
+static int numa_allocate_cpuset2(const kg_cluster_view *v, const kg_numa_spec *numa, int need, int required, int take,
+                                 int excl, int strategy, uint8_t *out) {
     const int n = numa->n_cpus;
     if (n <= 0 || n > 1024 || numa->first_cpu < 0 || numa->first_cpu + n > v->n_cpus) return 0;
     const kg_cpu_info *ci = v->cpus + numa->first_cpu;
@@ -953,14 +964,15 @@ static int numa_allocate_cpuset(const kg_cluster_view *v, const kg_numa_spec *nu
     const kgo_cpu_topo t = {n, sock, node, core};
     const int max_ref = numa->max_ref_count > 0 ? numa->max_ref_count : 1;
     kgo_available_cpus(&t, max_ref, ref, reserved, NULL, avail, NULL);
-    kgo_filter_required_bind(&t, acc_bind(bind), avail);   /* options.requiredCPUBindPolicy is true here */
+    if (required != KG_CPU_BIND_UNSET) kgo_filter_required_bind(&t, acc_bind(required), avail);
     int navail = 0;
     for (int i = 0; i < n; i++) navail += avail[i];
     if (navail < need) return 0;
-    /* the NUMA allocate strategy orders candidates only; whether a cpuset is found does not depend on it */
-    if (kgo_take_preferred_cpus(&t, max_ref, avail, NULL, ref, ex, need, acc_bind(bind), acc_excl(excl), 1, got) != 0)
+    if (kgo_take_preferred_cpus(&t, max_ref, avail, NULL, ref, ex, need, acc_bind(take), acc_excl(excl), strategy, got) != 0)
         return 0;
-    return kgo_satisfied_required_bind(&t, acc_bind(bind), got);
+    if (required != KG_CPU_BIND_UNSET && !kgo_satisfied_required_bind(&t, acc_bind(required), got)) return 0;
+    if (out) memcpy(out, got, (size_t)n);
+    return 1;
 }
 
 /* FilterByNUMANode + Score for a cpuset request on a node with a NUMA topology policy: the options of
@@ -970,7 +982,8 @@ static int numa_allocate_cpuset(const kg_cluster_view *v, const kg_numa_spec *nu
  * the CPU accumulator — and the score over calculateAllocatableAndRequested (scoring.go:118-164). */
 static int numa_pair_cpuset(const kg_config *c, const kg_cluster_view *v, const kg_node_spec *n,
                             const kg_numa_spec *numa, int policy, const kg_resource_list *preq, int64_t pod_cpu,
-                            int need, int required, int take_policy, int excl, int64_t *score, numa_hint *hint) {
+                            int need, int required, int take_policy, int excl, int64_t *score, numa_hint *hint,
+                            int strategy, uint8_t *out_cpus, kg_resource_list *out_zg, int *out_gz, int *out_ng) {
     const int ncpu = numa->n_cpus;
     if (ncpu <= 0 || ncpu > 1024 || numa->first_cpu < 0 || numa->first_cpu + ncpu > v->n_cpus) return 0;
     const kg_cpu_info *ci = v->cpus + numa->first_cpu;
@@ -1031,8 +1044,8 @@ static int numa_pair_cpuset(const kg_config *c, const kg_cluster_view *v, const 
             }
             int want = (int)(get(&zg[j], KG_RES_CPU) / 1000);
             if (want < cnt) cnt = want;
-            if (kgo_take_preferred_cpus(&t, max_ref, zav, NULL, ref, ex, cnt, acc_bind(take_policy), acc_excl(excl), 1,
-                                        got) != 0)
+            if (kgo_take_preferred_cpus(&t, max_ref, zav, NULL, ref, ex, cnt, acc_bind(take_policy), acc_excl(excl),
+                                        strategy, got) != 0)
                 return 0;
             for (int k = 0; k < ncpu; k++)
                 if (got[k] && !result[k]) { result[k] = 1; taken++; }
@@ -1042,12 +1055,20 @@ static int numa_pair_cpuset(const kg_config *c, const kg_cluster_view *v, const 
     }
     if (left > 0) {
         for (int k = 0; k < ncpu; k++) zav[k] = (uint8_t)(avail[k] && !result[k]);
-        if (kgo_take_preferred_cpus(&t, max_ref, zav, NULL, ref, ex, left, acc_bind(take_policy), acc_excl(excl), 1,
+        if (kgo_take_preferred_cpus(&t, max_ref, zav, NULL, ref, ex, left, acc_bind(take_policy), acc_excl(excl), strategy,
                                     got) != 0)
             return 0;
         for (int k = 0; k < ncpu; k++) result[k] |= got[k];
     }
     if (required != KG_CPU_BIND_UNSET && !kgo_satisfied_required_bind(&t, acc_bind(required), result)) return 0;
+    if (out_cpus) {   /* Reserve: the PodAllocation (cpuset + NUMANodeResources) */
+        memcpy(out_cpus, result, (size_t)ncpu);
+        for (int j = 0; j < ng; j++) {
+            out_zg[j] = zg[j];
+            out_gz[j] = gz[j];
+        }
+        *out_ng = ng;
+    }
     /* Score: the node's cpuset CPUs (amplified) as the requested cpu */
     const int64_t cs = amplify((int64_t)numa->cpuset_cpus * 1000, numa->cpu_amplification_ratio);
     if (ng > 0) {
@@ -1152,7 +1173,7 @@ static int numa_pair(const kg_config *c, const kg_cluster_view *v, const kg_pod_
             /* getCPUBindPolicy (util.go:85-103): the required policy, else the preferred one */
             const int take_policy = required != KG_CPU_BIND_UNSET ? required : state_policy;
             return numa_pair_cpuset(c, v, n, numa, policy, &preq, pod_cpu, need, required, take_policy, state_excl,
-                                    score, hint);
+                                    score, hint, 1, NULL, NULL, NULL, NULL);
         }
     }
     numa_zones z;
@@ -1211,6 +1232,81 @@ static void numa_reserve(const kg_config *c, const kg_cluster_view *v, const kg_
     int ng, gz[KG_MAX_ZONES];
     if (numa_allocate(&z, &hint, &preq, got, &ng, gz) != 0) return;
     for (int i = 0; i < ng; i++) rl_add(&numa->zone_allocated[gz[i]], &got[i]);
+}
+
+/* Reserve's cpuset decision (plugin.go:375-404): the PreFilter state (plugin.go:232-262), requestCPUBind
+ * (util.go:105-122) and getCPUBindPolicy (util.go:85-103).  1 ⇔ the pod binds a cpuset on the node; *required
+ * (UNSET ⇔ not required), *take (cpuBindPolicy), *excl (preferredCPUExclusivePolicy of the PreFilter state). */
+static int numa_reserve_binds(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod,
+                              const kg_numa_spec *numa, int *required, int *take, int *excl) {
+    kg_resource_list preq;
+    numa_pod_requests(v, pod, &preq);
+    *required = *take = KG_CPU_BIND_UNSET;
+    *excl = KG_CPU_EXCL_UNSET;
+    if (numa_skip(&preq)) return 0;
+    const int64_t pcpu = get(&preq, KG_RES_CPU);
+    int state_bind = 0, state_required = KG_CPU_BIND_UNSET, state_policy = KG_CPU_BIND_UNSET;
+    if ((pod->label_qos == KG_QOS_LSE || pod->label_qos == KG_QOS_LSR) && kgo_priority_class(v, pod) == KG_PRIO_PROD) {
+        int bind = pod->cpu_bind_preferred;
+        if (bind == KG_CPU_BIND_UNSET || bind == KG_CPU_BIND_DEFAULT) bind = c->numa_default_cpu_bind_policy;
+        int req = pod->cpu_bind_required;
+        if (req == KG_CPU_BIND_DEFAULT) req = c->numa_default_cpu_bind_policy;
+        if (req != KG_CPU_BIND_UNSET) bind = req;
+        if (bind == KG_CPU_BIND_FULL_PCPUS || bind == KG_CPU_BIND_SPREAD_BY_PCPUS) {
+            if (pcpu % 1000 != 0) return 0;   /* PreFilter failed: never reserved */
+            if (pcpu > 0) {
+                state_bind = 1;
+                state_required = req;
+                state_policy = bind;
+                *excl = pod->cpu_exclusive;
+            }
+        }
+    }
+    const int node_bind = numa ? numa->node_cpu_bind_policy : KG_NODE_CPU_BIND_NONE;
+    if (!state_bind) {   /* requestCPUBind by the node's CPU bind policy */
+        if (pcpu == 0 || node_bind == KG_NODE_CPU_BIND_NONE || pcpu % 1000 != 0) return 0;
+    }
+    if (state_required != KG_CPU_BIND_UNSET) {
+        *required = state_required;
+        *take = state_required;
+        return 1;
+    }
+    *take = state_policy;
+    if (node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) *required = *take = KG_CPU_BIND_SPREAD_BY_PCPUS;
+    else if (node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) *required = *take = KG_CPU_BIND_FULL_PCPUS;
+    return 1;
+}
+
+/* GetNUMAAllocateStrategy (util.go:27-41): the node label, else NUMAMostAllocated iff the plugin's
+ * NUMAScoringStrategy is MostAllocated; the accumulator only tests for NUMAMostAllocated */
+static int numa_alloc_strategy(const kg_config *c, const kg_numa_spec *numa) {
+    if (numa->numa_allocate_strategy == KG_NUMA_ALLOC_MOST) return 1;
+    if (numa->numa_allocate_strategy != KG_NUMA_ALLOC_DEFAULT) return 0;
+    return c->numa_hint_strategy == KG_STRATEGY_MOST_ALLOCATED;
+}
+
+/* resourceManager.Allocate for a cpuset pod (resource_manager.go:171-375) on the chosen node: the Filter's
+ * hint and allocateResourcesByHint (numa_pair_cpuset on a topology-policy node), else allocateCPUSet
+ * node-wide.  1 ⇔ allocated: out_cpus (per cpu of the node), the zone allocations zg / gz / *ng. */
+static int numa_reserve_cpuset(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod,
+                               const kg_node_spec *n, const kg_numa_spec *numa, int required, int take, int excl,
+                               uint8_t *out_cpus, kg_resource_list *zg, int *gz, int *ng) {
+    *ng = 0;
+    if (numa->cpu_topology_valid != 1 || numa->n_cpus <= 0) return 0;   /* ErrInvalidCPUTopology */
+    kg_resource_list preq;
+    numa_pod_requests(v, pod, &preq);
+    const int64_t pcpu = get(&preq, KG_RES_CPU);
+    const int need = (int)(pcpu / 1000);   /* numCPUsNeeded */
+    const int strategy = numa_alloc_strategy(c, numa);
+    if (numa->policy != KG_NUMA_NONE) {
+        const double ratio = numa->cpu_amplification_ratio;
+        const int64_t pod_cpu = pcpu != 0 && ratio > 1.0 ? amplify(pcpu, ratio) : pcpu;   /* getResourceOptions */
+        int64_t score;
+        numa_hint h;
+        return numa_pair_cpuset(c, v, n, numa, numa->policy, &preq, pod_cpu, need, required, take, excl, &score, &h,
+                                strategy, out_cpus, zg, gz, ng);
+    }
+    return numa_allocate_cpuset2(v, numa, need, required, take, excl, strategy, out_cpus);
 }
 
 int kgo_numa_eval(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n,
@@ -1706,11 +1802,21 @@ int kgo_eval_matrix5(const kg_config *c, const kg_cluster_view *v, const int32_t
 
 /* Reserve of the chosen node for one pod: AssumePod, NodeNUMAResource zones, Reservation, ElasticQuota,
  * LoadAware assign (the sequential cycle's state updates). */
-static void reserve_pod(const kg_config *c, kg_cluster_view *vv, const kg_cluster_view *v, node_state *st,
-                        rsv_index *ri, kg_quota *quotas, const kg_pod_spec *pod, int32_t best_n, int nom,
-                        int64_t now_ns) {
-    /* Reserve: AssumePod → NodeInfo.AddPod (calculateResource) */
+static int reserve_pod(const kg_config *c, kg_cluster_view *vv, const kg_cluster_view *v, node_state *st,
+                       rsv_index *ri, kg_quota *quotas, const kg_pod_spec *pod, int32_t best_n, int nom,
+                       int64_t now_ns) {
     node_state *s = &st[best_n];
+    /* NodeNUMAResource.Reserve → Allocate of a cpuset: when it fails the Reserve fails, the plugins that
+     * reserved are unreserved and the pod is forgotten — nothing changes and the pod is not placed */
+    int bound = 0, required = 0, take = 0, excl = 0, ng = 0, gz[KG_MAX_ZONES];
+    kg_resource_list zg[KG_MAX_ZONES];
+    uint8_t taken[1024];
+    if ((c->enabled_plugins & KG_PLUGIN_NUMA) && s->has_numa &&
+        numa_reserve_binds(c, vv, pod, &s->numa, &required, &take, &excl)) {
+        if (!numa_reserve_cpuset(c, vv, pod, &s->spec, &s->numa, required, take, excl, taken, zg, gz, &ng)) return 0;
+        bound = 1;
+    }
+    /* Reserve: AssumePod → NodeInfo.AddPod (calculateResource) */
     fw_resource req;
     fit_pod_request(vv, pod, &req);
     for (int r = 0; r < KG_NUM_RES; r++) {
@@ -1734,7 +1840,26 @@ static void reserve_pod(const kg_config *c, kg_cluster_view *vv, const kg_cluste
     s->spec.pod_count += 1;
     /* NodeNUMAResource.Reserve → resourceManager.Update: zone allocations of the stored hint (the
      * zone state is the one the pod was filtered on, so re-admitting reproduces that hint) */
-    if ((c->enabled_plugins & KG_PLUGIN_NUMA) && s->has_numa) numa_reserve(c, vv, pod, &s->numa);
+    if ((c->enabled_plugins & KG_PLUGIN_NUMA) && s->has_numa && !bound) numa_reserve(c, vv, pod, &s->numa);
+    if (bound) {   /* Update → NodeAllocation.addPodAllocation (node_allocation.go:72-100) */
+        kg_numa_spec *numa = &s->numa;
+        for (int i = 0; i < ng; i++) rl_add(&numa->zone_allocated[gz[i]], &zg[i]);
+        kg_cpu_info *ci = (kg_cpu_info *)vv->cpus + numa->first_cpu;   /* the cycle's mutable copy */
+        for (int k = 0; k < numa->n_cpus; k++)
+            if (taken[k]) {
+                ci[k].refcount++;
+                ci[k].exclusive = excl;
+            }
+        /* allocatedCPUs and its CPUsInNUMANodes, which the Filter's amplified-cpu terms read */
+        numa->cpuset_cpus = 0;
+        for (int z = 0; z < KG_MAX_ZONES; z++) numa->zone_cpuset_cpus[z] = 0;
+        for (int k = 0; k < numa->n_cpus; k++) {
+            if (ci[k].refcount <= 0) continue;
+            numa->cpuset_cpus++;
+            for (int z = 0; z < numa->n_zones; z++)
+                if (numa->zone_id[z] == ci[k].node) numa->zone_cpuset_cpus[z]++;
+        }
+    }
     kg_resource_list preq;
     numa_pod_requests(vv, pod, &preq);
     /* Reservation.Reserve → reservationCache.assumePod → ReservationInfo.AddAssignedPod
@@ -1758,17 +1883,23 @@ static void reserve_pod(const kg_config *c, kg_cluster_view *vv, const kg_cluste
         s->assigned[s->n_assigned].ts = now_ns;
         s->n_assigned++;
     }
+    return 1;
 }
 
 /* Sequential reference cycle over pod_index[0..P) in queue order.
  * out_node[p] = chosen node or -1; out_score[p] = weighted total or -1.  out_rsv / out_quota
  * (may be NULL) receive the reservation / quota states after the last Reserve. */
-int kgo_schedule2(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
-                  int32_t *out_node, int64_t *out_score, kg_reservation *out_rsv, kg_quota *out_quota) {
+/* (out_cpus, may be NULL: the nodes' logical CPUs — kg_cluster_view.cpus — after the last Reserve) */
+int kgo_schedule3(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
+                  int32_t *out_node, int64_t *out_score, kg_reservation *out_rsv, kg_quota *out_quota,
+                  kg_cpu_info *out_cpus) {
     int32_t N = v->n_nodes;
     if (quota_inputs_valid(c, v, pod_index, P) != 0) return -2;
     node_state *st = states_build(v, N);
     kg_cluster_view vv = *v;
+    kg_cpu_info *cpus = (kg_cpu_info *)malloc(sizeof(kg_cpu_info) * (size_t)(v->n_cpus > 0 ? v->n_cpus : 1));
+    if (v->n_cpus > 0) memcpy(cpus, v->cpus, sizeof(kg_cpu_info) * (size_t)v->n_cpus);
+    vv.cpus = cpus;
     rsv_index ri;
     if (rsv_index_build(v, N, &ri) != 0) { rsv_index_free(&ri); states_free(st, N); return -1; }
     kg_quota *quotas = (kg_quota *)calloc((size_t)(v->n_quotas > 0 ? v->n_quotas : 1), sizeof(kg_quota));
@@ -1781,15 +1912,22 @@ int kgo_schedule2(const kg_config *c, const kg_cluster_view *v, const int32_t *p
         out_node[p] = best_n;
         out_score[p] = best_n < 0 ? -1 : best;
         if (best_n < 0) continue;
-        reserve_pod(c, &vv, v, st, &ri, quotas, pod, best_n, nom, now_ns);
+        if (!reserve_pod(c, &vv, v, st, &ri, quotas, pod, best_n, nom, now_ns)) out_node[p] = -1, out_score[p] = -1;
     }
     if (out_rsv)
         for (int32_t i = 0; i < v->n_reservations; i++) out_rsv[i] = ri.states[i].r;
     if (out_quota && v->n_quotas > 0) memcpy(out_quota, quotas, sizeof(kg_quota) * (size_t)v->n_quotas);
+    if (out_cpus && v->n_cpus > 0) memcpy(out_cpus, cpus, sizeof(kg_cpu_info) * (size_t)v->n_cpus);
+    free(cpus);
     free(quotas);
     rsv_index_free(&ri);
     states_free(st, N);
     return 0;
+}
+
+int kgo_schedule2(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
+                  int32_t *out_node, int64_t *out_score, kg_reservation *out_rsv, kg_quota *out_quota) {
+    return kgo_schedule3(c, v, pod_index, P, now_ns, out_node, out_score, out_rsv, out_quota, NULL);
 }
 
 int kgo_schedule(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P, int64_t now_ns,
@@ -1951,8 +2089,11 @@ int kgo_schedule_parallel(const kg_config *c, const kg_cluster_view *v, const in
     int32_t N = v->n_nodes;
     node_state *st = states_build(v, N);
     kg_cluster_view vv = *v;
+    kg_cpu_info *cpus = (kg_cpu_info *)malloc(sizeof(kg_cpu_info) * (size_t)(v->n_cpus > 0 ? v->n_cpus : 1));
+    if (v->n_cpus > 0) memcpy(cpus, v->cpus, sizeof(kg_cpu_info) * (size_t)v->n_cpus);
+    vv.cpus = cpus;
     rsv_index ri;
-    if (rsv_index_build(v, N, &ri) != 0) { rsv_index_free(&ri); states_free(st, N); return -1; }
+    if (rsv_index_build(v, N, &ri) != 0) { rsv_index_free(&ri); states_free(st, N); free(cpus); return -1; }
     sched_pool pl;
     memset(&pl, 0, sizeof(pl));
     pl.c = c;
@@ -1991,7 +2132,7 @@ int kgo_schedule_parallel(const kg_config *c, const kg_cluster_view *v, const in
         int32_t node = (int32_t)(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFF));
         out_node[p] = node;
         out_score[p] = (b >> 32) - 1;
-        reserve_pod(c, &vv, v, st, &ri, NULL, pod, node, -1, now_ns);
+        if (!reserve_pod(c, &vv, v, st, &ri, NULL, pod, node, -1, now_ns)) out_node[p] = -1, out_score[p] = -1;
     }
     pl.stop = 1;
     pthread_barrier_wait(&pl.start);
@@ -2001,6 +2142,7 @@ int kgo_schedule_parallel(const kg_config *c, const kg_cluster_view *v, const in
     free(th);
     free(args);
     free(pl.best);
+    free(cpus);
     rsv_index_free(&ri);
     states_free(st, N);
     return 0;

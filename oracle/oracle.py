@@ -314,3 +314,21 @@ def take_cpus(topo, max_ref, available, need, bind, excl="None", strategy="MostA
         st = L.kgo_take_preferred_cpus(*args, pf.ctypes.data, ref.ctypes.data, ex.ctypes.data, need, BIND[bind],
                                        EXCLUSIVE[excl], NUMA_STRATEGY[strategy], out.ctypes.data)
     return None if st != 0 else [int(i) for i in np.flatnonzero(out)]
+
+
+def schedule_cpus(cfg, view, pod_index, now_ns):
+    """Sequential cycle with cpuset Reserve; returns (nodes, scores, the view's logical CPUs after the last
+    Reserve as a CPU_INFO array)."""
+    from koordinator_amd import _native as nat
+    idx = np.ascontiguousarray(pod_index, dtype=np.int32)
+    nodes = np.zeros(len(idx), np.int32)
+    scores = np.zeros(len(idx), np.int64)
+    cpus = np.zeros(view.c_view.n_cpus, dtype=nat.CPU_INFO)
+    L = lib()
+    L.kgo_schedule3.restype = ctypes.c_int
+    L.kgo_schedule3.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32, ctypes.c_int64] + [ctypes.c_void_p] * 5
+    st = L.kgo_schedule3(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, len(idx), now_ns, nodes.ctypes.data,
+                         scores.ctypes.data, None, None, cpus.ctypes.data if len(cpus) else None)
+    if st != 0:
+        raise RuntimeError("kgo_schedule3 failed")
+    return nodes, scores, cpus

@@ -91,3 +91,25 @@ def make_bind_cluster(n_nodes: int, n_pods: int, seed: int, numa_frac: float = 0
 
 def bind_config(**kw):
     return make_config(plugins=("NodeNUMAResource",), **kw)
+
+
+def make_reserve_fail_cluster():
+    """A Reserve that fails after the Filter passed (resource_manager.go:296-299 "not enough cpus available to
+    satisfy request"): node n0 has 8 logical CPUs, 2 of them reserved, and 8 cpu allocatable; a pod preferring
+    FullPCPUs for 8 CPUs passes Fit and the Filter (no required policy, no NUMA topology policy: no Allocate
+    there), its Reserve finds 6 available CPUs and fails, and the next pods still land on the node."""
+    cl = Cluster()
+    node = Node("n0", allocatable={"cpu": "8", "memory": "32Gi"})
+    node.numa_zones = []
+    node.cpu_detail = [(0, 0, c // 2) for c in range(8)]
+    node.cpu_allocated = {}
+    node.reserved_cpus = [0, 1]
+    cl.add_node(node, requested={"cpu": "0", "memory": "0"})
+    cl.add_node(Node("n1", allocatable={"cpu": "1", "memory": "32Gi"}))   # too small for any of the pods
+    pods = []
+    for i, cpu in enumerate(["8", "2", "4"]):
+        req = {"cpu": cpu, "memory": "1Gi"}
+        pods.append(Pod(name=f"p{i}", containers=[Container(requests=req, limits=req)], priority=9999,
+                        labels={"koordinator.sh/qosClass": "LSR"}, cpu_bind_preferred="FullPCPUs"))
+    view = cl.view(extra_pods=pods)
+    return cl, view, [view.pod_index(p) for p in pods]
