@@ -100,7 +100,8 @@ struct kg_consts {
     int32_t weight_rsv;          // Reservation profile weight
     int32_t la_extra;            // LoadAware weights beyond cpu / memory: every node takes kg_pair_exact
     int32_t la_wx[KG_NUM_RES - 2]; // their weights (resources 2..7; included in la_wsum)
-    int32_t _pad;
+    int32_t numa_bz;             // placement of a batch that binds cpusets on NUMA-policy nodes: the chunk and
+                                 // resolve kernels answer those pairs (kg_numa_pair_bz) instead of leaving them out
 };
 
 #define KG_NEUTRAL_REQ INT64_MIN  // request that passes every Fit compare
@@ -975,6 +976,21 @@ void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &
 #else
     kg_numa_pair_z(c, row, p, o, kg_zone_calc{row}, requested, reserve);
 #endif
+}
+
+// kg_numa_pair with the cpuset-on-NUMA-policy path answered (the placement kernels of a binding batch call
+// it behind kg_consts.numa_bz; out of line like kg_numa_pair)
+#if defined(__HIPCC__)
+static __host__ __device__ __noinline__
+#else
+inline
+#endif
+void kg_numa_pair_bz(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o) {
+    kg_numa_pair_z<kg_zone_calc, true>(c, row, p, o, kg_zone_calc{row});
+}
+KG_HD void kg_numa_pair_any(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o) {
+    if (c.numa_bz) kg_numa_pair_bz(c, row, p, o);
+    else kg_numa_pair(c, row, p, o);
 }
 
 // Reserve's cpuset decision for a pair (plugin.go:375-404): requestCPUBind (util.go:105-122) and

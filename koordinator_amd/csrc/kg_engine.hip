@@ -1466,7 +1466,7 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
     if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
     if (c.plugins & KG_PLUGIN_NUMA) {
         kg_numa_out o;
-        kg_numa_pair(c, pl.rows[node], p, o);
+        kg_numa_pair_any(c, pl.rows[node], p, o);
         if (!o.feasible) return 0ull;
         numa = o.score;
     }
@@ -1509,7 +1509,7 @@ __global__ __launch_bounds__(256) void k_eval_numa_chunk(kg_consts c, kg_planes 
         uint32_t fit, la;
         if (in_range && eval_pair(c, pl, lp, nr, node, a.now_ns, fit, la)) {
             kg_numa_out o;
-            kg_numa_pair(c, pl.rows[node], lp, o);
+            kg_numa_pair_any(c, pl.rows[node], lp, o);
             if (o.feasible)
                 key = ((total_of(c, fit, la, o.score) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local);
         }
@@ -1741,7 +1741,7 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
     if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
     if (c.plugins & KG_PLUGIN_NUMA) {
         kg_numa_out o;
-        kg_numa_pair(c, crow, p, o);   // the LDS copy of the canonical row
+        kg_numa_pair_any(c, crow, p, o);   // the LDS copy of the canonical row
         if (!o.feasible) return 0ull;
         numa = o.score;
     }
@@ -2501,7 +2501,9 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
                                e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr);
         }
         HIP_TRY(e, hipGetLastError());
-        if (!topk && e->n_numa_policy_nodes > 0 && (e->batch_bind || e->n_node_bind_nodes > 0)) {
+        // cpusets on NUMA-policy nodes: patched in after the hot kernel (matrix planes, or the one-key-per-tile
+        // partials of a large placement chunk)
+        if ((!topk || e->consts.numa_bz) && e->n_numa_policy_nodes > 0 && (e->batch_bind || e->n_node_bind_nodes > 0)) {
             const int64_t width = e->shard_end - e->shard_begin;
             dim3 grid((unsigned)((width + 255) / 256), (unsigned)(n < 65535 ? n : 65535));
             hipLaunchKernelGGL(k_numa_bind_fix, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
@@ -3218,6 +3220,12 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
     // policy) ends its chunk, and its Reserve runs on the host before the next chunk is evaluated
     const bool bind_mode = (e->consts.plugins & KG_PLUGIN_NUMA) && (e->batch_bind || e->n_node_bind_nodes > 0);
     const uint8_t may_mask = e->n_node_bind_nodes > 0 ? 3 : 1;
+    // the placement kernels answer cpusets on NUMA-policy nodes for this batch (kg_consts.numa_bz)
+    struct BzScope {
+        kg_consts &k;
+        BzScope(kg_consts &c, bool on) : k(c) { k.numa_bz = on ? 1 : 0; }
+        ~BzScope() { k.numa_bz = 0; }
+    } bz_scope(e->consts, bind_mode && e->n_numa_policy_nodes > 0);
     for (int32_t b = 0; b < P;) {
         int32_t n = P - b < chunk ? P - b : chunk;
         bool defer = false;
