@@ -162,6 +162,7 @@ enum kg_cpu_bind_policy {          /* ResourceSpec Required/PreferredCPUBindPoli
     KG_CPU_BIND_FULL_PCPUS = 2,
     KG_CPU_BIND_SPREAD_BY_PCPUS = 3,
     KG_CPU_BIND_CONSTRAINED_BURST = 4,
+    KG_CPU_BIND_OTHER = 5,         /* any other annotation value (PreFilter binds nothing for it) */
 };
 enum kg_cpu_exclusive_policy {     /* ResourceSpec.PreferredCPUExclusivePolicy / CPUInfo.ExclusivePolicy */
     KG_CPU_EXCL_UNSET = 0, KG_CPU_EXCL_NONE = 1, KG_CPU_EXCL_PCPU_LEVEL = 2, KG_CPU_EXCL_NUMA_NODE_LEVEL = 3,

@@ -34,7 +34,7 @@ MAX_ZONES = 8
 
 POD_HAS_REQUEST, POD_DAEMONSET, POD_PROD, POD_LA_PROD_SCORE, POD_VALID = 0x1, 0x2, 0x4, 0x8, 0x80000000
 POD_NUMA_SKIP, POD_NUMA_CPU_BIND, POD_NON_PREEMPTIBLE, POD_NUMA_BIND_INVALID = 0x10, 0x20, 0x40, 0x100
-CPU_BIND_UNSET, CPU_BIND_DEFAULT, CPU_BIND_FULL_PCPUS, CPU_BIND_SPREAD_BY_PCPUS, CPU_BIND_CONSTRAINED_BURST = range(5)
+CPU_BIND_UNSET, CPU_BIND_DEFAULT, CPU_BIND_FULL_PCPUS, CPU_BIND_SPREAD_BY_PCPUS, CPU_BIND_CONSTRAINED_BURST, CPU_BIND_OTHER = range(6)
 CPU_EXCL_UNSET, CPU_EXCL_NONE, CPU_EXCL_PCPU_LEVEL, CPU_EXCL_NUMA_NODE_LEVEL = range(4)
 NODE_CPU_BIND_NONE, NODE_CPU_BIND_FULL_PCPUS_ONLY, NODE_CPU_BIND_SPREAD_BY_PCPUS = range(3)
 NUMA_ALLOC_DEFAULT, NUMA_ALLOC_MOST, NUMA_ALLOC_LEAST, NUMA_ALLOC_DISTRIBUTE_EVENLY = range(4)

@@ -495,7 +495,7 @@ kg_status kg_build_pod_rows(const kg_config *cfg, const kg_cluster_view *view, c
             int32_t required = pv.p.cpu_bind_required;
             if (required == KG_CPU_BIND_DEFAULT) required = dflt;
             if (required != KG_CPU_BIND_UNSET) bind = required;
-            if (required < 0 || required > KG_CPU_BIND_CONSTRAINED_BURST || bind < 0 || bind > KG_CPU_BIND_CONSTRAINED_BURST ||
+            if (required < 0 || required > KG_CPU_BIND_OTHER || bind < 0 || bind > KG_CPU_BIND_OTHER ||
                 pv.p.cpu_exclusive < 0 || pv.p.cpu_exclusive > KG_CPU_EXCL_NUMA_NODE_LEVEL)
                 return KG_ERR_INVALID_ARG;
             const int64_t cpu = row.numa_request[KG_RES_CPU];

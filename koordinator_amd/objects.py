@@ -381,8 +381,8 @@ def pod_spec_record(p: Pod, containers: list, name_id: int) -> np.ndarray:
     rec["status_qos"] = KUBE_QOS[p.qos_status]
     rec["is_daemonset"] = int(p.daemonset)
     rec["is_terminated"] = int(p.terminated)
-    rec["cpu_bind_required"] = CPU_BIND[p.cpu_bind_required]
-    rec["cpu_bind_preferred"] = CPU_BIND[p.cpu_bind_preferred]
+    rec["cpu_bind_required"] = CPU_BIND.get(p.cpu_bind_required, nat.CPU_BIND_OTHER)
+    rec["cpu_bind_preferred"] = CPU_BIND.get(p.cpu_bind_preferred, nat.CPU_BIND_OTHER)
     rec["cpu_exclusive"] = CPU_EXCLUSIVE[p.cpu_exclusive]
     rec["name_id"] = name_id
     rec["rsv_owner_class"] = getattr(p, "rsv_owner_class", -1)

@@ -975,6 +975,29 @@ static int numa_allocate_cpuset2(const kg_cluster_view *v, const kg_numa_spec *n
     return 1;
 }
 
+/* trimNUMANodeResources (resource_manager.go:141-169) for a required bind policy: a zone's available cpu is
+ * capped by its available CPUs, after the policy's filter when those are at least the quantity */
+static void numa_trim_zones(const kgo_cpu_topo *t, const uint8_t *avail, const int32_t *node, int required,
+                            numa_zones *zt) {
+    uint8_t zav[1024];
+    for (int i = 0; i < zt->n; i++) {
+        const int64_t q = get(&zt->avail[i], KG_RES_CPU);
+        if (q == 0) continue;
+        int raw = 0;
+        for (int k = 0; k < t->n_cpus; k++) {
+            zav[k] = (uint8_t)(avail[k] && node[k] == zt->id[i]);
+            raw += zav[k];
+        }
+        int cnt = raw;
+        if ((int64_t)raw * 1000 >= q) {
+            kgo_filter_required_bind(t, acc_bind(required), zav);
+            cnt = 0;
+            for (int k = 0; k < t->n_cpus; k++) cnt += zav[k];
+        }
+        if ((int64_t)cnt * 1000 < q) zt->avail[i].v[KG_RES_CPU] = (int64_t)cnt * 1000;
+    }
+}
+
 /* FilterByNUMANode + Score for a cpuset request on a node with a NUMA topology policy: the options of
  * getResourceOptions (plugin.go:481-527: cpu request amplified), GetTopologyHints with
  * trimNUMANodeResources for a required policy (resource_manager.go:122-169), Admit, then Allocate with
@@ -1004,24 +1027,7 @@ static int numa_pair_cpuset(const kg_config *c, const kg_cluster_view *v, const 
     numa_zones z, zt;
     numa_zones_of(numa, &z);
     zt = z;
-    if (required != KG_CPU_BIND_UNSET) {   /* trimNUMANodeResources */
-        for (int i = 0; i < zt.n; i++) {
-            const int64_t q = get(&zt.avail[i], KG_RES_CPU);
-            if (q == 0) continue;
-            int raw = 0;
-            for (int k = 0; k < ncpu; k++) {
-                zav[k] = (uint8_t)(avail[k] && node[k] == zt.id[i]);
-                raw += zav[k];
-            }
-            int cnt = raw;
-            if ((int64_t)raw * 1000 >= q) {
-                kgo_filter_required_bind(&t, acc_bind(required), zav);
-                cnt = 0;
-                for (int k = 0; k < ncpu; k++) cnt += zav[k];
-            }
-            if ((int64_t)cnt * 1000 < q) zt.avail[i].v[KG_RES_CPU] = (int64_t)cnt * 1000;
-        }
-    }
+    if (required != KG_CPU_BIND_UNSET) numa_trim_zones(&t, avail, node, required, &zt);
     if (!numa_admit(c, &zt, policy, &pr, hint)) return 0;
     kg_resource_list zg[KG_MAX_ZONES];
     int ng, gz[KG_MAX_ZONES];
@@ -1307,6 +1313,61 @@ static int numa_reserve_cpuset(const kg_config *c, const kg_cluster_view *v, con
                                 strategy, out_cpus, zg, gz, ng);
     }
     return numa_allocate_cpuset2(v, numa, need, required, take, excl, strategy, out_cpus);
+}
+
+/* GetTopologyHints of resourceManager (resource_manager.go:122-169 + generateResourceHints :418-532) for one
+ * pair, as TestResourceManagerGetTopologyHint checks it: the pod's requests (cpu amplified when `bind` and the
+ * node amplifies), the zones' availability, trimmed for a `required` bind policy (UNSET ⇔ none).  Per
+ * resource r (kg_resource id): present[r] (the map has the key; possibly an empty list), count[r], masks[r][k]
+ * and preferred[r][k] for k < count[r] (MAX_HINTS per resource).  0 on success. */
+int kgo_numa_hint_lists(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n,
+                        int bind, int required, uint8_t *present, int32_t *count, uint64_t *masks, uint8_t *preferred) {
+    if (n->numa < 0) return -1;
+    const kg_numa_spec *numa = &v->numa[n->numa];
+    kg_resource_list preq;
+    numa_pod_requests(v, pod, &preq);
+    const int64_t pcpu = get(&preq, KG_RES_CPU);
+    if (bind && pcpu != 0 && numa->cpu_amplification_ratio > 1.0) preq.v[KG_RES_CPU] = amplify(pcpu, numa->cpu_amplification_ratio);
+    numa_zones z;
+    numa_zones_of(numa, &z);
+    if (required != KG_CPU_BIND_UNSET) {
+        const int ncpu = numa->n_cpus;
+        if (ncpu <= 0 || ncpu > 1024 || numa->first_cpu < 0 || numa->first_cpu + ncpu > v->n_cpus) return -1;
+        const kg_cpu_info *ci = v->cpus + numa->first_cpu;
+        int32_t sock[1024], node[1024], core[1024], ref[1024];
+        uint8_t reserved[1024], avail[1024];
+        for (int i = 0; i < ncpu; i++) {
+            sock[i] = ci[i].socket, node[i] = ci[i].node, core[i] = ci[i].core;
+            ref[i] = ci[i].refcount;
+            reserved[i] = (uint8_t)(ci[i].reserved != 0);
+        }
+        const kgo_cpu_topo t = {ncpu, sock, node, core};
+        kgo_available_cpus(&t, numa->max_ref_count > 0 ? numa->max_ref_count : 1, ref, reserved, NULL, avail, NULL);
+        numa_trim_zones(&t, avail, node, required, &z);
+    }
+    static __thread hint_list lists[KG_NUM_RES];
+    numa_generate_hints(c, &z, &preq, lists);
+    for (int r = 0; r < KG_NUM_RES; r++) {
+        present[r] = (uint8_t)lists[r].present;
+        count[r] = lists[r].n;
+        for (int k = 0; k < lists[r].n; k++) {
+            masks[r * MAX_HINTS + k] = lists[r].h[k].mask;
+            preferred[r * MAX_HINTS + k] = (uint8_t)lists[r].h[k].pref;
+        }
+    }
+    return 0;
+}
+
+/* The affinity the Filter stores (topologymanager.Store, TestFilterWithNUMANodeScoring): 1 ⇔ feasible with a
+ * hint, *mask its NUMA node bits (0 with a nil hint). */
+int kgo_numa_hint(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n,
+                  uint64_t *mask) {
+    numa_hint h;
+    int64_t score;
+    const kg_numa_spec *numa = n->numa >= 0 ? &v->numa[n->numa] : NULL;
+    const int ok = numa_pair(c, v, pod, n, numa, &score, &h);
+    *mask = h.nil ? 0 : h.mask;
+    return ok;
 }
 
 int kgo_numa_eval(const kg_config *c, const kg_cluster_view *v, const kg_pod_spec *pod, const kg_node_spec *n,

@@ -134,6 +134,34 @@ def numa_eval(cfg, view, pod_i, node_j):
     return bool(ok), int(sc.value)
 
 
+def numa_hint(cfg, view, pod_i, node_j):
+    """The NUMA affinity the Filter stores for one pair → (feasible, mask bits as an int; 0 ⇔ nil)."""
+    m = ctypes.c_uint64(0)
+    L = lib()
+    L.kgo_numa_hint.restype = ctypes.c_int
+    L.kgo_numa_hint.argtypes = [ctypes.c_void_p] * 5
+    ok = L.kgo_numa_hint(_cfg(cfg), ctypes.byref(view.c_view), _pod(view, pod_i), _node(view, node_j), ctypes.byref(m))
+    return bool(ok), int(m.value)
+
+
+def numa_hint_lists(cfg, view, pod_i, node_j, bind=False, required=0):
+    """GetTopologyHints of one pair → {resource id: [(mask bits, preferred), ...]} for the resources with a
+    list (possibly empty)."""
+    MAX_HINTS = 256
+    present = np.zeros(8, np.uint8)
+    count = np.zeros(8, np.int32)
+    masks = np.zeros((8, MAX_HINTS), np.uint64)
+    pref = np.zeros((8, MAX_HINTS), np.uint8)
+    L = lib()
+    L.kgo_numa_hint_lists.restype = ctypes.c_int
+    L.kgo_numa_hint_lists.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4
+    if L.kgo_numa_hint_lists(_cfg(cfg), ctypes.byref(view.c_view), _pod(view, pod_i), _node(view, node_j), int(bind),
+                             int(required), present.ctypes.data, count.ctypes.data, masks.ctypes.data,
+                             pref.ctypes.data) != 0:
+        raise RuntimeError("kgo_numa_hint_lists failed")
+    return {r: [(int(masks[r, k]), bool(pref[r, k])) for k in range(count[r])] for r in range(8) if present[r]}
+
+
 def numa_merge(policy, numa_nodes, lists):
     """Topology-manager Merge over provider lists: each list is None (nil list), [] (empty) or
     [(mask_bits | None, preferred[, score]), ...]. Returns (admit, mask_bits | None, preferred)."""

@@ -164,3 +164,26 @@ def test_pods_set_rejects_numa_shapes_off_the_engine_path():
         with pytest.raises(engine.EngineError, match="hint lists"):
             eng.set_pods(bad)
         eng.set_pods(rows)   # the batch itself is fine
+
+
+@pytest.mark.parametrize("case", load("numa_plugin_score_kat.json")["cases"], ids=lambda c: c["name"])
+def test_kat_plugin_score_gpu(case):
+    """TestPlugin_Score (scoring_test.go:332-551): cpuset-pod node scores through kg_eval."""
+    from test_numa_plugin_kat2 import score_cluster
+    cfg, view, pi = score_cluster(case)
+    with _engine_for(cfg, view, [pi]) as eng:
+        res = eng.eval(0)
+    assert bool(engine.unpack_mask(res["mask"], 1)[0, 0])
+    assert int(res["numa_scores"][0, 0]) == case["want"]
+
+
+@pytest.mark.parametrize("case", load("numa_node_scoring_kat.json")["cases"], ids=lambda c: c["name"])
+def test_kat_filter_with_numa_node_scoring_gpu(case):
+    """TestFilterWithNUMANodeScoring (plugin_test.go:1649-1877): kg_commit allocates on the stored hint's zone."""
+    from test_numa_plugin_kat2 import node_scoring_cluster
+    cfg, view, pi = node_scoring_cluster(case)
+    with _engine_for(cfg, view, [pi]) as eng:
+        before = eng.download()["zone_allocated"][0].copy()
+        assert eng.commit(0, 0)
+        after = eng.download()["zone_allocated"][0]
+    assert np.flatnonzero((after != before).any(axis=1)).tolist() == [case["want_zone"]]
