@@ -105,9 +105,9 @@ static int excl_pcpu(const acc_t *a, int c) { return a->excl_policy == EXCL_PCPU
 static int excl_numa(const acc_t *a, int c) { return a->excl_policy == EXCL_NUMA && a->excl_node[a->T->node_ix[c]]; }
 
 /* ---- sort helpers (comparators read a file-scope context: the oracle is single-threaded per call) ---- */
-static const acc_t *g_acc;
-static const int *g_key1, *g_key2;   /* per compact index */
-static int g_most;
+static __thread const acc_t *g_acc;
+static __thread const int *g_key1, *g_key2;   /* per compact index */
+static __thread int g_most;
 
 static int core_refcount(const acc_t *a, int core_ix) {   /* getCoreRefCount over allocatableCPUs */
     int r = 0;
@@ -178,8 +178,8 @@ static int skip_both(const acc_t *a, int c) { return excl_pcpu(a, c) || excl_num
 static void free_cores_in(const acc_t *a, int level, int full_only, skip_fn skip, groups_t *out) {
     const topo_t *T = a->T;
     const int n = T->t->n_cpus;
-    static int core_cnt[KGO_MAX_CPUS], sock_free[KGO_MAX_CPUS], grp_len[KGO_MAX_CPUS], sock_of_grp[KGO_MAX_CPUS];
-    static int cores_of[KGO_MAX_CPUS], ncores_of[KGO_MAX_CPUS], order[KGO_MAX_CPUS];
+    static __thread int core_cnt[KGO_MAX_CPUS], sock_free[KGO_MAX_CPUS], grp_len[KGO_MAX_CPUS], sock_of_grp[KGO_MAX_CPUS];
+    static __thread int cores_of[KGO_MAX_CPUS], ncores_of[KGO_MAX_CPUS], order[KGO_MAX_CPUS];
     memset(core_cnt, 0, sizeof(int) * T->ncores);
     memset(sock_free, 0, sizeof(int) * T->nsockets);
     for (int c = 0; c < n; c++) {
@@ -199,7 +199,7 @@ static void free_cores_in(const acc_t *a, int level, int full_only, skip_fn skip
             if (level == 0) sock_of_grp[T->node_ix[c]] = T->sock_ix[c];
         }
     /* per group: its cores (compact), in any order; sorted below */
-    static int members[KGO_MAX_CPUS * 2];
+    static __thread int members[KGO_MAX_CPUS * 2];
     int pos = 0;
     for (int g = 0; g < ng; g++) {
         cores_of[g] = pos;
@@ -219,7 +219,7 @@ static void free_cores_in(const acc_t *a, int level, int full_only, skip_fn skip
         if (ncores_of[g] > 0) order[m++] = g;
     g_most = a->strategy == STRATEGY_MOST;
     if (level == 0) {
-        static int sock_free_of_node[KGO_MAX_CPUS];
+        static __thread int sock_free_of_node[KGO_MAX_CPUS];
         for (int g = 0; g < ng; g++) sock_free_of_node[g] = sock_free[sock_of_grp[g]];
         g_key1 = grp_len;
         g_key2 = sock_free_of_node;
@@ -246,7 +246,7 @@ static void free_cores_in(const acc_t *a, int level, int full_only, skip_fn skip
 
 /* extractCPU: the first cpu of each core, in list order */
 static int extract_cpu(const acc_t *a, int *cpus, int n) {
-    static uint8_t seen[KGO_MAX_CPUS];
+    static __thread uint8_t seen[KGO_MAX_CPUS];
     memset(seen, 0, (size_t)a->T->ncores);
     int w = 0;
     for (int i = 0; i < n; i++) {
@@ -263,8 +263,8 @@ static void free_cpus_in(const acc_t *a, int level, int filter_excl, groups_t *o
     const topo_t *T = a->T;
     const int n = T->t->n_cpus;
     const skip_fn skip = !filter_excl ? skip_none : level == 0 ? skip_both : skip_pcpu;
-    static int node_free[KGO_MAX_CPUS], sock_free[KGO_MAX_CPUS], sock_of[KGO_MAX_CPUS], len[KGO_MAX_CPUS];
-    static int order[KGO_MAX_CPUS], buf[KGO_MAX_CPUS], bstart[KGO_MAX_CPUS + 1];
+    static __thread int node_free[KGO_MAX_CPUS], sock_free[KGO_MAX_CPUS], sock_of[KGO_MAX_CPUS], len[KGO_MAX_CPUS];
+    static __thread int order[KGO_MAX_CPUS], buf[KGO_MAX_CPUS], bstart[KGO_MAX_CPUS + 1];
     const int ng = level == 0 ? T->nnodes : T->nsockets;
     memset(node_free, 0, sizeof(int) * T->nnodes);
     memset(sock_free, 0, sizeof(int) * T->nsockets);
@@ -290,7 +290,7 @@ static void free_cpus_in(const acc_t *a, int level, int filter_excl, groups_t *o
     g_acc = a;
     g_most = a->strategy == STRATEGY_MOST;
     if (level == 0) {
-        static int sf[KGO_MAX_CPUS];
+        static __thread int sf[KGO_MAX_CPUS];
         for (int g = 0; g < ng; g++) sf[g] = sock_free[sock_of[g]];
         g_key1 = node_free;     /* counted before extractCPU (cpu_accumulator.go:544, :575) */
         g_key2 = sf;
@@ -312,7 +312,7 @@ static void free_cpus_in(const acc_t *a, int level, int filter_excl, groups_t *o
 
 /* freeCPUs: cores sorted by result colocation of their socket, socket / node free scores, core free
  * count, socket, refcount, core id; each core's cpus ascending (then by refcount) */
-static int *g_colo, *g_sfree, *g_nfree, *g_ccnt, *g_csock, *g_cnode;
+static __thread int *g_colo, *g_sfree, *g_nfree, *g_ccnt, *g_csock, *g_cnode;
 static int cmp_free_core(const void *x, const void *y) {
     const int i = *(const int *)x, j = *(const int *)y;
     const int si = g_csock[i], sj = g_csock[j];
@@ -335,8 +335,8 @@ static int free_cpus(const acc_t *a, int filter_excl, int *out) {
     const topo_t *T = a->T;
     const int n = T->t->n_cpus;
     const skip_fn skip = filter_excl ? skip_both : skip_none;
-    static int colo[KGO_MAX_CPUS], sfree[KGO_MAX_CPUS], nfree[KGO_MAX_CPUS], ccnt[KGO_MAX_CPUS];
-    static int csock[KGO_MAX_CPUS], cnode[KGO_MAX_CPUS], cores[KGO_MAX_CPUS];
+    static __thread int colo[KGO_MAX_CPUS], sfree[KGO_MAX_CPUS], nfree[KGO_MAX_CPUS], ccnt[KGO_MAX_CPUS];
+    static __thread int csock[KGO_MAX_CPUS], cnode[KGO_MAX_CPUS], cores[KGO_MAX_CPUS];
     memset(sfree, 0, sizeof(int) * T->nsockets);
     memset(nfree, 0, sizeof(int) * T->nnodes);
     memset(ccnt, 0, sizeof(int) * T->ncores);
@@ -371,8 +371,8 @@ static int free_cpus(const acc_t *a, int filter_excl, int *out) {
 /* spreadCPUs: round-robin over cores, one cpu per core per pass, in list order */
 static int spread_cpus(const acc_t *a, int *cpus, int n) {
     if (n <= a->T->cpus_per_core) return n;
-    static int prep[KGO_MAX_CPUS], res[KGO_MAX_CPUS], rest[KGO_MAX_CPUS];
-    static uint8_t seen[KGO_MAX_CPUS];
+    static __thread int prep[KGO_MAX_CPUS], res[KGO_MAX_CPUS], rest[KGO_MAX_CPUS];
+    static __thread uint8_t seen[KGO_MAX_CPUS];
     memcpy(prep, cpus, sizeof(int) * n);
     int np = n, w = 0;
     while (np > 0) {
@@ -417,10 +417,10 @@ static void sort_groups_by_len(const groups_t *g, int *idx, int m, int desc) {
  * Returns 0 on success, −1 on failure. */
 int kgo_take_cpus(const kgo_cpu_topo *topo, int max_ref, const uint8_t *available, const int32_t *alloc_ref,
                   const int8_t *alloc_excl, int need, int bind, int excl_policy, int strategy, uint8_t *result) {
-    static topo_t T;
-    static acc_t A;
-    static groups_t G;
-    static int list[KGO_MAX_CPUS];
+    static __thread topo_t T;
+    static __thread acc_t A;
+    static __thread groups_t G;
+    static __thread int list[KGO_MAX_CPUS];
     if (topo->n_cpus > KGO_MAX_CPUS) return -2;
     topo_init(&T, topo);
     acc_t *a = &A;
@@ -584,7 +584,7 @@ void kgo_available_cpus(const kgo_cpu_topo *topo, int max_ref, const int32_t *al
 /* filterCPUsByRequiredCPUBindPolicy (resource_manager.go:534-566): FullPCPUs keeps the cpus of cores
  * whose every cpu is available; SpreadByPCPUs keeps the first (lowest) available cpu of each core */
 void kgo_filter_required_bind(const kgo_cpu_topo *topo, int bind, uint8_t *available) {
-    static topo_t T;
+    static __thread topo_t T;
     topo_init(&T, topo);
     const int n = topo->n_cpus;
     int cnt[KGO_MAX_CPUS] = {0}, first[KGO_MAX_CPUS];
@@ -603,7 +603,7 @@ void kgo_filter_required_bind(const kgo_cpu_topo *topo, int bind, uint8_t *avail
 
 /* satisfiedRequiredCPUBindPolicy (resource_manager.go:568-589) */
 int kgo_satisfied_required_bind(const kgo_cpu_topo *topo, int bind, const uint8_t *cpus) {
-    static topo_t T;
+    static __thread topo_t T;
     topo_init(&T, topo);
     uint8_t seen[KGO_MAX_CPUS] = {0};
     int ncpu = 0, ncore = 0;

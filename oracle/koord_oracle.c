@@ -761,17 +761,20 @@ static void merge_iterate(merge_state *m, numa_hint **lists, const int *lens, in
     }
 }
 
+/* filterSingleNumaHints (policy_single_numa_node.go:48-78): a nil hint survives when preferred, a non-nil one
+ * when preferred and on exactly one NUMA node */
+static int single_numa_keeps(const numa_hint *h) {
+    return (h->nil && h->pref) || (!h->nil && popcount64(h->mask) == 1 && h->pref);
+}
+
 /* policy.Merge over already-filtered provider lists (filterProvidersHints output) */
 static int numa_merge_lists(int policy, uint64_t dflt, numa_hint **plist, int *plen, int nl, numa_hint *best) {
     static __thread numa_hint filtered[KG_NUM_RES + 8][MAX_HINTS];
     if (policy == KG_NUMA_SINGLE_NUMA_NODE) {
-        /* filterSingleNumaHints (policy_single_numa_node.go:48-78) */
         for (int i = 0; i < nl; i++) {
             int n = 0;
-            for (int j = 0; j < plen[i] && n < MAX_HINTS; j++) {
-                const numa_hint *h = &plist[i][j];
-                if ((h->nil && h->pref) || (!h->nil && popcount64(h->mask) == 1 && h->pref)) filtered[i][n++] = *h;
-            }
+            for (int j = 0; j < plen[i] && n < MAX_HINTS; j++)
+                if (single_numa_keeps(&plist[i][j])) filtered[i][n++] = plist[i][j];
             plist[i] = filtered[i];
             plen[i] = n;
         }
@@ -829,6 +832,27 @@ int kgo_numa_merge(int policy, const int32_t *numa_nodes, int nn, int n_lists, c
     *out_nil = best.nil;
     *out_pref = best.pref;
     return admit;
+}
+
+/* filterSingleNumaHints alone (TestPolicySingleNumaNodeFilterHints): n_lists lists of list_len[i] hints
+ * (masks / nils / prefs flattened); out_len[i] and the kept hints flattened in the same layout. */
+int kgo_filter_single_numa_hints(int n_lists, const int32_t *list_len, const uint64_t *masks, const int32_t *nils,
+                                 const int32_t *prefs, int32_t *out_len, uint64_t *out_masks, int32_t *out_nils,
+                                 int32_t *out_prefs) {
+    int k = 0, o = 0;
+    for (int i = 0; i < n_lists; i++) {
+        out_len[i] = 0;
+        for (int j = 0; j < list_len[i]; j++, k++) {
+            const numa_hint h = {masks[k], nils[k], prefs[k], 0};
+            if (!single_numa_keeps(&h)) continue;
+            out_masks[o] = h.mask;
+            out_nils[o] = h.nil;
+            out_prefs[o] = h.pref;
+            o++;
+            out_len[i]++;
+        }
+    }
+    return 0;
 }
 
 /* Admit (manager.go:58-80): returns admit, writes the best hint */

@@ -162,6 +162,27 @@ def numa_hint_lists(cfg, view, pod_i, node_j, bind=False, required=0):
     return {r: [(int(masks[r, k]), bool(pref[r, k])) for k in range(count[r])] for r in range(8) if present[r]}
 
 
+def filter_single_numa_hints(lists):
+    """filterSingleNumaHints over lists of (mask bits | None, preferred) → the kept hints per list."""
+    lens = np.array([len(l) for l in lists], np.int32)
+    flat = [h for l in lists for h in l]
+    masks = np.array([0 if m is None else m for m, _ in flat] or [0], np.uint64)
+    nils = np.array([int(m is None) for m, _ in flat] or [0], np.int32)
+    prefs = np.array([int(p) for _, p in flat] or [0], np.int32)
+    out_len = np.zeros(max(1, len(lists)), np.int32)
+    om, on, op = np.zeros(len(masks), np.uint64), np.zeros(len(masks), np.int32), np.zeros(len(masks), np.int32)
+    L = lib()
+    L.kgo_filter_single_numa_hints.restype = ctypes.c_int
+    L.kgo_filter_single_numa_hints.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 8
+    L.kgo_filter_single_numa_hints(len(lists), lens.ctypes.data, masks.ctypes.data, nils.ctypes.data, prefs.ctypes.data,
+                                   out_len.ctypes.data, om.ctypes.data, on.ctypes.data, op.ctypes.data)
+    out, k = [], 0
+    for i in range(len(lists)):
+        out.append([(None if on[k + j] else int(om[k + j]), bool(op[k + j])) for j in range(out_len[i])])
+        k += out_len[i]
+    return out
+
+
 def numa_merge(policy, numa_nodes, lists):
     """Topology-manager Merge over provider lists: each list is None (nil list), [] (empty) or
     [(mask_bits | None, preferred[, score]), ...]. Returns (admit, mask_bits | None, preferred)."""

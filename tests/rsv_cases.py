@@ -16,7 +16,7 @@ INT64_MAX = (1 << 63) - 1
 def _rl(d):
     out = np.zeros((), dtype=nat.RESOURCE_LIST)
     for k, v in (d or {}).items():
-        r = {"cpu": nat.RES_CPU, "memory": nat.RES_MEMORY}[k]
+        r = {"cpu": nat.RES_CPU, "memory": nat.RES_MEMORY, "ephemeral-storage": nat.RES_EPHEMERAL_STORAGE}[k]
         out["v"][r] = v
         out["present"] |= np.uint32(1 << r)
     return out
@@ -135,10 +135,10 @@ def _kat_view(node_docs, rsv_docs, pod, affinity=False):
            "Restricted": nat.RSV_POLICY_RESTRICTED}
     for i, d in enumerate(rsv_docs):
         rsv[i]["node"] = d.get("node", 0)
-        rsv[i]["flags"] = nat.RSV_AVAILABLE
+        rsv[i]["flags"] = nat.RSV_AVAILABLE | (nat.RSV_ALLOCATE_ONCE if d.get("allocate_once") else 0)
         rsv[i]["policy"] = pol[d.get("policy", "Default")]
         rsv[i]["owner_classes"] = 1 if d.get("matches_pod", True) else 0
-        rsv[i]["affinity_classes"] = 1 if d.get("matches_pod", True) else 0
+        rsv[i]["affinity_classes"] = 1 if d.get("affinity", d.get("matches_pod", True)) else 0
         rsv[i]["order"] = d.get("order", 0)
         rsv[i]["allocatable"] = _rl(d["allocatable"])
         rsv[i]["allocated"] = _rl(d.get("allocated"))
