@@ -630,12 +630,15 @@ kg_status kg_cpuset_take(const kg_cpu_info *cpus, int32_t n_cpus, int32_t max_re
                          int32_t need, int32_t bind_policy, int32_t exclusive_policy, int32_t numa_strategy,
                          uint8_t *result);
 /* The logical CPUs of snapshot nodes (NodeNUMAResource's NodeAllocation.allocatedCPUs + CPUTopology +
- * ReservedCPUs, with MaxRefCount and the node's NUMA allocate strategy): snapshot node k gets the CPU detail
- * of view node node_index[k] (node_index NULL ⇔ k itself; n nodes).  Replaces every table; kg_snapshot_reset
- * drops them, kg_snapshot_remove drops the node's.  kg_place / kg_commit take cpusets from these tables at
- * Reserve (the host runs the CPU accumulator for the chosen node between device chunks) and write the
- * node's cpuset counts back to its row.  kg_cpus_download reads one node's table (n = its CPU count). */
-kg_status kg_cpus_set(kg_engine *eng, const kg_cluster_view *view, const int32_t *node_index, int32_t n);
+ * ReservedCPUs, with MaxRefCount and the node's NUMA allocate strategy): for k < n, snapshot node
+ * snap_index[k] takes the CPU detail of view node view_index[k] (either array NULL ⇔ k itself); a listed node
+ * without CPU detail loses its table, unlisted nodes keep theirs (the feeders push the nodes an event
+ * changed, next to their rows).  kg_snapshot_reset drops every table, kg_snapshot_remove the node's.
+ * kg_place / kg_commit take cpusets from these tables at Reserve (the host runs the CPU accumulator for the
+ * chosen node between device chunks) and write the node's cpuset counts back to its row.
+ * kg_cpus_download reads one node's table (n = its CPU count). */
+kg_status kg_cpus_set(kg_engine *eng, const kg_cluster_view *view, const int32_t *view_index, const int32_t *snap_index,
+                      int32_t n);
 kg_status kg_cpus_download(kg_engine *eng, int32_t node, kg_cpu_info *out, int32_t n);
 /* Restrict kg_eval/kg_place evaluation to nodes [begin, end) (node sharding across GPUs);
  * node indices stay global.  begin must be a multiple of 1024 unless the shard is empty. */

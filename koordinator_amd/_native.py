@@ -251,7 +251,7 @@ def lib() -> ctypes.CDLL:
         "kg_snapshot_generation": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
         "kg_cpuset_take": (i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp]),
         "kg_row_reserve": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
-        "kg_cpus_set": (i32, [vp, vp, vp, i32]), "kg_cpus_download": (i32, [vp, i32, vp, i32]),
+        "kg_cpus_set": (i32, [vp, vp, vp, vp, i32]), "kg_cpus_download": (i32, [vp, i32, vp, i32]),
     }
     for name, (res, args) in sig.items():
         if host_only and not hasattr(L, name):

@@ -3266,30 +3266,38 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
     return KG_OK;
 }
 
-kg_status kg_cpus_set(kg_engine *e, const kg_cluster_view *view, const int32_t *node_index, int32_t n) {
+kg_status kg_cpus_set(kg_engine *e, const kg_cluster_view *view, const int32_t *view_index, const int32_t *snap_index,
+                      int32_t n) {
     kg_status st = check_engine(e);
     if (st) return st;
-    if (!view || n < 0 || (!node_index && n > view->n_nodes)) return set_err(e, KG_ERR_INVALID_ARG, "bad CPU table arguments");
-    if (n > e->n_nodes) return set_err(e, KG_ERR_RANGE, "%d CPU tables for %lld nodes", n, (long long)e->n_nodes);
-    std::unordered_map<int32_t, kg_engine::CpuTable> tab;
+    if (!view || n < 0) return set_err(e, KG_ERR_INVALID_ARG, "bad CPU table arguments");
+    // validate everything first: a failed call changes no table
+    std::vector<std::pair<int32_t, kg_engine::CpuTable>> tab;
+    std::vector<int32_t> dropped;
     for (int32_t k = 0; k < n; k++) {
-        const int32_t vi = node_index ? node_index[k] : k;
+        const int32_t vi = view_index ? view_index[k] : k, si = snap_index ? snap_index[k] : k;
         if (vi < 0 || vi >= view->n_nodes) return set_err(e, KG_ERR_RANGE, "view node %d out of range", vi);
+        if (si < 0 || si >= e->n_nodes) return set_err(e, KG_ERR_RANGE, "snapshot node %d out of range", si);
         const kg_node_spec &ns = view->nodes[vi];
-        if (ns.numa < 0) continue;
-        if (ns.numa >= view->n_numa || !view->numa) return set_err(e, KG_ERR_RANGE, "node %d: bad NUMA spec index", vi);
-        const kg_numa_spec &nm = view->numa[ns.numa];
-        if (nm.n_cpus <= 0) continue;
+        const kg_numa_spec *nmp = ns.numa >= 0 && ns.numa < view->n_numa && view->numa ? &view->numa[ns.numa] : nullptr;
+        if (ns.numa >= 0 && !nmp) return set_err(e, KG_ERR_RANGE, "node %d: bad NUMA spec index", vi);
+        if (!nmp || nmp->n_cpus <= 0) {
+            dropped.push_back(si);
+            continue;
+        }
+        const kg_numa_spec &nm = *nmp;
         if (nm.n_cpus > KG_MAX_NODE_CPUS || nm.first_cpu < 0 || nm.first_cpu + (int64_t)nm.n_cpus > view->n_cpus || !view->cpus)
             return set_err(e, KG_ERR_RANGE, "node %d: bad CPU range", vi);
         if (nm.numa_allocate_strategy < KG_NUMA_ALLOC_DEFAULT || nm.numa_allocate_strategy > KG_NUMA_ALLOC_DISTRIBUTE_EVENLY)
             return set_err(e, KG_ERR_INVALID_ARG, "node %d: bad NUMA allocate strategy", vi);
-        kg_engine::CpuTable &t = tab[k];
+        kg_engine::CpuTable t;
         t.max_ref = nm.max_ref_count > 0 ? nm.max_ref_count : 1;
         t.strategy = kg_cpuset_strategy(e->cfg, nm.numa_allocate_strategy);
         t.cpus.assign(view->cpus + nm.first_cpu, view->cpus + nm.first_cpu + nm.n_cpus);
+        tab.emplace_back(si, std::move(t));
     }
-    e->cpu_tab.swap(tab);
+    for (int32_t si : dropped) e->cpu_tab.erase(si);
+    for (auto &kv : tab) e->cpu_tab[kv.first] = std::move(kv.second);
     return KG_OK;
 }
 

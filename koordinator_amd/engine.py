@@ -131,13 +131,15 @@ class Engine:
         rows = np.ascontiguousarray(rows, dtype=nat.NODE_ROW)
         _check(nat.lib().kg_snapshot_upsert(self._h, nat.ptr(idx), nat.ptr(rows), len(idx)), self, "kg_snapshot_upsert")
 
-    def set_cpus(self, view, node_index: Optional[Sequence[int]] = None) -> None:
-        """kg_cpus_set: snapshot node k takes the CPU detail of view node node_index[k] (default k)."""
-        if node_index is None:
-            _check(nat.lib().kg_cpus_set(self._h, ctypes.byref(view.c_view), None, len(view.nodes)), self, "kg_cpus_set")
-            return
-        idx = np.ascontiguousarray(node_index, dtype=np.int32)
-        _check(nat.lib().kg_cpus_set(self._h, ctypes.byref(view.c_view), nat.ptr(idx), len(idx)), self, "kg_cpus_set")
+    def set_cpus(self, view, view_index: Optional[Sequence[int]] = None,
+                 snap_index: Optional[Sequence[int]] = None) -> None:
+        """kg_cpus_set: snapshot node snap_index[k] takes the CPU detail of view node view_index[k] (both
+        default to k over every view node); other nodes keep their tables."""
+        n = len(view.nodes) if view_index is None else len(view_index)
+        vi = None if view_index is None else np.ascontiguousarray(view_index, dtype=np.int32)
+        si = None if snap_index is None else np.ascontiguousarray(snap_index, dtype=np.int32)
+        _check(nat.lib().kg_cpus_set(self._h, ctypes.byref(view.c_view), nat.ptr(vi), nat.ptr(si), n), self,
+               "kg_cpus_set")
 
     def download_cpus(self, node: int, n_cpus: int) -> np.ndarray:
         out = np.zeros(n_cpus, dtype=nat.CPU_INFO)

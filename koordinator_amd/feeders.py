@@ -199,8 +199,13 @@ class SnapshotFeeder:
     # ---- rows ------------------------------------------------------------------------------------
     def _rows_for(self, names: List[str]) -> np.ndarray:
         """kg_node_row of each named node from the current cache state (the C-ABI row builder)."""
+        rows, _ = self._rows_view_for(names)
+        return rows
+
+    def _rows_view_for(self, names: List[str]):
+        """(rows, the flat view they were built from: view node k ⇔ names[k])."""
         if not names:
-            return np.zeros(0, dtype=nat.NODE_ROW)
+            return np.zeros(0, dtype=nat.NODE_ROW), None
         uids: Set[str] = set()
         for n in names:
             uids.update(self.bound.get(n, ()))
@@ -215,15 +220,21 @@ class SnapshotFeeder:
             now_ns=int(self.now_fn()), assign_cache={n: self.assign_cache[n] for n in names if n in self.assign_cache})
         # cluster_from_objects binds every given non-terminated pod to its node: pods given only for the
         # lister are bound to nodes outside `names` (or terminated), so NodeInfo stays the bound set
-        return _engine.build_node_rows(self.cfg, cl.view())
+        view = cl.view()
+        return _engine.build_node_rows(self.cfg, view), view
 
     def take_deltas(self) -> Tuple[np.ndarray, np.ndarray, List[int]]:
         """(indices, rows) of every node changed since the last call, and the indices removed since."""
+        idx, rows, removed, _ = self._take()
+        return idx, rows, removed
+
+    def _take(self):
         names = sorted(n for n in self._dirty if n in self.nodes)
         self._dirty.clear()
         removed, self._removed = self._removed, []
         idx = np.array([self.index[n] for n in names], dtype=np.int32)
-        return idx, self._rows_for(names), removed
+        rows, view = self._rows_view_for(names)
+        return idx, rows, removed, view
 
     def full_rows(self) -> Tuple[np.ndarray, np.ndarray]:
         """(indices, rows) of every live node, built from scratch (the reference point of the deltas)."""
@@ -231,13 +242,15 @@ class SnapshotFeeder:
         return np.array([self.index[n] for n in names], dtype=np.int32), self._rows_for(names)
 
     def flush(self, eng: "_engine.Engine") -> int:
-        """Apply the pending deltas to an engine whose snapshot holds ≥ n_index rows; returns rows written."""
-        idx, rows, removed = self.take_deltas()
+        """Apply the pending deltas to an engine whose snapshot holds ≥ n_index rows — the changed rows and,
+        for a cpuset Reserve, the changed nodes' CPU tables (kg_cpus_set); returns rows written."""
+        idx, rows, removed, view = self._take()
         for i in removed:
             if i not in set(idx.tolist()):
                 eng.remove(i)
         if len(idx):
             eng.upsert(idx, rows)
+            eng.set_cpus(view, np.arange(len(idx)), idx)
         return len(idx)
 
     def cluster(self) -> "ingest.ob.Cluster":
