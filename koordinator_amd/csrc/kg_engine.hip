@@ -2126,6 +2126,12 @@ struct kg_engine {
     std::vector<uint8_t> pod_may_bind;   // bit 0: binds by its own PreFilter; bit 1: a cpu request (node policy)
     bool profiling = false;
     bool mat_kernel = false;            // matrix mode with planes through k_mat (else k_eval3); KG_MATRIX_KERNEL
+    int64_t cls_target_blocks = 2048;   // k_eval3 work items per class ≈ this / tiles (KG_CLS_TARGET_BLOCKS)
+    // the class kinds' launches on two streams (kinds 1 / 3 on stream2), so one kind's grid tail is filled by
+    // the other's workgroups (KG_CLS_CONCURRENT)
+    bool cls_concurrent = false;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // Reservation / ElasticQuota (config 5)
     void *rsv_mem = nullptr;            // slots | rfirst | rnode | E | O
     kg_reservation *rsv = nullptr;      // slots grouped by node (stable)
@@ -2178,8 +2184,7 @@ kg_status ensure_scratch(kg_engine *e, size_t bytes) {
 
 int64_t tiles_total(const kg_engine *e) { return e->pl.cap / KG_TILE; }
 
-int pods_per_block_for(int64_t n_pods, int64_t tiles) {
-    const int64_t target_blocks = 2048;
+int pods_per_block_for(int64_t n_pods, int64_t tiles, int64_t target_blocks = 2048) {
     int64_t ppb = (n_pods * tiles + target_blocks - 1) / target_blocks;
     ppb = (ppb + KG_POD_CHUNK - 1) / KG_POD_CHUNK * KG_POD_CHUNK;
     if (ppb < KG_POD_CHUNK) ppb = KG_POD_CHUNK;
@@ -2348,7 +2353,7 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
         for (size_t c = 0; c < descs.size(); c++) {
             if (descs[c].kind != kind) continue;
             const int32_t n = descs[c].count;
-            const int32_t ppb = pods_per_block_for(n, shard_tiles);
+            const int32_t ppb = pods_per_block_for(n, shard_tiles, e->cls_target_blocks);
             for (int32_t b = 0; b < n; b += ppb) work.push_back(kg_cls_work{(int32_t)c, b, b + ppb < n ? b + ppb : n, 0});
         }
         e->cls_kind_work[kind][1] = (int32_t)work.size() - e->cls_kind_work[kind][0];
@@ -2392,24 +2397,24 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
 
 template <bool MOST, bool FIT_ON, bool LA_ON, bool W1, int KIND>
 void launch_cls_kind(kg_engine *e, dim3 grid, const HotArgs &a, const kg_cls_desc *descs, const kg_cls_work *work,
-                     const char *rows, uint64_t *mask, uint16_t *scores, uint32_t *partials) {
+                     const char *rows, uint64_t *mask, uint16_t *scores, uint32_t *partials, hipStream_t stream) {
     const int32_t first = e->cls_kind_work[KIND][0], count = e->cls_kind_work[KIND][1];
     if (count == 0) return;
     grid.y = (unsigned)count;
     if (mask && e->mat_kernel) {
         const int32_t shard_tiles = (int32_t)grid.x;
         grid.x = (unsigned)((shard_tiles + KG_MAT_XCDS - 1) / KG_MAT_XCDS * KG_MAT_XCDS);
-        hipLaunchKernelGGL((k_mat<MOST, FIT_ON, LA_ON, W1, KIND>), grid, dim3(KG_TILE / 2), 0, e->stream, e->consts, e->pl,
+        hipLaunchKernelGGL((k_mat<MOST, FIT_ON, LA_ON, W1, KIND>), grid, dim3(KG_TILE / 2), 0, stream, e->consts, e->pl,
                            a, descs, work + first, rows, mask, scores, partials, shard_tiles);
         return;
     }
     // matrix mode: 8-pod chunks, score segments staged in LDS and written as 1 KiB wave stores
     // two nodes per lane (four: 92 VGPRs, 5 waves per SIMD, 1.98 vs 0.88 ms per config-2 pass)
     if (mask)
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, 8, true, KIND, 2>), grid, dim3(KG_TILE / 2), 0, e->stream,
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, 8, true, KIND, 2>), grid, dim3(KG_TILE / 2), 0, stream,
                            e->consts, e->pl, a, descs, work + first, rows, mask, scores, partials);
     else
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, 16, false, KIND, 2>), grid, dim3(KG_TILE / 2), 0, e->stream,
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, 16, false, KIND, 2>), grid, dim3(KG_TILE / 2), 0, stream,
                            e->consts, e->pl, a, descs, work + first, rows, mask, scores, partials);
 }
 
@@ -2419,10 +2424,25 @@ void launch_cls4(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint
     const kg_cls_desc *descs = (const kg_cls_desc *)m;
     const kg_cls_work *work = (const kg_cls_work *)(m + e->cls_work_off);
     const char *rows = m + e->cls_rows_off;
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 0>(e, grid, a, descs, work, rows, mask, scores, partials);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 1>(e, grid, a, descs, work, rows, mask, scores, partials);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 2>(e, grid, a, descs, work, rows, mask, scores, partials);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 3>(e, grid, a, descs, work, rows, mask, scores, partials);
+    hipStream_t s2 = e->stream;
+    if (e->cls_concurrent) {   // fork: stream2 starts after everything already queued on the engine stream
+        if (!e->stream2) {
+            (void)hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking);
+            (void)hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+            (void)hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
+        }
+        (void)hipEventRecord(e->ev_fork, e->stream);
+        (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
+        s2 = e->stream2;
+    }
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 0>(e, grid, a, descs, work, rows, mask, scores, partials, e->stream);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 1>(e, grid, a, descs, work, rows, mask, scores, partials, s2);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 2>(e, grid, a, descs, work, rows, mask, scores, partials, e->stream);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 3>(e, grid, a, descs, work, rows, mask, scores, partials, s2);
+    if (e->cls_concurrent) {   // join: the engine stream continues after both kinds
+        (void)hipEventRecord(e->ev_join, s2);
+        (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
+    }
 }
 
 template <bool MOST, bool FIT_ON, bool LA_ON>
@@ -2664,6 +2684,10 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
     // measurement switch: KG_MATRIX_KERNEL=eval3 | mat selects the matrix-mode kernel with planes
     const char *mk = getenv("KG_MATRIX_KERNEL");
     e->mat_kernel = mk && strcmp(mk, "mat") == 0;
+    const char *tb = getenv("KG_CLS_TARGET_BLOCKS");   // measurement switches (tools/ab_cls.sh)
+    if (tb && atoll(tb) > 0) e->cls_target_blocks = atoll(tb);
+    const char *cc = getenv("KG_CLS_CONCURRENT");
+    e->cls_concurrent = cc && atoi(cc) != 0;
     *out = e;
     return KG_OK;
 }
@@ -2682,6 +2706,9 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->gate) (void)hipFree(e->gate);
     if (e->numa_perm) (void)hipFree(e->numa_perm);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->stream2) (void)hipStreamDestroy(e->stream2);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     for (int k = 0; k < kg_engine::kRing; k++) {
         if (e->ev0[k]) (void)hipEventDestroy(e->ev0[k]);
         if (e->ev1[k]) (void)hipEventDestroy(e->ev1[k]);
