@@ -2129,7 +2129,7 @@ struct kg_engine {
     int64_t cls_target_blocks = 2048;   // k_eval3 work items per class ≈ this / tiles (KG_CLS_TARGET_BLOCKS)
     // the class kinds' launches on two streams (kinds 1 / 3 on stream2), so one kind's grid tail is filled by
     // the other's workgroups (KG_CLS_CONCURRENT)
-    bool cls_concurrent = false;
+    bool cls_concurrent = true;
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // Reservation / ElasticQuota (config 5)
@@ -2686,8 +2686,8 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
     e->mat_kernel = mk && strcmp(mk, "mat") == 0;
     const char *tb = getenv("KG_CLS_TARGET_BLOCKS");   // measurement switches (tools/ab_cls.sh)
     if (tb && atoll(tb) > 0) e->cls_target_blocks = atoll(tb);
-    const char *cc = getenv("KG_CLS_CONCURRENT");
-    e->cls_concurrent = cc && atoi(cc) != 0;
+    const char *cc = getenv("KG_CLS_CONCURRENT");   // default on: 0.84 vs 0.87 ms per config-2 pass (r03 A/B)
+    e->cls_concurrent = !cc || atoi(cc) != 0;
     *out = e;
     return KG_OK;
 }
