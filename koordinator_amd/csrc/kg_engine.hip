@@ -1759,10 +1759,15 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                                                                 int64_t n_nodes, int64_t now_ns, int32_t *out_node,
                                                                 int64_t *out_score, RsvArgs ra, int32_t kslots,
                                                                 int32_t *slow_list, int32_t *slow_count,
-                                                                int32_t rescore_slow, int32_t defer_last) {
+                                                                int32_t rescore_slow, int32_t defer_last,
+                                                                const int32_t *prev_nodes, int32_t n_prev) {
     constexpr int POD_DW = (int)(sizeof(kg_pod_dev) / 4);
     static_assert(sizeof(kg_pod_dev) % 4 == 0 && POD_DW <= KG_RESOLVE_THREADS, "pod rows are staged one dword per thread");
     __shared__ int32_t touched[KG_MAX_CHUNK];
+    // pipelined placement: the previous chunk's placements, committed while this chunk's keys were being
+    // evaluated — treated as touched (their keys may predate the commit; re-scored like touched nodes)
+    __shared__ int32_t prevt[KG_MAX_CHUNK];
+    __shared__ int32_t n_prevt;
     __shared__ uint8_t ttile[KG_MAX_TILES];   // the tile holds a touched node (the key lists of others are exact)
     __shared__ int32_t rescan[KG_MAX_TILES];
     __shared__ unsigned long long red[KG_RESOLVE_THREADS / 64];
@@ -1809,11 +1814,22 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         n_touched = 0;
         n_rescan[0] = n_rescan[1] = 0;
         n_slow = *slow_count;
+        n_prevt = 0;
     }
     for (int t = tid; t < tiles_total; t += KG_RESOLVE_THREADS) ttile[t] = 0;
     if (tid < POD_DW && n > 0) reinterpret_cast<uint32_t *>(&lpod[0])[tid] = reinterpret_cast<const uint32_t *>(pods + pod_begin)[tid];
     load_keys(0, kcur);
     __syncthreads();
+    if (n_prev > 0) {
+        for (int q = tid; q < n_prev; q += KG_RESOLVE_THREADS) {
+            const int32_t node = prev_nodes[q];
+            if (node < 0) continue;
+            prevt[atomicAdd(&n_prevt, 1)] = node;
+            ttile[node / KG_TILE] = 1;
+        }
+        __syncthreads();
+    }
+    const int np_prev = n_prevt;
     for (int j = 0; j < n; j++) {
         const int par = j & 1;
         const kg_pod_dev &pd = lpod[par];
@@ -1844,8 +1860,10 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 if (!k) continue;
                 const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
                 bool hit = false;
-                if (ttile[t])
+                if (ttile[t]) {
                     for (int q = 0; q < nt; q++) hit |= touched[q] == node;
+                    for (int q = 0; q < np_prev; q++) hit |= prevt[q] == node;
+                }
                 if (hit) rescan[atomicAdd(&n_rescan[par], 1)] = t;
                 else best = best > k ? best : k;
                 continue;
@@ -1868,6 +1886,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                     const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
                     bool hit = false;
                     for (int q = 0; q < nt; q++) hit |= touched[q] == node;
+                    for (int q = 0; q < np_prev; q++) hit |= prevt[q] == node;
                     if (!hit) {
                         cand = k;
                         found = true;
@@ -1882,6 +1901,10 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         for (int q = tid; q < nt && plain_ok; q += KG_RESOLVE_THREADS) {
             const unsigned long long k = q < KG_NCACHE ? pair_key_cached(c, pl, pd, ncache[q], nrow[q], touched[q], now_ns)
                                                        : pair_key(c, pl, pd, touched[q], n_nodes, now_ns);
+            best = best > k ? best : k;
+        }
+        for (int q = tid; q < np_prev && plain_ok; q += KG_RESOLVE_THREADS) {   // the previous chunk's nodes
+            const unsigned long long k = pair_key(c, pl, pd, prevt[q], n_nodes, now_ns);
             best = best > k ? best : k;
         }
         // nodes outside the fp64 bounds are not in the lists: re-scored exactly, every pod
@@ -2132,6 +2155,8 @@ struct kg_engine {
     bool cls_concurrent = true;
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool place_pipeline = true;         // kg_place overlaps chunk i + 1's evaluation with chunk i's resolve
+    hipEvent_t ev_res[3] = {};          // (KG_PLACE_PIPELINE=0 turns it off)
     // Reservation / ElasticQuota (config 5)
     void *rsv_mem = nullptr;            // slots | rfirst | rnode | E | O
     kg_reservation *rsv = nullptr;      // slots grouped by node (stable)
@@ -2686,6 +2711,8 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
     e->mat_kernel = mk && strcmp(mk, "mat") == 0;
     const char *tb = getenv("KG_CLS_TARGET_BLOCKS");   // measurement switches (tools/ab_cls.sh)
     if (tb && atoll(tb) > 0) e->cls_target_blocks = atoll(tb);
+    const char *pp = getenv("KG_PLACE_PIPELINE");
+    e->place_pipeline = !pp || atoi(pp) != 0;
     const char *cc = getenv("KG_CLS_CONCURRENT");   // default on: 0.84 vs 0.87 ms per config-2 pass (r03 A/B)
     e->cls_concurrent = !cc || atoi(cc) != 0;
     *out = e;
@@ -2709,6 +2736,8 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    for (int k = 0; k < 3; k++)
+        if (e->ev_res[k]) (void)hipEventDestroy(e->ev_res[k]);
     for (int k = 0; k < kg_engine::kRing; k++) {
         if (e->ev0[k]) (void)hipEventDestroy(e->ev0[k]);
         if (e->ev1[k]) (void)hipEventDestroy(e->ev1[k]);
@@ -3121,7 +3150,8 @@ kg_status chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n,
 
 // defer_last: the chunk's last pod is only selected (out_node / out_score); its Reserve is host_reserve's
 kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, const uint32_t *partial_dev,
-                        int32_t *out_node_dev, int64_t *out_score_dev, bool defer_last) {
+                        int32_t *out_node_dev, int64_t *out_score_dev, bool defer_last,
+                        const int32_t *prev_nodes_dev = nullptr, int32_t n_prev = 0) {
     if (pod_begin < 0 || n < 0 || n > KG_MAX_CHUNK || pod_begin + (int64_t)n > e->n_pods)
         return set_err(e, KG_ERR_RANGE, "bad chunk");
     if (n == 0) return KG_OK;
@@ -3138,7 +3168,7 @@ kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t
                        partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev, ra,
                        numa && n > KG_NUMA_CHUNK_PODS ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count,
                        numa ? 0 : 1,   // the NUMA chunk kernels list slow nodes themselves (exact pair path)
-                       defer_last ? 1 : 0);
+                       defer_last ? 1 : 0, prev_nodes_dev, n_prev);
     HIP_TRY(e, hipGetLastError());
     e->generation++;   // the resolve commits the chunk's winners to the snapshot
     return KG_OK;
@@ -3220,6 +3250,65 @@ kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin
     return chunk_resolve(e, now_ns, pod_begin, n, partial_dev, out_node_dev, out_score_dev, false);
 }
 
+}  // extern "C"
+
+namespace {
+
+// Pipelined placement: chunk i + 1's evaluation (second stream) runs while chunk i resolves.  It starts once
+// chunk i − 1's resolve is done, so the snapshot it reads differs from chunk i + 1's true pre-state only by
+// chunk i's commits — and those nodes go to chunk i + 1's resolve as touched (prev_nodes): their keys are
+// skipped and they are re-scored exactly, while every other node's key is exact (its planes did not change).
+// Partial buffers alternate; a buffer is rewritten only after the resolve that read it (eval i + 2 waits for
+// resolve i).  Not used with reservations (one entry buffer) or cpuset pods (host Reserve between chunks).
+kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score, int32_t chunk) {
+    const int32_t P = e->n_pods;
+    const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS;
+    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+    kg_status st = ensure_scratch(e, 2 * up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + 256);
+    if (st) return st;
+    char *s = (char *)e->scratch;
+    uint32_t *part[2] = {(uint32_t *)s, (uint32_t *)(s + up(part_b))};
+    int32_t *dnode = (int32_t *)(s + 2 * up(part_b));
+    int64_t *dscore = (int64_t *)(s + 2 * up(part_b) + up((size_t)P * 4));
+    if (!e->stream2) {
+        HIP_TRY(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+        HIP_TRY(e, hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+        HIP_TRY(e, hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+    }
+    if (!e->ev_res[0])
+        for (int k = 0; k < 3; k++) HIP_TRY(e, hipEventCreateWithFlags(&e->ev_res[k], hipEventDisableTiming));
+    hipStream_t main_s = e->stream, eval_s = e->stream2;
+    HIP_TRY(e, hipEventRecord(e->ev_fork, main_s));   // the eval stream starts after everything queued so far
+    HIP_TRY(e, hipStreamWaitEvent(eval_s, e->ev_fork, 0));
+    int32_t prev_b = 0, prev_n = 0;
+    int32_t i = 0;
+    for (int32_t b = 0; b < P; b += chunk, i++) {
+        const int32_t n = P - b < chunk ? P - b : chunk;
+        if (i >= 2) HIP_TRY(e, hipStreamWaitEvent(eval_s, e->ev_res[(i - 2) % 3], 0));
+        e->stream = eval_s;   // chunk_eval launches on e->stream
+        st = chunk_eval(e, now_ns, b, n, part[i & 1]);
+        e->stream = main_s;
+        if (st) return st;
+        HIP_TRY(e, hipEventRecord(e->ev_join, eval_s));
+        HIP_TRY(e, hipStreamWaitEvent(main_s, e->ev_join, 0));
+        st = chunk_resolve(e, now_ns, b, n, part[i & 1], dnode + b, dscore + b, false, i ? dnode + prev_b : nullptr,
+                           i ? prev_n : 0);
+        if (st) return st;
+        HIP_TRY(e, hipEventRecord(e->ev_res[i % 3], main_s));
+        prev_b = b;
+        prev_n = n;
+    }
+    HIP_TRY(e, hipMemcpyAsync(out_node, dnode, (size_t)P * 4, hipMemcpyDeviceToHost, main_s));
+    HIP_TRY(e, hipMemcpyAsync(out_score, dscore, (size_t)P * 8, hipMemcpyDeviceToHost, main_s));
+    HIP_TRY(e, hipStreamSynchronize(main_s));
+    HIP_TRY(e, hipStreamSynchronize(eval_s));
+    return KG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score) {
     kg_status st = check_engine(e);
     if (st) return st;
@@ -3247,6 +3336,7 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
     // policy) ends its chunk, and its Reserve runs on the host before the next chunk is evaluated
     const bool bind_mode = (e->consts.plugins & KG_PLUGIN_NUMA) && (e->batch_bind || e->n_node_bind_nodes > 0);
     const uint8_t may_mask = e->n_node_bind_nodes > 0 ? 3 : 1;
+    if (!bind_mode && !rsv_args(e).rsv && e->place_pipeline) return place_pipelined(e, now_ns, out_node, out_score, chunk);
     // the placement kernels answer cpusets on NUMA-policy nodes for this batch (kg_consts.numa_bz)
     struct BzScope {
         kg_consts &k;
