@@ -614,6 +614,9 @@ KG_HD void kg_numa_fold(kg_numa_best &b, uint64_t m, bool pref, uint32_t score) 
 // score of a hint mask (generateResourceHints: the NUMA scorer over requested = total − available)
 template <class ZS>
 KG_HD uint32_t kg_hint_score(const kg_consts &c, const ZS &zs, const kg_pod_dev &p, uint32_t m, int64_t pod_cpu) {
+#if defined(KG_NUMA_ABLATE) && defined(__HIP_DEVICE_COMPILE__)
+    if (KG_NUMA_ABLATE & 1) return m & 7u;   // measurement builds only (tools/build_variants.sh): no hint score
+#endif
     int64_t tot[2], av[2];
     zs.sums(m, tot, av);
     const int64_t used[2] = {tot[0] - av[0], tot[1] - av[1]};

@@ -1388,6 +1388,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             const kg_node_row &row = lrow_s[wave];
             const bool zoned = (row.flags & KG_NODE_NUMA_OPTIONS) && row.numa_policy != KG_NUMA_NONE &&
                                row.n_zones > 0;   // n_zones ≤ KG_MAX_ZONES (kg_build_node_rows)
+#ifdef KG_NUMA_ABLATE   // 4 = no zone table fill
+            if (KG_NUMA_ABLATE & 4) {
+            } else
+#endif
             if (zoned) {  // wave-uniform; the previous node's reads precede these writes (in-order LDS per wave)
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
@@ -1399,6 +1403,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                 asm volatile("" ::: "memory");
             }
             kg_numa_out o;   // a node without zones returns before the hint enumeration reads the table
+#ifdef KG_NUMA_ABLATE   // measurement builds only: 2 = no pair evaluation after the table fill
+            if (KG_NUMA_ABLATE & 2) {
+                o.feasible = true;
+                o.score = zt.succ[lane & 63] + (uint32_t)pd.numa_req[0];
+            } else
+#endif
             kg_numa_pair_z<kg_zone_tab, false>(c, row, pd, o, kg_zone_tab{zt});
             ok = ok && o.feasible;
             nsc = o.score;
