@@ -63,17 +63,19 @@ def parse():
 
 def pmc_traffic(kernel_prefix: str = "k_eval"):
     """HBM bytes per launch of the hot kernel from the committed rocprofv3 PMC passes of this same
-    command (profiles/<CURRENT>/summary.json, written by tools/summarize_profile.py), or None."""
+    command (profiles/<CURRENT>/summary.json, written by tools/summarize_profile.py), its rocprofv3
+    average duration (ms, all class-kind launches of one pass), and the source directory; Nones if absent."""
     try:
         with open(os.path.join(ROOT, "profiles", "CURRENT")) as f:
             tag = f.read().strip()
         with open(os.path.join(ROOT, "profiles", tag, "summary.json")) as f:
             s = json.load(f)
-        if not s.get("hbm_traffic_per_launch") or kernel_prefix not in (s.get("hot_kernel") or {}).get("name", ""):
-            return None, None
-        return s["hbm_traffic_per_launch"]["total_bytes"], f"profiles/{tag}"
+        hot = s.get("hot_kernel") or {}
+        if not s.get("hbm_traffic_per_launch") or kernel_prefix not in hot.get("name", ""):
+            return None, None, None
+        return s["hbm_traffic_per_launch"]["total_bytes"], hot["avg_ns"] / 1e6, f"profiles/{tag}"
     except (OSError, ValueError, KeyError):
-        return None, None
+        return None, None, None
 
 
 def cpu_model() -> str:
@@ -486,7 +488,7 @@ def main():
 
     # the committed PMC passes profile the default workload (tools/profile.sh: config 2, one GPU)
     profiled = world == 1 and args.scaling == "strong" and P == 10_000 and total == 100_000
-    traffic, traffic_src = pmc_traffic() if profiled else (None, None)
+    traffic, prof_ms, traffic_src = pmc_traffic() if profiled else (None, None, None)
     if rank == 0:
         line = {
             "metric": "pod×node Filter+Score evals/sec (LoadAwareScheduling + NodeResourcesFit, matrix mode)",
@@ -507,6 +509,11 @@ def main():
                        "pods": P, "nodes": total, "nodes_per_gpu": N, "parallelism": f"node-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK, 4),
+                         "frac_source": "this run's HIP-event kernel time (kernel_ms); frac_rocprof uses the committed "
+                                        "rocprofv3 --kernel-trace --stats average of the same command (a different box: "
+                                        "box-to-box spread ≈ 10 %)",
+                         "kernel_ms_rocprof": None if prof_ms is None else round(prof_ms, 4),
+                         "frac_rocprof": None if prof_ms is None else round(algo_bytes / (prof_ms * 1e-3) / HBM_PEAK, 4),
                          "traffic": None if traffic is None else int(traffic), "traffic_unit": "bytes per launch (PMC)",
                          "traffic_source": traffic_src,
                          "kernel": "k_eval3", "kernel_ms": round(k_ms, 4),
