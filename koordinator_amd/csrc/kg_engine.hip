@@ -3346,7 +3346,10 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
     // policy) ends its chunk, and its Reserve runs on the host before the next chunk is evaluated
     const bool bind_mode = (e->consts.plugins & KG_PLUGIN_NUMA) && (e->batch_bind || e->n_node_bind_nodes > 0);
     const uint8_t may_mask = e->n_node_bind_nodes > 0 ? 3 : 1;
-    if (!bind_mode && !rsv_args(e).rsv && e->place_pipeline) return place_pipelined(e, now_ns, out_node, out_score, chunk);
+    // the pipeline pays two cross-stream event hops per chunk: it wins where the chunk evaluation is long
+    // (NodeNUMAResource: config 3 5.0k → 6.1k pods/s) and loses where it is short (config 2: 82k → 61k)
+    if (!bind_mode && !rsv_args(e).rsv && e->place_pipeline && (e->consts.plugins & KG_PLUGIN_NUMA))
+        return place_pipelined(e, now_ns, out_node, out_score, chunk);
     // the placement kernels answer cpusets on NUMA-policy nodes for this batch (kg_consts.numa_bz)
     struct BzScope {
         kg_consts &k;
