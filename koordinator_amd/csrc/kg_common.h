@@ -385,6 +385,12 @@ struct kg_numa_out {
 // and a single exact int64 multiply-compare settles it; every other operand takes the division
 KG_HD int64_t kg_qdiv(int64_t n, int64_t d) {
     if (n < 0 || d <= 0 || d >= (1LL << 40) || n >= (d << 7)) return n / d;
+#if defined(KG_QDIV_F64) && defined(__HIP_DEVICE_COMPILE__)
+    // n < 2^47 and d < 2^40 convert to double exactly; the quotient (< 128) has an ulp ≤ 2^-46 while a
+    // non-integer n / d lies ≥ 1 / d > 2^-40 below the next integer, so the correctly rounded division
+    // never reaches it and truncation gives the floor
+    return (int64_t)((double)n / (double)d);
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
     const float r = __builtin_amdgcn_rcpf((float)d);
 #else

@@ -1345,7 +1345,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                                                     const kg_node_row *__restrict__ rows,
                                                     unsigned long long *__restrict__ mask,
                                                     uint16_t *__restrict__ scores, uint8_t *__restrict__ numa_scores,
-                                                    uint32_t *__restrict__ partials, const int32_t *__restrict__ perm) {
+                                                    uint32_t *__restrict__ partials, const int32_t *__restrict__ perm,
+                                                    BatchMasks bm) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t tile = (int64_t)a.tile_begin + blockIdx.x;
@@ -1357,7 +1358,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     // small placement chunks (one pod block) still put ≥ 1.5 waves on every SIMD
     const int npw = KG_NUMA2_NODES / (int)gridDim.z;
     const int64_t base = tile * KG_TILE + wave * KG_NUMA2_NODES + (int64_t)blockIdx.z * npw;
-    const BatchMasks bm{0xFFu, 0xFFu};
     // per-wave zone table of the current node (every index mask's sums and id mask, prefix sums of
     // the descending totals): filled by the wave's 64 lanes, read by the hint enumeration of its pods
     __shared__ kg_zone_tab_data ztab[256 / 64];
@@ -1368,6 +1368,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     uint64_t mword = 0;
     uint32_t sacc[4] = {0u, 0u, 0u, 0u};
     uint32_t nacc[4] = {0u, 0u, 0u, 0u};
+    // the canonical row of the wave's next node, in flight in registers (one 16-byte word per lane) while
+    // the current node is evaluated
+    constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16);
+    uint4 row_next = make_uint4(0u, 0u, 0u, 0u);
+    if (lane < ROW_U4 && base < a.node_end) row_next = reinterpret_cast<const uint4 *>(rows + base)[lane];
     for (int k = 0; k < npw; k++) {
         const int64_t node = base + k;
         const bool in_range = node < a.node_end;
@@ -1381,8 +1386,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             // its zone fields in every loop of every lane
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
-            if (lane < (int)(sizeof(kg_node_row) / 16))
-                reinterpret_cast<uint4 *>(&lrow_s[wave])[lane] = reinterpret_cast<const uint4 *>(rows + node)[lane];
+            if (lane < ROW_U4) reinterpret_cast<uint4 *>(&lrow_s[wave])[lane] = row_next;
+            if (lane < ROW_U4 && node + 1 < a.node_end && k + 1 < npw)
+                row_next = reinterpret_cast<const uint4 *>(rows + node + 1)[lane];
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
             const kg_node_row &row = lrow_s[wave];
@@ -2117,6 +2123,7 @@ struct kg_engine {
     int32_t *numa_perm = nullptr;   // NodeNUMAResource matrix mode: pod rows grouped by hint-list shape
     bool numa_perm_on = false;
     BatchMasks bm{0, 0};
+    bool numa_bm_all = false;       // k_eval_numa2 loads every resource plane (KG_NUMA_BM_ALL, measurement)
     bool la_prod = false;           // some pod of the batch scores with the prod-usage variant
     bool pow2 = true;               // every Fit / LoadAware weight sum of the batch is a power of two
     // class-specialised matrix mode (k_eval3): built from the batch in kg_pods_set, laid out for
@@ -2553,7 +2560,8 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
             dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), n <= 64 ? 4u : 1u);
             hipLaunchKernelGGL(k_eval_numa2, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
                                e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials,
-                               e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr);
+                               e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr,
+                               e->numa_bm_all ? BatchMasks{0xFFu, 0xFFu} : e->bm);
         }
         HIP_TRY(e, hipGetLastError());
         // cpusets on NUMA-policy nodes: patched in after the hot kernel (matrix planes, or the one-key-per-tile
@@ -2721,6 +2729,8 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
     e->mat_kernel = mk && strcmp(mk, "mat") == 0;
     const char *tb = getenv("KG_CLS_TARGET_BLOCKS");   // measurement switches (tools/ab_cls.sh)
     if (tb && atoll(tb) > 0) e->cls_target_blocks = atoll(tb);
+    const char *bma = getenv("KG_NUMA_BM_ALL");
+    e->numa_bm_all = bma && atoi(bma) != 0;
     const char *pp = getenv("KG_PLACE_PIPELINE");
     e->place_pipeline = !pp || atoi(pp) != 0;
     const char *cc = getenv("KG_CLS_CONCURRENT");   // default on: 0.84 vs 0.87 ms per config-2 pass (r03 A/B)
@@ -3346,7 +3356,10 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
     // policy) ends its chunk, and its Reserve runs on the host before the next chunk is evaluated
     const bool bind_mode = (e->consts.plugins & KG_PLUGIN_NUMA) && (e->batch_bind || e->n_node_bind_nodes > 0);
     const uint8_t may_mask = e->n_node_bind_nodes > 0 ? 3 : 1;
-    if (!bind_mode && !rsv_args(e).rsv && e->place_pipeline) return place_pipelined(e, now_ns, out_node, out_score, chunk);
+    // the pipeline pays two cross-stream event hops per chunk: it wins where the chunk evaluation is long
+    // (NodeNUMAResource: config 3 5.0k → 6.1k pods/s) and loses where it is short (config 2: 82k → 61k)
+    if (!bind_mode && !rsv_args(e).rsv && e->place_pipeline && (e->consts.plugins & KG_PLUGIN_NUMA))
+        return place_pipelined(e, now_ns, out_node, out_score, chunk);
     // the placement kernels answer cpusets on NUMA-policy nodes for this batch (kg_consts.numa_bz)
     struct BzScope {
         kg_consts &k;
