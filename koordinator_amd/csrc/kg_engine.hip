@@ -1340,7 +1340,10 @@ __global__ __launch_bounds__(256) void k_numa_bind_fix(kg_consts c, kg_planes pl
 // row: 64 feasibility bits per u64 word, 8 score pairs per 16-byte store, 16 NUMA scores per 16-byte
 // store, the per-(pod, tile) key as a lane-private max (one atomicMax per wave).
 #define KG_NUMA2_NODES 256
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_eval_numa2(kg_consts c, kg_planes pl, HotArgs a,
+#ifndef KG_NUMA2_WPE
+#define KG_NUMA2_WPE 3   // waves per SIMD the register budget is sized for (measurement builds vary it)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WPE))) void k_eval_numa2(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_pod_dev *__restrict__ pods,
                                                     const kg_node_row *__restrict__ rows,
                                                     unsigned long long *__restrict__ mask,
@@ -1368,11 +1371,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     uint64_t mword = 0;
     uint32_t sacc[4] = {0u, 0u, 0u, 0u};
     uint32_t nacc[4] = {0u, 0u, 0u, 0u};
-    // the canonical row of the wave's next node, in flight in registers (one 16-byte word per lane) while
-    // the current node is evaluated
     constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16);
+#ifdef KG_NUMA2_PREFETCH   // measurement builds: the next node's row in flight in registers (measured slower)
     uint4 row_next = make_uint4(0u, 0u, 0u, 0u);
     if (lane < ROW_U4 && base < a.node_end) row_next = reinterpret_cast<const uint4 *>(rows + base)[lane];
+#endif
     for (int k = 0; k < npw; k++) {
         const int64_t node = base + k;
         const bool in_range = node < a.node_end;
@@ -1386,9 +1389,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             // its zone fields in every loop of every lane
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
+#ifdef KG_NUMA2_PREFETCH
             if (lane < ROW_U4) reinterpret_cast<uint4 *>(&lrow_s[wave])[lane] = row_next;
             if (lane < ROW_U4 && node + 1 < a.node_end && k + 1 < npw)
                 row_next = reinterpret_cast<const uint4 *>(rows + node + 1)[lane];
+#else
+            if (lane < ROW_U4) reinterpret_cast<uint4 *>(&lrow_s[wave])[lane] = reinterpret_cast<const uint4 *>(rows + node)[lane];
+#endif
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
             const kg_node_row &row = lrow_s[wave];
