@@ -381,11 +381,12 @@ struct kg_numa_out {
 };
 
 // n / d (Go int64 division) for the score quotients: when 0 ≤ n < 128·d and d < 2^40 the quotient
-// is < 128, so one fp32 estimate (relative error < 2^-21, absolute < 2^-14) is off by at most one
-// and a single exact int64 multiply-compare settles it; every other operand takes the division
+// is < 128; on the device one correctly rounded fp64 division gives it (below), on the host one fp32
+// estimate (relative error < 2^-21, absolute < 2^-14) is off by at most one and a single exact int64
+// multiply-compare settles it; every other operand takes the division
 // Go int64 division kept out of line on the device: the kernels reach it only on the rare operands the
 // fast quotients exclude, and one shared body keeps its long expansion out of every inlined caller
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(KG_DIV_INLINE)
 __device__ __attribute__((noinline)) int64_t kg_div_slow(int64_t n, int64_t d) { return n / d; }
 #else
 inline int64_t kg_div_slow(int64_t n, int64_t d) { return n / d; }
@@ -393,7 +394,7 @@ inline int64_t kg_div_slow(int64_t n, int64_t d) { return n / d; }
 
 KG_HD int64_t kg_qdiv(int64_t n, int64_t d) {
     if (n < 0 || d <= 0 || d >= (1LL << 40) || n >= (d << 7)) return kg_div_slow(n, d);
-#if defined(KG_QDIV_F64) && defined(__HIP_DEVICE_COMPILE__)
+#if !defined(KG_QDIV_F32) && defined(__HIP_DEVICE_COMPILE__)
     // n < 2^47 and d < 2^40 convert to double exactly; the quotient (< 128) has an ulp ≤ 2^-46 while a
     // non-integer n / d lies ≥ 1 / d > 2^-40 below the next integer, so the correctly rounded division
     // never reaches it and truncation gives the floor
