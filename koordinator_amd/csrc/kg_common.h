@@ -389,7 +389,7 @@ struct kg_numa_out {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(KG_DIV_INLINE)
 __device__ __attribute__((noinline)) int64_t kg_div_slow(int64_t n, int64_t d) { return n / d; }
 #else
-inline int64_t kg_div_slow(int64_t n, int64_t d) { return n / d; }
+KG_HD int64_t kg_div_slow(int64_t n, int64_t d) { return n / d; }
 #endif
 
 KG_HD int64_t kg_qdiv(int64_t n, int64_t d) {
