@@ -1340,33 +1340,19 @@ __global__ __launch_bounds__(256) void k_numa_bind_fix(kg_consts c, kg_planes pl
 // row: 64 feasibility bits per u64 word, 8 score pairs per 16-byte store, 16 NUMA scores per 16-byte
 // store, the per-(pod, tile) key as a lane-private max (one atomicMax per wave).
 #define KG_NUMA2_NODES 256
+#define KG_NUMA2_SEG 32   // nodes per work item of the queued form (whole 32-bit halves of the mask words)
 #ifndef KG_NUMA2_WPE
 #define KG_NUMA2_WPE 3   // waves per SIMD the register budget is sized for (measurement builds vary it)
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WPE))) void k_eval_numa2(kg_consts c, kg_planes pl, HotArgs a,
-                                                    const kg_pod_dev *__restrict__ pods,
-                                                    const kg_node_row *__restrict__ rows,
-                                                    unsigned long long *__restrict__ mask,
-                                                    uint16_t *__restrict__ scores, uint8_t *__restrict__ numa_scores,
-                                                    uint32_t *__restrict__ partials, const int32_t *__restrict__ perm,
-                                                    BatchMasks bm) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t tile = (int64_t)a.tile_begin + blockIdx.x;
-    const int slot = blockIdx.y * 64 + lane;
-    const bool live = slot < a.n_pods;
-    const int p = live && perm ? perm[slot] : slot;   // the pod row this lane evaluates and writes
-    const kg_pod_dev pd = pods[live ? p : 0];
-    // blockIdx.z splits each wave's 256 nodes into gridDim.z runs of ≥ 64 (whole mask words), so
-    // small placement chunks (one pod block) still put ≥ 1.5 waves on every SIMD
-    const int npw = KG_NUMA2_NODES / (int)gridDim.z;
-    const int64_t base = tile * KG_TILE + wave * KG_NUMA2_NODES + (int64_t)blockIdx.z * npw;
-    // per-wave zone table of the current node (every index mask's sums and id mask, prefix sums of
-    // the descending totals): filled by the wave's 64 lanes, read by the hint enumeration of its pods
-    __shared__ kg_zone_tab_data ztab[256 / 64];
-    __shared__ __attribute__((aligned(16))) kg_node_row lrow_s[256 / 64];
-    static_assert(sizeof(kg_node_row) % 16 == 0, "rows are staged as 16-byte words");
-    kg_zone_tab_data &zt = ztab[wave];
+// one wave's run of `npw` nodes from `base` (inside tile `tile`) for the 64 pods of its lanes; npw is a
+// multiple of 32, runs start on a 32-node boundary
+__device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &pl, const HotArgs &a,
+                                          const kg_pod_dev &pd, int p, bool live, int64_t tile, int64_t base, int npw,
+                                          const kg_node_row *__restrict__ rows, unsigned long long *__restrict__ mask,
+                                          uint16_t *__restrict__ scores, uint8_t *__restrict__ numa_scores,
+                                          uint32_t *__restrict__ partials, const BatchMasks &bm,
+                                          kg_zone_tab_data &zt, kg_node_row &lrow) {
+    const int lane = threadIdx.x & 63;
     uint32_t best = 0;
     uint64_t mword = 0;
     uint32_t sacc[4] = {0u, 0u, 0u, 0u};
@@ -1390,15 +1376,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WP
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
 #ifdef KG_NUMA2_PREFETCH
-            if (lane < ROW_U4) reinterpret_cast<uint4 *>(&lrow_s[wave])[lane] = row_next;
+            if (lane < ROW_U4) reinterpret_cast<uint4 *>(&lrow)[lane] = row_next;
             if (lane < ROW_U4 && node + 1 < a.node_end && k + 1 < npw)
                 row_next = reinterpret_cast<const uint4 *>(rows + node + 1)[lane];
 #else
-            if (lane < ROW_U4) reinterpret_cast<uint4 *>(&lrow_s[wave])[lane] = reinterpret_cast<const uint4 *>(rows + node)[lane];
+            if (lane < ROW_U4) reinterpret_cast<uint4 *>(&lrow)[lane] = reinterpret_cast<const uint4 *>(rows + node)[lane];
 #endif
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
-            const kg_node_row &row = lrow_s[wave];
+            const kg_node_row &row = lrow;
             const bool zoned = (row.flags & KG_NODE_NUMA_OPTIONS) && row.numa_policy != KG_NUMA_NONE &&
                                row.n_zones > 0;   // n_zones ≤ KG_MAX_ZONES (kg_build_node_rows)
 #ifdef KG_NUMA_ABLATE   // 4 = no zone table fill
@@ -1455,7 +1441,69 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WP
             mword = 0;
         }
     }
+    if (npw & 63) {  // a 32-node run: its half of the mask word (little-endian: low half = first 32 nodes)
+        const int64_t c0 = base + npw - 32 - a.col_begin;
+        if (live && mask && c0 < (int64_t)a.mask_words * 64)
+            reinterpret_cast<uint32_t *>(mask + (int64_t)p * a.mask_words)[c0 >> 5] = (uint32_t)mword;
+    }
     if (live && best) atomicMax(&partials[(int64_t)p * a.tiles_total + tile], best);
+}
+
+// NodeNUMAResource enabled (config 3; matrix mode and placement chunks), pod per lane: a wave holds 64 pods and
+// walks a run of nodes one node at a time, so every node-side value (derived planes, canonical row with its
+// zones) is wave-uniform (one cache line per load, served to all 64 pods) and the NUMA hint enumeration runs
+// on the node's structure for 64 requests at once.  Outputs accumulate per lane along the pod's own row: 64
+// feasibility bits per u64 word (32 per half), 8 score pairs per 16-byte store, 16 NUMA scores per 16-byte
+// store, the per-(pod, tile) key as a lane-private max (one atomicMax per run).
+// Two launch forms:
+//  * grid (tiles, pod blocks, z): wave w of a workgroup takes nodes [w·256, w·256 + 256) of its tile, split
+//    z ways (small placement chunks: one pod block still puts ≥ 1.5 waves on every SIMD);
+//  * queued (queue != nullptr): a resident grid whose waves take 32-node work items
+//    (tile, 32-node run, pod block), pod block fastest, from a device counter until `n_items` are taken —
+//    the whole-workgroup grid of the first form leaves a last partial round of workgroups on a few CUs
+//    (1568 workgroups over 768 resident slots is 3 rounds for 2.04 rounds of work).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WPE))) void k_eval_numa2(kg_consts c, kg_planes pl, HotArgs a,
+                                                    const kg_pod_dev *__restrict__ pods,
+                                                    const kg_node_row *__restrict__ rows,
+                                                    unsigned long long *__restrict__ mask,
+                                                    uint16_t *__restrict__ scores, uint8_t *__restrict__ numa_scores,
+                                                    uint32_t *__restrict__ partials, const int32_t *__restrict__ perm,
+                                                    BatchMasks bm, int32_t *queue, int32_t n_items) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // per-wave zone table of the current node (every index mask's sums and id mask, prefix sums of
+    // the descending totals): filled by the wave's 64 lanes, read by the hint enumeration of its pods
+    __shared__ kg_zone_tab_data ztab[256 / 64];
+    __shared__ __attribute__((aligned(16))) kg_node_row lrow_s[256 / 64];
+    static_assert(sizeof(kg_node_row) % 16 == 0, "rows are staged as 16-byte words");
+    const int n_pb = (a.n_pods + 63) / 64;
+    for (int it = 0;; it++) {   // grid form: one pass; queued: every wave leaves once the counter passes n_items
+        int64_t tile, base;
+        int npw, pb;
+        if (queue == nullptr) {
+            if (it > 0) break;
+            tile = (int64_t)a.tile_begin + blockIdx.x;
+            pb = blockIdx.y;
+            npw = KG_NUMA2_NODES / (int)gridDim.z;
+            base = tile * KG_TILE + wave * KG_NUMA2_NODES + (int64_t)blockIdx.z * npw;
+        } else {
+            int item = 0;
+            if (lane == 0) item = atomicAdd(queue, 1);
+            item = __builtin_amdgcn_readfirstlane(item);
+            if (item >= n_items) break;
+            pb = item % n_pb;
+            const int run = item / n_pb;   // 32-node run of the launch's node range, from tile_begin · KG_TILE
+            tile = (int64_t)a.tile_begin + run / (KG_TILE / KG_NUMA2_SEG);
+            base = (int64_t)a.tile_begin * KG_TILE + (int64_t)run * KG_NUMA2_SEG;
+            npw = KG_NUMA2_SEG;
+        }
+        const int slot = pb * 64 + lane;
+        const bool live = slot < a.n_pods;
+        const int p = live && perm ? perm[slot] : slot;   // the pod row this lane evaluates and writes
+        const kg_pod_dev pd = pods[live ? p : 0];
+        numa2_run(c, pl, a, pd, p, live, tile, base, npw, rows, mask, scores, numa_scores, partials, bm, ztab[wave],
+                  lrow_s[wave]);
+    }
 }
 
 __device__ __forceinline__ unsigned long long decode_partial(uint32_t k, int tile) {
@@ -2131,6 +2179,9 @@ struct kg_engine {
     bool numa_perm_on = false;
     BatchMasks bm{0, 0};
     bool numa_bm_all = false;       // k_eval_numa2 loads every resource plane (KG_NUMA_BM_ALL, measurement)
+    bool numa_queue_on = true;      // k_eval_numa2's queued form (KG_NUMA_QUEUE=0: the grid form, measurement)
+    int64_t numa_resident_wgs = 0;  // resident k_eval_numa2 workgroups of the device (queried at first use)
+    int32_t *numa_queue = nullptr;  // its work-item counter
     bool la_prod = false;           // some pod of the batch scores with the prod-usage variant
     bool pow2 = true;               // every Fit / LoadAware weight sum of the batch is a power of two
     // class-specialised matrix mode (k_eval3): built from the batch in kg_pods_set, laid out for
@@ -2563,12 +2614,30 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     }
     if (e->consts.plugins & KG_PLUGIN_NUMA) {
         if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
-        {  // pod per lane; a single pod block splits each wave's node run 4 ways
-            dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), n <= 64 ? 4u : 1u);
-            hipLaunchKernelGGL(k_eval_numa2, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
-                               e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials,
-                               e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr,
-                               e->numa_bm_all ? BatchMasks{0xFFu, 0xFFu} : e->bm);
+        {  // pod per lane; queued 32-node items when they fill every resident wave slot several times over,
+           // else a grid where a single pod block splits each wave's node run 4 ways
+            const int64_t n_items = shard_tiles * (KG_TILE / KG_NUMA2_SEG) * ((n + 63) / 64);
+            const int32_t *perm = e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr;
+            const BatchMasks bm = e->numa_bm_all ? BatchMasks{0xFFu, 0xFFu} : e->bm;
+            if (e->numa_resident_wgs == 0) {
+                int dev_cus = 0, per_cu = 0;
+                HIP_TRY(e, hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->device));
+                HIP_TRY(e, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_eval_numa2, 256, 0));
+                e->numa_resident_wgs = (int64_t)dev_cus * (per_cu > 0 ? per_cu : 1);
+                HIP_TRY(e, hipMalloc(&e->numa_queue, sizeof(int32_t)));
+            }
+            if (e->numa_queue_on && n_items >= 4 * 4 * e->numa_resident_wgs && n_items < INT32_MAX) {
+                HIP_TRY(e, hipMemsetAsync(e->numa_queue, 0, sizeof(int32_t), e->stream));
+                const int64_t wgs = std::min<int64_t>(e->numa_resident_wgs, (n_items + 3) / 4);
+                hipLaunchKernelGGL(k_eval_numa2, dim3((unsigned)wgs), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                                   e->pods + pod_begin, e->pl.rows, (unsigned long long *)mask, scores, numa_scores,
+                                   partials, perm, bm, e->numa_queue, (int32_t)n_items);
+            } else {
+                dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), n <= 64 ? 4u : 1u);
+                hipLaunchKernelGGL(k_eval_numa2, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
+                                   e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials, perm, bm,
+                                   (int32_t *)nullptr, 0);
+            }
         }
         HIP_TRY(e, hipGetLastError());
         // cpusets on NUMA-policy nodes: patched in after the hot kernel (matrix planes, or the one-key-per-tile
@@ -2738,6 +2807,8 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
     if (tb && atoll(tb) > 0) e->cls_target_blocks = atoll(tb);
     const char *bma = getenv("KG_NUMA_BM_ALL");
     e->numa_bm_all = bma && atoi(bma) != 0;
+    const char *nq = getenv("KG_NUMA_QUEUE");
+    e->numa_queue_on = !nq || atoi(nq) != 0;
     const char *pp = getenv("KG_PLACE_PIPELINE");
     e->place_pipeline = !pp || atoi(pp) != 0;
     const char *cc = getenv("KG_CLS_CONCURRENT");   // default on: 0.84 vs 0.87 ms per config-2 pass (r03 A/B)
@@ -2759,6 +2830,7 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->quota) (void)hipFree(e->quota);
     if (e->gate) (void)hipFree(e->gate);
     if (e->numa_perm) (void)hipFree(e->numa_perm);
+    if (e->numa_queue) (void)hipFree(e->numa_queue);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
