@@ -2179,7 +2179,8 @@ struct kg_engine {
     bool numa_perm_on = false;
     BatchMasks bm{0, 0};
     bool numa_bm_all = false;       // k_eval_numa2 loads every resource plane (KG_NUMA_BM_ALL, measurement)
-    bool numa_queue_on = true;      // k_eval_numa2's queued form (KG_NUMA_QUEUE=0: the grid form, measurement)
+    int numa_queue_mode = 1;        // k_eval_numa2's form: 1 queued for large launches, 0 grid (KG_NUMA_QUEUE=0,
+                                    // measurement), 2 queued for every launch (KG_NUMA_QUEUE=2, tests)
     int64_t numa_resident_wgs = 0;  // resident k_eval_numa2 workgroups of the device (queried at first use)
     int32_t *numa_queue = nullptr;  // its work-item counter
     bool la_prod = false;           // some pod of the batch scores with the prod-usage variant
@@ -2626,7 +2627,8 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
                 e->numa_resident_wgs = (int64_t)dev_cus * (per_cu > 0 ? per_cu : 1);
                 HIP_TRY(e, hipMalloc(&e->numa_queue, sizeof(int32_t)));
             }
-            if (e->numa_queue_on && n_items >= 4 * 4 * e->numa_resident_wgs && n_items < INT32_MAX) {
+            const bool queued = e->numa_queue_mode == 2 || (e->numa_queue_mode == 1 && n_items >= 4 * 4 * e->numa_resident_wgs);
+            if (queued && n_items < INT32_MAX) {
                 HIP_TRY(e, hipMemsetAsync(e->numa_queue, 0, sizeof(int32_t), e->stream));
                 const int64_t wgs = std::min<int64_t>(e->numa_resident_wgs, (n_items + 3) / 4);
                 hipLaunchKernelGGL(k_eval_numa2, dim3((unsigned)wgs), dim3(256), 0, e->stream, e->consts, e->pl, a,
@@ -2808,7 +2810,7 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
     const char *bma = getenv("KG_NUMA_BM_ALL");
     e->numa_bm_all = bma && atoi(bma) != 0;
     const char *nq = getenv("KG_NUMA_QUEUE");
-    e->numa_queue_on = !nq || atoi(nq) != 0;
+    e->numa_queue_mode = nq ? atoi(nq) : 1;
     const char *pp = getenv("KG_PLACE_PIPELINE");
     e->place_pipeline = !pp || atoi(pp) != 0;
     const char *cc = getenv("KG_CLS_CONCURRENT");   // default on: 0.84 vs 0.87 ms per config-2 pass (r03 A/B)

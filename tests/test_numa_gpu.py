@@ -81,6 +81,15 @@ def test_matrix_numa_shard():
     _check_matrix3(numa_config(), cl, 40, begin=1024, end=2500)
 
 
+@pytest.mark.parametrize("pods,begin,end", [(40, 0, None), (333, 0, None), (97, 1024, 2500)])
+def test_matrix_numa_queued_form(monkeypatch, pods, begin, end):
+    # KG_NUMA_QUEUE=2: k_eval_numa2's queued form (32-node work items from a device counter, half mask
+    # words) on launches the default keeps on the grid form — the full-size launches take it by default
+    monkeypatch.setenv("KG_NUMA_QUEUE", "2")
+    cl = make_numa_edge_cluster(2_500, pods, seed=21 + pods)
+    _check_matrix3(numa_config(), cl, pods, begin=begin, end=end)
+
+
 @pytest.mark.parametrize("case", SCORE["cases"], ids=lambda c: c["name"])
 def test_kat_numa_node_score(case):
     """TestNUMANodeScore (nodenumaresource/scoring_test.go) through kg_eval."""
