@@ -684,7 +684,7 @@ struct kg_zone_trim {
     KG_HD int min_k(int r, int64_t q, int Z) const { return kg_zone_calc{row}.min_k(r, q, Z); }
 };
 
-template <class ZS>
+template <class ZS, bool REC = true>
 KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                          const ZS &zs, const int64_t *requested, int policy, int64_t pcpu, const kg_numa_bind *bd);
 
@@ -706,8 +706,10 @@ void kg_numa_bind_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod
 // node with reservations, transformer.go:49-291 restores the snapshot NodeInfo every plugin reads).
 // `reserve`: the Reserve path (Allocate on the stored hint, plugin.go:406-416) — no Filter-only checks.
 // BZ: answer cpusets on NUMA-policy nodes here (host, k_numa_bind_fix); the hot device kernels pass false
-// and leave those pairs infeasible for the fix-up kernel, so they carry no call into the cpuset path
-template <class ZS, bool BZ = true>
+// and leave those pairs infeasible for the fix-up kernel, so they carry no call into the cpuset path.
+// REC: record the allocation (o.zone / o.alloc, what Reserve needs); Filter / Score callers pass false and
+// get o.feasible, o.score and o.n_alloc only (no per-lane arrays written at a run-time index)
+template <class ZS, bool BZ = true, bool REC = true>
 KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                           const ZS &zs, const int64_t *requested = nullptr, bool reserve = false) {
     if (!requested) requested = row.requested;
@@ -788,12 +790,12 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
         else o.feasible = false;   // the caller re-evaluates these pairs (k_numa_bind_fix)
         return;
     }
-    kg_numa_zoned(c, row, p, o, zs, requested, policy, pcpu, (const kg_numa_bind *)nullptr);
+    kg_numa_zoned<ZS, REC>(c, row, p, o, zs, requested, policy, pcpu, (const kg_numa_bind *)nullptr);
 }
 
 // hint generation, merge, Admit, allocateResourcesByHint and the zone score (the part of Filter / Score
 // that depends on the zone provider); `pcpu`: the cpu request (a cpuset-bound pod's amplified one)
-template <class ZS>
+template <class ZS, bool REC>
 KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                          const ZS &zs, const int64_t *requested, int policy, int64_t pcpu, const kg_numa_bind *bd) {
     const int Z = row.n_zones;
@@ -893,6 +895,11 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
         o.feasible = false;
         return;
     }
+    // per allocated zone, as it is allocated: calculateAllocatableAndRequested's sums (scoring.go:118-164) and
+    // allocateCPUSet's per-zone CPUs (below)
+    int64_t z_tot[2] = {0, 0}, z_used[2] = {0, 0}, bd_sum = 0;
+    bool bd_whole = true;
+    const int req_pol = bd ? bd->required : KG_CPU_BIND_UNSET;
     if (!(single && best.mask == dflt)) {   // SingleNUMANode: the all-zones hint is nil
         // allocateResourcesByHint: zones of the hint in ascending affinity id, greedily
         // allocateResourcesByHint takes a cpuset request's original (unamplified) requests
@@ -916,10 +923,26 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
                 req[r] -= got[r];
             }
             if (got[0] != 0 || got[1] != 0) {
-                o.zone[o.n_alloc] = zi;
-                o.alloc[o.n_alloc][0] = got[0];
-                o.alloc[o.n_alloc][1] = got[1];
+                if constexpr (REC) {
+                    o.zone[o.n_alloc] = zi;
+                    o.alloc[o.n_alloc][0] = got[0];
+                    o.alloc[o.n_alloc][1] = got[1];
+                }
                 o.n_alloc++;
+                for (int r = 0; r < 2; r++) {
+                    z_tot[r] += kg_zone_total(row, zi, r);
+                    const int64_t u = kg_zone_alloc(row, zi, r);
+                    z_used[r] += u > 0 ? u : 0;
+                }
+                if (bd) {
+                    const int64_t zav = req_pol == KG_CPU_BIND_FULL_PCPUS ? row.zone_cpus_full[zi]
+                                      : req_pol == KG_CPU_BIND_SPREAD_BY_PCPUS ? row.zone_cores_free[zi] : row.zone_cpus_avail[zi];
+                    int64_t n = got[0] / 1000;
+                    if (zav < n) n = zav;
+                    if (req_pol == KG_CPU_BIND_FULL_PCPUS && (row.cpus_per_core <= 0 || n % row.cpus_per_core != 0))
+                        bd_whole = false;
+                    bd_sum += n;
+                }
             }
         }
         if ((inter[0] && req[0] != 0) || (inter[1] && req[1] != 0)) {
@@ -933,23 +956,10 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
         // must cover the request; each allocated zone gives min(its available CPUs, its cpu / 1000), which
         // takeCPUs always finds, and those must add up to the request exactly; a required FullPCPUs
         // policy needs whole cores from every zone (satisfiedRequiredCPUBindPolicy)
-        const int req_pol = bd->required;
         const int64_t node_av = req_pol == KG_CPU_BIND_FULL_PCPUS ? row.cpuset_full_free_cpus
                               : req_pol == KG_CPU_BIND_SPREAD_BY_PCPUS ? row.cpuset_free_cores : row.cpuset_avail_cpus;
         bool ok = node_av >= bd->need;
-        if (ok && o.n_alloc > 0) {
-            int64_t sum = 0;
-            for (int j = 0; j < o.n_alloc; j++) {
-                const int zi = o.zone[j];
-                const int64_t zav = req_pol == KG_CPU_BIND_FULL_PCPUS ? row.zone_cpus_full[zi]
-                                  : req_pol == KG_CPU_BIND_SPREAD_BY_PCPUS ? row.zone_cores_free[zi] : row.zone_cpus_avail[zi];
-                int64_t n = o.alloc[j][0] / 1000;
-                if (zav < n) n = zav;
-                if (req_pol == KG_CPU_BIND_FULL_PCPUS && (row.cpus_per_core <= 0 || n % row.cpus_per_core != 0)) ok = false;
-                sum += n;
-            }
-            ok = ok && sum == bd->need;
-        }
+        if (ok && o.n_alloc > 0) ok = bd_whole && bd_sum == bd->need;
         if (!ok) {
             o.feasible = false;
             o.n_alloc = 0;
@@ -959,17 +969,8 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
     if (o.n_alloc > 0) {
         // calculateAllocatableAndRequested (scoring.go:118-164) over the allocated zones; with a cpuset the
         // requested cpu is the node's amplified cpuset CPUs
-        int64_t tot[2] = {0, 0}, used[2] = {0, 0};
-        for (int j = 0; j < o.n_alloc; j++) {
-            const int zi = o.zone[j];
-            for (int r = 0; r < 2; r++) {
-                tot[r] += kg_zone_total(row, zi, r);
-                const int64_t u = kg_zone_alloc(row, zi, r);
-                used[r] += u > 0 ? u : 0;
-            }
-        }
-        if (bd) used[KG_RES_CPU] = row.cpuset_amp_milli;
-        o.score = kg_numa_score_zones(c, c.numa_most != 0, used, tot, p, pcpu);
+        if (bd) z_used[KG_RES_CPU] = row.cpuset_amp_milli;
+        o.score = kg_numa_score_zones(c, c.numa_most != 0, z_used, z_tot, p, pcpu);
     } else if (bd) {
         int64_t rq[KG_NUM_RES];
         for (int r = 0; r < KG_NUM_RES; r++) rq[r] = requested[r];
@@ -1009,6 +1010,20 @@ void kg_numa_pair_bz(const kg_consts &c, const kg_node_row &row, const kg_pod_de
 KG_HD void kg_numa_pair_any(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o) {
     if (c.numa_bz) kg_numa_pair_bz(c, row, p, o);
     else kg_numa_pair(c, row, p, o);
+}
+
+// Filter + Score only (no allocation record), by value: feasible << 32 | score (the chunk and resolve kernels'
+// per-pair calls, out of line like kg_numa_pair)
+#if defined(__HIPCC__)
+static __host__ __device__ __noinline__
+#else
+inline
+#endif
+uint64_t kg_numa_eval_any(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p) {
+    kg_numa_out o;
+    if (c.numa_bz) kg_numa_pair_z<kg_zone_calc, true, false>(c, row, p, o, kg_zone_calc{row});
+    else kg_numa_pair_z<kg_zone_calc, false, false>(c, row, p, o, kg_zone_calc{row});
+    return ((uint64_t)(o.feasible ? 1u : 0u) << 32) | o.score;
 }
 
 // Reserve's cpuset decision for a pair (plugin.go:375-404): requestCPUBind (util.go:105-122) and

@@ -1341,6 +1341,7 @@ __global__ __launch_bounds__(256) void k_numa_bind_fix(kg_consts c, kg_planes pl
 // store, the per-(pod, tile) key as a lane-private max (one atomicMax per wave).
 #define KG_NUMA2_NODES 256
 #define KG_NUMA2_SEG 32   // nodes per work item of the queued form (whole 32-bit halves of the mask words)
+#define KG_NUMA2_SEG_TOPK 8   // ... of a placement chunk (keys only: no mask or score planes)
 #ifndef KG_NUMA2_WPE
 #define KG_NUMA2_WPE 3   // waves per SIMD the register budget is sized for (measurement builds vary it)
 #endif
@@ -1408,7 +1409,7 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
                 o.score = zt.succ[lane & 63] + (uint32_t)pd.numa_req[0];
             } else
 #endif
-            kg_numa_pair_z<kg_zone_tab, false>(c, row, pd, o, kg_zone_tab{zt});
+            kg_numa_pair_z<kg_zone_tab, false, false>(c, row, pd, o, kg_zone_tab{zt});
             ok = ok && o.feasible;
             nsc = o.score;
         }
@@ -1468,7 +1469,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WP
                                                     unsigned long long *__restrict__ mask,
                                                     uint16_t *__restrict__ scores, uint8_t *__restrict__ numa_scores,
                                                     uint32_t *__restrict__ partials, const int32_t *__restrict__ perm,
-                                                    BatchMasks bm, int32_t *queue, int32_t n_items) {
+                                                    BatchMasks bm, int32_t *queue, int32_t n_items, int32_t seg) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // per-wave zone table of the current node (every index mask's sums and id mask, prefix sums of
@@ -1493,9 +1494,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WP
             if (item >= n_items) break;
             pb = item % n_pb;
             const int run = item / n_pb;   // 32-node run of the launch's node range, from tile_begin · KG_TILE
-            tile = (int64_t)a.tile_begin + run / (KG_TILE / KG_NUMA2_SEG);
-            base = (int64_t)a.tile_begin * KG_TILE + (int64_t)run * KG_NUMA2_SEG;
-            npw = KG_NUMA2_SEG;
+            tile = (int64_t)a.tile_begin + run / (KG_TILE / seg);
+            base = (int64_t)a.tile_begin * KG_TILE + (int64_t)run * seg;
+            npw = seg;
         }
         const int slot = pb * 64 + lane;
         const bool live = slot < a.n_pods;
@@ -1536,10 +1537,9 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
     uint32_t fit, la, numa = 0;
     if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
     if (c.plugins & KG_PLUGIN_NUMA) {
-        kg_numa_out o;
-        kg_numa_pair_any(c, pl.rows[node], p, o);
-        if (!o.feasible) return 0ull;
-        numa = o.score;
+        const uint64_t ns = kg_numa_eval_any(c, pl.rows[node], p);
+        if (!(ns >> 32)) return 0ull;
+        numa = (uint32_t)ns;
     }
     return ((unsigned long long)(total_of(c, fit, la, numa) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
 }
@@ -1579,10 +1579,9 @@ __global__ __launch_bounds__(256) void k_eval_numa_chunk(kg_consts c, kg_planes 
         uint32_t key = 0;
         uint32_t fit, la;
         if (in_range && eval_pair(c, pl, lp, nr, node, a.now_ns, fit, la)) {
-            kg_numa_out o;
-            kg_numa_pair_any(c, pl.rows[node], lp, o);
-            if (o.feasible)
-                key = ((total_of(c, fit, la, o.score) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local);
+            const uint64_t ns = kg_numa_eval_any(c, pl.rows[node], lp);
+            if (ns >> 32)
+                key = ((total_of(c, fit, la, (uint32_t)ns) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local);
         }
         kbuf[local] = key;
     }
@@ -1811,10 +1810,9 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
     uint32_t fit, la, numa = 0;
     if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
     if (c.plugins & KG_PLUGIN_NUMA) {
-        kg_numa_out o;
-        kg_numa_pair_any(c, crow, p, o);   // the LDS copy of the canonical row
-        if (!o.feasible) return 0ull;
-        numa = o.score;
+        const uint64_t ns = kg_numa_eval_any(c, crow, p);   // the LDS copy of the canonical row
+        if (!(ns >> 32)) return 0ull;
+        numa = (uint32_t)ns;
     }
     return ((unsigned long long)(total_of(c, fit, la, numa) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
 }
@@ -2183,6 +2181,8 @@ struct kg_engine {
                                     // measurement), 2 queued for every launch (KG_NUMA_QUEUE=2, tests)
     int64_t numa_resident_wgs = 0;  // resident k_eval_numa2 workgroups of the device (queried at first use)
     int32_t *numa_queue = nullptr;  // its work-item counter
+    int32_t numa_chunk_pods = KG_NUMA_CHUNK_PODS;   // placement chunks up to this many pods take k_eval_numa_chunk
+                                                    // (KG_NUMA_CHUNK_PODS=0: k_eval_numa2 for every chunk, measurement)
     bool la_prod = false;           // some pod of the batch scores with the prod-usage variant
     bool pow2 = true;               // every Fit / LoadAware weight sum of the batch is a power of two
     // class-specialised matrix mode (k_eval3): built from the batch in kg_pods_set, laid out for
@@ -2601,7 +2601,7 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     a.fit_cap = e->consts.fit_most ? 100u : 0xFFFFFFFFu;
     for (int s = 0; s < 8; s++) a.slot_res[s] = s < e->nslot ? e->slot_res[s] : -1;
     a.now_ns = now_ns;
-    if ((e->consts.plugins & KG_PLUGIN_NUMA) && topk && n <= KG_NUMA_CHUNK_PODS) {
+    if ((e->consts.plugins & KG_PLUGIN_NUMA) && topk && n <= e->numa_chunk_pods) {
         if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
         const unsigned blocks = (unsigned)((shard_tiles + KG_XCDS - 1) / KG_XCDS * KG_XCDS * n);
         hipLaunchKernelGGL(k_eval_numa_chunk, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
@@ -2617,7 +2617,9 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
         if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
         {  // pod per lane; queued 32-node items when they fill every resident wave slot several times over,
            // else a grid where a single pod block splits each wave's node run 4 ways
-            const int64_t n_items = shard_tiles * (KG_TILE / KG_NUMA2_SEG) * ((n + 63) / 64);
+            // segment: 32 nodes (half mask words); 8 for a placement chunk's keys-only launch
+            const int32_t seg = mask == nullptr && scores == nullptr && numa_scores == nullptr ? KG_NUMA2_SEG_TOPK : KG_NUMA2_SEG;
+            const int64_t n_items = shard_tiles * (KG_TILE / seg) * ((n + 63) / 64);
             const int32_t *perm = e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr;
             const BatchMasks bm = e->numa_bm_all ? BatchMasks{0xFFu, 0xFFu} : e->bm;
             if (e->numa_resident_wgs == 0) {
@@ -2627,18 +2629,19 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
                 e->numa_resident_wgs = (int64_t)dev_cus * (per_cu > 0 ? per_cu : 1);
                 HIP_TRY(e, hipMalloc(&e->numa_queue, sizeof(int32_t)));
             }
-            const bool queued = e->numa_queue_mode == 2 || (e->numa_queue_mode == 1 && n_items >= 4 * 4 * e->numa_resident_wgs);
+            const bool queued = e->numa_queue_mode == 2 ||
+                                (e->numa_queue_mode == 1 && (topk || n_items >= 4 * 4 * e->numa_resident_wgs));
             if (queued && n_items < INT32_MAX) {
                 HIP_TRY(e, hipMemsetAsync(e->numa_queue, 0, sizeof(int32_t), e->stream));
                 const int64_t wgs = std::min<int64_t>(e->numa_resident_wgs, (n_items + 3) / 4);
                 hipLaunchKernelGGL(k_eval_numa2, dim3((unsigned)wgs), dim3(256), 0, e->stream, e->consts, e->pl, a,
                                    e->pods + pod_begin, e->pl.rows, (unsigned long long *)mask, scores, numa_scores,
-                                   partials, perm, bm, e->numa_queue, (int32_t)n_items);
+                                   partials, perm, bm, e->numa_queue, (int32_t)n_items, seg);
             } else {
                 dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), n <= 64 ? 4u : 1u);
                 hipLaunchKernelGGL(k_eval_numa2, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
                                    e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials, perm, bm,
-                                   (int32_t *)nullptr, 0);
+                                   (int32_t *)nullptr, 0, 0);
             }
         }
         HIP_TRY(e, hipGetLastError());
@@ -2809,6 +2812,8 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
     if (tb && atoll(tb) > 0) e->cls_target_blocks = atoll(tb);
     const char *bma = getenv("KG_NUMA_BM_ALL");
     e->numa_bm_all = bma && atoi(bma) != 0;
+    const char *ncp = getenv("KG_NUMA_CHUNK_PODS");
+    if (ncp) e->numa_chunk_pods = std::min(atoi(ncp), KG_NUMA_CHUNK_PODS);
     const char *nq = getenv("KG_NUMA_QUEUE");
     e->numa_queue_mode = nq ? atoi(nq) : 1;
     const char *pp = getenv("KG_PLACE_PIPELINE");
@@ -3236,7 +3241,7 @@ kg_status chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n,
     // the top-k kernel writes every slot of every tile of its shard; the NUMA kernel merges with atomics
     // and a shard leaves the other ranks' tiles to the merge: those start from zeros
     const bool whole = e->shard_begin == 0 && e->shard_end == e->n_nodes;
-    if (((e->consts.plugins & KG_PLUGIN_NUMA) && n > KG_NUMA_CHUNK_PODS) || !whole)
+    if (((e->consts.plugins & KG_PLUGIN_NUMA) && n > e->numa_chunk_pods) || !whole)
         HIP_TRY(e, hipMemsetAsync(partial_dev, 0, (size_t)n * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS, e->stream));
     kg_status st = launch_eval(e, now_ns, pod_begin, n, nullptr, nullptr, partial_dev, false, nullptr, true);
     if (st) return st;
@@ -3267,7 +3272,7 @@ kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t
     const bool numa = (e->consts.plugins & KG_PLUGIN_NUMA) != 0;
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream, e->consts, e->pl, e->pods, pod_begin, n,
                        partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev, ra,
-                       numa && n > KG_NUMA_CHUNK_PODS ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count,
+                       numa && n > e->numa_chunk_pods ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count,
                        numa ? 0 : 1,   // the NUMA chunk kernels list slow nodes themselves (exact pair path)
                        defer_last ? 1 : 0, prev_nodes_dev, n_prev);
     HIP_TRY(e, hipGetLastError());

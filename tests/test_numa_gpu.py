@@ -121,8 +121,10 @@ def test_kat_amplified_filter(case):
     assert bool(engine.unpack_mask(res["mask"], 1)[0, 0]) == case["want"]
 
 
-@pytest.mark.parametrize("chunk", [1, 16, 64])
-def test_placement_numa_matches_sequential_cycle(chunk):
+@pytest.mark.parametrize("chunk,numa2", [(1, False), (16, False), (64, False), (1, True), (16, True)])
+def test_placement_numa_matches_sequential_cycle(monkeypatch, chunk, numa2):
+    if numa2:   # every chunk through k_eval_numa2's queued form (one key per tile) instead of k_eval_numa_chunk
+        monkeypatch.setenv("KG_NUMA_CHUNK_PODS", "0")
     cl = make_numa_edge_cluster(700, 200, seed=21)
     cfg = numa_config(weight_numa=2, place_chunk=chunk)
     idx = np.arange(200)
