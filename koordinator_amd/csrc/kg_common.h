@@ -580,16 +580,23 @@ KG_HD void kg_zone_tab_fill(const kg_node_row &row, int lane, int nlanes, kg_zon
     }
     for (int m = lane; m < (1 << Z); m += nlanes) d.succ[m] = (uint8_t)kg_combo_next((uint32_t)m, Z);
     for (int r = lane; r < 2; r += nlanes) {
-        int64_t t[KG_MAX_ZONES];
-        for (int i = 0; i < Z; i++) t[i] = kg_zone_total(row, i, r);
+        // kg_zone_calc::min_k's picks (the first largest remaining total each time), remaining zones as a bit
+        // set instead of an array written at a run-time index
+        uint32_t left = (1u << Z) - 1u;
         int64_t acc = 0;
         d.pref[r][0] = 0;
         for (int k = 1; k <= Z; k++) {
+            int64_t bt = -1;
             int best_i = 0;
-            for (int i = 1; i < Z; i++)
-                if (t[i] > t[best_i]) best_i = i;
-            acc += t[best_i];
-            t[best_i] = -1;
+            for (int i = 0; i < Z; i++) {
+                const int64_t t = kg_zone_total(row, i, r);
+                if (((left >> i) & 1u) && t > bt) {
+                    bt = t;
+                    best_i = i;
+                }
+            }
+            left &= ~(1u << best_i);
+            acc += bt;
             d.pref[r][k] = acc;
         }
     }
@@ -830,7 +837,10 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
             o.feasible = false;
             return;
         }
-        L[nl++] = l;
+        // constant indices only: the two lists stay in registers
+        if (nl == 0) L[0] = l;
+        else L[1] = l;
+        nl++;
     }
     const bool single = policy == KG_NUMA_SINGLE_NUMA_NODE;
     const uint64_t dflt = zs.idmask(full);
@@ -838,9 +848,9 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
     if (nl == 0) {
         best = kg_numa_best{dflt, true, 0u};   // no provider hints: any affinity, preferred
     } else {
-        bool can_pref = true;
-        for (int i = 0; i < nl; i++)
-            if (!L[i].any || (single && L[i].k != 1)) can_pref = false;
+        static_assert(KG_NUMA_MAX_LISTS == 2, "the enumeration below is written for two lists");
+        bool can_pref = L[0].any && !(single && L[0].k != 1);
+        if (nl > 1 && (!L[1].any || (single && L[1].k != 1))) can_pref = false;
         if (can_pref) {
             for (uint32_t a = (1u << L[0].k) - 1u; a; a = zs.next(a, Z)) {
                 if (!kg_list_fits(zs, L[0], a)) continue;

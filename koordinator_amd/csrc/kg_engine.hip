@@ -1501,7 +1501,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WP
         const int slot = pb * 64 + lane;
         const bool live = slot < a.n_pods;
         const int p = live && perm ? perm[slot] : slot;   // the pod row this lane evaluates and writes
+#ifdef KG_NUMA2_PD_REF   // measurement builds: the pod's fields read from memory where used
+        const kg_pod_dev &pd = pods[live ? p : 0];
+#else
         const kg_pod_dev pd = pods[live ? p : 0];
+#endif
         numa2_run(c, pl, a, pd, p, live, tile, base, npw, rows, mask, scores, numa_scores, partials, bm, ztab[wave],
                   lrow_s[wave]);
     }
