@@ -380,7 +380,7 @@ struct kg_numa_out {
     int64_t alloc[KG_MAX_ZONES][2];   // allocated cpu, memory
 };
 
-// n / d (Go int64 division) for the score quotients: when 0 ≤ n < 128·d and d < 2^40 the quotient
+// n / d (Go int64 division) for the score quotients: when 0 ≤ n < 128·d and d < 2^46 (device; 2^40 host) the quotient
 // is < 128; on the device one correctly rounded fp64 division gives it (below), on the host one fp32
 // estimate (relative error < 2^-21, absolute < 2^-14) is off by at most one and a single exact int64
 // multiply-compare settles it; every other operand takes the division
@@ -393,11 +393,15 @@ KG_HD int64_t kg_div_slow(int64_t n, int64_t d) { return n / d; }
 #endif
 
 KG_HD int64_t kg_qdiv(int64_t n, int64_t d) {
-    if (n < 0 || d <= 0 || d >= (1LL << 40) || n >= (d << 7)) return kg_div_slow(n, d);
 #if !defined(KG_QDIV_F32) && defined(__HIP_DEVICE_COMPILE__)
-    // n < 2^47 and d < 2^40 convert to double exactly; the quotient (< 128) has an ulp ≤ 2^-46 while a
-    // non-integer n / d lies ≥ 1 / d > 2^-40 below the next integer, so the correctly rounded division
-    // never reaches it and truncation gives the floor
+    if (n < 0 || d <= 0 || d >= (1LL << 46) || n >= (d << 7)) return kg_div_slow(n, d);
+#else
+    if (n < 0 || d <= 0 || d >= (1LL << 40) || n >= (d << 7)) return kg_div_slow(n, d);
+#endif
+#if !defined(KG_QDIV_F32) && defined(__HIP_DEVICE_COMPILE__)
+    // n < 2^53 and d < 2^46 convert to double exactly; the quotient (< 128) has an ulp ≤ 2^-46, so the
+    // correctly rounded division is within 2^-47 of n / d, while a non-integer n / d lies ≥ 1 / d > 2^-46
+    // below the next integer: the rounded value never reaches it and truncation gives the floor
     return (int64_t)((double)n / (double)d);
 #endif
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -81,6 +81,20 @@ def test_matrix_numa_shard():
     _check_matrix3(numa_config(), cl, 40, begin=1024, end=2500)
 
 
+def test_matrix_numa_huge_zone_memory():
+    # zone memory totals of 2^42..2^48 bytes: the device's score quotients take one fp64 division up to a
+    # divisor of 2^46 and the exact int64 division beyond (kg_qdiv), both against the oracle's int64 quotients
+    cl = make_numa_edge_cluster(2_100, 64, seed=41)
+    numa = cl.numa_arr
+    for j in range(len(cl.nodes)):
+        f = (1, 64, 1024)[j % 3]
+        for z in range(int(numa["n_zones"][j])):
+            numa["zone_total"][j, z]["v"][nat.RES_MEMORY] *= f
+            numa["zone_allocated"][j, z]["v"][nat.RES_MEMORY] *= f
+    assert (numa["zone_total"]["v"][:, :, nat.RES_MEMORY].astype(np.float64) >= 2.0 ** 46).any()
+    _check_matrix3(numa_config(), cl, 64)
+
+
 @pytest.mark.parametrize("pods,begin,end", [(40, 0, None), (333, 0, None), (97, 1024, 2500)])
 def test_matrix_numa_queued_form(monkeypatch, pods, begin, end):
     # KG_NUMA_QUEUE=2: k_eval_numa2's queued form (32-node work items from a device counter, half mask
