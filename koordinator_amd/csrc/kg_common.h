@@ -538,6 +538,7 @@ struct kg_zone_tab_data {
     uint64_t idm[KG_ZTAB_MASKS];
     uint8_t succ[KG_ZTAB_MASKS];         // kg_combo_next(m, n_zones)
     int64_t pref[2][KG_MAX_ZONES + 1];   // pref[r][k]: the acc of kg_zone_calc::min_k after k picks
+    int64_t srt[2][KG_MAX_ZONES];        // the zone totals of resource r in descending order (fill scratch)
 };
 
 struct kg_zone_tab {
@@ -557,52 +558,70 @@ struct kg_zone_tab {
     }
 };
 
-// the table of one node, filled by `nlanes` cooperating lanes (1 on the host): the sums and id masks
-// by subset recurrence over the highest zone, table[2^b | x] = table[x] + zone b for x < 2^b, in the
-// ascending-zone order kg_mask_sums adds them; `sync` orders the rounds (a wave barrier on the device);
-// the combination successors per mask; the prefix sums of the descending totals (cpu, memory)
+// the table of one node, filled by `nlanes` cooperating lanes (1 on the host) in two rounds, `sync` (a wave
+// barrier on the device) between them and after:
+//  1. the sums and id masks of the masks inside one half (zones 0-3: m < 16; zones 4-7: m = h << 4) by
+//     adding their zones; the descending-total order of the zones (rank, the first largest first — the
+//     picks of kg_zone_calc::min_k) and each total at its rank;
+//  2. every other mask as its low half + its high half (int64 sums: the order of the adds is immaterial);
+//     the prefix sums of the ranked totals; the combination successors when `succ` (they depend on Z only:
+//     the caller skips them while consecutive nodes keep the same zone count)
 template <class Sync>
-KG_HD void kg_zone_tab_fill(const kg_node_row &row, int lane, int nlanes, kg_zone_tab_data &d, Sync sync) {
+KG_HD void kg_zone_tab_fill(const kg_node_row &row, int lane, int nlanes, kg_zone_tab_data &d, Sync sync,
+                            bool succ = true) {
+    static_assert(KG_MAX_ZONES == 8, "the table splits masks into two 4-zone halves");
     const int Z = row.n_zones;
-    if (lane == 0) {
-        d.tot[0][0] = d.tot[1][0] = d.av[0][0] = d.av[1][0] = 0;
-        d.idm[0] = 0;
-    }
-    for (int b = 0; b < Z; b++) {
-        sync();
-        const int64_t t0 = kg_zone_total(row, b, 0), t1 = kg_zone_total(row, b, 1);
-        const int64_t a0 = kg_zone_avail(row, b, 0), a1 = kg_zone_avail(row, b, 1);
-        const uint64_t id = 1ull << row.zone_id[b];
-        for (int x = lane; x < (1 << b); x += nlanes) {
-            const int m = (1 << b) | x;
-            d.tot[0][m] = d.tot[0][x] + t0;
-            d.tot[1][m] = d.tot[1][x] + t1;
-            d.av[0][m] = d.av[0][x] + a0;
-            d.av[1][m] = d.av[1][x] + a1;
-            d.idm[m] = d.idm[x] | id;
-        }
-    }
-    for (int m = lane; m < (1 << Z); m += nlanes) d.succ[m] = (uint8_t)kg_combo_next((uint32_t)m, Z);
-    for (int r = lane; r < 2; r += nlanes) {
-        // kg_zone_calc::min_k's picks (the first largest remaining total each time), remaining zones as a bit
-        // set instead of an array written at a run-time index
-        uint32_t left = (1u << Z) - 1u;
-        int64_t acc = 0;
-        d.pref[r][0] = 0;
-        for (int k = 1; k <= Z; k++) {
-            int64_t bt = -1;
-            int best_i = 0;
-            for (int i = 0; i < Z; i++) {
-                const int64_t t = kg_zone_total(row, i, r);
-                if (((left >> i) & 1u) && t > bt) {
-                    bt = t;
-                    best_i = i;
-                }
+    const int n_masks = 1 << Z;
+    for (int x = lane; x < 48; x += nlanes) {
+        if (x < 32) {   // round 1a: half masks (x < 16: m = x; 16 ≤ x < 31: m = (x − 15) << 4)
+            if (x == 31) continue;
+            const uint32_t m = x < 16 ? (uint32_t)x : (uint32_t)(x - 15) << 4;
+            if ((int)m >= n_masks) continue;
+            int64_t t0 = 0, t1 = 0, a0 = 0, a1 = 0;
+            uint64_t id = 0;
+            for (int i = 0; i < KG_MAX_ZONES; i++) {
+                if (!((m >> i) & 1u)) continue;
+                t0 += kg_zone_total(row, i, 0);
+                t1 += kg_zone_total(row, i, 1);
+                a0 += kg_zone_avail(row, i, 0);
+                a1 += kg_zone_avail(row, i, 1);
+                id |= 1ull << row.zone_id[i];
             }
-            left &= ~(1u << best_i);
-            acc += bt;
-            d.pref[r][k] = acc;
+            d.tot[0][m] = t0;
+            d.tot[1][m] = t1;
+            d.av[0][m] = a0;
+            d.av[1][m] = a1;
+            d.idm[m] = id;
+        } else {        // round 1b: the rank of zone i's total of resource r, the total stored at its rank
+            const int r = (x - 32) >> 3, i = (x - 32) & 7;
+            if (i >= Z) continue;
+            const int64_t t = kg_zone_total(row, i, r);
+            int rank = 0;
+            for (int j = 0; j < Z; j++) {
+                const int64_t u = kg_zone_total(row, j, r);
+                rank += (u > t || (u == t && j < i)) ? 1 : 0;
+            }
+            d.srt[r][rank] = t;
         }
+    }
+    sync();
+    for (int m = lane; m < n_masks; m += nlanes) {   // round 2
+        const uint32_t lo = (uint32_t)m & 15u, hi = (uint32_t)m & 0xF0u;
+        if (lo && hi) {
+            d.tot[0][m] = d.tot[0][lo] + d.tot[0][hi];
+            d.tot[1][m] = d.tot[1][lo] + d.tot[1][hi];
+            d.av[0][m] = d.av[0][lo] + d.av[0][hi];
+            d.av[1][m] = d.av[1][lo] + d.av[1][hi];
+            d.idm[m] = d.idm[lo] | d.idm[hi];
+        }
+        if (succ) d.succ[m] = (uint8_t)kg_combo_next((uint32_t)m, Z);
+    }
+    for (int x = lane; x < 2 * (KG_MAX_ZONES + 1); x += nlanes) {
+        const int r = x / (KG_MAX_ZONES + 1), k = x % (KG_MAX_ZONES + 1);
+        if (k > Z) continue;
+        int64_t acc = 0;
+        for (int j = 0; j < k; j++) acc += d.srt[r][j];
+        d.pref[r][k] = acc;
     }
 }
 

@@ -1359,6 +1359,7 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
     uint32_t sacc[4] = {0u, 0u, 0u, 0u};
     uint32_t nacc[4] = {0u, 0u, 0u, 0u};
     constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16);
+    int succ_z = -1;   // the zone count the wave's table holds combination successors for
 #ifdef KG_NUMA2_PREFETCH   // measurement builds: the next node's row in flight in registers (measured slower)
     uint4 row_next = make_uint4(0u, 0u, 0u, 0u);
     if (lane < ROW_U4 && base < a.node_end) row_next = reinterpret_cast<const uint4 *>(rows + base)[lane];
@@ -1398,7 +1399,8 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
                 kg_zone_tab_fill(row, lane, 64, zt, [] {
                     __builtin_amdgcn_wave_barrier();
                     asm volatile("" ::: "memory");
-                });
+                }, row.n_zones != succ_z);
+                succ_z = row.n_zones;
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
             }
