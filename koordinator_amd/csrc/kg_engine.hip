@@ -1559,7 +1559,14 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
 // L2 serves the tile's rows to all of them.
 #define KG_NUMA_CHUNK_PODS 16
 #define KG_XCDS 8
-__global__ __launch_bounds__(256) void k_eval_numa_chunk(kg_consts c, kg_planes pl, HotArgs a,
+// BZ (kg_consts.numa_bz): the launch answers cpusets on NUMA-policy nodes (a call into the cpuset path); the
+// common BZ = false form inlines the whole pair and carries no call, so its register budget is its own
+// (a call would charge it the callee's full-ABI budget: 254 VGPRs + 132 AGPRs, one wave per SIMD)
+#ifndef KG_CHUNK_WPE
+#define KG_CHUNK_WPE 2
+#endif
+template <bool BZ>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_CHUNK_WPE))) void k_eval_numa_chunk(kg_consts c, kg_planes pl, HotArgs a,
                                                          const kg_pod_dev *__restrict__ pods, int32_t shard_tiles,
                                                          uint32_t *__restrict__ partials) {
     __shared__ __attribute__((aligned(16))) kg_pod_dev lp;
@@ -1585,9 +1592,11 @@ __global__ __launch_bounds__(256) void k_eval_numa_chunk(kg_consts c, kg_planes 
         uint32_t key = 0;
         uint32_t fit, la;
         if (in_range && eval_pair(c, pl, lp, nr, node, a.now_ns, fit, la)) {
-            const uint64_t ns = kg_numa_eval_any(c, pl.rows[node], lp);
-            if (ns >> 32)
-                key = ((total_of(c, fit, la, (uint32_t)ns) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local);
+            kg_numa_out o;
+            const kg_node_row &row = pl.rows[node];
+            kg_numa_pair_z<kg_zone_calc, BZ, false>(c, row, lp, o, kg_zone_calc{row});
+            if (o.feasible)
+                key = ((total_of(c, fit, la, o.score) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local);
         }
         kbuf[local] = key;
     }
@@ -2610,8 +2619,12 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     if ((e->consts.plugins & KG_PLUGIN_NUMA) && topk && n <= e->numa_chunk_pods) {
         if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
         const unsigned blocks = (unsigned)((shard_tiles + KG_XCDS - 1) / KG_XCDS * KG_XCDS * n);
-        hipLaunchKernelGGL(k_eval_numa_chunk, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
-                           e->pods + pod_begin, (int32_t)shard_tiles, partials);
+        if (e->consts.numa_bz)
+            hipLaunchKernelGGL(k_eval_numa_chunk<true>, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                               e->pods + pod_begin, (int32_t)shard_tiles, partials);
+        else
+            hipLaunchKernelGGL(k_eval_numa_chunk<false>, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                               e->pods + pod_begin, (int32_t)shard_tiles, partials);
         HIP_TRY(e, hipGetLastError());
         if (e->profiling) {
             HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
