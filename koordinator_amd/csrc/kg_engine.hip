@@ -1563,7 +1563,7 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
 // common BZ = false form inlines the whole pair and carries no call, so its register budget is its own
 // (a call would charge it the callee's full-ABI budget: 254 VGPRs + 132 AGPRs, one wave per SIMD)
 #ifndef KG_CHUNK_WPE
-#define KG_CHUNK_WPE 2
+#define KG_CHUNK_WPE 3   // r03 A/B: 9.5k pods/s at 3, 8.5k at 2 (config-3 placement)
 #endif
 template <bool BZ>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_CHUNK_WPE))) void k_eval_numa_chunk(kg_consts c, kg_planes pl, HotArgs a,
