@@ -707,6 +707,9 @@ __device__ __forceinline__ void write_lanes(uint32_t &w0, uint32_t &w1, uint32_t
 }
 #pragma clang diagnostic pop
 
+#ifndef KG_EVAL3_SROW
+#define KG_EVAL3_SROW 0 // pod rows of the pod loop by scalar loads instead of LDS reads (measurement switch)
+#endif
 #ifndef KG_EVAL3_NT
 #define KG_EVAL3_NT 1   // non-temporal staged score stores of k_eval3 (a write-once stream)
 #endif
@@ -720,7 +723,7 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
                                          const unsigned long long (&okm)[NPL], const char *lrows, int p0, int p1,
                                          uint16_t *__restrict__ scores, uint32_t scol, const bool (&seg)[NPL],
                                          const uint32_t (&kb)[NPL], uint32_t *kbuf, uint32_t (&mb)[2 * NPL],
-                                         uint16_t *sst) {
+                                         uint16_t *sst, const kg_pod_cls_t<NC, NF> *__restrict__ grows) {
     constexpr int BT = KG_TILE / NPL;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -729,8 +732,13 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
     const int np = UNR ? CC : p1 - p0;
     const kg_u16x2 shifts = {(uint16_t)d.fit_shift, (uint16_t)c.la_shift};
     auto pod = [&](const int i) {
+#if KG_EVAL3_SROW
+        // wave-uniform pod row straight from global memory through the scalar cache (s_load into SGPRs)
+        const kg_pod_cls_t<NC, NF> pd = grows[i];
+#else
         const kg_pod_cls_t<NC, NF> pd =
             *reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(lrows + i * (int)sizeof(kg_pod_cls_t<NC, NF>));
+#endif
         unsigned long long m[NPL];
 #pragma unroll
         for (int j = 0; j < NPL; j++) m[j] = cls_ok_mask<NC, NF>(pd, n[j], okm[j]);
@@ -825,6 +833,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     const uint32_t *gsrc = reinterpret_cast<const uint32_t *>(rows_base + d.rows_offset);
     const int64_t last_dw = (int64_t)w.end * (RB / 4) - 1;        // stay inside the class's rows
     uint32_t *lbuf = reinterpret_cast<uint32_t *>(lrows);
+    const kg_pod_cls_t<NC, NF> *grows = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(rows_base + d.rows_offset);
     if (tid < CHUNK_DW) {
         const int64_t src = (int64_t)w.begin * (RB / 4) + tid;
         lbuf[tid] = gsrc[src < last_dw ? src : last_dw];
@@ -850,7 +859,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         for (int j = 0; j < 2 * NPL; j++) mb[j] = 0u;
 #define KG_CLS_PODS(FULL_, UNR_)                                                                                    \
     cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, STAGE, CC, UNR_, NPL>(c, d, n, okm, cur, p0, p1, scores, scol, \
-                                                                               seg, kb, kbuf, mb, sst)
+                                                                               seg, kb, kbuf, mb, sst, grows + p0)
         if (full && p1 - p0 == CC) KG_CLS_PODS(true, true);
         else if (full) KG_CLS_PODS(true, false);
         else KG_CLS_PODS(false, false);

@@ -45,6 +45,18 @@ def main(src: str, dst: str) -> None:
         hot = {"name": " + ".join(k["name"].split("(")[0] for k in parts), "calls": calls,
                "avg_ns": sum(k["avg_ns"] for k in parts), "percent": sum(k["percent"] for k in parts),
                "parts": parts}
+    # the kinds run on two streams (KG_CLS_CONCURRENT): their durations overlap, so the pass time is the
+    # wall span from the first kind's start to the last kind's end, taken per pass from the kernel trace
+    trace = os.path.join(src, "trace", "trace_kernel_trace.csv")
+    if hot and os.path.exists(trace):
+        disp = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in _rows(trace) if HOT in r["Kernel_Name"])
+        k = len(parts)
+        spans = [max(e for _, e in disp[i:i + k]) - disp[i][0] for i in range(0, len(disp) - k + 1, k)]
+        if spans:
+            hot["sum_of_kinds_ns"] = hot["avg_ns"]
+            hot["pass_spans_ns"] = spans
+            hot["avg_ns"] = sum(spans) / len(spans)
+            hot["avg_ns_source"] = "mean wall span per pass (first kind start → last kind end) from the kernel trace"
     pmc = {}
     for name in sorted(os.listdir(src)):
         d = os.path.join(src, name)
