@@ -153,6 +153,12 @@ struct kg_cls_desc {
     uint32_t over_mask;    // natives with a zero request on a pod with requests: fail an overcommitted node
     int64_t row_bytes;     // sizeof(kg_pod_cls_t<NC, NF>)
     int64_t rows_offset;   // byte offset of the class's rows in the row buffer
+    // scored resources whose Fit request is the same for every pod of the class (e.g. the NonZero cpu /
+    // memory defaults of batch pods): their least-requested terms depend on the node only and are summed
+    // once per node (ClsNode::cq) instead of per pair; the class's rows carry only the other slots
+    int32_t uni_res[4];    // resource of each uniform slot (−1 pad)
+    uint32_t uni_w[4];     // its Fit weight
+    double uni_pr[4];      // its request, signed like kg_pod_cls_t::pr
 };
 
 // one workgroup row of the launch grid: a pod range of one class

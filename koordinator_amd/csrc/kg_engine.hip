@@ -550,10 +550,11 @@ struct ClsNode {
     double R[NF], F[NF];   // Fit fma operands of the scored resources
     double laR[2], laF[2]; // LoadAware fma operands (the class's usage variant)
     uint32_t w;            // Σ Fit weights of the scored resources the node has
+    uint32_t cq;           // Σ weight · score of the class's uniform slots (kg_cls_desc::uni_res) on this node
     bool ok;               // node-only filters for the class (valid, pods, overcommit, LoadAware thresholds)
 };
 
-template <int NC, int NF, bool FIT_ON, bool LA_ON>
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON>
 __device__ __forceinline__ void load_cls_node(const kg_consts &c, const kg_planes &pl, const kg_cls_desc &d,
                                               int64_t node, int64_t node_end, int64_t now_ns, ClsNode<NC, NF> &n) {
     const int64_t cap = pl.cap;
@@ -574,6 +575,20 @@ __device__ __forceinline__ void load_cls_node(const kg_consts &c, const kg_plane
         n.R[f] = use ? pl.fit_R[r * cap + node] : 0.0;
         n.F[f] = use ? pl.fit_F[r * cap + node] : 0.0;
         if (FIT_ON && r >= 0 && ((nfm >> r) & 1u)) n.w += d.fit_w[f];
+    }
+    n.cq = 0;
+    if (FIT_ON) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int r = d.uni_res[u];   // workgroup-uniform: a scalar branch
+            if (r < 0) continue;
+            const bool use = in_range && !slow;
+            const double R = use ? pl.fit_R[r * cap + node] : 0.0, F = use ? pl.fit_F[r * cap + node] : 0.0;
+            uint32_t q = cvt_u32_sat(__builtin_fma(d.uni_pr[u], R, F));
+            if (MOST) q = q < 100u ? q : 100u;
+            n.cq += d.uni_w[u] * q;
+            if ((nfm >> r) & 1u) n.w += d.uni_w[u];
+        }
     }
     bool expired = false;
 #pragma unroll
@@ -632,7 +647,7 @@ __device__ __forceinline__ void cls_scores(const kg_consts &c, const kg_cls_desc
                                            const ClsNode<NC, NF> &n, uint32_t &fit, uint32_t &la) {
     fit = 0;
     if (FIT_ON) {
-        uint32_t sum = 0;
+        uint32_t sum = n.cq;
 #pragma unroll
         for (int f = 0; f < NF; f++) {
             uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n.R[f], n.F[f]));
@@ -658,7 +673,7 @@ typedef uint16_t kg_u16x2 __attribute__((ext_vector_type(2)));
 template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON>
 __device__ __forceinline__ uint32_t cls_packed(const kg_pod_cls_t<NC, NF> &pd, const ClsNode<NC, NF> &n,
                                                kg_u16x2 shifts) {
-    uint32_t sf = 0;
+    uint32_t sf = FIT_ON ? n.cq : 0u;
     if (FIT_ON) {
 #pragma unroll
         for (int f = 0; f < NF; f++) {
@@ -708,8 +723,13 @@ __device__ __forceinline__ void write_lanes(uint32_t &w0, uint32_t &w1, uint32_t
 #pragma clang diagnostic pop
 
 #ifndef KG_EVAL3_SROW
-#define KG_EVAL3_SROW 0 // pod rows of the pod loop by scalar loads instead of LDS reads (measurement switch)
+#define KG_EVAL3_SROW 1 // pod rows of the pod loop by scalar loads (s_load) instead of LDS reads; 0: LDS (A/B r03a: 0.808 vs 0.818 ms)
 #endif
+#ifndef KG_EVAL3_1BAR
+#define KG_EVAL3_1BAR 0 // one workgroup barrier per chunk: key buffer ×2, row buffer ×3 (measurement switch)
+#endif
+#define KG_EVAL3_NKB (KG_EVAL3_1BAR ? 2 : 1)
+#define KG_EVAL3_NRB (KG_EVAL3_1BAR ? 3 : 2)
 #ifndef KG_EVAL3_NT
 #define KG_EVAL3_NT 1   // non-temporal staged score stores of k_eval3 (a write-once stream)
 #endif
@@ -813,7 +833,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     bool full_l = true;
 #pragma unroll
     for (int j = 0; j < NPL; j++) {
-        load_cls_node<NC, NF, FIT_ON, LA_ON>(c, pl, d, wave_base + 64 * j + lane, a.node_end, a.now_ns, n[j]);
+        load_cls_node<NC, NF, MOST, FIT_ON, LA_ON>(c, pl, d, wave_base + 64 * j + lane, a.node_end, a.now_ns, n[j]);
         okm[j] = __builtin_amdgcn_ballot_w64(n[j].ok);
         full_l = full_l && (n[j].w == (1u << d.fit_shift) || wave_base + 64 * j + lane >= a.node_end);
     }
@@ -844,9 +864,11 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     __syncthreads();
     const int rj = tid / G, rg = tid % G;
     uint16_t *sst = sstage + wave * (CC * SEGW);
-    int buf = 0;
+    int buf = 0, kpar = 0;
     for (int p0 = w.begin; p0 < w.end; p0 += CC) {
         const int p1 = min(p0 + CC, w.end);
+        const int nbuf = buf + 1 == KG_EVAL3_NRB ? 0 : buf + 1;
+        uint32_t *kcur = kbuf + kpar * (CC * BT);
         uint32_t staged = 0;
         const bool more = p1 < w.end;
         if (more && tid < CHUNK_DW) {
@@ -859,7 +881,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         for (int j = 0; j < 2 * NPL; j++) mb[j] = 0u;
 #define KG_CLS_PODS(FULL_, UNR_)                                                                                    \
     cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, STAGE, CC, UNR_, NPL>(c, d, n, okm, cur, p0, p1, scores, scol, \
-                                                                               seg, kb, kbuf, mb, sst, grows + p0)
+                                                                               seg, kb, kcur, mb, sst, grows + p0)
         if (full && p1 - p0 == CC) KG_CLS_PODS(true, true);
         else if (full) KG_CLS_PODS(true, false);
         else KG_CLS_PODS(false, false);
@@ -867,7 +889,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         // the next chunk's rows go to the other LDS buffer before this chunk's global stores are issued:
         // waiting for the row load (vmcnt) after the stores would wait for the stores too (vmcnt counts
         // both), stalling every chunk on the HBM write latency
-        if (more && tid < CHUNK_DW) lbuf[(buf ^ 1) * (CC * RB / 4) + tid] = staged;
+        if (more && tid < CHUNK_DW) lbuf[nbuf * (CC * RB / 4) + tid] = staged;
         if (OUT && STAGE) {
             // LP lanes × 16 B cover one pod's SEGW columns: 64 / LP pods per wave-wide 1 KiB store.  The
             // reads see the other lanes' ds_writes: a wave's LDS operations complete in order.
@@ -903,7 +925,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
                 if (seg[j]) mw[j] = (uint64_t)mb[2 * j] | ((uint64_t)mb[2 * j + 1] << 32);
         }
         lds_barrier();
-        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * BT + rg * CC);
+        const uint4 *src = reinterpret_cast<const uint4 *>(kcur + rj * BT + rg * CC);
         uint32_t mx = 0;
 #pragma unroll
         for (int k = 0; k < CC / 4; k++) {
@@ -922,8 +944,11 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
             const int32_t row = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[rj].row;
             partials[(int64_t)row * a.tiles_total + tile] = mx;
         }
-        lds_barrier();
-        buf ^= 1;
+        // KG_EVAL3_1BAR: the next chunk writes the other key buffer and a third row buffer, and a wave can
+        // only get two chunks ahead of another by passing the barrier the other has not left yet
+        if (!KG_EVAL3_1BAR) lds_barrier();
+        buf = nbuf;
+        kpar = KG_EVAL3_1BAR ? kpar ^ 1 : 0;
     }
 }
 
@@ -935,8 +960,8 @@ __device__ __forceinline__ void k_eval3_body(const kg_consts &c, const kg_planes
                                              const char *__restrict__ rows, uint64_t *__restrict__ mask,
                                              uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
     constexpr int BT = KG_TILE / NPL;
-    __shared__ __attribute__((aligned(16))) uint32_t kbuf[CC * BT];
-    __shared__ __attribute__((aligned(64))) char lrows[2 * CC * 128];
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_EVAL3_NKB * CC * BT];
+    __shared__ __attribute__((aligned(64))) char lrows[KG_EVAL3_NRB * CC * 128];
     __shared__ __attribute__((aligned(16))) uint16_t sstage[STAGE ? (BT / 64) * CC * 64 * NPL : 8];
     const kg_cls_work w = work[blockIdx.y];
     const kg_cls_desc d = descs[w.cls];
@@ -1160,7 +1185,7 @@ __device__ __forceinline__ void mat_block(const kg_consts &c, const kg_planes &p
 #pragma unroll
     for (int j = 0; j < 2; j++) {
         const int64_t node = wave_base + 2 * lane + j;
-        load_cls_node<NC, NF, FIT_ON, LA_ON>(c, pl, d, node, a.node_end, a.now_ns, n[j]);
+        load_cls_node<NC, NF, MOST, FIT_ON, LA_ON>(c, pl, d, node, a.node_end, a.now_ns, n[j]);
         okm[j] = __builtin_amdgcn_ballot_w64(n[j].ok);
         full_l = full_l && (n[j].w == (1u << d.fit_shift) || node >= a.node_end);
     }
@@ -2249,6 +2274,7 @@ struct kg_engine {
     std::vector<uint8_t> pod_may_bind;   // bit 0: binds by its own PreFilter; bit 1: a cpu request (node policy)
     bool profiling = false;
     bool mat_kernel = false;            // matrix mode with planes through k_mat (else k_eval3); KG_MATRIX_KERNEL
+    bool cls_fold_uniform = true;       // class-uniform scored slots folded per node (KG_CLS_FOLD_UNIFORM=0: off)
     int64_t cls_target_blocks = 2048;   // k_eval3 work items per class ≈ this / tiles (KG_CLS_TARGET_BLOCKS)
     // the class kinds' launches on two streams (kinds 1 / 3 on stream2), so one kind's grid tail is filled by
     // the other's workgroups (KG_CLS_CONCURRENT)
@@ -2417,18 +2443,39 @@ void cls_prepare(kg_engine *e) {
         const ClsKey &k = keys[c];
         kg_cls_desc d;
         memset(&d, 0, sizeof(d));
-        const int nc = __builtin_popcount(k.nzc) <= 2 ? 2 : 4, nf = __builtin_popcount(k.fitm) <= 2 ? 2 : 4;
+        // scored resources whose request is one value over the whole class fold into a per-node term when
+        // that leaves at most two per-pod slots (a four-slot class then runs as a two-slot kind)
+        const std::vector<int32_t> &mem = e->cls_members[c];
+        uint32_t unim = 0;
+        for (int r = 0; r < KG_NUM_RES; r++) {
+            if (!((k.fitm >> r) & 1u)) continue;
+            const int64_t v0 = e->pod_rows_h[mem[0]].fit_score_request[r];
+            bool same = true;
+            for (size_t j = 1; j < mem.size() && same; j++) same = e->pod_rows_h[mem[j]].fit_score_request[r] == v0;
+            if (same) unim |= 1u << r;
+        }
+        if (__builtin_popcount(k.fitm) <= 2 || __builtin_popcount(k.fitm & ~unim) > 2 || !e->cls_fold_uniform) unim = 0;
+        const uint32_t varm = k.fitm & ~unim;
+        const int nc = __builtin_popcount(k.nzc) <= 2 ? 2 : 4, nf = __builtin_popcount(varm) <= 2 ? 2 : 4;
         d.kind = (nc == 2 ? 0 : 2) + (nf == 2 ? 0 : 1);
         d.count = (int32_t)e->cls_members[c].size();
-        int a = 0, b = 0;
+        int a = 0, b = 0, u = 0;
         uint32_t w = 0;
-        for (int s = 0; s < 4; s++) d.cmp_res[s] = d.fit_res[s] = -1;
+        const bool most = e->cfg.fit_strategy == KG_STRATEGY_MOST_ALLOCATED;
+        for (int s = 0; s < 4; s++) d.cmp_res[s] = d.fit_res[s] = d.uni_res[s] = -1;
         for (int r = 0; r < KG_NUM_RES; r++) {
             if ((k.nzc >> r) & 1u) d.cmp_res[a++] = r;
-            if ((k.fitm >> r) & 1u) {
+            if ((varm >> r) & 1u) {
                 d.fit_w[b] = (uint32_t)e->cfg.fit_resource_weight[r];
                 w += d.fit_w[b];
                 d.fit_res[b++] = r;
+            }
+            if ((unim >> r) & 1u) {
+                d.uni_w[u] = (uint32_t)e->cfg.fit_resource_weight[r];
+                w += d.uni_w[u];
+                const double pr = (double)e->pod_rows_h[mem[0]].fit_score_request[r];
+                d.uni_pr[u] = most ? pr : -pr;
+                d.uni_res[u++] = r;
             }
         }
         d.fit_shift = w ? (uint32_t)__builtin_ctz(w) : 0u;
@@ -2577,7 +2624,7 @@ void launch_cls3(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint
     bool unit = e->consts.weight_fit == 1 && e->consts.weight_la == 1;
     if (LA_ON) unit = unit && e->consts.la_w[0] == 1 && e->consts.la_w[1] == 1;
     for (const kg_cls_desc &d : e->cls_desc)
-        for (int f = 0; f < 4; f++) unit = unit && d.fit_w[f] <= 1u;
+        for (int f = 0; f < 4; f++) unit = unit && d.fit_w[f] <= 1u && d.uni_w[f] <= 1u;
     if (unit) launch_cls4<MOST, FIT_ON, LA_ON, true>(e, grid, a, mask, scores, partials);
     else launch_cls4<MOST, FIT_ON, LA_ON, false>(e, grid, a, mask, scores, partials);
 }
@@ -2838,6 +2885,8 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
     e->mat_kernel = mk && strcmp(mk, "mat") == 0;
     const char *tb = getenv("KG_CLS_TARGET_BLOCKS");   // measurement switches (tools/ab_cls.sh)
     if (tb && atoll(tb) > 0) e->cls_target_blocks = atoll(tb);
+    const char *fu = getenv("KG_CLS_FOLD_UNIFORM");
+    e->cls_fold_uniform = !(fu && atoi(fu) == 0);
     const char *bma = getenv("KG_NUMA_BM_ALL");
     e->numa_bm_all = bma && atoi(bma) != 0;
     const char *ncp = getenv("KG_NUMA_CHUNK_PODS");

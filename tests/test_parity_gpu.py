@@ -64,6 +64,21 @@ def test_matrix_parity_config1_shape(profile):
     _check_matrix(cfg, cl, np.arange(96), cl.now_ns)
 
 
+@pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("profile", ["least4", "most4", "w2"])
+def test_matrix_parity_uniform_slot_fold(profile, fold, monkeypatch):
+    """Batch pods score cpu / memory at the NonZero defaults (one value for the whole class): the class
+    path folds those slots into a per-node term (kg_cls_desc::uni_res), KG_CLS_FOLD_UNIFORM=0 keeps them
+    per pair; both must equal the oracle under LeastAllocated / MostAllocated and non-unit weights."""
+    monkeypatch.setenv("KG_CLS_FOLD_UNIFORM", fold)
+    four = ("cpu", "memory", "kubernetes.io/batch-cpu", "kubernetes.io/batch-memory")
+    cfg = {"least4": lambda: make_config(fit_resources={r: 1 for r in four}),
+           "most4": lambda: make_config(fit_strategy="MostAllocated", fit_resources={r: 1 for r in four}),
+           "w2": lambda: make_config(fit_resources={r: 2 for r in four})}[profile]()
+    cl = synth.make_cluster(3_000, 160, seed=21)
+    _check_matrix(cfg, cl, np.arange(160), cl.now_ns)
+
+
 @pytest.mark.parametrize("n_nodes", [1, 63, 64, 511, 513, 1500])
 def test_matrix_parity_ragged_node_counts(n_nodes):
     cl = synth.make_cluster(n_nodes, 70, seed=n_nodes)
