@@ -7,6 +7,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _native as nat
+from . import debug
 
 
 class EngineError(RuntimeError):
@@ -226,6 +227,9 @@ class Engine:
             out.rsv_scores = res["rsv_scores"].ctypes.data
         out.out_on_device = 0
         _check(nat.lib().kg_eval(self._h, int(now_ns), ctypes.byref(out)), self, "kg_eval")
+        top_n = debug.debug_top_n()   # --debug-scores (frameworkext/debug.go:32-48)
+        if top_n:
+            debug.dump_eval(self.cfg, res, min(self.n_nodes, self.score_stride), top_n)
         return res
 
     def eval_device(self, now_ns: int, mask_ptr: int = 0, scores_ptr: int = 0, top1_ptr: int = 0,

@@ -215,3 +215,25 @@ def test_snapshot_generation_counts_mutations():
         assert eng.generation() == g0 + 2
         eng.place(cl.now_ns)                                      # 16 pods in 8-pod chunks: 2 resolves
         assert eng.generation() == g0 + 4
+
+
+def test_debug_scores_dump_from_engine(monkeypatch, caplog):
+    """KOORD_GPU_DEBUG_TOPN (frameworkext/debug.go --debug-scores): Engine.eval logs one top-N table per
+    pod; its first row is the pod's top-1 and its totals are the oracle's weighted sums."""
+    import logging
+    monkeypatch.setenv("KOORD_GPU_DEBUG_TOPN", "5")
+    cl = synth.make_cluster(600, 12, seed=5)
+    cfg = shipped_profile()
+    with caplog.at_level(logging.INFO, logger="koordinator_amd.debug"):
+        with _engine_for(cfg, cl, np.arange(12)) as eng:
+            res = eng.eval(cl.now_ns)
+    tables = [r.getMessage() for r in caplog.records if r.name == "koordinator_amd.debug"]
+    assert len(tables) == 12
+    m_ref, fit_ref, la_ref = oracle.eval_matrix(cfg, cl, np.arange(12), cl.now_ns)
+    node, tot = engine.decode_top1(res["top1"])
+    for p, t in enumerate(tables):
+        rows = [ln for ln in t.splitlines() if ln.startswith("| 0 |") or ln.startswith("| 1 |")]
+        cells = rows[0].split(" | ")
+        assert cells[2] == f"node-{node[p]}" and int(cells[3]) == tot[p]
+        total = np.where(m_ref[p], fit_ref[p].astype(int) * int(cfg["weight_fit"]) + la_ref[p].astype(int) * int(cfg["weight_loadaware"]), -1)
+        assert sorted(total[m_ref[p]], reverse=True)[:2] == [int(r.split(" | ")[3]) for r in rows]
