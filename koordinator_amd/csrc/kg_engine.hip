@@ -725,6 +725,9 @@ __device__ __forceinline__ void write_lanes(uint32_t &w0, uint32_t &w1, uint32_t
 #ifndef KG_EVAL3_SROW
 #define KG_EVAL3_SROW 1 // pod rows of the pod loop by scalar loads (s_load) instead of LDS reads; 0: LDS (A/B r03a: 0.808 vs 0.818 ms)
 #endif
+#ifndef KG_EVAL3_WPE0
+#define KG_EVAL3_WPE0 6 // waves per SIMD k_eval3's (2, 2) kind is register-allocated for
+#endif
 #ifndef KG_EVAL3_1BAR
 #define KG_EVAL3_1BAR 0 // one workgroup barrier per chunk: key buffer ×2, row buffer ×3 (measurement switch)
 #endif
@@ -976,7 +979,7 @@ __device__ __forceinline__ void k_eval3_body(const kg_consts &c, const kg_planes
 // One launch per class kind (the work table is grouped by kind): each kernel is register-allocated for
 // its own kind.  NPL nodes per lane: a 1024-node tile is KG_TILE / NPL threads.
 template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE, int KIND, int NPL>
-__global__ __launch_bounds__(KG_TILE / NPL) __attribute__((amdgpu_waves_per_eu(NPL == 4 ? 4 : KIND == 0 ? 6 : KIND == 2 ? 5 : 4))) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
+__global__ __launch_bounds__(KG_TILE / NPL) __attribute__((amdgpu_waves_per_eu(NPL == 4 ? 4 : KIND == 0 ? KG_EVAL3_WPE0 : KIND == 2 ? 5 : 4))) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_cls_desc *__restrict__ descs,
                                                     const kg_cls_work *__restrict__ work,
                                                     const char *__restrict__ rows, uint64_t *__restrict__ mask,
