@@ -1874,6 +1874,17 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
 // One workgroup; per pod: (A) every tile's best untouched candidate and the re-scored touched nodes →
 // block max; (B) Reserve, one thread per part, and the committed node's planes.  The next pod's row
 // and tile keys are prefetched while the current pod is resolved.
+#ifndef KG_RESOLVE_LDSBAR
+#define KG_RESOLVE_LDSBAR 0   // k_resolve's mid-Reserve barriers order LDS only (no wait for the global stores)
+#endif
+__device__ __forceinline__ void resolve_mid_barrier() {
+#if KG_RESOLVE_LDSBAR
+    lds_barrier();
+#else
+    __syncthreads();
+#endif
+}
+
 __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_planes pl,
                                                                 const kg_pod_dev *__restrict__ pods, int32_t pod_begin,
                                                                 int32_t n, const uint32_t *partials, int32_t tiles_total,
@@ -2094,7 +2105,9 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 rsv_commit(pl, ra, pd, node);
                 kg_numa_commit(c, srow, pd);
             }
-            __syncthreads();
+            // the parts below read only srow (LDS); tid 0's global writes are ordered for the next pod by
+            // the full barrier that ends this pod
+            resolve_mid_barrier();
         }
         // the node's slot in the touched list (and node cache): its position, or the next one
         int slot = nt;
@@ -2169,7 +2182,9 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             out_node[j] = node;
             out_score[j] = (int64_t)(w >> 32) - 1;
         }
-        __syncthreads();
+        // the flags step reads the parts' LDS results only: their global stores (row, planes) complete under
+        // the full barrier that ends this pod, before the next pod reads them
+        resolve_mid_barrier();
         if (numa_on && ce && tid >= 128 && tid < 128 + ROW_U4)   // the committed row into the node cache
             reinterpret_cast<uint4 *>(&nrow[slot])[tid - 128] = reinterpret_cast<const uint4 *>(&srow)[tid - 128];
         if (tid == 0) {   // kg_finalize_flags from the parts (metric and the static bits are unchanged)
