@@ -286,6 +286,29 @@ KG_HD bool kg_finalize_la_r(const kg_consts &c, const kg_planes &pl, int64_t i, 
     }
     return slow;
 }
+// one usage variant v (0 non-prod, 1 prod) of kg_finalize_la_r, for the placement resolve's split Reserve (two
+// threads per resource, each one division chain): R is written by v = 0.  When only the other variant is out of
+// the fp64 bounds this variant keeps its plane values, which the fast paths never read: the node is slow.
+KG_HD bool kg_finalize_la_rv(const kg_consts &c, const kg_planes &pl, int64_t i, const kg_node_row &row, int r, int v,
+                             double *R_out, double *F_out) {
+    const int64_t cap = pl.cap;
+    bool slow = c.la_extra != 0;
+    const int64_t a = row.la_alloc[r];
+    double R = 0.0, F = 0.0;
+    if (a != 0) {
+        if (a < 0 || a >= KG_CAP_LIMIT || kg_abs64(row.la_used[v][r]) >= KG_VAL_LIMIT) {
+            slow = true;
+        } else {
+            R = 100.0 / (double)a;
+            F = kg_scaled_ratio(a - row.la_used[v][r], a);
+        }
+    }
+    if (v == 0) pl.la_R[r * cap + i] = R;
+    pl.la_F[(v * 2 + r) * cap + i] = F;
+    *R_out = R;
+    *F_out = F;
+    return slow;
+}
 KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, int r, double *R_out = nullptr,
                           double *F0_out = nullptr, double *F1_out = nullptr) {
     return kg_finalize_la_r(c, pl, i, pl.rows[i], r, R_out, F0_out, F1_out);

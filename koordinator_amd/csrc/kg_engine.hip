@@ -1874,6 +1874,9 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
 // One workgroup; per pod: (A) every tile's best untouched candidate and the re-scored touched nodes →
 // block max; (B) Reserve, one thread per part, and the committed node's planes.  The next pod's row
 // and tile keys are prefetched while the current pod is resolved.
+#ifndef KG_RESOLVE_LA_SPLIT
+#define KG_RESOLVE_LA_SPLIT 0   // k_resolve's LoadAware Reserve part on two threads per resource (one per usage variant)
+#endif
 #ifndef KG_RESOLVE_LDSBAR
 #define KG_RESOLVE_LDSBAR 0   // k_resolve's mid-Reserve barriers order LDS only (no wait for the global stores)
 #endif
@@ -1908,7 +1911,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     // commits nothing ends without a barrier, so the next pod must not overwrite what a slower wave of
     // this pod may still read
     __shared__ int32_t n_touched, n_rescan[2], gate_ok[2];
-    __shared__ uint32_t fin[KG_NUM_RES + 2];
+    __shared__ uint32_t fin[KG_NUM_RES + 4];
     __shared__ int32_t fl_pods_full;
     __shared__ uint32_t fl_over[3];
     __shared__ uint32_t fl_old_df;
@@ -2137,7 +2140,37 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 ce->n.fit_R[r] = R;
                 ce->n.fit_F[r] = F;
             }
-        } else if (tid >= 64 + KG_NUM_RES && tid < 64 + KG_NUM_RES + 2) {
+        } else if (KG_RESOLVE_LA_SPLIT && tid >= 64 + KG_NUM_RES && tid < 64 + KG_NUM_RES + 4) {
+            // LoadAware: two threads per resource, one per usage variant (each one division chain)
+            const int x = tid - 64 - KG_NUM_RES, r = x >> 1, v = x & 1;
+            if (v == 0) {
+                srow.la_used[0][r] += pd.la_est_i[r];
+                row.la_used[0][r] = srow.la_used[0][r];
+                if (r == 0 && c.la_extra) {   // LoadAware weights beyond cpu / memory
+                    for (int q = 0; q < KG_NUM_RES - 2; q++) {
+                        srow.la_used_x[0][q] += pd.la_est_x[q];
+                        row.la_used_x[0][q] = srow.la_used_x[0][q];
+                        if (pd.flags & KG_POD_PROD) {
+                            srow.la_used_x[1][q] += pd.la_est_x[q];
+                            row.la_used_x[1][q] = srow.la_used_x[1][q];
+                        }
+                    }
+                }
+            } else if (pd.flags & KG_POD_PROD) {
+                srow.la_used[1][r] += pd.la_est_i[r];
+                row.la_used[1][r] = srow.la_used[1][r];
+            }
+            double R, F;
+            fin[KG_NUM_RES + x] = kg_finalize_la_rv(c, pl, node, srow, r, v, &R, &F) ? 1u : 0u;
+            if (ce) {
+                if (v == 0) {
+                    ce->n.la_R[r] = R;
+                    ce->n.la_F0[r] = F;
+                } else {
+                    ce->n.la_F1[r] = F;
+                }
+            }
+        } else if (!KG_RESOLVE_LA_SPLIT && tid >= 64 + KG_NUM_RES && tid < 64 + KG_NUM_RES + 2) {
             const int r = tid - 64 - KG_NUM_RES;
             srow.la_used[0][r] += pd.la_est_i[r];
             row.la_used[0][r] = srow.la_used[0][r];
@@ -2190,7 +2223,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         if (tid == 0) {   // kg_finalize_flags from the parts (metric and the static bits are unchanged)
             bool slow = false;
             uint32_t fmask = 0;
-            for (int r = 0; r < KG_NUM_RES + 2; r++) slow = slow || (fin[r] & 1u);
+            for (int r = 0; r < KG_NUM_RES + (KG_RESOLVE_LA_SPLIT ? 4 : 2); r++) slow = slow || (fin[r] & 1u);
             for (int r = 0; r < KG_NUM_RES; r++)
                 if (fin[r] & 2u) fmask |= 1u << r;
             const bool over[3] = {fl_over[0] != 0, fl_over[1] != 0, fl_over[2] != 0};
