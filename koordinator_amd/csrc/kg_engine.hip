@@ -728,6 +728,9 @@ __device__ __forceinline__ void write_lanes(uint32_t &w0, uint32_t &w1, uint32_t
 #ifndef KG_EVAL3_WPE0
 #define KG_EVAL3_WPE0 6 // waves per SIMD k_eval3's (2, 2) kind is register-allocated for
 #endif
+#ifndef KG_EVAL3_MSTORE
+#define KG_EVAL3_MSTORE 0 // feasibility words stored per pod by lane 0 instead of gathered with v_writelane
+#endif
 #ifndef KG_EVAL3_1BAR
 #define KG_EVAL3_1BAR 0 // one workgroup barrier per chunk: key buffer ×2, row buffer ×3 (measurement switch)
 #endif
@@ -746,7 +749,8 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
                                          const unsigned long long (&okm)[NPL], const char *lrows, int p0, int p1,
                                          uint16_t *__restrict__ scores, uint32_t scol, const bool (&seg)[NPL],
                                          const uint32_t (&kb)[NPL], uint32_t *kbuf, uint32_t (&mb)[2 * NPL],
-                                         uint16_t *sst, const kg_pod_cls_t<NC, NF> *__restrict__ grows) {
+                                         uint16_t *sst, const kg_pod_cls_t<NC, NF> *__restrict__ grows,
+                                         uint64_t *__restrict__ mask, int64_t mcol) {
     constexpr int BT = KG_TILE / NPL;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -790,9 +794,19 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
         }
         kbuf[i * BT + tid] = kmax;
         if (OUT) {
+#if KG_EVAL3_MSTORE
+            // lane 0 stores the wave's feasibility words of this pod (the waves of a workgroup fill one line)
+            if (lane == 0 && seg[0]) {
+                uint64_t *mw = mask + pd.mask_off + mcol;
+#pragma unroll
+                for (int j = 0; j < NPL; j++)
+                    if (j == 0 || seg[j]) mw[j] = m[j];
+            }
+#else
 #pragma unroll
             for (int j = 0; j < NPL; j += 2)
                 write_lanes(mb[2 * j], mb[2 * j + 1], mb[2 * j + 2], mb[2 * j + 3], (uint32_t)i, m[j], m[j + 1]);
+#endif
             if (STAGE) {  // the wave's 64·NPL-column score segment of this pod, written out per chunk
 #pragma unroll
                 for (int j = 0; j < NPL; j++) sst[i * (64 * NPL) + 64 * j + lane] = (uint16_t)s[j];
@@ -884,7 +898,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         for (int j = 0; j < 2 * NPL; j++) mb[j] = 0u;
 #define KG_CLS_PODS(FULL_, UNR_)                                                                                    \
     cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, STAGE, CC, UNR_, NPL>(c, d, n, okm, cur, p0, p1, scores, scol, \
-                                                                               seg, kb, kcur, mb, sst, grows + p0)
+                                                                               seg, kb, kcur, mb, sst, grows + p0, mask, col0 >> 6)
         if (full && p1 - p0 == CC) KG_CLS_PODS(true, true);
         else if (full) KG_CLS_PODS(true, false);
         else KG_CLS_PODS(false, false);
@@ -918,7 +932,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
                 }
             }
         }
-        if (OUT && lane < p1 - p0 && seg[0]) {
+        if (OUT && !KG_EVAL3_MSTORE && lane < p1 - p0 && seg[0]) {
             // lane l writes the NPL feasibility words of pod p0 + l
             const kg_pod_cls_t<NC, NF> &pr = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[lane];
             uint64_t *mw = mask + pr.mask_off + (col0 >> 6);
