@@ -159,6 +159,9 @@ struct kg_cls_desc {
     int32_t uni_res[4];    // resource of each uniform slot (−1 pad)
     uint32_t uni_w[4];     // its Fit weight
     double uni_pr[4];      // its request, signed like kg_pod_cls_t::pr
+    // pods [0, la_uni_end) of the class come in whole k_eval3 chunks of one EstimatePod each (cls_order_la)
+    int32_t la_uni_end;
+    int32_t _pad0;
 };
 
 // one workgroup row of the launch grid: a pod range of one class
@@ -284,29 +287,6 @@ KG_HD bool kg_finalize_la_r(const kg_consts &c, const kg_planes &pl, int64_t i, 
         *F0_out = F0;
         *F1_out = F1;
     }
-    return slow;
-}
-// one usage variant v (0 non-prod, 1 prod) of kg_finalize_la_r, for the placement resolve's split Reserve (two
-// threads per resource, each one division chain): R is written by v = 0.  When only the other variant is out of
-// the fp64 bounds this variant keeps its plane values, which the fast paths never read: the node is slow.
-KG_HD bool kg_finalize_la_rv(const kg_consts &c, const kg_planes &pl, int64_t i, const kg_node_row &row, int r, int v,
-                             double *R_out, double *F_out) {
-    const int64_t cap = pl.cap;
-    bool slow = c.la_extra != 0;
-    const int64_t a = row.la_alloc[r];
-    double R = 0.0, F = 0.0;
-    if (a != 0) {
-        if (a < 0 || a >= KG_CAP_LIMIT || kg_abs64(row.la_used[v][r]) >= KG_VAL_LIMIT) {
-            slow = true;
-        } else {
-            R = 100.0 / (double)a;
-            F = kg_scaled_ratio(a - row.la_used[v][r], a);
-        }
-    }
-    if (v == 0) pl.la_R[r * cap + i] = R;
-    pl.la_F[(v * 2 + r) * cap + i] = F;
-    *R_out = R;
-    *F_out = F;
     return slow;
 }
 KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, int r, double *R_out = nullptr,
@@ -688,9 +668,6 @@ KG_HD void kg_numa_fold(kg_numa_best &b, uint64_t m, bool pref, uint32_t score) 
 // score of a hint mask (generateResourceHints: the NUMA scorer over requested = total − available)
 template <class ZS>
 KG_HD uint32_t kg_hint_score(const kg_consts &c, const ZS &zs, const kg_pod_dev &p, uint32_t m, int64_t pod_cpu) {
-#if defined(KG_NUMA_ABLATE) && defined(__HIP_DEVICE_COMPILE__)
-    if (KG_NUMA_ABLATE & 1) return m & 7u;   // measurement builds only (tools/build_variants.sh): no hint score
-#endif
     int64_t tot[2], av[2];
     zs.sums(m, tot, av);
     const int64_t used[2] = {tot[0] - av[0], tot[1] - av[1]};

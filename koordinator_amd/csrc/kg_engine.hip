@@ -37,6 +37,7 @@
 
 #define KG_POD_CHUNK 64          // pods between two LDS partial combines in k_eval
 #define KG_RESOLVE_THREADS 512
+#define KG_CLS_ITEM_MAX 1024        // pods per k_eval3 work item
 #define KG_MAX_CHUNK KG_PLACE_CHUNK_MAX   // max pods per resolve call (touched-list capacity)
 #define KG_MAX_TILES 4096        // max tiles per snapshot in k_resolve (2M nodes)
 
@@ -667,28 +668,32 @@ __device__ __forceinline__ void cls_scores(const kg_consts &c, const kg_cls_desc
 
 typedef uint16_t kg_u16x2 __attribute__((ext_vector_type(2)));
 
-// FULL + UNIT scores of one pair packed as H = fit | la << 16 (u16 halves): the Fit sum and the
-// LoadAware sum << 16 meet in one v_add3 (every term ≤ 100, so each half holds its sum without carry),
-// and one v_pk_lshrrev_b16 applies both plugins' weight-sum shifts (shifts = fit_shift | la_shift << 16)
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON>
-__device__ __forceinline__ uint32_t cls_packed(const kg_pod_cls_t<NC, NF> &pd, const ClsNode<NC, NF> &n,
-                                               kg_u16x2 shifts) {
-    uint32_t sf = FIT_ON ? n.cq : 0u;
+// Packed pair scores (FULL + unit weights): H = fit | la << 16 in u16 halves.  The Fit sum and the
+// LoadAware sum << 16 meet in one v_add3 (every term ≤ 100, so each half holds its sum without carry) and
+// one v_pk_lshrrev_b16 applies both plugins' weight-sum shifts.  `base` is the node's per-node part of the
+// sums: the class's uniform Fit slots (ClsNode::cq) and, in a chunk whose pods share one EstimatePod, the
+// LoadAware sum << 16 (cls_la_sum, evaluated once per node and chunk).
+template <int NC, int NF, bool MOST, bool FIT_ON>
+__device__ __forceinline__ uint32_t cls_fit_sum(const kg_pod_cls_t<NC, NF> &pd, const ClsNode<NC, NF> &n, uint32_t base) {
+    uint32_t s = base;
     if (FIT_ON) {
 #pragma unroll
         for (int f = 0; f < NF; f++) {
             uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n.R[f], n.F[f]));
             if (MOST) q = q < 100u ? q : 100u;
-            sf += q;
+            s += q;
         }
     }
-    uint32_t sl = 0;
-    if (LA_ON) {
-        const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la[0], n.laR[0], n.laF[0]));
-        const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la[1], n.laR[1], n.laF[1]));
-        sl = (q0 + q1) << 16;
-    }
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(kg_u16x2, sf + sl) >> shifts);
+    return s;
+}
+
+// LoadAware least-requested sum (unit weights) of one EstimatePod (la0, la1 = −estimate) on the node, << 16
+template <int NC, int NF, bool LA_ON>
+__device__ __forceinline__ uint32_t cls_la_sum(double la0, double la1, const ClsNode<NC, NF> &n) {
+    if (!LA_ON) return 0u;
+    const uint32_t q0 = cvt_u32_sat(__builtin_fma(la0, n.laR[0], n.laF[0]));
+    const uint32_t q1 = cvt_u32_sat(__builtin_fma(la1, n.laR[1], n.laF[1]));
+    return (q0 + q1) << 16;
 }
 
 // v_cndmask_b32 with a wave lane mask as the condition: v where the lane's bit is set, else 0
@@ -696,6 +701,27 @@ __device__ __forceinline__ uint32_t sel_lanes(unsigned long long m, uint32_t v) 
     uint32_t r;
     asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(m));
     return r;
+}
+
+// max(m0 ? k0 : 0, m1 ? k1 : 0) in two VALU instructions: the v_max runs under EXEC = m1, so lanes outside
+// m1 keep the first value.  EXEC is restored from its copy (lanes outside the incoming EXEC are don't-care).
+__device__ __forceinline__ uint32_t key_max2(unsigned long long m0, unsigned long long m1, uint32_t k0, uint32_t k1) {
+    uint32_t r = sel_lanes(m0, k0);
+    unsigned long long sv;
+    asm("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %2\n\tv_max_u32 %0, %0, %3\n\ts_mov_b64 exec, %1"
+        : "+v"(r), "=&s"(sv)
+        : "s"(m1), "v"(k1));
+    return r;
+}
+
+// lane i of the 64-bit VGPR pairs w0 / w1 := the wave-uniform words b0 / b1 (lanebit = 1 << i): two
+// v_mov_b64 under a one-lane EXEC, the feasibility words of pod i gathered for one coalesced store per chunk
+__device__ __forceinline__ void put_lane2(unsigned long long &w0, unsigned long long &w1, unsigned long long lanebit,
+                                          unsigned long long b0, unsigned long long b1) {
+    unsigned long long sv;
+    asm("s_mov_b64 %2, exec\n\ts_mov_b64 exec, %3\n\tv_mov_b64 %0, %4\n\tv_mov_b64 %1, %5\n\ts_mov_b64 exec, %2"
+        : "+v"(w0), "+v"(w1), "=&s"(sv)
+        : "s"(lanebit), "s"(b0), "s"(b1));
 }
 
 // Workgroup barrier that orders LDS only.  __syncthreads() is also a release of global memory, so it waits
@@ -708,114 +734,63 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// v_writelane_b32 ×4: lane `lane` of mb[0..3] := the wave-uniform words (no exec change; the
-// lane select goes through M0 because a VOP3 may read only one SGPR)
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"   // M0 is otherwise unused by these kernels (checked in the ISA)
-__device__ __forceinline__ void write_lanes(uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3, uint32_t lane,
-                                            unsigned long long b0, unsigned long long b1) {
-    asm("s_mov_b32 m0, %4\n\ts_nop 0\n\tv_writelane_b32 %0, %5, m0\n\tv_writelane_b32 %1, %6, m0\n\t"
-        "v_writelane_b32 %2, %7, m0\n\tv_writelane_b32 %3, %8, m0"
-        : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3)
-        : "s"(lane), "s"((uint32_t)b0), "s"((uint32_t)(b0 >> 32)), "s"((uint32_t)b1), "s"((uint32_t)(b1 >> 32))
-        : "m0");
-}
-#pragma clang diagnostic pop
+#define KG_EVAL3_CC 8    // pods per chunk (LDS key reduction, score staging, LoadAware-uniform chunks: KG_CLS_LA_ALIGN)
+#define KG_EVAL3_WPE0 6  // waves per SIMD k_eval3's (2, 2) kind is register-allocated for (r03 A/B: 5 / 6 / 8)
 
-#ifndef KG_EVAL3_SROW
-#define KG_EVAL3_SROW 1 // pod rows of the pod loop by scalar loads (s_load) instead of LDS reads; 0: LDS (A/B r03a: 0.808 vs 0.818 ms)
-#endif
-#ifndef KG_EVAL3_WPE0
-#define KG_EVAL3_WPE0 6 // waves per SIMD k_eval3's (2, 2) kind is register-allocated for
-#endif
-#ifndef KG_EVAL3_MSTORE
-#define KG_EVAL3_MSTORE 0 // feasibility words stored per pod by lane 0 instead of gathered with v_writelane
-#endif
-#ifndef KG_EVAL3_1BAR
-#define KG_EVAL3_1BAR 0 // one workgroup barrier per chunk: key buffer ×2, row buffer ×3 (measurement switch)
-#endif
-#define KG_EVAL3_NKB (KG_EVAL3_1BAR ? 2 : 1)
-#define KG_EVAL3_NRB (KG_EVAL3_1BAR ? 3 : 2)
-#ifndef KG_EVAL3_NT
-#define KG_EVAL3_NT 1   // non-temporal staged score stores of k_eval3 (a write-once stream)
-#endif
-// Pods [p0, p1) of one class against the lane's NPL nodes (columns 64·j + lane of the wave's segment);
-// rows come from the LDS chunk buffer.  The feasibility ballots of the chunk are collected into lanes
-// (p − p0) of 2·NPL VGPRs and written once per chunk; EDGE workgroups (the shard's last tile) check
-// that a segment lies in the row.
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool STAGE, int CC, bool UNR,
-          int NPL>
-__device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> (&n)[NPL],
-                                         const unsigned long long (&okm)[NPL], const char *lrows, int p0, int p1,
-                                         uint16_t *__restrict__ scores, uint32_t scol, const bool (&seg)[NPL],
-                                         const uint32_t (&kb)[NPL], uint32_t *kbuf, uint32_t (&mb)[2 * NPL],
-                                         uint16_t *sst, const kg_pod_cls_t<NC, NF> *__restrict__ grows,
-                                         uint64_t *__restrict__ mask, int64_t mcol) {
-    constexpr int BT = KG_TILE / NPL;
+// Pods [p0, p0 + np) of one class against the lane's two nodes (columns lane and 64 + lane of the wave's
+// 128-column segment).  Pod rows are wave-uniform scalar loads.  UNR: a whole chunk, unrolled, so every
+// LDS address and lane select is an immediate.  LAU: the chunk's pods share one EstimatePod; its LoadAware
+// sums are already in base[] and only the Fit terms are evaluated per pair.
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool UNR, bool LAU>
+__device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> (&n)[2],
+                                         const unsigned long long (&okm)[2], const uint32_t (&base)[2], int np_rt,
+                                         const uint32_t (&kb)[2], uint32_t *kbuf, unsigned long long (&mb)[2],
+                                         uint16_t *sst, const kg_pod_cls_t<NC, NF> *__restrict__ grows) {
+    constexpr int BT = KG_TILE / 2, CC = KG_EVAL3_CC;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    // UNR: a whole chunk, unrolled, so every LDS address (pod row, key buffer, score staging) and
-    // every write-lane select is an immediate
-    const int np = UNR ? CC : p1 - p0;
+    const int np = UNR ? CC : np_rt;
     const kg_u16x2 shifts = {(uint16_t)d.fit_shift, (uint16_t)c.la_shift};
     auto pod = [&](const int i) {
-#if KG_EVAL3_SROW
-        // wave-uniform pod row straight from global memory through the scalar cache (s_load into SGPRs)
-        const kg_pod_cls_t<NC, NF> pd = grows[i];
-#else
-        const kg_pod_cls_t<NC, NF> pd =
-            *reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(lrows + i * (int)sizeof(kg_pod_cls_t<NC, NF>));
-#endif
-        unsigned long long m[NPL];
+        const kg_pod_cls_t<NC, NF> pd = grows[i];   // s_load into SGPRs
+        unsigned long long m[2];
 #pragma unroll
-        for (int j = 0; j < NPL; j++) m[j] = cls_ok_mask<NC, NF>(pd, n[j], okm[j]);
-        uint32_t kmax = 0, s[NPL];
+        for (int j = 0; j < 2; j++) m[j] = cls_ok_mask<NC, NF>(pd, n[j], okm[j]);
+        uint32_t kmax, s01;
         if (FULL && W1) {
-            // packed pair scores: key = dot2(H, {1024, 1024}) + kb = (fit + la) << 10 + kb in one
-            // v_dot2_u32_u16; the staged u16 is the perm of H's low bytes (fit | la << 8)
+            // key = (fit + la) << 10 + kb in one v_dot2_u32_u16 of H; the staged u16 pair of both nodes is one
+            // v_perm of the two H: {fit0, la0, fit1, la1}
             const kg_u16x2 kw = {(uint16_t)(1u << KG_TILE_SHIFT), (uint16_t)(1u << KG_TILE_SHIFT)};
+            uint32_t h[2], k[2];
 #pragma unroll
-            for (int j = 0; j < NPL; j++) {
-                const uint32_t h = cls_packed<NC, NF, MOST, FIT_ON, LA_ON>(pd, n[j], shifts);
-                const uint32_t k = sel_lanes(m[j], __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h), kw, kb[j], false));
-                kmax = kmax > k ? kmax : k;
-                s[j] = __builtin_amdgcn_perm(h, h, 0x0c0c0200u);
+            for (int j = 0; j < 2; j++) {
+                const uint32_t b = LAU ? base[j] : base[j] + cls_la_sum<NC, NF, LA_ON>(pd.la[0], pd.la[1], n[j]);
+                const uint32_t s = cls_fit_sum<NC, NF, MOST, FIT_ON>(pd, n[j], b);
+                h[j] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(kg_u16x2, s) >> shifts);
+                k[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h[j]), kw, kb[j], false);
             }
+            kmax = key_max2(m[0], m[1], k[0], k[1]);
+            s01 = __builtin_amdgcn_perm(h[1], h[0], 0x06040200u);
         } else {
+            uint32_t s[2];
+            kmax = 0;
 #pragma unroll
-            for (int j = 0; j < NPL; j++) {
-                uint32_t fit, la, tot;
+            for (int j = 0; j < 2; j++) {
+                uint32_t fit, la;
                 cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n[j], fit, la);
-                tot = W1 ? fit + la : __umul24((uint32_t)c.weight_fit, fit) + __umul24((uint32_t)c.weight_la, la);
+                const uint32_t tot = W1 ? fit + la : __umul24((uint32_t)c.weight_fit, fit) + __umul24((uint32_t)c.weight_la, la);
                 const uint32_t k = sel_lanes(m[j], (tot << KG_TILE_SHIFT) + kb[j]);
                 kmax = kmax > k ? kmax : k;
                 s[j] = fit | (la << 8);
             }
+            s01 = s[0] | (s[1] << 16);
         }
         kbuf[i * BT + tid] = kmax;
         if (OUT) {
-#if KG_EVAL3_MSTORE
-            // lane 0 stores the wave's feasibility words of this pod (the waves of a workgroup fill one line)
-            if (lane == 0 && seg[0]) {
-                uint64_t *mw = mask + pd.mask_off + mcol;
-#pragma unroll
-                for (int j = 0; j < NPL; j++)
-                    if (j == 0 || seg[j]) mw[j] = m[j];
-            }
-#else
-#pragma unroll
-            for (int j = 0; j < NPL; j += 2)
-                write_lanes(mb[2 * j], mb[2 * j + 1], mb[2 * j + 2], mb[2 * j + 3], (uint32_t)i, m[j], m[j + 1]);
-#endif
-            if (STAGE) {  // the wave's 64·NPL-column score segment of this pod, written out per chunk
-#pragma unroll
-                for (int j = 0; j < NPL; j++) sst[i * (64 * NPL) + 64 * j + lane] = (uint16_t)s[j];
-            } else {
-                uint16_t *srow = scores + pd.score_off;
-#pragma unroll
-                for (int j = 0; j < NPL; j++)
-                    if (seg[j]) srow[scol + 64 * j] = (uint16_t)s[j];
-            }
+            put_lane2(mb[0], mb[1], 1ull << i, m[0], m[1]);
+            // the wave's 128-column score segment of this pod, written out per chunk
+            sst[i * 128 + lane] = (uint16_t)s01;
+            sst[i * 128 + 64 + lane] = (uint16_t)(s01 >> 16);
         }
     };
     if constexpr (UNR) {
@@ -826,47 +801,50 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
     }
 }
 
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE, int NPL>
+// One workgroup = one 1024-node tile (two nodes per lane, 8 waves) × a pod range of one class, walked in
+// KG_EVAL3_CC-pod chunks: per chunk the pods' keys go to LDS and are reduced to one key per (pod, tile), the
+// scores are staged in LDS and written as wave-wide 16-B-per-lane stores, the feasibility words as one u64
+// pair per pod.
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1>
 __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
                                           const kg_cls_work &w, const char *__restrict__ rows_base,
                                           uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
                                           uint32_t *__restrict__ partials, uint32_t *kbuf, char *lrows,
                                           uint16_t *sstage) {
-    constexpr int BT = KG_TILE / NPL;                     // threads of the workgroup
+    constexpr int CC = KG_EVAL3_CC;
+    constexpr int BT = KG_TILE / 2;                       // threads of the workgroup
     constexpr int RB = (int)sizeof(kg_pod_cls_t<NC, NF>);
     constexpr int CHUNK_DW = CC * RB / 4;                 // dwords of one chunk of rows (≤ BT)
     constexpr int G = BT / CC;                            // threads reducing one pod's keys
-    constexpr int SEGW = 64 * NPL;                        // score columns of one wave
-    static_assert(NPL == 2 || NPL == 4, "two or four nodes per lane");
-    static_assert(G == 32 || G == 64, "key reduction groups are half or whole waves");
+    constexpr int SEGW = 128;                             // score columns of one wave
+    static_assert(G == 64, "key reduction groups are whole waves");
     static_assert(CHUNK_DW <= BT, "one dword per thread stages a chunk");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tile = a.tile_begin + blockIdx.x;
     const int64_t wave_base = (int64_t)tile * KG_TILE + wave * SEGW;
-    ClsNode<NC, NF> n[NPL];
-    unsigned long long okm[NPL];
+    ClsNode<NC, NF> n[2];
+    unsigned long long okm[2];
     bool full_l = true;
 #pragma unroll
-    for (int j = 0; j < NPL; j++) {
+    for (int j = 0; j < 2; j++) {
         load_cls_node<NC, NF, MOST, FIT_ON, LA_ON>(c, pl, d, wave_base + 64 * j + lane, a.node_end, a.now_ns, n[j]);
         okm[j] = __builtin_amdgcn_ballot_w64(n[j].ok);
         full_l = full_l && (n[j].w == (1u << d.fit_shift) || wave_base + 64 * j + lane >= a.node_end);
     }
     const bool full = !FIT_ON || __all(full_l);
     const int64_t col0 = wave_base - a.col_begin;
-    bool seg[NPL];
-    uint32_t kb[NPL];
+    bool seg[2];
+    uint32_t kb[2];
     const uint32_t local0 = (uint32_t)(wave * SEGW + lane);
 #pragma unroll
-    for (int j = 0; j < NPL; j++) {
+    for (int j = 0; j < 2; j++) {
         seg[j] = col0 + 64 * j < a.score_stride;
         kb[j] = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0 - 64u * j;
     }
-    const uint32_t scol = (uint32_t)col0 + (uint32_t)lane;        // score column of n[0]
-    // pod rows are staged chunk by chunk into LDS (double buffer); the next chunk's global load is
-    // in flight while the current chunk is evaluated, so no pod pays a memory round trip
+    // the rows (output offsets) of each chunk are staged in LDS for the stores; the next chunk's global load
+    // is in flight while the current chunk is evaluated
     const uint32_t *gsrc = reinterpret_cast<const uint32_t *>(rows_base + d.rows_offset);
     const int64_t last_dw = (int64_t)w.end * (RB / 4) - 1;        // stay inside the class's rows
     uint32_t *lbuf = reinterpret_cast<uint32_t *>(lrows);
@@ -879,13 +857,11 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     // vector memory (its stores included)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __syncthreads();
-    const int rj = tid / G, rg = tid % G;
+    const int rj = tid / G;
     uint16_t *sst = sstage + wave * (CC * SEGW);
-    int buf = 0, kpar = 0;
+    int buf = 0;
     for (int p0 = w.begin; p0 < w.end; p0 += CC) {
         const int p1 = min(p0 + CC, w.end);
-        const int nbuf = buf + 1 == KG_EVAL3_NRB ? 0 : buf + 1;
-        uint32_t *kcur = kbuf + kpar * (CC * BT);
         uint32_t staged = 0;
         const bool more = p1 < w.end;
         if (more && tid < CHUNK_DW) {
@@ -893,56 +869,59 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
             staged = gsrc[src < last_dw ? src : last_dw];
         }
         const char *cur = lrows + buf * (CC * RB);
-        uint32_t mb[2 * NPL];
+        unsigned long long mb[2] = {0ull, 0ull};
+        // a chunk of one EstimatePod (the host puts whole chunks of equal estimates first, kg_cls_desc::
+        // la_uni_end): its LoadAware sums are per node, evaluated here once for the chunk's pods
+        const bool lau = LA_ON && W1 && full && p0 + CC <= d.la_uni_end;
+        uint32_t base[2];
+        if (lau) {
+            const double la0 = grows[p0].la[0], la1 = grows[p0].la[1];
 #pragma unroll
-        for (int j = 0; j < 2 * NPL; j++) mb[j] = 0u;
-#define KG_CLS_PODS(FULL_, UNR_)                                                                                    \
-    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, STAGE, CC, UNR_, NPL>(c, d, n, okm, cur, p0, p1, scores, scol, \
-                                                                               seg, kb, kcur, mb, sst, grows + p0, mask, col0 >> 6)
-        if (full && p1 - p0 == CC) KG_CLS_PODS(true, true);
-        else if (full) KG_CLS_PODS(true, false);
-        else KG_CLS_PODS(false, false);
+            for (int j = 0; j < 2; j++) base[j] = n[j].cq + cls_la_sum<NC, NF, LA_ON>(la0, la1, n[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 2; j++) base[j] = n[j].cq;
+        }
+#define KG_CLS_PODS(FULL_, UNR_, LAU_)                                                                        \
+    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, UNR_, LAU_>(c, d, n, okm, base, p1 - p0, kb, kbuf, mb, sst, \
+                                                                      grows + p0)
+        if (lau) KG_CLS_PODS(true, true, true);
+        else if (full && p1 - p0 == CC) KG_CLS_PODS(true, true, false);
+        else if (full) KG_CLS_PODS(true, false, false);
+        else KG_CLS_PODS(false, false, false);
 #undef KG_CLS_PODS
         // the next chunk's rows go to the other LDS buffer before this chunk's global stores are issued:
         // waiting for the row load (vmcnt) after the stores would wait for the stores too (vmcnt counts
         // both), stalling every chunk on the HBM write latency
-        if (more && tid < CHUNK_DW) lbuf[nbuf * (CC * RB / 4) + tid] = staged;
-        if (OUT && STAGE) {
-            // LP lanes × 16 B cover one pod's SEGW columns: 64 / LP pods per wave-wide 1 KiB store.  The
-            // reads see the other lanes' ds_writes: a wave's LDS operations complete in order.
+        if (more && tid < CHUNK_DW) lbuf[(buf ^ 1) * (CC * RB / 4) + tid] = staged;
+        if (OUT) {
+            // 16 lanes × 16 B cover one pod's 128 columns: 4 pods per wave-wide 1 KiB store.  The reads see
+            // the other lanes' ds_writes: a wave's LDS operations complete in order.
             constexpr int LP = SEGW / 8, PPS = 64 / LP;
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
-            const int np = p1 - p0, s8 = lane % LP, sj = s8 / 8;
-            bool segs = seg[0];
+            const int np = p1 - p0, s8 = lane % LP;
+            const bool segs = s8 < 8 ? seg[0] : seg[1];
 #pragma unroll
-            for (int j = 1; j < NPL; j++)
-                if (sj == j) segs = seg[j];
-            for (int it = 0; it * PPS < np; it++) {
+            for (int it = 0; it < CC / PPS; it++) {
                 const int pp = it * PPS + lane / LP;
                 if (pp < np && segs) {
                     const uint4 v = *reinterpret_cast<const uint4 *>(sst + pp * SEGW + s8 * 8);
                     const int64_t off = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[pp].score_off;
-#if KG_EVAL3_NT
                     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
                     __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(scores + off + col0 + s8 * 8));
-#else
-                    *reinterpret_cast<uint4 *>(scores + off + col0 + s8 * 8) = v;
-#endif
                 }
             }
-        }
-        if (OUT && !KG_EVAL3_MSTORE && lane < p1 - p0 && seg[0]) {
-            // lane l writes the NPL feasibility words of pod p0 + l
-            const kg_pod_cls_t<NC, NF> &pr = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[lane];
-            uint64_t *mw = mask + pr.mask_off + (col0 >> 6);
-            mw[0] = (uint64_t)mb[0] | ((uint64_t)mb[1] << 32);
-#pragma unroll
-            for (int j = 1; j < NPL; j++)
-                if (seg[j]) mw[j] = (uint64_t)mb[2 * j] | ((uint64_t)mb[2 * j + 1] << 32);
+            if (lane < np && seg[0]) {
+                // lane l writes the two feasibility words of pod p0 + l
+                const kg_pod_cls_t<NC, NF> &pr = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[lane];
+                uint64_t *mw = mask + pr.mask_off + (col0 >> 6);
+                mw[0] = mb[0];
+                if (seg[1]) mw[1] = mb[1];
+            }
         }
         lds_barrier();
-        const uint4 *src = reinterpret_cast<const uint4 *>(kcur + rj * BT + rg * CC);
+        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * BT + lane * CC);
         uint32_t mx = 0;
 #pragma unroll
         for (int k = 0; k < CC / 4; k++) {
@@ -956,332 +935,36 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         mx = dpp_max_step(mx, 2);
         mx = dpp_max_step(mx, 3);
         mx = dpp_max_step(mx, 4);
-        if (G == 64) mx = dpp_max_step(mx, 5);
-        if (rg == G - 1 && rj < p1 - p0) {
+        mx = dpp_max_step(mx, 5);
+        if (lane == 63 && rj < p1 - p0) {
             const int32_t row = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[rj].row;
             partials[(int64_t)row * a.tiles_total + tile] = mx;
         }
-        // KG_EVAL3_1BAR: the next chunk writes the other key buffer and a third row buffer, and a wave can
-        // only get two chunks ahead of another by passing the barrier the other has not left yet
-        if (!KG_EVAL3_1BAR) lds_barrier();
-        buf = nbuf;
-        kpar = KG_EVAL3_1BAR ? kpar ^ 1 : 0;
+        lds_barrier();
+        buf ^= 1;
     }
 }
 
 // One launch per class kind (the work table is grouped by kind): each kernel is register-allocated for
-// its own kind.  NPL nodes per lane: a 1024-node tile is KG_TILE / NPL threads.
-template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE, int KIND, int NPL>
-__device__ __forceinline__ void k_eval3_body(const kg_consts &c, const kg_planes &pl, const HotArgs &a,
-                                             const kg_cls_desc *__restrict__ descs, const kg_cls_work *__restrict__ work,
-                                             const char *__restrict__ rows, uint64_t *__restrict__ mask,
-                                             uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
-    constexpr int BT = KG_TILE / NPL;
-    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_EVAL3_NKB * CC * BT];
-    __shared__ __attribute__((aligned(64))) char lrows[KG_EVAL3_NRB * CC * 128];
-    __shared__ __attribute__((aligned(16))) uint16_t sstage[STAGE ? (BT / 64) * CC * 64 * NPL : 8];
-    const kg_cls_work w = work[blockIdx.y];
-    const kg_cls_desc d = descs[w.cls];
-#define KG_CLS_ARGS c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows, sstage
-    if constexpr (KIND == 0) cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, NPL>(KG_CLS_ARGS);
-    else if constexpr (KIND == 1) cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, NPL>(KG_CLS_ARGS);
-    else if constexpr (KIND == 2) cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, NPL>(KG_CLS_ARGS);
-    else cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, NPL>(KG_CLS_ARGS);
-#undef KG_CLS_ARGS
-}
-
-// One launch per class kind (the work table is grouped by kind): each kernel is register-allocated for
-// its own kind.  NPL nodes per lane: a 1024-node tile is KG_TILE / NPL threads.
-template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int CC, bool STAGE, int KIND, int NPL>
-__global__ __launch_bounds__(KG_TILE / NPL) __attribute__((amdgpu_waves_per_eu(NPL == 4 ? 4 : KIND == 0 ? KG_EVAL3_WPE0 : KIND == 2 ? 5 : 4))) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
+// its own kind.  OUT: the feasibility words and score planes are written (else per-(pod, tile) keys only).
+template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int KIND>
+__global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? KG_EVAL3_WPE0 : KIND == 2 ? 5 : 4))) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_cls_desc *__restrict__ descs,
                                                     const kg_cls_work *__restrict__ work,
                                                     const char *__restrict__ rows, uint64_t *__restrict__ mask,
                                                     uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
-    k_eval3_body<MOST, FIT_ON, LA_ON, OUT, W1, CC, STAGE, KIND, NPL>(c, pl, a, descs, work, rows, mask, scores, partials);
-}
-// ---------------------------------------------------------------------------------------
-// k_mat: matrix mode WITH planes (the bench's hot launch), class-specialised like k_eval3 (same class
-// rows, same work table) but laid out for the store stream instead of the LDS:
-//   * lane l of wave w holds the ADJACENT nodes 2l, 2l+1 of the wave's 128-node segment, so one dword
-//     per lane and pod ({fit, la} of both nodes) is the pod's whole 256-B score segment: the scores go
-//     from registers straight to HBM, one global_store_dword per pod and wave, no LDS staging;
-//   * class rows are staged through LDS 16 pods (a group) at a time: the next group's global load is in
-//     flight while the current group is evaluated and lands in LDS right after the group's score stores
-//     (an in-order vmcnt wait that skips the stores); the group barrier orders LDS only (lds_barrier), so
-//     no wave ever waits for its own score stores to reach HBM;
-//   * feasibility: per pod the two ballots (even nodes, odd nodes) are parked in lane (pod mod 64) of
-//     four VGPRs by v_writelane; every 64 pods (four groups) each lane bit-interleaves its pod's ballots into the two
-//     u64 mask words of the segment and stores them;
-//   * per-(pod, tile) keys: the lane's max of its two keys goes to the wave's own LDS slice; every 16
-//     pods the wave reduces them (a quad of lanes per pod) and ds_max's the result into the workgroup's
-//     per-pod key slots — no workgroup barrier inside the pod loop; the partials are written once per
-//     work item.
-// Grid: x = shard tiles padded to a multiple of the XCD count, so under the round-robin block→XCD
-// dispatch a tile always lands on the same XCD and its node planes are re-read from that XCD's L2 (a
-// placement assumption for speed only; any placement is correct).
-#define KG_MAT_KC 16                       // pods per wave-local key reduction
-#define KG_MAT_ITEM_MAX 1024               // pods per work item (the workgroup's key slots)
-#define KG_MAT_XCDS 8
-#ifndef KG_MAT_NT
-#define KG_MAT_NT 1                        // non-temporal score stores (a write-once stream)
-#endif
-
-// spread the 16 bits of x to the even bit positions of a 32-bit word
-__device__ __forceinline__ uint32_t spread16(uint32_t x) {
-    x &= 0xFFFFu;
-    x = (x | (x << 8)) & 0x00FF00FFu;
-    x = (x | (x << 4)) & 0x0F0F0F0Fu;
-    x = (x | (x << 2)) & 0x33333333u;
-    x = (x | (x << 1)) & 0x55555555u;
-    return x;
-}
-// the 64-bit mask word of 64 consecutive nodes from the even-node and odd-node ballot halves
-__device__ __forceinline__ uint64_t interleave32(uint32_t even, uint32_t odd) {
-    const uint32_t lo = spread16(even) | (spread16(odd) << 1);
-    const uint32_t hi = spread16(even >> 16) | (spread16(odd >> 16) << 1);
-    return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-
-// FAST: every node of the wave has all the class's scored resources (the Fit sum is a shift), unit weights
-// and the wave's whole 128-column segment inside the output rows; otherwise the generic per-node form.
-// FULLG: a whole group of KG_MAT_KC pods (the pod loop unrolled).
-// Pods [g0, g1) of one group (rows in LDS at `lr`, row g0 first), the group's pods at ballot lanes
-// win·16 + t.  The next group's staged row dword is written to LDS right after this group's score stores:
-// the stores were issued after its global load and vector memory completes in issue order, so on the
-// unrolled path the wait is vmcnt(stores of the group) — the load only, never the stores' HBM latency.
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool W1, bool FAST, bool FULLG>
-__device__ __forceinline__ void mat_group(const kg_consts &c, const kg_cls_desc &d, int item0, int g0, int g1,
-                                          const kg_pod_cls_t<NC, NF> *lr, const ClsNode<NC, NF> (&n)[2],
-                                          const unsigned long long (&okm)[2], int64_t col0, bool in_row, uint32_t kb0,
-                                          uint32_t *__restrict__ scores32, uint32_t *kws, uint32_t *wkey,
-                                          uint32_t (&mb)[4], int win, bool stage, uint32_t staged, uint32_t *stage_dst,
-                                          int64_t stride) {
-    using Row = kg_pod_cls_t<NC, NF>;
-    constexpr bool FULL = FAST;
-    const int lane = threadIdx.x & 63;
-    const kg_u16x2 shifts = {(uint16_t)d.fit_shift, (uint16_t)c.la_shift};
-    const kg_u16x2 kw2 = {(uint16_t)(1u << KG_TILE_SHIFT), (uint16_t)(1u << KG_TILE_SHIFT)};
-    // one pod: t = index in the group
-    auto pod = [&](const int t) {
-        const Row pd = lr[t];   // the whole row into registers (broadcast ds_read_b128s), read once
-        unsigned long long m[2];
-        uint32_t k[2], s;
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            m[j] = okm[j];
-#pragma unroll
-            for (int q = 0; q < NC; q++) m[j] &= __builtin_amdgcn_ballot_w64(pd.req[q] <= n[j].fr[q]);
-        }
-#ifdef KG_MAT_ABLATE
-        if (KG_MAT_ABLATE & 16) {   // no evaluation: the stores alone
-            s = pd.req[0] ^ lane;
-            k[0] = k[1] = 0u;
-        } else
-#endif
-        if (FAST && W1) {
-            uint32_t h[2];
-#pragma unroll
-            for (int j = 0; j < 2; j++) {
-                uint32_t sf = 0, sl = 0;
-#ifdef KG_MAT_ABLATE
-                if (KG_MAT_ABLATE & 8) {   // Fit terms only
-                    uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.pr[0], n[j].R[0], n[j].F[0]));
-                    uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.pr[1], n[j].R[1], n[j].F[1]));
-                    sf = q0 + q1;
-                } else
-#endif
-                {
-                    if (FIT_ON) {
-#pragma unroll
-                        for (int f = 0; f < NF; f++) {
-                            uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n[j].R[f], n[j].F[f]));
-                            if (MOST) q = q < 100u ? q : 100u;
-                            sf += q;
-                        }
-                    }
-                    if (LA_ON) {
-                        const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la[0], n[j].laR[0], n[j].laF[0]));
-                        const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la[1], n[j].laR[1], n[j].laF[1]));
-                        sl = (q0 + q1) << 16;
-                    }
-                }
-                // v_dot2_u32_u16 of the packed {fit, la} with the tile weights: the key's total
-                h[j] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(kg_u16x2, sf + sl) >> shifts);
-                k[j] = sel_lanes(m[j], __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h[j]), kw2, kb0 - j, false));
-            }
-            s = __builtin_amdgcn_perm(h[1], h[0], 0x06040200u);   // fit0 | la0 << 8 | fit1 << 16 | la1 << 24
-        } else {
-            uint32_t fit[2], la[2];
-#pragma unroll
-            for (int j = 0; j < 2; j++) {
-                cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n[j], fit[j], la[j]);
-                const uint32_t tot = W1 ? fit[j] + la[j]
-                                        : __umul24((uint32_t)c.weight_fit, fit[j]) + __umul24((uint32_t)c.weight_la, la[j]);
-                k[j] = sel_lanes(m[j], (tot << KG_TILE_SHIFT) + kb0 - j);
-            }
-            s = fit[0] | (la[0] << 8) | (fit[1] << 16) | (la[1] << 24);
-        }
-        // the output row is wave-uniform: one readfirstlane, the row × stride address in SALU, so the
-        // store is saddr + the lane's offset (score_off = row × stride, kg_cls_row)
-        const int64_t orow = __builtin_amdgcn_readfirstlane(pd.row);
-        uint32_t *dst = scores32 + ((orow * stride + col0) >> 1);
-#ifdef KG_MAT_ABLATE   // measurement builds only (tools/ablate_mat.sh): drop parts of the pod body
-        if (KG_MAT_ABLATE & 1) asm volatile("" ::"v"(s)); else
-#endif
-#if KG_MAT_NT
-        if (FAST || in_row) __builtin_nontemporal_store(s, dst + lane);
-#else
-        if (FAST || in_row) dst[lane] = s;
-#endif
-#ifdef KG_MAT_ABLATE
-        if (KG_MAT_ABLATE & 2) asm volatile("" ::"v"(k[0] > k[1] ? k[0] : k[1])); else
-#endif
-        kws[t * 64 + lane] = k[0] > k[1] ? k[0] : k[1];
-#ifdef KG_MAT_ABLATE
-        if (KG_MAT_ABLATE & 4) asm volatile("" ::"s"(m[0]), "s"(m[1])); else
-#endif
-        write_lanes(mb[0], mb[1], mb[2], mb[3], (uint32_t)(win * KG_MAT_KC + t), m[0], m[1]);
-    };
-    if (FULLG) {
-#pragma unroll
-        for (int t = 0; t < KG_MAT_KC; t++) pod(t);
-    } else {
-        for (int t = 0; t < g1 - g0; t++) pod(t);
-    }
-    if (stage) *stage_dst = staged;
-    // the wave's keys of these pods: lane l reduces pod l / 4's quarter (l % 4) of the 64 lane keys;
-    // a wave's LDS operations complete in order, so the reads see this wave's writes
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    const uint4 *src = reinterpret_cast<const uint4 *>(kws + (lane >> 2) * 64 + (lane & 3) * 16);
-    uint32_t mx = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const uint4 v = src[q];
-        const uint32_t a0 = v.x > v.y ? v.x : v.y, a1 = v.z > v.w ? v.z : v.w;
-        const uint32_t a2 = a0 > a1 ? a0 : a1;
-        mx = mx > a2 ? mx : a2;
-    }
-    uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
-    mx = mx > o ? mx : o;
-    o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x4E, 0xf, 0xf, false);            // quad_perm [2,3,0,1]
-    mx = mx > o ? mx : o;
-    if ((lane & 3) == 0 && (lane >> 2) < g1 - g0 && mx) atomicMax(&wkey[g0 - item0 + (lane >> 2)], mx);
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-}
-
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool W1>
-__device__ __forceinline__ void mat_block(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
-                                          const kg_cls_work &w, int tile, const char *__restrict__ rows_base,
-                                          uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
-                                          uint32_t *__restrict__ partials, uint32_t *kw, uint32_t *wkey, char *lrows) {
-    using Row = kg_pod_cls_t<NC, NF>;
-    constexpr int RB = (int)sizeof(Row);
-    constexpr int BT = KG_TILE / 2;                     // threads
-    constexpr int G_DW = KG_MAT_KC * RB / 4;            // dwords of one group's rows (one per staging thread)
-    static_assert((KG_MAT_KC * RB) % 4 == 0 && G_DW <= BT, "a group's rows are one dword per thread");
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t wave_base = (int64_t)tile * KG_TILE + wave * 128;
-    const Row *rows = reinterpret_cast<const Row *>(rows_base + d.rows_offset);
-    const uint32_t *gsrc = reinterpret_cast<const uint32_t *>(rows);
-    const int64_t last_dw = (int64_t)w.end * (RB / 4) - 1;     // stay inside the class's rows
-    uint32_t *lbuf = reinterpret_cast<uint32_t *>(lrows);
-    const int np = w.end - w.begin;
-    for (int i = tid; i < np; i += BT) wkey[i] = 0u;
-    if (tid < G_DW) {   // group 0 → buffer 0
-        const int64_t src = (int64_t)w.begin * (RB / 4) + tid;
-        lbuf[tid] = gsrc[src < last_dw ? src : last_dw];
-    }
-    ClsNode<NC, NF> n[2];
-    unsigned long long okm[2];
-    bool full_l = true;
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const int64_t node = wave_base + 2 * lane + j;
-        load_cls_node<NC, NF, MOST, FIT_ON, LA_ON>(c, pl, d, node, a.node_end, a.now_ns, n[j]);
-        okm[j] = __builtin_amdgcn_ballot_w64(n[j].ok);
-        full_l = full_l && (n[j].w == (1u << d.fit_shift) || node >= a.node_end);
-    }
-    const int64_t col0 = wave_base - a.col_begin;
-    const bool in_row = col0 + 2 * lane < a.score_stride;
-    const bool fast = W1 && (!FIT_ON || __all(full_l)) && __all(in_row);
-    const bool mseg0 = col0 < a.score_stride, mseg1 = col0 + 64 < a.score_stride;
-    const uint32_t kb0 = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - (uint32_t)(wave * 128 + 2 * lane);
-    uint32_t *kws = kw + wave * (KG_MAT_KC * 64);
-    uint32_t *scores32 = reinterpret_cast<uint32_t *>(scores);
-    // every node-plane load lands before the pod loop, so inside it the only vector-memory operations in
-    // flight are the score stores and the next group's row load (the waits there count the stores)
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-    __syncthreads();   // key slots zeroed, group 0 staged (no score store issued yet)
-    uint32_t mb[4] = {0u, 0u, 0u, 0u};   // ballots of the window's pod l in lane l: even lo, even hi, odd lo, odd hi
-    for (int g0 = w.begin, gi = 0; g0 < w.end; g0 += KG_MAT_KC, gi++) {
-        const int g1 = min(g0 + KG_MAT_KC, w.end);
-        const int win = gi & 3;   // the group's quarter of the 64-pod mask window
-        const bool more = g1 < w.end;
-        const bool stage = more && tid < G_DW;
-        uint32_t staged = 0;
-        if (stage) {   // the next group's rows are in flight while this group is evaluated
-            const int64_t src = (int64_t)g1 * (RB / 4) + tid;
-            staged = gsrc[src < last_dw ? src : last_dw];
-        }
-        // LDS ring of 8 group slots: the window being evaluated (4 slots, kept for its mask offsets) and
-        // the next window's first group, staged while this group is evaluated
-        const Row *lr = reinterpret_cast<const Row *>(lrows + (gi & 7) * (KG_MAT_KC * RB));
-        uint32_t *stage_dst = lbuf + ((gi + 1) & 7) * G_DW + tid;
-#define KG_MAT_GROUP(F, G)                                                                                             \
-    mat_group<NC, NF, MOST, FIT_ON, LA_ON, W1, F, G>(c, d, w.begin, g0, g1, lr, n, okm, col0, in_row, kb0, scores32, kws, \
-                                                    wkey, mb, win, stage, staged, stage_dst, a.score_stride)
-        if (fast && g1 - g0 == KG_MAT_KC) KG_MAT_GROUP(true, true);
-        else if (fast) KG_MAT_GROUP(true, false);
-        else KG_MAT_GROUP(false, false);
-#undef KG_MAT_GROUP
-        if (win == 3 || !more) {
-            // mask words of the window's pods: lane l writes pod l's two words of this segment
-            const int wn = g1 - (g0 - win * KG_MAT_KC);
-            if (lane < wn) {
-                const Row *wr = reinterpret_cast<const Row *>(lrows + (gi & 4) * (KG_MAT_KC * RB));
-                uint64_t *mw = mask + wr[lane].mask_off + (col0 >> 6);
-                if (mseg0) mw[0] = interleave32(mb[0], mb[2]);
-                if (mseg1) mw[1] = interleave32(mb[1], mb[3]);
-            }
-            mb[0] = mb[1] = mb[2] = mb[3] = 0u;
-        }
-        lds_barrier();
-    }
-    for (int i = tid; i < np; i += BT) partials[(int64_t)rows[w.begin + i].row * a.tiles_total + tile] = wkey[i];
-}
-
-#ifndef KG_MAT_WPE0
-#define KG_MAT_WPE0 5   // waves per SIMD the register allocation of k_mat kind 0 targets (others: KG_MAT_WPE1)
-#endif
-#ifndef KG_MAT_WPE1
-#define KG_MAT_WPE1 4
-#endif
-template <bool MOST, bool FIT_ON, bool LA_ON, bool W1, int KIND>
-__global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? KG_MAT_WPE0 : KG_MAT_WPE1))) void k_mat(kg_consts c, kg_planes pl, HotArgs a,
-                                                     const kg_cls_desc *__restrict__ descs,
-                                                     const kg_cls_work *__restrict__ work, const char *__restrict__ rows,
-                                                     uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
-                                                     uint32_t *__restrict__ partials, int32_t shard_tiles) {
-    __shared__ __attribute__((aligned(16))) uint32_t kw[(KG_TILE / 128) * KG_MAT_KC * 64];
-    __shared__ uint32_t wkey[KG_MAT_ITEM_MAX];
-    constexpr int RB = KIND == 0 ? (int)sizeof(kg_pod_cls_t<2, 2>) : KIND == 1 ? (int)sizeof(kg_pod_cls_t<2, 4>)
-                     : KIND == 2 ? (int)sizeof(kg_pod_cls_t<4, 2>) : (int)sizeof(kg_pod_cls_t<4, 4>);
-    __shared__ __attribute__((aligned(64))) char lrows[8 * KG_MAT_KC * RB];
-    if ((int)blockIdx.x >= shard_tiles) return;   // XCD padding of the grid (whole workgroup)
-    const int tile = a.tile_begin + blockIdx.x;
+    constexpr int CC = KG_EVAL3_CC, BT = KG_TILE / 2;
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[CC * BT];
+    __shared__ __attribute__((aligned(64))) char lrows[2 * CC * 128];
+    __shared__ __attribute__((aligned(16))) uint16_t sstage[OUT ? (BT / 64) * CC * 128 : 8];
     const kg_cls_work w = work[blockIdx.y];
     const kg_cls_desc d = descs[w.cls];
-#define KG_MAT_ARGS c, pl, a, d, w, tile, rows, mask, scores, partials, kw, wkey, lrows
-    if constexpr (KIND == 0) mat_block<2, 2, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);
-    else if constexpr (KIND == 1) mat_block<2, 4, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);
-    else if constexpr (KIND == 2) mat_block<4, 2, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);
-    else mat_block<4, 4, MOST, FIT_ON, LA_ON, W1>(KG_MAT_ARGS);
-#undef KG_MAT_ARGS
+#define KG_CLS_ARGS c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows, sstage
+    if constexpr (KIND == 0) cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
+    else if constexpr (KIND == 1) cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
+    else if constexpr (KIND == 2) cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
+    else cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
+#undef KG_CLS_ARGS
 }
 
 // Slow nodes (outside the fp64 exactness bounds) come out of k_eval2 as infeasible with
@@ -1411,10 +1094,6 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
     uint32_t nacc[4] = {0u, 0u, 0u, 0u};
     constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16);
     int succ_z = -1;   // the zone count the wave's table holds combination successors for
-#ifdef KG_NUMA2_PREFETCH   // measurement builds: the next node's row in flight in registers (measured slower)
-    uint4 row_next = make_uint4(0u, 0u, 0u, 0u);
-    if (lane < ROW_U4 && base < a.node_end) row_next = reinterpret_cast<const uint4 *>(rows + base)[lane];
-#endif
     for (int k = 0; k < npw; k++) {
         const int64_t node = base + k;
         const bool in_range = node < a.node_end;
@@ -1428,22 +1107,12 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
             // its zone fields in every loop of every lane
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
-#ifdef KG_NUMA2_PREFETCH
-            if (lane < ROW_U4) reinterpret_cast<uint4 *>(&lrow)[lane] = row_next;
-            if (lane < ROW_U4 && node + 1 < a.node_end && k + 1 < npw)
-                row_next = reinterpret_cast<const uint4 *>(rows + node + 1)[lane];
-#else
             if (lane < ROW_U4) reinterpret_cast<uint4 *>(&lrow)[lane] = reinterpret_cast<const uint4 *>(rows + node)[lane];
-#endif
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
             const kg_node_row &row = lrow;
             const bool zoned = (row.flags & KG_NODE_NUMA_OPTIONS) && row.numa_policy != KG_NUMA_NONE &&
                                row.n_zones > 0;   // n_zones ≤ KG_MAX_ZONES (kg_build_node_rows)
-#ifdef KG_NUMA_ABLATE   // 4 = no zone table fill
-            if (KG_NUMA_ABLATE & 4) {
-            } else
-#endif
             if (zoned) {  // wave-uniform; the previous node's reads precede these writes (in-order LDS per wave)
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
@@ -1456,12 +1125,6 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
                 asm volatile("" ::: "memory");
             }
             kg_numa_out o;   // a node without zones returns before the hint enumeration reads the table
-#ifdef KG_NUMA_ABLATE   // measurement builds only: 2 = no pair evaluation after the table fill
-            if (KG_NUMA_ABLATE & 2) {
-                o.feasible = true;
-                o.score = zt.succ[lane & 63] + (uint32_t)pd.numa_req[0];
-            } else
-#endif
             kg_numa_pair_z<kg_zone_tab, false, false>(c, row, pd, o, kg_zone_tab{zt});
             ok = ok && o.feasible;
             nsc = o.score;
@@ -1554,11 +1217,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WP
         const int slot = pb * 64 + lane;
         const bool live = slot < a.n_pods;
         const int p = live && perm ? perm[slot] : slot;   // the pod row this lane evaluates and writes
-#ifdef KG_NUMA2_PD_REF   // measurement builds: the pod's fields read from memory where used
-        const kg_pod_dev &pd = pods[live ? p : 0];
-#else
         const kg_pod_dev pd = pods[live ? p : 0];
-#endif
         numa2_run(c, pl, a, pd, p, live, tile, base, npw, rows, mask, scores, numa_scores, partials, bm, ztab[wave],
                   lrow_s[wave]);
     }
@@ -1888,19 +1547,6 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
 // One workgroup; per pod: (A) every tile's best untouched candidate and the re-scored touched nodes →
 // block max; (B) Reserve, one thread per part, and the committed node's planes.  The next pod's row
 // and tile keys are prefetched while the current pod is resolved.
-#ifndef KG_RESOLVE_LA_SPLIT
-#define KG_RESOLVE_LA_SPLIT 0   // k_resolve's LoadAware Reserve part on two threads per resource (one per usage variant)
-#endif
-#ifndef KG_RESOLVE_LDSBAR
-#define KG_RESOLVE_LDSBAR 0   // k_resolve's mid-Reserve barriers order LDS only (no wait for the global stores)
-#endif
-__device__ __forceinline__ void resolve_mid_barrier() {
-#if KG_RESOLVE_LDSBAR
-    lds_barrier();
-#else
-    __syncthreads();
-#endif
-}
 
 __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_planes pl,
                                                                 const kg_pod_dev *__restrict__ pods, int32_t pod_begin,
@@ -2124,7 +1770,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             }
             // the parts below read only srow (LDS); tid 0's global writes are ordered for the next pod by
             // the full barrier that ends this pod
-            resolve_mid_barrier();
+            __syncthreads();
         }
         // the node's slot in the touched list (and node cache): its position, or the next one
         int slot = nt;
@@ -2154,37 +1800,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 ce->n.fit_R[r] = R;
                 ce->n.fit_F[r] = F;
             }
-        } else if (KG_RESOLVE_LA_SPLIT && tid >= 64 + KG_NUM_RES && tid < 64 + KG_NUM_RES + 4) {
-            // LoadAware: two threads per resource, one per usage variant (each one division chain)
-            const int x = tid - 64 - KG_NUM_RES, r = x >> 1, v = x & 1;
-            if (v == 0) {
-                srow.la_used[0][r] += pd.la_est_i[r];
-                row.la_used[0][r] = srow.la_used[0][r];
-                if (r == 0 && c.la_extra) {   // LoadAware weights beyond cpu / memory
-                    for (int q = 0; q < KG_NUM_RES - 2; q++) {
-                        srow.la_used_x[0][q] += pd.la_est_x[q];
-                        row.la_used_x[0][q] = srow.la_used_x[0][q];
-                        if (pd.flags & KG_POD_PROD) {
-                            srow.la_used_x[1][q] += pd.la_est_x[q];
-                            row.la_used_x[1][q] = srow.la_used_x[1][q];
-                        }
-                    }
-                }
-            } else if (pd.flags & KG_POD_PROD) {
-                srow.la_used[1][r] += pd.la_est_i[r];
-                row.la_used[1][r] = srow.la_used[1][r];
-            }
-            double R, F;
-            fin[KG_NUM_RES + x] = kg_finalize_la_rv(c, pl, node, srow, r, v, &R, &F) ? 1u : 0u;
-            if (ce) {
-                if (v == 0) {
-                    ce->n.la_R[r] = R;
-                    ce->n.la_F0[r] = F;
-                } else {
-                    ce->n.la_F1[r] = F;
-                }
-            }
-        } else if (!KG_RESOLVE_LA_SPLIT && tid >= 64 + KG_NUM_RES && tid < 64 + KG_NUM_RES + 2) {
+        } else if (tid >= 64 + KG_NUM_RES && tid < 64 + KG_NUM_RES + 2) {
             const int r = tid - 64 - KG_NUM_RES;
             srow.la_used[0][r] += pd.la_est_i[r];
             row.la_used[0][r] = srow.la_used[0][r];
@@ -2231,13 +1847,13 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         }
         // the flags step reads the parts' LDS results only: their global stores (row, planes) complete under
         // the full barrier that ends this pod, before the next pod reads them
-        resolve_mid_barrier();
+        __syncthreads();
         if (numa_on && ce && tid >= 128 && tid < 128 + ROW_U4)   // the committed row into the node cache
             reinterpret_cast<uint4 *>(&nrow[slot])[tid - 128] = reinterpret_cast<const uint4 *>(&srow)[tid - 128];
         if (tid == 0) {   // kg_finalize_flags from the parts (metric and the static bits are unchanged)
             bool slow = false;
             uint32_t fmask = 0;
-            for (int r = 0; r < KG_NUM_RES + (KG_RESOLVE_LA_SPLIT ? 4 : 2); r++) slow = slow || (fin[r] & 1u);
+            for (int r = 0; r < KG_NUM_RES + 2; r++) slow = slow || (fin[r] & 1u);
             for (int r = 0; r < KG_NUM_RES; r++)
                 if (fin[r] & 2u) fmask |= 1u << r;
             const bool over[3] = {fl_over[0] != 0, fl_over[1] != 0, fl_over[2] != 0};
@@ -2290,7 +1906,6 @@ struct kg_engine {
     int32_t *numa_perm = nullptr;   // NodeNUMAResource matrix mode: pod rows grouped by hint-list shape
     bool numa_perm_on = false;
     BatchMasks bm{0, 0};
-    bool numa_bm_all = false;       // k_eval_numa2 loads every resource plane (KG_NUMA_BM_ALL, measurement)
     int numa_queue_mode = 1;        // k_eval_numa2's form: 1 queued for large launches, 0 grid (KG_NUMA_QUEUE=0,
                                     // measurement), 2 queued for every launch (KG_NUMA_QUEUE=2, tests)
     int64_t numa_resident_wgs = 0;  // resident k_eval_numa2 workgroups of the device (queried at first use)
@@ -2338,8 +1953,8 @@ struct kg_engine {
     std::unordered_map<int32_t, CpuTable> cpu_tab;
     std::vector<uint8_t> pod_may_bind;   // bit 0: binds by its own PreFilter; bit 1: a cpu request (node policy)
     bool profiling = false;
-    bool mat_kernel = false;            // matrix mode with planes through k_mat (else k_eval3); KG_MATRIX_KERNEL
     bool cls_fold_uniform = true;       // class-uniform scored slots folded per node (KG_CLS_FOLD_UNIFORM=0: off)
+    bool cls_fold_la = true;            // LoadAware-uniform chunks (KG_CLS_FOLD_LA=0: off; parity tests of both forms)
     int64_t cls_target_blocks = 2048;   // k_eval3 work items per class ≈ this / tiles (KG_CLS_TARGET_BLOCKS)
     // the class kinds' launches on two streams (kinds 1 / 3 on stream2), so one kind's grid tail is filled by
     // the other's workgroups (KG_CLS_CONCURRENT)
@@ -2404,7 +2019,7 @@ int pods_per_block_for(int64_t n_pods, int64_t tiles, int64_t target_blocks = 20
     int64_t ppb = (n_pods * tiles + target_blocks - 1) / target_blocks;
     ppb = (ppb + KG_POD_CHUNK - 1) / KG_POD_CHUNK * KG_POD_CHUNK;
     if (ppb < KG_POD_CHUNK) ppb = KG_POD_CHUNK;
-    if (ppb > KG_MAT_ITEM_MAX) ppb = KG_MAT_ITEM_MAX;   // k_mat's per-workgroup key slots
+    if (ppb > KG_CLS_ITEM_MAX) ppb = KG_CLS_ITEM_MAX;
     return (int)ppb;
 }
 
@@ -2479,6 +2094,33 @@ bool pod_class(const kg_config &cfg, const kg_pod_row &row, ClsKey &key) {
     return true;
 }
 
+// LoadAware-uniform chunks: a class's pods regrouped by EstimatePod, the whole KG_EVAL3_CC-pod chunks of one
+// estimate first (aligned to the class start, so every chunk k_eval3 walks there is one estimate: its LoadAware
+// least-requested sums depend on the node only and are evaluated once per node and chunk, the way the uniform
+// Fit slots fold into ClsNode::cq), the remainders after them.  Rows carry their own output offsets, so the
+// order within a class is free.  Returns the end of the uniform region.
+int32_t cls_order_la(const kg_engine *e, std::vector<int32_t> &mem) {
+    const bool la_on = (e->cfg.enabled_plugins & KG_PLUGIN_LOADAWARE) != 0;
+    if (!la_on || !e->cls_fold_la) return 0;
+    auto est = [&](int32_t i) { return std::make_pair(e->pod_rows_h[i].la_estimate[0], e->pod_rows_h[i].la_estimate[1]); };
+    std::vector<int32_t> s = mem;
+    std::stable_sort(s.begin(), s.end(), [&](int32_t x, int32_t y) { return est(x) < est(y); });
+    std::vector<int32_t> head, tail;
+    head.reserve(s.size());
+    for (size_t a = 0; a < s.size();) {
+        size_t b = a + 1;
+        while (b < s.size() && est(s[b]) == est(s[a])) b++;
+        const size_t whole = (b - a) / KG_EVAL3_CC * KG_EVAL3_CC;
+        head.insert(head.end(), s.begin() + a, s.begin() + a + whole);
+        tail.insert(tail.end(), s.begin() + a + whole, s.begin() + b);
+        a = b;
+    }
+    const int32_t end = (int32_t)head.size();
+    head.insert(head.end(), tail.begin(), tail.end());
+    mem.swap(head);
+    return end;
+}
+
 void cls_prepare(kg_engine *e) {
     e->cls_ok = false;
     e->cls_dirty = true;
@@ -2508,6 +2150,7 @@ void cls_prepare(kg_engine *e) {
         const ClsKey &k = keys[c];
         kg_cls_desc d;
         memset(&d, 0, sizeof(d));
+        d.la_uni_end = cls_order_la(e, e->cls_members[c]);
         // scored resources whose request is one value over the whole class fold into a per-node term when
         // that leaves at most two per-pod slots (a four-slot class then runs as a two-slot kind)
         const std::vector<int32_t> &mem = e->cls_members[c];
@@ -2595,7 +2238,7 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
         }
         e->cls_kind_work[kind][1] = (int32_t)work.size() - e->cls_kind_work[kind][0];
     }
-    std::vector<char> rows(rows_bytes + 256, 0);   // + padding: k_mat prefetches one row past a class's end
+    std::vector<char> rows(rows_bytes + 256, 0);
     for (size_t c = 0; c < descs.size(); c++) {
         const kg_cls_desc &d = descs[c];
         for (int32_t j = 0; j < d.count; j++) {
@@ -2638,20 +2281,13 @@ void launch_cls_kind(kg_engine *e, dim3 grid, const HotArgs &a, const kg_cls_des
     const int32_t first = e->cls_kind_work[KIND][0], count = e->cls_kind_work[KIND][1];
     if (count == 0) return;
     grid.y = (unsigned)count;
-    if (mask && e->mat_kernel) {
-        const int32_t shard_tiles = (int32_t)grid.x;
-        grid.x = (unsigned)((shard_tiles + KG_MAT_XCDS - 1) / KG_MAT_XCDS * KG_MAT_XCDS);
-        hipLaunchKernelGGL((k_mat<MOST, FIT_ON, LA_ON, W1, KIND>), grid, dim3(KG_TILE / 2), 0, stream, e->consts, e->pl,
-                           a, descs, work + first, rows, mask, scores, partials, shard_tiles);
-        return;
-    }
-    // matrix mode: 8-pod chunks, score segments staged in LDS and written as 1 KiB wave stores
-    // two nodes per lane (four: 92 VGPRs, 5 waves per SIMD, 1.98 vs 0.88 ms per config-2 pass)
+    // matrix mode: 8-pod chunks, score segments staged in LDS and written as 1 KiB wave stores; two nodes per
+    // lane (four: 92 VGPRs, 5 waves per SIMD, 1.98 vs 0.88 ms per config-2 pass, round 2)
     if (mask)
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, 8, true, KIND, 2>), grid, dim3(KG_TILE / 2), 0, stream,
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, KIND>), grid, dim3(KG_TILE / 2), 0, stream,
                            e->consts, e->pl, a, descs, work + first, rows, mask, scores, partials);
     else
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, 16, false, KIND, 2>), grid, dim3(KG_TILE / 2), 0, stream,
+        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, KIND>), grid, dim3(KG_TILE / 2), 0, stream,
                            e->consts, e->pl, a, descs, work + first, rows, mask, scores, partials);
 }
 
@@ -2761,7 +2397,7 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
             const int32_t seg = mask == nullptr && scores == nullptr && numa_scores == nullptr ? KG_NUMA2_SEG_TOPK : KG_NUMA2_SEG;
             const int64_t n_items = shard_tiles * (KG_TILE / seg) * ((n + 63) / 64);
             const int32_t *perm = e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr;
-            const BatchMasks bm = e->numa_bm_all ? BatchMasks{0xFFu, 0xFFu} : e->bm;
+            const BatchMasks bm = e->bm;
             if (e->numa_resident_wgs == 0) {
                 int dev_cus = 0, per_cu = 0;
                 HIP_TRY(e, hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->device));
@@ -2945,15 +2581,12 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
         return KG_ERR_HIP;
     }
     e->own_stream = true;
-    // measurement switch: KG_MATRIX_KERNEL=eval3 | mat selects the matrix-mode kernel with planes
-    const char *mk = getenv("KG_MATRIX_KERNEL");
-    e->mat_kernel = mk && strcmp(mk, "mat") == 0;
     const char *tb = getenv("KG_CLS_TARGET_BLOCKS");   // measurement switches (tools/ab_cls.sh)
     if (tb && atoll(tb) > 0) e->cls_target_blocks = atoll(tb);
     const char *fu = getenv("KG_CLS_FOLD_UNIFORM");
     e->cls_fold_uniform = !(fu && atoi(fu) == 0);
-    const char *bma = getenv("KG_NUMA_BM_ALL");
-    e->numa_bm_all = bma && atoi(bma) != 0;
+    const char *fl = getenv("KG_CLS_FOLD_LA");
+    e->cls_fold_la = !(fl && atoi(fl) == 0);
     const char *ncp = getenv("KG_NUMA_CHUNK_PODS");
     if (ncp) e->numa_chunk_pods = std::min(atoi(ncp), KG_NUMA_CHUNK_PODS);
     const char *nq = getenv("KG_NUMA_QUEUE");

@@ -79,6 +79,24 @@ def test_matrix_parity_uniform_slot_fold(profile, fold, monkeypatch):
     _check_matrix(cfg, cl, np.arange(160), cl.now_ns)
 
 
+@pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("profile", ["shipped", "default", "prod_usage", "most_w"])
+def test_matrix_parity_la_uniform_chunks(profile, fold, monkeypatch):
+    """k_eval3 groups a class's pods by EstimatePod and evaluates the LoadAware sums of a whole chunk of one
+    estimate once per node (kg_cls_desc::la_uni_end); KG_CLS_FOLD_LA=0 evaluates them per pair.  1,600 pods
+    of ~105 request shapes give both uniform chunks and a mixed tail per class; some nodes are beyond the fp64
+    bounds and the node count is ragged."""
+    monkeypatch.setenv("KG_CLS_FOLD_LA", fold)
+    cfg = {"shipped": shipped_profile, "default": make_config,
+           "prod_usage": lambda: shipped_profile(score_according_prod_usage=True),
+           "most_w": lambda: make_config(fit_strategy="MostAllocated", fit_resources={"cpu": 2, "memory": 1})}[profile]()
+    cl = synth.make_cluster(1_100, 1_600, seed=31)
+    big = np.arange(3, 1_100, 97)
+    cl.nodes["allocatable"]["v"][big, 1] = (1 << 43) + 99
+    cl = cl.with_nodes(cl.nodes)
+    _check_matrix(cfg, cl, np.arange(1_600), cl.now_ns)
+
+
 @pytest.mark.parametrize("n_nodes", [1, 63, 64, 511, 513, 1500])
 def test_matrix_parity_ragged_node_counts(n_nodes):
     cl = synth.make_cluster(n_nodes, 70, seed=n_nodes)
