@@ -128,21 +128,18 @@ struct alignas(64) kg_pod_hot_t {
 // take the same node-filter variant and the same LoadAware usage variant form a class.  Within a
 // class every per-pair branch is a compile-time constant: NC compared resources (int64), NF scored
 // resources (fp64 fma), padded to 2 or 4.  Rows are stored class after class (queue order inside a
-// class) and carry their output offsets.
+// class); the output row of each is in a parallel int32 array (kg_cls_desc::ids_first).
 #define KG_CLS_MAX 16                // classes per batch on the specialised path
 template <int NC, int NF>
-struct alignas(64) kg_pod_cls_t {
+struct alignas(16) kg_pod_cls_t {
     int64_t req[NC];       // Fit filter request of the compared resources (INT64_MIN pads)
     double pr[NF];         // signed Fit pod request of the scored resources (0 pads)
     double la[2];          // −EstimatePod (cpu, memory)
-    int64_t score_off;     // output row × score stride (elements)
-    int32_t mask_off;      // output row × mask words
-    int32_t row;           // output row (partial keys)
 };
 
 struct kg_cls_desc {
     int32_t kind;          // 0: (2,2)  1: (2,4)  2: (4,2)  3: (4,4)   (NC, NF)
-    int32_t first;         // first row of the class in the class-sorted pod array
+    int32_t ids_first;     // the class's first entry in the output-row array
     int32_t count;
     int32_t cmp_res[4];    // resource of each compared slot (−1 pad)
     int32_t fit_res[4];    // resource of each scored slot (−1 pad)

@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <map>
 #include <unordered_map>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -37,7 +38,7 @@
 
 #define KG_POD_CHUNK 64          // pods between two LDS partial combines in k_eval
 #define KG_RESOLVE_THREADS 512
-#define KG_CLS_ITEM_MAX 1024        // pods per k_eval3 work item
+#define KG_CLS_ITEM_MAX 512         // pods per k_eval3 work item (one output-row entry per thread)
 #define KG_MAX_CHUNK KG_PLACE_CHUNK_MAX   // max pods per resolve call (touched-list capacity)
 #define KG_MAX_TILES 4096        // max tiles per snapshot in k_resolve (2M nodes)
 
@@ -542,17 +543,20 @@ __global__ __launch_bounds__(KG_BLOCK) void k_eval2(kg_consts c, kg_planes pl, H
 }
 
 // ---------------------------------------------------------------------------------------
-// k_eval3: class-specialised matrix mode (one launch; each workgroup = one 1024-node tile × a pod
-// range of ONE class, so every per-pair branch is resolved at compile time or per workgroup)
+// k_eval3: class-specialised matrix mode (each workgroup = one 1024-node tile × a pod range of ONE class, so
+// every per-pair branch is resolved at compile time or per workgroup)
 // ---------------------------------------------------------------------------------------
 template <int NC, int NF>
 struct ClsNode {
     int64_t fr[NC];        // Allocatable − Requested of the compared resources
     double R[NF], F[NF];   // Fit fma operands of the scored resources
-    double laR[2], laF[2]; // LoadAware fma operands (the class's usage variant)
     uint32_t w;            // Σ Fit weights of the scored resources the node has
     uint32_t cq;           // Σ weight · score of the class's uniform slots (kg_cls_desc::uni_res) on this node
     bool ok;               // node-only filters for the class (valid, pods, overcommit, LoadAware thresholds)
+    bool la_use;           // the node's LoadAware planes are valid for this class (else every LoadAware term is 0)
+};
+struct ClsLa {
+    double laR[2], laF[2]; // LoadAware fma operands (the class's usage variant); 0 where !la_use
 };
 
 template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON>
@@ -592,17 +596,10 @@ __device__ __forceinline__ void load_cls_node(const kg_consts &c, const kg_plane
         }
     }
     bool expired = false;
-#pragma unroll
-    for (int r = 0; r < 2; r++) n.laR[r] = n.laF[r] = 0.0;
+    n.la_use = false;
     if (LA_ON) {
         expired = kg_metric_expired(c, df, in_range ? pl.metric_ns[node] : 0, now_ns);
-        if (in_range && !slow && kg_la_valid(c, df, expired)) {  // invalid NodeMetric ⇒ score 0 via R = F = 0
-#pragma unroll
-            for (int r = 0; r < 2; r++) {
-                n.laR[r] = pl.la_R[r * cap + node];
-                n.laF[r] = pl.la_F[(d.la_variant * 2 + r) * cap + node];
-            }
-        }
+        n.la_use = in_range && !slow && kg_la_valid(c, df, expired);   // invalid NodeMetric ⇒ score 0 via R = F = 0
     }
     const uint32_t variant = d.node_ok_sel % 3u;
     bool ok = (df & KGD_VALID) && !slow;
@@ -616,18 +613,14 @@ __device__ __forceinline__ void load_cls_node(const kg_consts &c, const kg_plane
     n.ok = ok;
 }
 
-template <int NC, int NF>
-__device__ __forceinline__ kg_pod_cls_t<NC, NF> load_cls_row(const kg_pod_cls_t<NC, NF> *__restrict__ p) {
-    constexpr int NB = sizeof(kg_pod_cls_t<NC, NF>) / 64;
-    union U {
-        kg_u32x16 v[NB];
-        kg_pod_cls_t<NC, NF> h;
-        __device__ U() {}
-    } u;
-    const kg_u32x16 *src = reinterpret_cast<const kg_u32x16 *>(p);
+template <bool LA_ON>
+__device__ __forceinline__ void load_cls_la(const kg_planes &pl, const kg_cls_desc &d, int64_t node, bool use, ClsLa &l) {
+    const int64_t cap = pl.cap;
 #pragma unroll
-    for (int i = 0; i < NB; i++) u.v[i] = src[i];
-    return u.h;
+    for (int r = 0; r < 2; r++) {
+        l.laR[r] = (LA_ON && use) ? pl.la_R[r * cap + node] : 0.0;
+        l.laF[r] = (LA_ON && use) ? pl.la_F[(d.la_variant * 2 + r) * cap + node] : 0.0;
+    }
 }
 
 // Fit compares of one pod against the lane's node as a wave lane mask: each int64 compare writes an
@@ -641,29 +634,29 @@ __device__ __forceinline__ unsigned long long cls_ok_mask(const kg_pod_cls_t<NC,
     return m;
 }
 
-// Fit and LoadAware scores of one pair.  UNIT: every Fit / LoadAware resource weight is 1, so the
-// weighted sums are plain sums.
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool FULL, bool UNIT>
-__device__ __forceinline__ void cls_scores(const kg_consts &c, const kg_cls_desc &d, const kg_pod_cls_t<NC, NF> &pd,
-                                           const ClsNode<NC, NF> &n, uint32_t &fit, uint32_t &la) {
-    fit = 0;
-    if (FIT_ON) {
-        uint32_t sum = n.cq;
+// LoadAware weighted least-requested sum (before the weight-sum shift) of one EstimatePod (la0, la1 =
+// −estimate) on the node
+template <bool LA_ON, bool UNIT>
+__device__ __forceinline__ uint32_t cls_la_sum(const kg_consts &c, double la0, double la1, const ClsLa &l) {
+    if (!LA_ON) return 0u;
+    const uint32_t q0 = cvt_u32_sat(__builtin_fma(la0, l.laR[0], l.laF[0]));
+    const uint32_t q1 = cvt_u32_sat(__builtin_fma(la1, l.laR[1], l.laF[1]));
+    return UNIT ? q0 + q1 : __umul24((uint32_t)c.la_w[0], q0) + __umul24((uint32_t)c.la_w[1], q1);
+}
+
+// Fit score of one pair (sum >> shift when the node has every scored resource, else ÷ its own weight sum)
+template <int NC, int NF, bool MOST, bool FIT_ON, bool FULL, bool UNIT>
+__device__ __forceinline__ uint32_t cls_fit(const kg_cls_desc &d, const kg_pod_cls_t<NC, NF> &pd, const ClsNode<NC, NF> &n) {
+    if (!FIT_ON) return 0u;
+    uint32_t sum = n.cq;
 #pragma unroll
-        for (int f = 0; f < NF; f++) {
-            uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n.R[f], n.F[f]));
-            if (MOST) q = q < 100u ? q : 100u;
-            sum = UNIT ? sum + q : __umul24(d.fit_w[f], q) + sum;
-        }
-        if (FULL) fit = sum >> d.fit_shift;
-        else fit = n.w ? sum / n.w : 0u;  // the node lacks a scored resource: its weight drops out
+    for (int f = 0; f < NF; f++) {
+        uint32_t q = cvt_u32_sat(__builtin_fma(pd.pr[f], n.R[f], n.F[f]));
+        if (MOST) q = q < 100u ? q : 100u;
+        sum = UNIT ? sum + q : __umul24(d.fit_w[f], q) + sum;
     }
-    la = 0;
-    if (LA_ON) {
-        const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la[0], n.laR[0], n.laF[0]));
-        const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la[1], n.laR[1], n.laF[1]));
-        la = (UNIT ? q0 + q1 : __umul24((uint32_t)c.la_w[0], q0) + __umul24((uint32_t)c.la_w[1], q1)) >> c.la_shift;
-    }
+    if (FULL) return sum >> d.fit_shift;
+    return n.w ? sum / n.w : 0u;  // the node lacks a scored resource: its weight drops out
 }
 
 typedef uint16_t kg_u16x2 __attribute__((ext_vector_type(2)));
@@ -672,7 +665,7 @@ typedef uint16_t kg_u16x2 __attribute__((ext_vector_type(2)));
 // LoadAware sum << 16 meet in one v_add3 (every term ≤ 100, so each half holds its sum without carry) and
 // one v_pk_lshrrev_b16 applies both plugins' weight-sum shifts.  `base` is the node's per-node part of the
 // sums: the class's uniform Fit slots (ClsNode::cq) and, in a chunk whose pods share one EstimatePod, the
-// LoadAware sum << 16 (cls_la_sum, evaluated once per node and chunk).
+// LoadAware sum << 16 (evaluated once per node and estimate).
 template <int NC, int NF, bool MOST, bool FIT_ON>
 __device__ __forceinline__ uint32_t cls_fit_sum(const kg_pod_cls_t<NC, NF> &pd, const ClsNode<NC, NF> &n, uint32_t base) {
     uint32_t s = base;
@@ -685,15 +678,6 @@ __device__ __forceinline__ uint32_t cls_fit_sum(const kg_pod_cls_t<NC, NF> &pd, 
         }
     }
     return s;
-}
-
-// LoadAware least-requested sum (unit weights) of one EstimatePod (la0, la1 = −estimate) on the node, << 16
-template <int NC, int NF, bool LA_ON>
-__device__ __forceinline__ uint32_t cls_la_sum(double la0, double la1, const ClsNode<NC, NF> &n) {
-    if (!LA_ON) return 0u;
-    const uint32_t q0 = cvt_u32_sat(__builtin_fma(la0, n.laR[0], n.laF[0]));
-    const uint32_t q1 = cvt_u32_sat(__builtin_fma(la1, n.laR[1], n.laF[1]));
-    return (q0 + q1) << 16;
 }
 
 // v_cndmask_b32 with a wave lane mask as the condition: v where the lane's bit is set, else 0
@@ -724,6 +708,24 @@ __device__ __forceinline__ void put_lane2(unsigned long long &w0, unsigned long 
         : "s"(lanebit), "s"(b0), "s"(b1));
 }
 
+// f(integral_constant<int, I>) for I = 0, 1, …: a fully unrolled loop whose index is a constant expression
+template <int... I, class F>
+__device__ __forceinline__ void unroll_seq(std::integer_sequence<int, I...>, F &&f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
+// key_max2 and put_lane2 of pod I in one EXEC window (the lane select an immediate):
+//   kmax (= m0 ? k0 : 0) := max(kmax, k1) on the lanes of m1;  lane I of w0 / w1 := m0 / m1
+template <int I>
+__device__ __forceinline__ void key_max_put(uint32_t &kmax, unsigned long long &w0, unsigned long long &w1,
+                                            unsigned long long m0, unsigned long long m1, uint32_t k1) {
+    unsigned long long sv;
+    asm("s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, %[m1]\n\tv_max_u32 %[k], %[k], %[k1]\n\t"
+        "s_mov_b64 exec, %[lb]\n\tv_mov_b64 %[w0], %[m0]\n\tv_mov_b64 %[w1], %[m1]\n\ts_mov_b64 exec, %[sv]"
+        : [k] "+v"(kmax), [w0] "+v"(w0), [w1] "+v"(w1), [sv] "=&s"(sv)
+        : [m0] "s"(m0), [m1] "s"(m1), [k1] "v"(k1), [lb] "n"(1ull << I));
+}
+
 // Workgroup barrier that orders LDS only.  __syncthreads() is also a release of global memory, so it waits
 // for every outstanding vector-memory operation of the wave (s_waitcnt vmcnt(0)) — including the score
 // stores, which then stall each chunk for the HBM write latency.  The pod loops share only LDS between
@@ -734,25 +736,46 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-#define KG_EVAL3_CC 8    // pods per chunk (LDS key reduction, score staging, LoadAware-uniform chunks: KG_CLS_LA_ALIGN)
+// k_eval3's key buffer: pod i of a chunk at kg_kofs(i) (dwords) — even pods in the first 2048 dwords, odd pods
+// 32 dwords (half the banks) further on, so the reducing wave's 16-lane read groups (two pods each) never
+// share a bank
+__device__ __forceinline__ int kg_kofs(int i) { return (i >> 1) * 512 + (i & 1) * (2048 + 32); }
+#define KG_KBUF_DW (4096 + 32)
+
+#if defined(KG_AB) && (KG_AB & 64)
+#define KG_AB_LDSROW 1
+#else
+#define KG_AB_LDSROW 0
+#endif
+#define KG_EVAL3_CC 8    // pods per chunk (LDS key reduction, score staging, LoadAware-uniform chunks)
 #define KG_EVAL3_WPE0 6  // waves per SIMD k_eval3's (2, 2) kind is register-allocated for (r03 A/B: 5 / 6 / 8)
 
 // Pods [p0, p0 + np) of one class against the lane's two nodes (columns lane and 64 + lane of the wave's
 // 128-column segment).  Pod rows are wave-uniform scalar loads.  UNR: a whole chunk, unrolled, so every
-// LDS address and lane select is an immediate.  LAU: the chunk's pods share one EstimatePod; its LoadAware
-// sums are already in base[] and only the Fit terms are evaluated per pair.
+// LDS address and lane select is an immediate.  LAU: the chunk's pods share one EstimatePod, whose LoadAware
+// sums are lsum[] (per node); otherwise they are evaluated per pair from la[].
 template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool UNR, bool LAU>
 __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> (&n)[2],
-                                         const unsigned long long (&okm)[2], const uint32_t (&base)[2], int np_rt,
-                                         const uint32_t (&kb)[2], uint32_t *kbuf, unsigned long long (&mb)[2],
-                                         uint16_t *sst, const kg_pod_cls_t<NC, NF> *__restrict__ grows) {
-    constexpr int BT = KG_TILE / 2, CC = KG_EVAL3_CC;
+                                         const ClsLa (&la)[2], const unsigned long long (&okm)[2],
+                                         const uint32_t (&lsum)[2], int np_rt, const uint32_t (&kb)[2], uint32_t *kbuf,
+                                         unsigned long long (&mb)[2], uint16_t *sst,
+                                         const kg_pod_cls_t<NC, NF> *__restrict__ grows, const kg_pod_cls_t<NC, NF> *lrw) {
+    constexpr int CC = KG_EVAL3_CC;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int np = UNR ? CC : np_rt;
     const kg_u16x2 shifts = {(uint16_t)d.fit_shift, (uint16_t)c.la_shift};
-    auto pod = [&](const int i) {
+    // ic: std::integral_constant<int, I> in the unrolled chunk (immediate lane selects), else the runtime index
+    auto pod = [&](auto ic) {
+        constexpr bool CT = !std::is_same<decltype(ic), int>::value;
+        const int i = (int)ic;
+#if defined(KG_AB) && (KG_AB & 2)
+        const kg_pod_cls_t<NC, NF> pd = grows[0];
+#elif defined(KG_AB) && (KG_AB & 64)
+        const kg_pod_cls_t<NC, NF> pd = lrw[i];   // ds_read: wave-uniform values in VGPRs
+#else
         const kg_pod_cls_t<NC, NF> pd = grows[i];   // s_load into SGPRs
+#endif
         unsigned long long m[2];
 #pragma unroll
         for (int j = 0; j < 2; j++) m[j] = cls_ok_mask<NC, NF>(pd, n[j], okm[j]);
@@ -764,72 +787,86 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
             uint32_t h[2], k[2];
 #pragma unroll
             for (int j = 0; j < 2; j++) {
-                const uint32_t b = LAU ? base[j] : base[j] + cls_la_sum<NC, NF, LA_ON>(pd.la[0], pd.la[1], n[j]);
-                const uint32_t s = cls_fit_sum<NC, NF, MOST, FIT_ON>(pd, n[j], b);
+                const uint32_t ls = LAU ? lsum[j] : cls_la_sum<LA_ON, true>(c, pd.la[0], pd.la[1], la[j]);
+                const uint32_t s = cls_fit_sum<NC, NF, MOST, FIT_ON>(pd, n[j], n[j].cq + (ls << 16));
                 h[j] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(kg_u16x2, s) >> shifts);
                 k[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(kg_u16x2, h[j]), kw, kb[j], false);
             }
-            kmax = key_max2(m[0], m[1], k[0], k[1]);
+            if constexpr (CT && OUT) {
+                kmax = sel_lanes(m[0], k[0]);
+                key_max_put<decltype(ic)::value>(kmax, mb[0], mb[1], m[0], m[1], k[1]);
+            } else {
+                kmax = key_max2(m[0], m[1], k[0], k[1]);
+                if (OUT) put_lane2(mb[0], mb[1], 1ull << i, m[0], m[1]);
+            }
             s01 = __builtin_amdgcn_perm(h[1], h[0], 0x06040200u);
         } else {
             uint32_t s[2];
             kmax = 0;
 #pragma unroll
             for (int j = 0; j < 2; j++) {
-                uint32_t fit, la;
-                cls_scores<NC, NF, MOST, FIT_ON, LA_ON, FULL, W1>(c, d, pd, n[j], fit, la);
-                const uint32_t tot = W1 ? fit + la : __umul24((uint32_t)c.weight_fit, fit) + __umul24((uint32_t)c.weight_la, la);
+                const uint32_t fit = cls_fit<NC, NF, MOST, FIT_ON, FULL, W1>(d, pd, n[j]);
+                const uint32_t ls = LAU ? lsum[j] : cls_la_sum<LA_ON, W1>(c, pd.la[0], pd.la[1], la[j]);
+                const uint32_t lv = LA_ON ? ls >> c.la_shift : 0u;
+                const uint32_t tot = W1 ? fit + lv : __umul24((uint32_t)c.weight_fit, fit) + __umul24((uint32_t)c.weight_la, lv);
                 const uint32_t k = sel_lanes(m[j], (tot << KG_TILE_SHIFT) + kb[j]);
                 kmax = kmax > k ? kmax : k;
-                s[j] = fit | (la << 8);
+                s[j] = fit | (lv << 8);
             }
             s01 = s[0] | (s[1] << 16);
+            if (OUT) put_lane2(mb[0], mb[1], 1ull << i, m[0], m[1]);
         }
-        kbuf[i * BT + tid] = kmax;
+        kbuf[kg_kofs(i) + tid] = kmax;
         if (OUT) {
-            put_lane2(mb[0], mb[1], 1ull << i, m[0], m[1]);
             // the wave's 128-column score segment of this pod, written out per chunk
             sst[i * 128 + lane] = (uint16_t)s01;
             sst[i * 128 + 64 + lane] = (uint16_t)(s01 >> 16);
         }
     };
+#if defined(KG_AB) && (KG_AB & 16)
+    if (true) {
+        for (int i = 0; i < np; i++) { kbuf[kg_kofs(i) + tid] = 5; if (OUT) { sst[i * 128 + lane] = 7; sst[i * 128 + 64 + lane] = 9; } }
+        return;
+    }
+#endif
     if constexpr (UNR) {
-#pragma unroll
-        for (int i = 0; i < CC; i++) pod(i);
+        unroll_seq(std::make_integer_sequence<int, CC>{}, pod);
     } else {
         for (int i = 0; i < np; i++) pod(i);
     }
 }
 
 // One workgroup = one 1024-node tile (two nodes per lane, 8 waves) × a pod range of one class, walked in
-// KG_EVAL3_CC-pod chunks: per chunk the pods' keys go to LDS and are reduced to one key per (pod, tile), the
-// scores are staged in LDS and written as wave-wide 16-B-per-lane stores, the feasibility words as one u64
-// pair per pod.
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1>
+// KG_EVAL3_CC-pod chunks: per chunk the pods' keys go to LDS and one wave (rotating) reduces them to one key per
+// (pod, tile) while the others go on; the scores are staged in LDS and written as wave-wide 16-B-per-lane
+// stores, the feasibility words as one u64 pair per pod.  LAU: a work item of LoadAware-uniform chunks (the
+// host puts whole chunks of one EstimatePod first in each class, kg_cls_desc::la_uni_end): the LoadAware sums
+// are per node, evaluated when the estimate changes from one chunk to the next, with the LoadAware planes
+// loaded just for that (no registers held for them across the pod loops).
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, bool LAU>
 __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
                                           const kg_cls_work &w, const char *__restrict__ rows_base,
-                                          uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
-                                          uint32_t *__restrict__ partials, uint32_t *kbuf, char *lrows,
-                                          uint16_t *sstage) {
+                                          const int32_t *__restrict__ ids, uint64_t *__restrict__ mask,
+                                          uint16_t *__restrict__ scores, uint32_t *__restrict__ partials,
+                                          uint32_t *kbuf, int32_t *lid, char *lrows, uint16_t *sstage) {
     constexpr int CC = KG_EVAL3_CC;
     constexpr int BT = KG_TILE / 2;                       // threads of the workgroup
-    constexpr int RB = (int)sizeof(kg_pod_cls_t<NC, NF>);
-    constexpr int CHUNK_DW = CC * RB / 4;                 // dwords of one chunk of rows (≤ BT)
-    constexpr int G = BT / CC;                            // threads reducing one pod's keys
     constexpr int SEGW = 128;                             // score columns of one wave
-    static_assert(G == 64, "key reduction groups are whole waves");
-    static_assert(CHUNK_DW <= BT, "one dword per thread stages a chunk");
+    static_assert(CC == 8 && BT == 512, "the key reduction maps one wave's lanes to 8 pods × 8 lanes");
+    static_assert(KG_CLS_ITEM_MAX <= BT, "one output-row entry per thread");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tile = a.tile_begin + blockIdx.x;
     const int64_t wave_base = (int64_t)tile * KG_TILE + wave * SEGW;
     ClsNode<NC, NF> n[2];
+    ClsLa la[2];
     unsigned long long okm[2];
     bool full_l = true;
 #pragma unroll
     for (int j = 0; j < 2; j++) {
         load_cls_node<NC, NF, MOST, FIT_ON, LA_ON>(c, pl, d, wave_base + 64 * j + lane, a.node_end, a.now_ns, n[j]);
+        if (!LAU) load_cls_la<LA_ON>(pl, d, wave_base + 64 * j + lane, n[j].la_use, la[j]);
         okm[j] = __builtin_amdgcn_ballot_w64(n[j].ok);
         full_l = full_l && (n[j].w == (1u << d.fit_shift) || wave_base + 64 * j + lane >= a.node_end);
     }
@@ -843,57 +880,70 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         seg[j] = col0 + 64 * j < a.score_stride;
         kb[j] = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0 - 64u * j;
     }
-    // the rows (output offsets) of each chunk are staged in LDS for the stores; the next chunk's global load
-    // is in flight while the current chunk is evaluated
-    const uint32_t *gsrc = reinterpret_cast<const uint32_t *>(rows_base + d.rows_offset);
-    const int64_t last_dw = (int64_t)w.end * (RB / 4) - 1;        // stay inside the class's rows
-    uint32_t *lbuf = reinterpret_cast<uint32_t *>(lrows);
+    // the work item's output rows (for the stores and the partial keys) go to LDS once: the chunk loop issues no
+    // vector loads, so nothing in it waits on vmcnt — i.e. on its own score stores
     const kg_pod_cls_t<NC, NF> *grows = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(rows_base + d.rows_offset);
-    if (tid < CHUNK_DW) {
-        const int64_t src = (int64_t)w.begin * (RB / 4) + tid;
-        lbuf[tid] = gsrc[src < last_dw ? src : last_dw];
+#if defined(KG_AB) && (KG_AB & 8)
+    if (tid < w.end - w.begin) lid[tid] = d.ids_first + w.begin + tid;
+#else
+    if (tid < w.end - w.begin) lid[tid] = ids[d.ids_first + w.begin + tid];
+#endif
+    // pod rows through LDS (KG_AB & 64): chunk k's rows in slot k % 3, loaded two chunks ahead (the load is waited
+    // for after the chunk's own stores, so only stores a chunk older are waited for with it)
+    constexpr int RB = (int)sizeof(kg_pod_cls_t<NC, NF>), CHUNK_DW = KG_EVAL3_CC * RB / 4;
+    static_assert(CHUNK_DW <= 512, "one dword per thread stages a chunk of rows");
+    uint32_t *lrw32 = reinterpret_cast<uint32_t *>(lrows);
+    const uint32_t *gsrc = reinterpret_cast<const uint32_t *>(grows);
+    const int64_t src_end = (int64_t)w.end * (RB / 4);
+    const bool row_lds = KG_AB_LDSROW;
+    if (row_lds && tid < CHUNK_DW) {
+        for (int k = 0; k < 2; k++) {
+            const int64_t src = ((int64_t)w.begin + k * KG_EVAL3_CC) * (RB / 4) + tid;
+            if (src < src_end) lrw32[k * CHUNK_DW + tid] = gsrc[src];
+        }
     }
     // every node-plane load has landed before the pod loop: the loop itself then never waits on
     // vector memory (its stores included)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __syncthreads();
-    const int rj = tid / G;
     uint16_t *sst = sstage + wave * (CC * SEGW);
-    int buf = 0;
-    for (int p0 = w.begin; p0 < w.end; p0 += CC) {
+    // LAU: the estimate (bit patterns) whose LoadAware sums lsum holds
+    uint64_t la_prev0 = 0, la_prev1 = 0;
+    bool la_have = false;
+    uint32_t lsum[2] = {0u, 0u};
+    int ci = 0;
+    for (int p0 = w.begin; p0 < w.end; p0 += CC, ci++) {
         const int p1 = min(p0 + CC, w.end);
+        const int kslot = ci & 1;
+        const int32_t *cur = lid + (p0 - w.begin);   // output rows of the chunk's pods
+        const kg_pod_cls_t<NC, NF> *crow = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(lrows + (ci % 3) * (CHUNK_DW * 4));
         uint32_t staged = 0;
-        const bool more = p1 < w.end;
-        if (more && tid < CHUNK_DW) {
-            const int64_t src = (int64_t)p1 * (RB / 4) + tid;
-            staged = gsrc[src < last_dw ? src : last_dw];
-        }
-        const char *cur = lrows + buf * (CC * RB);
+        const int64_t src2 = ((int64_t)p0 + 2 * KG_EVAL3_CC) * (RB / 4) + tid;
+        const bool ahead = row_lds && tid < CHUNK_DW && src2 < src_end;
+        if (ahead) staged = gsrc[src2];
+        uint32_t *kcur = kbuf + kslot * KG_KBUF_DW;
         unsigned long long mb[2] = {0ull, 0ull};
-        // a chunk of one EstimatePod (the host puts whole chunks of equal estimates first, kg_cls_desc::
-        // la_uni_end): its LoadAware sums are per node, evaluated here once for the chunk's pods
-        const bool lau = LA_ON && W1 && full && p0 + CC <= d.la_uni_end;
-        uint32_t base[2];
-        if (lau) {
-            const double la0 = grows[p0].la[0], la1 = grows[p0].la[1];
+        if (LAU) {
+            const uint64_t e0 = __builtin_bit_cast(uint64_t, grows[p0].la[0]), e1 = __builtin_bit_cast(uint64_t, grows[p0].la[1]);
+            if (!la_have || e0 != la_prev0 || e1 != la_prev1) {
+                ClsLa l[2];
 #pragma unroll
-            for (int j = 0; j < 2; j++) base[j] = n[j].cq + cls_la_sum<NC, NF, LA_ON>(la0, la1, n[j]);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 2; j++) base[j] = n[j].cq;
+                for (int j = 0; j < 2; j++) {
+                    load_cls_la<LA_ON>(pl, d, wave_base + 64 * j + lane, n[j].la_use, l[j]);
+                    lsum[j] = cls_la_sum<LA_ON, W1>(c, __builtin_bit_cast(double, e0), __builtin_bit_cast(double, e1), l[j]);
+                }
+                la_prev0 = e0;
+                la_prev1 = e1;
+                la_have = true;
+            }
         }
-#define KG_CLS_PODS(FULL_, UNR_, LAU_)                                                                        \
-    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, UNR_, LAU_>(c, d, n, okm, base, p1 - p0, kb, kbuf, mb, sst, \
-                                                                      grows + p0)
-        if (lau) KG_CLS_PODS(true, true, true);
-        else if (full && p1 - p0 == CC) KG_CLS_PODS(true, true, false);
-        else if (full) KG_CLS_PODS(true, false, false);
-        else KG_CLS_PODS(false, false, false);
+#define KG_CLS_PODS(FULL_, UNR_)                                                                              \
+    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, UNR_, LAU>(c, d, n, la, okm, lsum, p1 - p0, kb, kcur, mb, sst, \
+                                                                     grows + p0, crow)
+        if (full && p1 - p0 == CC) KG_CLS_PODS(true, true);
+        else if (full) KG_CLS_PODS(true, false);
+        else KG_CLS_PODS(false, false);
 #undef KG_CLS_PODS
-        // the next chunk's rows go to the other LDS buffer before this chunk's global stores are issued:
-        // waiting for the row load (vmcnt) after the stores would wait for the stores too (vmcnt counts
-        // both), stalling every chunk on the HBM write latency
-        if (more && tid < CHUNK_DW) lbuf[(buf ^ 1) * (CC * RB / 4) + tid] = staged;
         if (OUT) {
             // 16 lanes × 16 B cover one pod's 128 columns: 4 pods per wave-wide 1 KiB store.  The reads see
             // the other lanes' ds_writes: a wave's LDS operations complete in order.
@@ -902,68 +952,92 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
             asm volatile("" ::: "memory");
             const int np = p1 - p0, s8 = lane % LP;
             const bool segs = s8 < 8 ? seg[0] : seg[1];
+            const bool whole = np == CC && seg[1];   // wave-uniform: every lane stores
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
             for (int it = 0; it < CC / PPS; it++) {
                 const int pp = it * PPS + lane / LP;
-                if (pp < np && segs) {
+#if defined(KG_AB) && (KG_AB & 1)
+                if (false) {
+#else
+                if (whole || (pp < np && segs)) {
+#endif
                     const uint4 v = *reinterpret_cast<const uint4 *>(sst + pp * SEGW + s8 * 8);
-                    const int64_t off = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[pp].score_off;
-                    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                    const int64_t off = (int64_t)cur[pp] * a.score_stride;
+#if defined(KG_AB) && (KG_AB & 32)
+                    *reinterpret_cast<u32x4 *>(scores + off + col0 + s8 * 8) = u32x4{v.x, v.y, v.z, v.w};
+#elif defined(KG_AB) && (KG_AB & 128)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(scores + off + col0 + s8 * 8), "v"(u32x4{v.x, v.y, v.z, v.w}) : "memory");
+#elif defined(KG_AB) && (KG_AB & 256)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(scores + off + col0 + s8 * 8), "v"(u32x4{v.x, v.y, v.z, v.w}) : "memory");
+#elif defined(KG_AB) && (KG_AB & 512)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(scores + off + col0 + s8 * 8), "v"(u32x4{v.x, v.y, v.z, v.w}) : "memory");
+#elif defined(KG_AB) && (KG_AB & 1024)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(scores + off + col0 + s8 * 8), "v"(u32x4{v.x, v.y, v.z, v.w}) : "memory");
+#else
                     __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(scores + off + col0 + s8 * 8));
+#endif
                 }
             }
+#if defined(KG_AB) && (KG_AB & 4)
+            if (false) {
+#else
             if (lane < np && seg[0]) {
+#endif
                 // lane l writes the two feasibility words of pod p0 + l
-                const kg_pod_cls_t<NC, NF> &pr = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[lane];
-                uint64_t *mw = mask + pr.mask_off + (col0 >> 6);
+                uint64_t *mw = mask + (int64_t)cur[lane] * a.mask_words + (col0 >> 6);
                 mw[0] = mb[0];
                 if (seg[1]) mw[1] = mb[1];
             }
         }
+        if (ahead) lrw32[((ci + 2) % 3) * CHUNK_DW + tid] = staged;
+        // one barrier per chunk: after it, one wave (rotating) reduces the chunk's keys while the others go on
+        // with the next chunk, whose keys go to the other key buffer.  A key buffer is written again two chunks
+        // later, after the next barrier, which the reducing wave reaches only after its reduction.
         lds_barrier();
-        const uint4 *src = reinterpret_cast<const uint4 *>(kbuf + rj * BT + lane * CC);
-        uint32_t mx = 0;
+        if (wave == ci % (BT / 64)) {
+            // lane (p, q) = (l / 8, l % 8) takes 64 of pod p's 512 keys (16-B reads: each 16-lane group reads
+            // two pods' 128 B at disjoint banks), then the 8 lanes of a pod meet by DPP
+            const int p = lane >> 3, q = lane & 7;
+            const uint4 *src = reinterpret_cast<const uint4 *>(kcur + kg_kofs(p)) + q;
+            uint32_t mx = 0;
 #pragma unroll
-        for (int k = 0; k < CC / 4; k++) {
-            const uint4 v = src[k];
-            const uint32_t a0 = v.x > v.y ? v.x : v.y, a1 = v.z > v.w ? v.z : v.w;
-            const uint32_t a2 = a0 > a1 ? a0 : a1;
-            mx = mx > a2 ? mx : a2;
+            for (int k = 0; k < 16; k++) {
+                const uint4 v = src[8 * k];
+                mx = max(mx, max(max(v.x, v.y), max(v.z, v.w)));
+            }
+            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x141, 0xf, 0xf, false));  // row_half_mirror
+            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
+            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+            if (q == 0 && p < p1 - p0) {
+                partials[(int64_t)cur[p] * a.tiles_total + tile] = mx;
+            }
         }
-        mx = dpp_max_step(mx, 0);
-        mx = dpp_max_step(mx, 1);
-        mx = dpp_max_step(mx, 2);
-        mx = dpp_max_step(mx, 3);
-        mx = dpp_max_step(mx, 4);
-        mx = dpp_max_step(mx, 5);
-        if (lane == 63 && rj < p1 - p0) {
-            const int32_t row = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(cur)[rj].row;
-            partials[(int64_t)row * a.tiles_total + tile] = mx;
-        }
-        lds_barrier();
-        buf ^= 1;
     }
 }
 
-// One launch per class kind (the work table is grouped by kind): each kernel is register-allocated for
+// One launch per (class kind, LAU) (the work table is grouped that way): each kernel is register-allocated for
 // its own kind.  OUT: the feasibility words and score planes are written (else per-(pod, tile) keys only).
-template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int KIND>
+template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int KIND, bool LAU>
 __global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? KG_EVAL3_WPE0 : KIND == 2 ? 5 : 4))) void k_eval3(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_cls_desc *__restrict__ descs,
                                                     const kg_cls_work *__restrict__ work,
-                                                    const char *__restrict__ rows, uint64_t *__restrict__ mask,
-                                                    uint16_t *__restrict__ scores, uint32_t *__restrict__ partials) {
+                                                    const char *__restrict__ rows, const int32_t *__restrict__ ids,
+                                                    uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
+                                                    uint32_t *__restrict__ partials) {
     constexpr int CC = KG_EVAL3_CC, BT = KG_TILE / 2;
-    __shared__ __attribute__((aligned(16))) uint32_t kbuf[CC * BT];
-    __shared__ __attribute__((aligned(64))) char lrows[2 * CC * 128];
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[2 * KG_KBUF_DW];
+    static_assert(CC * BT <= 4096, "a chunk's keys fit the key buffer");
+    __shared__ int32_t lid[KG_CLS_ITEM_MAX];
+    __shared__ __attribute__((aligned(16))) char lrows[KG_AB_LDSROW ? 3 * CC * (int)sizeof(kg_pod_cls_t<4, 4>) : 16];
     __shared__ __attribute__((aligned(16))) uint16_t sstage[OUT ? (BT / 64) * CC * 128 : 8];
     const kg_cls_work w = work[blockIdx.y];
     const kg_cls_desc d = descs[w.cls];
-#define KG_CLS_ARGS c, pl, a, d, w, rows, mask, scores, partials, kbuf, lrows, sstage
-    if constexpr (KIND == 0) cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
-    else if constexpr (KIND == 1) cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
-    else if constexpr (KIND == 2) cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
-    else cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
+#define KG_CLS_ARGS c, pl, a, d, w, rows, ids, mask, scores, partials, kbuf, lid, lrows, sstage
+    if constexpr (KIND == 0) cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1, LAU>(KG_CLS_ARGS);
+    else if constexpr (KIND == 1) cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1, LAU>(KG_CLS_ARGS);
+    else if constexpr (KIND == 2) cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1, LAU>(KG_CLS_ARGS);
+    else cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1, LAU>(KG_CLS_ARGS);
 #undef KG_CLS_ARGS
 }
 
@@ -1925,8 +1999,8 @@ struct kg_engine {
     void *cls_mem = nullptr;                // device: descs | work | rows
     size_t cls_mem_bytes = 0;
     int32_t cls_nwork = 0;
-    int32_t cls_kind_work[4][2] = {};   // [kind] = (first work item, count)
-    size_t cls_work_off = 0, cls_rows_off = 0;
+    int32_t cls_kind_work[8][2] = {};   // [2 · kind + LoadAware-uniform] = (first work item, count)
+    size_t cls_work_off = 0, cls_rows_off = 0, cls_ids_off = 0;
     int32_t *slow_list = nullptr;   // [cap] nodes outside the fast-path bounds, whole snapshot
     int32_t *slow_count = nullptr;
     bool slow_valid = false;        // the list matches the planes (rebuilt lazily after host-side changes;
@@ -2198,8 +2272,7 @@ void cls_prepare(kg_engine *e) {
 }
 
 template <int NC, int NF>
-void cls_fill_row(const kg_engine *e, const kg_cls_desc &d, const kg_pod_row &r, int32_t row, int64_t stride,
-                  int64_t words, char *dst) {
+void cls_fill_row(const kg_engine *e, const kg_cls_desc &d, const kg_pod_row &r, char *dst) {
     kg_pod_cls_t<NC, NF> h;
     memset(&h, 0, sizeof(h));
     const bool most = e->cfg.fit_strategy == KG_STRATEGY_MOST_ALLOCATED;
@@ -2210,9 +2283,6 @@ void cls_fill_row(const kg_engine *e, const kg_cls_desc &d, const kg_pod_row &r,
     }
     h.la[0] = -(double)r.la_estimate[0];
     h.la[1] = -(double)r.la_estimate[1];
-    h.score_off = (int64_t)row * stride;
-    h.mask_off = (int32_t)((int64_t)row * words);
-    h.row = row;
     memcpy(dst, &h, sizeof(h));
 }
 
@@ -2224,36 +2294,46 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
     std::vector<kg_cls_desc> descs = e->cls_desc;
     std::vector<kg_cls_work> work;
     size_t rows_bytes = 0;
+    int32_t n_ids = 0;
     for (size_t c = 0; c < descs.size(); c++) {
         descs[c].rows_offset = (int64_t)rows_bytes;
         rows_bytes += (size_t)descs[c].row_bytes * (size_t)descs[c].count;
+        descs[c].ids_first = n_ids;
+        n_ids += descs[c].count;
     }
-    for (int kind = 0; kind < 4; kind++) {   // the work table grouped by kind: one launch per kind
-        e->cls_kind_work[kind][0] = (int32_t)work.size();
+    // the work table grouped by (kind, LoadAware-uniform): one launch each; a class's LoadAware-uniform region
+    // [0, la_uni_end) and its tail are split into work items separately
+    for (int g = 0; g < 8; g++) {
+        const int kind = g >> 1;
+        const bool lau = (g & 1) != 0;
+        e->cls_kind_work[g][0] = (int32_t)work.size();
         for (size_t c = 0; c < descs.size(); c++) {
             if (descs[c].kind != kind) continue;
-            const int32_t n = descs[c].count;
-            const int32_t ppb = pods_per_block_for(n, shard_tiles, e->cls_target_blocks);
-            for (int32_t b = 0; b < n; b += ppb) work.push_back(kg_cls_work{(int32_t)c, b, b + ppb < n ? b + ppb : n, 0});
+            const int32_t b0 = lau ? 0 : descs[c].la_uni_end, b1 = lau ? descs[c].la_uni_end : descs[c].count;
+            if (b1 <= b0) continue;
+            const int32_t ppb = pods_per_block_for(b1 - b0, shard_tiles, e->cls_target_blocks);
+            for (int32_t b = b0; b < b1; b += ppb) work.push_back(kg_cls_work{(int32_t)c, b, b + ppb < b1 ? b + ppb : b1, 0});
         }
-        e->cls_kind_work[kind][1] = (int32_t)work.size() - e->cls_kind_work[kind][0];
+        e->cls_kind_work[g][1] = (int32_t)work.size() - e->cls_kind_work[g][0];
     }
-    std::vector<char> rows(rows_bytes + 256, 0);
+    std::vector<char> rows(rows_bytes, 0);
+    std::vector<int32_t> ids((size_t)n_ids + 1, 0);
     for (size_t c = 0; c < descs.size(); c++) {
         const kg_cls_desc &d = descs[c];
         for (int32_t j = 0; j < d.count; j++) {
             const int32_t i = e->cls_members[c][j];
+            ids[(size_t)d.ids_first + (size_t)j] = i;
             char *dst = rows.data() + d.rows_offset + (size_t)j * (size_t)d.row_bytes;
             const kg_pod_row &r = e->pod_rows_h[i];
-            if (d.kind == 0) cls_fill_row<2, 2>(e, d, r, i, stride, words, dst);
-            else if (d.kind == 1) cls_fill_row<2, 4>(e, d, r, i, stride, words, dst);
-            else if (d.kind == 2) cls_fill_row<4, 2>(e, d, r, i, stride, words, dst);
-            else cls_fill_row<4, 4>(e, d, r, i, stride, words, dst);
+            if (d.kind == 0) cls_fill_row<2, 2>(e, d, r, dst);
+            else if (d.kind == 1) cls_fill_row<2, 4>(e, d, r, dst);
+            else if (d.kind == 2) cls_fill_row<4, 2>(e, d, r, dst);
+            else cls_fill_row<4, 4>(e, d, r, dst);
         }
     }
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t desc_b = sizeof(kg_cls_desc) * KG_CLS_MAX, work_b = sizeof(kg_cls_work) * (work.size() + 1);
-    const size_t need = up(desc_b) + up(work_b) + up(rows.size());
+    const size_t need = up(desc_b) + up(work_b) + up(rows.size()) + up(ids.size() * 4);
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     if (need > e->cls_mem_bytes) {
         if (e->cls_mem) HIP_TRY(e, hipFree(e->cls_mem));
@@ -2267,7 +2347,9 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
     char *m = (char *)e->cls_mem;
     HIP_TRY(e, hipMemcpy(m, descs.data(), sizeof(kg_cls_desc) * descs.size(), hipMemcpyHostToDevice));
     if (!work.empty()) HIP_TRY(e, hipMemcpy(m + e->cls_work_off, work.data(), sizeof(kg_cls_work) * work.size(), hipMemcpyHostToDevice));
-    HIP_TRY(e, hipMemcpy(m + e->cls_rows_off, rows.data(), rows.size(), hipMemcpyHostToDevice));
+    e->cls_ids_off = e->cls_rows_off + up(rows.size());
+    if (!rows.empty()) HIP_TRY(e, hipMemcpy(m + e->cls_rows_off, rows.data(), rows.size(), hipMemcpyHostToDevice));
+    HIP_TRY(e, hipMemcpy(m + e->cls_ids_off, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
     e->cls_nwork = (int32_t)work.size();
     e->cls_width = width;
     e->cls_tiles = shard_tiles;
@@ -2275,20 +2357,24 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
     return KG_OK;
 }
 
-template <bool MOST, bool FIT_ON, bool LA_ON, bool W1, int KIND>
+template <bool MOST, bool FIT_ON, bool LA_ON, bool W1, int KIND, bool LAU>
 void launch_cls_kind(kg_engine *e, dim3 grid, const HotArgs &a, const kg_cls_desc *descs, const kg_cls_work *work,
-                     const char *rows, uint64_t *mask, uint16_t *scores, uint32_t *partials, hipStream_t stream) {
-    const int32_t first = e->cls_kind_work[KIND][0], count = e->cls_kind_work[KIND][1];
+                     const char *rows, const int32_t *ids, uint64_t *mask, uint16_t *scores, uint32_t *partials,
+                     hipStream_t stream) {
+    const int32_t first = e->cls_kind_work[2 * KIND + LAU][0], count = e->cls_kind_work[2 * KIND + LAU][1];
     if (count == 0) return;
-    grid.y = (unsigned)count;
-    // matrix mode: 8-pod chunks, score segments staged in LDS and written as 1 KiB wave stores; two nodes per
-    // lane (four: 92 VGPRs, 5 waves per SIMD, 1.98 vs 0.88 ms per config-2 pass, round 2)
-    if (mask)
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, KIND>), grid, dim3(KG_TILE / 2), 0, stream,
-                           e->consts, e->pl, a, descs, work + first, rows, mask, scores, partials);
-    else
-        hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, KIND>), grid, dim3(KG_TILE / 2), 0, stream,
-                           e->consts, e->pl, a, descs, work + first, rows, mask, scores, partials);
+    if constexpr (LAU && !LA_ON) return;   // (no such work items: cls_order_la)
+    else {
+        grid.y = (unsigned)count;
+        // matrix mode: 8-pod chunks, score segments staged in LDS and written as 1 KiB wave stores; two nodes per
+        // lane (four: 92 VGPRs, 5 waves per SIMD, 1.98 vs 0.88 ms per config-2 pass, round 2)
+        if (mask)
+            hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, true, W1, KIND, LAU>), grid, dim3(KG_TILE / 2), 0, stream,
+                               e->consts, e->pl, a, descs, work + first, rows, ids, mask, scores, partials);
+        else
+            hipLaunchKernelGGL((k_eval3<MOST, FIT_ON, LA_ON, false, W1, KIND, LAU>), grid, dim3(KG_TILE / 2), 0, stream,
+                               e->consts, e->pl, a, descs, work + first, rows, ids, mask, scores, partials);
+    }
 }
 
 template <bool MOST, bool FIT_ON, bool LA_ON, bool W1>
@@ -2297,6 +2383,7 @@ void launch_cls4(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint
     const kg_cls_desc *descs = (const kg_cls_desc *)m;
     const kg_cls_work *work = (const kg_cls_work *)(m + e->cls_work_off);
     const char *rows = m + e->cls_rows_off;
+    const int32_t *ids = (const int32_t *)(m + e->cls_ids_off);
     hipStream_t s2 = e->stream;
     if (e->cls_concurrent) {   // fork: stream2 starts after everything already queued on the engine stream
         if (!e->stream2) {
@@ -2308,10 +2395,15 @@ void launch_cls4(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint
         (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
         s2 = e->stream2;
     }
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 0>(e, grid, a, descs, work, rows, mask, scores, partials, e->stream);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 1>(e, grid, a, descs, work, rows, mask, scores, partials, s2);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 2>(e, grid, a, descs, work, rows, mask, scores, partials, e->stream);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 3>(e, grid, a, descs, work, rows, mask, scores, partials, s2);
+    // LoadAware-uniform work on the engine stream, the rest on stream2: one grid's tail is filled by the other's
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 0, true>(e, grid, a, descs, work, rows, ids, mask, scores, partials, e->stream);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 0, false>(e, grid, a, descs, work, rows, ids, mask, scores, partials, s2);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 1, true>(e, grid, a, descs, work, rows, ids, mask, scores, partials, e->stream);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 1, false>(e, grid, a, descs, work, rows, ids, mask, scores, partials, s2);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 2, true>(e, grid, a, descs, work, rows, ids, mask, scores, partials, e->stream);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 2, false>(e, grid, a, descs, work, rows, ids, mask, scores, partials, s2);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 3, true>(e, grid, a, descs, work, rows, ids, mask, scores, partials, e->stream);
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 3, false>(e, grid, a, descs, work, rows, ids, mask, scores, partials, s2);
     if (e->cls_concurrent) {   // join: the engine stream continues after both kinds
         (void)hipEventRecord(e->ev_join, s2);
         (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
@@ -2747,6 +2839,9 @@ kg_status kg_snapshot_upsert(kg_engine *e, const int32_t *node_index, const kg_n
         e->n_no_detail_nodes += (int)((facts[k] >> 2) & 1) - (int)((old >> 2) & 1);
         old = facts[k];
     }
+    // a new row invalidates the node's CPU table: bind_ready then asks for the matching kg_cpus_set (the feeders
+    // send both together), so a cpuset Reserve never runs the accumulator on CPUs of an older row
+    for (int32_t k = 0; k < n; k++) e->cpu_tab.erase(node_index[k]);
     const size_t rb = sizeof(kg_node_row) * (size_t)n, ib = sizeof(int32_t) * (size_t)n;
     st = ensure_scratch(e, rb + ib + 256);
     if (st) return st;
@@ -3062,6 +3157,12 @@ kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t
 // + ForgetPod).  Otherwise the device commits every plugin's Reserve (k_commit_one: zone allocations of the
 // same hint, AssumePod, LoadAware, ElasticQuota) and the host writes the taken CPUs into the table and the
 // node's cpuset counts into its row.
+// host_reserve's upload area at the head of the scratch buffer: the row, then (256-B aligned) its node index;
+// kg_place keeps its partial keys after it
+constexpr size_t kHostRowOff = 0, kHostNodeOff = (sizeof(kg_node_row) + 255) / 256 * 256;
+constexpr size_t kHostReserveHead = kHostNodeOff + 256;
+static_assert(kHostNodeOff >= kHostRowOff + sizeof(kg_node_row) && kHostNodeOff + 4 <= kHostReserveHead,
+              "the row and its node index fit the head");
 kg_status host_reserve(kg_engine *e, int32_t pod, int32_t node, bool *failed) {
     *failed = false;
     kg_node_row row;
@@ -3095,13 +3196,13 @@ kg_status host_reserve(kg_engine *e, int32_t pod, int32_t node, bool *failed) {
         HIP_TRY(e, hipStreamSynchronize(e->stream));
         kg_cpuset_row_fields(row, tab->cpus.data(), nc, tab->max_ref);
         // the row back, its planes re-derived (k_upsert)
-        kg_status st = ensure_scratch(e, sizeof(row) + 512);
+        kg_status st = ensure_scratch(e, kHostReserveHead);
         if (st) return st;
         char *sc = (char *)e->scratch;
-        HIP_TRY(e, hipMemcpyAsync(sc, &row, sizeof(row), hipMemcpyHostToDevice, e->stream));
-        HIP_TRY(e, hipMemcpyAsync(sc + (sizeof(row) + 255) / 256 * 256, &node, 4, hipMemcpyHostToDevice, e->stream));
-        hipLaunchKernelGGL(k_upsert, dim3(1), dim3(256), 0, e->stream, e->consts, e->pl, (const kg_node_row *)sc,
-                           (const int32_t *)(sc + (sizeof(row) + 255) / 256 * 256), 1);
+        HIP_TRY(e, hipMemcpyAsync(sc + kHostRowOff, &row, sizeof(row), hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(e, hipMemcpyAsync(sc + kHostNodeOff, &node, 4, hipMemcpyHostToDevice, e->stream));
+        hipLaunchKernelGGL(k_upsert, dim3(1), dim3(256), 0, e->stream, e->consts, e->pl, (const kg_node_row *)(sc + kHostRowOff),
+                           (const int32_t *)(sc + kHostNodeOff), 1);
         HIP_TRY(e, hipGetLastError());
     }
     HIP_TRY(e, hipStreamSynchronize(e->stream));
@@ -3205,8 +3306,8 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
     if (chunk > KG_MAX_CHUNK) chunk = KG_MAX_CHUNK;
     const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS;
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
-    // the host Reserve's row upload reuses the head of the scratch buffer: the partials live after it
-    const size_t head = 1024;
+    // the host Reserve's row upload uses the head of the scratch buffer: the partials live after it
+    const size_t head = kHostReserveHead;
     st = ensure_scratch(e, head + up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + 256);
     if (st) return st;
     char *s = (char *)e->scratch + head;

@@ -639,6 +639,16 @@ kg_status kg_build_node_rows(const kg_config *cfg, const kg_cluster_view *view, 
                 const int32_t max_ref = nm.max_ref_count > 0 ? nm.max_ref_count : 1;
                 if (kg_cpuset_row_fields(row, view->cpus + nm.first_cpu, nm.n_cpus, max_ref) != nm.cpuset_cpus)
                     return KG_ERR_INVALID_ARG;
+                // … and so must the per-zone counts (the rows of nodes with and without CPU detail take the zones'
+                // cpuset CPUs from the same facts)
+                for (int z = 0; z < nm.n_zones; z++) {
+                    int32_t held = 0;
+                    for (int32_t c = 0; c < nm.n_cpus; c++) {
+                        const kg_cpu_info &ci = view->cpus[nm.first_cpu + c];
+                        if (ci.refcount > 0 && ci.node == nm.zone_id[z]) held++;
+                    }
+                    if (held != nm.zone_cpuset_cpus[z]) return KG_ERR_INVALID_ARG;
+                }
             }
         }
     }
