@@ -397,6 +397,7 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     eng.set_profiling(True)
+    eng.reset_counters()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -407,6 +408,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    ctr = eng.counters()   # kg_counters_get over the timed steps (SURVEY §5 metrics)
     kernel_ms = eng.eval_kernel_times(args.steps)
     eng.set_profiling(False)
     elapsed = t1 - t0
@@ -526,6 +528,11 @@ def main():
             "config3": config3,
             "config5": config5,
             "pods_with_feasible_node": feasible_pods,
+            "engine_counters": {**ctr, "source": "kg_counters_get over the timed steps of rank 0",
+                                "evals_per_kernel_s": round(ctr["evals"] / (ctr["kernel_ns"] * 1e-9), 1)
+                                if ctr["kernel_ns"] else None,
+                                "out_GB_per_kernel_s": round(ctr["out_bytes"] / ctr["kernel_ns"], 1)
+                                if ctr["kernel_ns"] else None},
         }
         print(json.dumps(line), flush=True)
     eng.close()

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 8
+#define KG_ABI_VERSION 9
 #define KG_QUOTA_MAX_DEPTH 64 /* longest kg_quota parent chain (cycles are rejected) */
 
 /* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
@@ -535,7 +535,7 @@ enum kg_struct_id {
     KG_SID_RESOURCE_LIST = 0, KG_SID_CONFIG, KG_SID_CONTAINER, KG_SID_POD_SPEC,
     KG_SID_AGGREGATED_USAGE, KG_SID_POD_METRIC, KG_SID_ASSIGNED_POD, KG_SID_NODE_SPEC,
     KG_SID_CLUSTER_VIEW, KG_SID_POD_ROW, KG_SID_NODE_ROW, KG_SID_EVAL_OUT, KG_SID_NUMA_SPEC,
-    KG_SID_RESERVATION, KG_SID_QUOTA, KG_SID_RSV_RESTORED, KG_SID_CPU_INFO, KG_SID_COUNT
+    KG_SID_RESERVATION, KG_SID_QUOTA, KG_SID_RSV_RESTORED, KG_SID_CPU_INFO, KG_SID_COUNTERS, KG_SID_COUNT
 };
 int64_t kg_struct_size(int32_t sid);
 
@@ -668,6 +668,17 @@ int32_t kg_num_tiles(const kg_engine *eng);
 kg_status kg_place_chunk_eval(kg_engine *eng, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev);
 kg_status kg_place_chunk_resolve(kg_engine *eng, int64_t now_ns, int32_t pod_begin, int32_t n,
                                  const uint32_t *partial_dev, int32_t *out_node_dev, int64_t *out_score_dev);
+/* The pipelined form (dist.place_sharded): chunk i + 1 is evaluated — on the eval stream, beside its partial
+ * merge — while chunk i is resolved on the engine stream, so its partials may predate chunk i's commits.
+ * kg_place_chunk_resolve_prev takes the nodes chunk i placed (prev_nodes_dev[0..n_prev), device, −1 = none)
+ * and re-scores them like nodes this chunk touches (their keys in the lists are not trusted), exactly as the
+ * one-GPU kg_place pipeline does.  The caller orders the streams: eval(i + 1) after resolve(i − 1), resolve(i)
+ * after eval(i) and its merge.  Not with reservations (their per-pod entries are written by chunk_eval).
+ * kg_set_eval_stream: the stream kg_place_chunk_eval launches on (NULL ⇒ the engine stream); no sync. */
+kg_status kg_place_chunk_resolve_prev(kg_engine *eng, int64_t now_ns, int32_t pod_begin, int32_t n,
+                                      const uint32_t *partial_dev, int32_t *out_node_dev, int64_t *out_score_dev,
+                                      const int32_t *prev_nodes_dev, int32_t n_prev);
+kg_status kg_set_eval_stream(kg_engine *eng, void *hip_stream);
 
 /* Reservation cache (KG_PLUGIN_RESERVATION): replaces every reservation slot; a node holds at most
  * KG_MAX_RSV_PER_NODE.  Nodes carrying slots are evaluated on the exact per-pair path with the
@@ -694,6 +705,25 @@ kg_status kg_commit(kg_engine *eng, int32_t pod, int32_t node);
  * (< 0 on error). */
 kg_status kg_set_profiling(kg_engine *eng, int32_t on);
 int32_t kg_eval_kernel_times(kg_engine *eng, float *ms, int32_t n);
+
+/* Engine counters since creation or kg_counters_reset (SURVEY §5 "Metrics"; the reference's analogue is the
+ * scheduler's Prometheus set, pkg/scheduler/metrics/metrics.go:28-41): pod×node pairs evaluated (matrix mode
+ * and placement chunk evaluations), matrix-mode output bytes written, pods walked by placement resolves and
+ * pods placed (kg_place / kg_commit, where the outcome reaches the host), host→device bytes uploaded, and the
+ * device time of the k_eval launches timed under kg_set_profiling (evals ÷ that time = evals/s, output
+ * bytes ÷ it = the achieved write rate). */
+typedef struct kg_counters {
+    uint64_t eval_calls;        /* kg_eval + kg_place_chunk_eval calls */
+    uint64_t evals;             /* pod × node pairs evaluated */
+    uint64_t out_bytes;         /* mask + score planes + top-1 bytes written by matrix mode */
+    uint64_t resolved;          /* pods walked by placement resolves (kg_place, kg_place_chunk_resolve*) */
+    uint64_t placed;            /* pods placed by kg_place / kg_commit */
+    uint64_t h2d_bytes;         /* host → device bytes (snapshot rows, pod rows, class tables, reservations, ...) */
+    uint64_t timed_launches;    /* k_eval launches whose device time is in kernel_ns */
+    uint64_t kernel_ns;         /* their device time (HIP events, kg_set_profiling) */
+} kg_counters;
+kg_status kg_counters_get(kg_engine *eng, kg_counters *out);
+kg_status kg_counters_reset(kg_engine *eng);
 
 /* Helpers for consumers of matrix-mode output. */
 static inline int kg_mask_test(const uint64_t *mask, int32_t n_nodes, int32_t p, int32_t n) {

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 NUM_RES = 8
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
  RES_EXTENDED) = range(8)
@@ -143,8 +143,11 @@ RSV_RESTORED = np.dtype([
     ("nonzero", "<i8", (2,)), ("pod_count", "<i4"), ("n_matched", "<i4"), ("has_state", "<i4"), ("_pad", "<i4"),
 ], align=True)
 
+COUNTERS = np.dtype([(k, "<u8") for k in ("eval_calls", "evals", "out_bytes", "resolved", "placed", "h2d_bytes",
+                                            "timed_launches", "kernel_ns")])
+
 STRUCT_IDS = [RESOURCE_LIST, CONFIG, CONTAINER, POD_SPEC, AGGREGATED_USAGE, POD_METRIC, ASSIGNED_POD, NODE_SPEC,
-              None, POD_ROW, NODE_ROW, None, NUMA_SPEC, RESERVATION, QUOTA, RSV_RESTORED, CPU_INFO]
+              None, POD_ROW, NODE_ROW, None, NUMA_SPEC, RESERVATION, QUOTA, RSV_RESTORED, CPU_INFO, COUNTERS]
 
 
 class ClusterView(ctypes.Structure):
@@ -207,6 +210,7 @@ EXPORTED = [
     "kg_place_chunk_eval", "kg_place_chunk_resolve", "kg_commit", "kg_set_profiling", "kg_eval_kernel_times",
     "kg_rsv_set", "kg_rsv_download", "kg_quota_set", "kg_quota_download", "kg_row_eval_rsv", "kg_row_rsv_restore",
     "kg_snapshot_generation", "kg_cpuset_take", "kg_row_reserve", "kg_cpus_set", "kg_cpus_download",
+    "kg_place_chunk_resolve_prev", "kg_set_eval_stream", "kg_counters_get", "kg_counters_reset",
 ]
 
 _lib = None
@@ -252,6 +256,8 @@ def lib() -> ctypes.CDLL:
         "kg_cpuset_take": (i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp]),
         "kg_row_reserve": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
         "kg_cpus_set": (i32, [vp, vp, vp, vp, i32]), "kg_cpus_download": (i32, [vp, i32, vp, i32]),
+        "kg_place_chunk_resolve_prev": (i32, [vp, i64, i32, i32, vp, vp, vp, vp, i32]),
+        "kg_set_eval_stream": (i32, [vp, vp]), "kg_counters_get": (i32, [vp, vp]), "kg_counters_reset": (i32, [vp]),
     }
     for name, (res, args) in sig.items():
         if host_only and not hasattr(L, name):

@@ -742,11 +742,6 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __forceinline__ int kg_kofs(int i) { return (i >> 1) * 512 + (i & 1) * (2048 + 32); }
 #define KG_KBUF_DW (4096 + 32)
 
-#if defined(KG_AB) && (KG_AB & 64)
-#define KG_AB_LDSROW 1
-#else
-#define KG_AB_LDSROW 0
-#endif
 #define KG_EVAL3_CC 8    // pods per chunk (LDS key reduction, score staging, LoadAware-uniform chunks)
 #define KG_EVAL3_WPE0 6  // waves per SIMD k_eval3's (2, 2) kind is register-allocated for (r03 A/B: 5 / 6 / 8)
 
@@ -759,7 +754,7 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
                                          const ClsLa (&la)[2], const unsigned long long (&okm)[2],
                                          const uint32_t (&lsum)[2], int np_rt, const uint32_t (&kb)[2], uint32_t *kbuf,
                                          unsigned long long (&mb)[2], uint16_t *sst,
-                                         const kg_pod_cls_t<NC, NF> *__restrict__ grows, const kg_pod_cls_t<NC, NF> *lrw) {
+                                         const kg_pod_cls_t<NC, NF> *__restrict__ grows) {
     constexpr int CC = KG_EVAL3_CC;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -769,13 +764,7 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
     auto pod = [&](auto ic) {
         constexpr bool CT = !std::is_same<decltype(ic), int>::value;
         const int i = (int)ic;
-#if defined(KG_AB) && (KG_AB & 2)
-        const kg_pod_cls_t<NC, NF> pd = grows[0];
-#elif defined(KG_AB) && (KG_AB & 64)
-        const kg_pod_cls_t<NC, NF> pd = lrw[i];   // ds_read: wave-uniform values in VGPRs
-#else
         const kg_pod_cls_t<NC, NF> pd = grows[i];   // s_load into SGPRs
-#endif
         unsigned long long m[2];
 #pragma unroll
         for (int j = 0; j < 2; j++) m[j] = cls_ok_mask<NC, NF>(pd, n[j], okm[j]);
@@ -823,12 +812,6 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
             sst[i * 128 + 64 + lane] = (uint16_t)(s01 >> 16);
         }
     };
-#if defined(KG_AB) && (KG_AB & 16)
-    if (true) {
-        for (int i = 0; i < np; i++) { kbuf[kg_kofs(i) + tid] = 5; if (OUT) { sst[i * 128 + lane] = 7; sst[i * 128 + 64 + lane] = 9; } }
-        return;
-    }
-#endif
     if constexpr (UNR) {
         unroll_seq(std::make_integer_sequence<int, CC>{}, pod);
     } else {
@@ -848,7 +831,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
                                           const kg_cls_work &w, const char *__restrict__ rows_base,
                                           const int32_t *__restrict__ ids, uint64_t *__restrict__ mask,
                                           uint16_t *__restrict__ scores, uint32_t *__restrict__ partials,
-                                          uint32_t *kbuf, int32_t *lid, char *lrows, uint16_t *sstage) {
+                                          uint32_t *kbuf, int32_t *lid, uint16_t *sstage) {
     constexpr int CC = KG_EVAL3_CC;
     constexpr int BT = KG_TILE / 2;                       // threads of the workgroup
     constexpr int SEGW = 128;                             // score columns of one wave
@@ -883,25 +866,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     // the work item's output rows (for the stores and the partial keys) go to LDS once: the chunk loop issues no
     // vector loads, so nothing in it waits on vmcnt — i.e. on its own score stores
     const kg_pod_cls_t<NC, NF> *grows = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(rows_base + d.rows_offset);
-#if defined(KG_AB) && (KG_AB & 8)
-    if (tid < w.end - w.begin) lid[tid] = d.ids_first + w.begin + tid;
-#else
     if (tid < w.end - w.begin) lid[tid] = ids[d.ids_first + w.begin + tid];
-#endif
-    // pod rows through LDS (KG_AB & 64): chunk k's rows in slot k % 3, loaded two chunks ahead (the load is waited
-    // for after the chunk's own stores, so only stores a chunk older are waited for with it)
-    constexpr int RB = (int)sizeof(kg_pod_cls_t<NC, NF>), CHUNK_DW = KG_EVAL3_CC * RB / 4;
-    static_assert(CHUNK_DW <= 512, "one dword per thread stages a chunk of rows");
-    uint32_t *lrw32 = reinterpret_cast<uint32_t *>(lrows);
-    const uint32_t *gsrc = reinterpret_cast<const uint32_t *>(grows);
-    const int64_t src_end = (int64_t)w.end * (RB / 4);
-    const bool row_lds = KG_AB_LDSROW;
-    if (row_lds && tid < CHUNK_DW) {
-        for (int k = 0; k < 2; k++) {
-            const int64_t src = ((int64_t)w.begin + k * KG_EVAL3_CC) * (RB / 4) + tid;
-            if (src < src_end) lrw32[k * CHUNK_DW + tid] = gsrc[src];
-        }
-    }
     // every node-plane load has landed before the pod loop: the loop itself then never waits on
     // vector memory (its stores included)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -916,11 +881,6 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         const int p1 = min(p0 + CC, w.end);
         const int kslot = ci & 1;
         const int32_t *cur = lid + (p0 - w.begin);   // output rows of the chunk's pods
-        const kg_pod_cls_t<NC, NF> *crow = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(lrows + (ci % 3) * (CHUNK_DW * 4));
-        uint32_t staged = 0;
-        const int64_t src2 = ((int64_t)p0 + 2 * KG_EVAL3_CC) * (RB / 4) + tid;
-        const bool ahead = row_lds && tid < CHUNK_DW && src2 < src_end;
-        if (ahead) staged = gsrc[src2];
         uint32_t *kcur = kbuf + kslot * KG_KBUF_DW;
         unsigned long long mb[2] = {0ull, 0ull};
         if (LAU) {
@@ -939,7 +899,7 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
         }
 #define KG_CLS_PODS(FULL_, UNR_)                                                                              \
     cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, UNR_, LAU>(c, d, n, la, okm, lsum, p1 - p0, kb, kcur, mb, sst, \
-                                                                     grows + p0, crow)
+                                                                     grows + p0)
         if (full && p1 - p0 == CC) KG_CLS_PODS(true, true);
         else if (full) KG_CLS_PODS(true, false);
         else KG_CLS_PODS(false, false);
@@ -957,40 +917,20 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
 #pragma unroll
             for (int it = 0; it < CC / PPS; it++) {
                 const int pp = it * PPS + lane / LP;
-#if defined(KG_AB) && (KG_AB & 1)
-                if (false) {
-#else
                 if (whole || (pp < np && segs)) {
-#endif
                     const uint4 v = *reinterpret_cast<const uint4 *>(sst + pp * SEGW + s8 * 8);
                     const int64_t off = (int64_t)cur[pp] * a.score_stride;
-#if defined(KG_AB) && (KG_AB & 32)
-                    *reinterpret_cast<u32x4 *>(scores + off + col0 + s8 * 8) = u32x4{v.x, v.y, v.z, v.w};
-#elif defined(KG_AB) && (KG_AB & 128)
-                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(scores + off + col0 + s8 * 8), "v"(u32x4{v.x, v.y, v.z, v.w}) : "memory");
-#elif defined(KG_AB) && (KG_AB & 256)
-                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(scores + off + col0 + s8 * 8), "v"(u32x4{v.x, v.y, v.z, v.w}) : "memory");
-#elif defined(KG_AB) && (KG_AB & 512)
-                    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(scores + off + col0 + s8 * 8), "v"(u32x4{v.x, v.y, v.z, v.w}) : "memory");
-#elif defined(KG_AB) && (KG_AB & 1024)
-                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(scores + off + col0 + s8 * 8), "v"(u32x4{v.x, v.y, v.z, v.w}) : "memory");
-#else
+                    // non-temporal (a write-once stream): plain stores of the same data measured 0.94 vs 0.67 ms per pass
                     __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(scores + off + col0 + s8 * 8));
-#endif
                 }
             }
-#if defined(KG_AB) && (KG_AB & 4)
-            if (false) {
-#else
             if (lane < np && seg[0]) {
-#endif
                 // lane l writes the two feasibility words of pod p0 + l
                 uint64_t *mw = mask + (int64_t)cur[lane] * a.mask_words + (col0 >> 6);
                 mw[0] = mb[0];
                 if (seg[1]) mw[1] = mb[1];
             }
         }
-        if (ahead) lrw32[((ci + 2) % 3) * CHUNK_DW + tid] = staged;
         // one barrier per chunk: after it, one wave (rotating) reduces the chunk's keys while the others go on
         // with the next chunk, whose keys go to the other key buffer.  A key buffer is written again two chunks
         // later, after the next barrier, which the reducing wave reaches only after its reduction.
@@ -1029,11 +969,10 @@ __global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIN
     __shared__ __attribute__((aligned(16))) uint32_t kbuf[2 * KG_KBUF_DW];
     static_assert(CC * BT <= 4096, "a chunk's keys fit the key buffer");
     __shared__ int32_t lid[KG_CLS_ITEM_MAX];
-    __shared__ __attribute__((aligned(16))) char lrows[KG_AB_LDSROW ? 3 * CC * (int)sizeof(kg_pod_cls_t<4, 4>) : 16];
     __shared__ __attribute__((aligned(16))) uint16_t sstage[OUT ? (BT / 64) * CC * 128 : 8];
     const kg_cls_work w = work[blockIdx.y];
     const kg_cls_desc d = descs[w.cls];
-#define KG_CLS_ARGS c, pl, a, d, w, rows, ids, mask, scores, partials, kbuf, lid, lrows, sstage
+#define KG_CLS_ARGS c, pl, a, d, w, rows, ids, mask, scores, partials, kbuf, lid, sstage
     if constexpr (KIND == 0) cls_block<2, 2, MOST, FIT_ON, LA_ON, OUT, W1, LAU>(KG_CLS_ARGS);
     else if constexpr (KIND == 1) cls_block<2, 4, MOST, FIT_ON, LA_ON, OUT, W1, LAU>(KG_CLS_ARGS);
     else if constexpr (KIND == 2) cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1, LAU>(KG_CLS_ARGS);
@@ -2035,7 +1974,8 @@ struct kg_engine {
     bool cls_concurrent = true;
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    bool place_pipeline = true;         // kg_place overlaps chunk i + 1's evaluation with chunk i's resolve
+    int place_pipeline = 1;             // kg_place overlaps chunk i + 1's evaluation with chunk i's resolve: 1 for
+                                        // NodeNUMAResource batches, 2 for every batch, 0 never (KG_PLACE_PIPELINE)
     hipEvent_t ev_res[3] = {};          // (KG_PLACE_PIPELINE=0 turns it off)
     // Reservation / ElasticQuota (config 5)
     void *rsv_mem = nullptr;            // slots | rfirst | rnode | E | O
@@ -2050,6 +1990,9 @@ struct kg_engine {
     int32_t n_quota = 0;
     int32_t max_pod_quota = -1;         // largest quota index of the batch
     uint8_t *gate = nullptr;            // [pods] ElasticQuota PreFilter outcome (matrix mode)
+    kg_counters ctr{};                  // kg_counters_get
+    int64_t ev_acc = 0;                 // profiled launches already summed into ctr.kernel_ns
+    hipStream_t eval_stream = nullptr;  // kg_set_eval_stream (kg_place_chunk_eval), nullptr ⇒ stream
     static constexpr int kRing = 256;   // event pairs: one per profiled k_eval launch
     hipEvent_t ev0[kRing] = {}, ev1[kRing] = {};
     int64_t ev_count = 0;               // launches recorded since kg_set_profiling
@@ -2076,6 +2019,12 @@ kg_status set_err(kg_engine *e, kg_status code, const char *fmt, ...) {
         hipError_t _st = (expr);                                                                 \
         if (_st != hipSuccess) return set_err(e, KG_ERR_HIP, "%s: %s", #expr, hipGetErrorString(_st)); \
     } while (0)
+
+// host → device copies go through here (kg_counters.h2d_bytes)
+hipError_t h2d(kg_engine *e, void *dst, const void *src, size_t bytes, hipStream_t s) {
+    e->ctr.h2d_bytes += bytes;
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+}
 
 kg_status ensure_scratch(kg_engine *e, size_t bytes) {
     if (e->scratch_bytes >= bytes) return KG_OK;
@@ -2289,7 +2238,7 @@ void cls_fill_row(const kg_engine *e, const kg_cls_desc &d, const kg_pod_row &r,
 // Lay the class rows out for the shard width (output offsets) and the work table for its tiles.
 kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
     if (!e->cls_dirty && e->cls_width == width && e->cls_tiles == shard_tiles) return KG_OK;
-    const int64_t words = (width + 63) / 64, stride = words * 64;
+    const int64_t words = (width + 63) / 64;
     if ((int64_t)e->pod_rows_h.size() * words >= (1LL << 31)) return set_err(e, KG_ERR_RANGE, "mask too large");
     std::vector<kg_cls_desc> descs = e->cls_desc;
     std::vector<kg_cls_work> work;
@@ -2345,11 +2294,12 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
     e->cls_work_off = up(desc_b);
     e->cls_rows_off = up(desc_b) + up(work_b);
     char *m = (char *)e->cls_mem;
-    HIP_TRY(e, hipMemcpy(m, descs.data(), sizeof(kg_cls_desc) * descs.size(), hipMemcpyHostToDevice));
-    if (!work.empty()) HIP_TRY(e, hipMemcpy(m + e->cls_work_off, work.data(), sizeof(kg_cls_work) * work.size(), hipMemcpyHostToDevice));
+    HIP_TRY(e, h2d(e, m, descs.data(), sizeof(kg_cls_desc) * descs.size(), e->stream));
+    if (!work.empty()) HIP_TRY(e, h2d(e, m + e->cls_work_off, work.data(), sizeof(kg_cls_work) * work.size(), e->stream));
     e->cls_ids_off = e->cls_rows_off + up(rows.size());
-    if (!rows.empty()) HIP_TRY(e, hipMemcpy(m + e->cls_rows_off, rows.data(), rows.size(), hipMemcpyHostToDevice));
-    HIP_TRY(e, hipMemcpy(m + e->cls_ids_off, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+    if (!rows.empty()) HIP_TRY(e, h2d(e, m + e->cls_rows_off, rows.data(), rows.size(), e->stream));
+    HIP_TRY(e, h2d(e, m + e->cls_ids_off, ids.data(), ids.size() * 4, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));   // the host vectors end with this call
     e->cls_nwork = (int32_t)work.size();
     e->cls_width = width;
     e->cls_tiles = shard_tiles;
@@ -2684,7 +2634,7 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
     const char *nq = getenv("KG_NUMA_QUEUE");
     e->numa_queue_mode = nq ? atoi(nq) : 1;
     const char *pp = getenv("KG_PLACE_PIPELINE");
-    e->place_pipeline = !pp || atoi(pp) != 0;
+    e->place_pipeline = pp ? atoi(pp) : 1;
     const char *cc = getenv("KG_CLS_CONCURRENT");   // default on: 0.84 vs 0.87 ms per config-2 pass (r03 A/B)
     e->cls_concurrent = !cc || atoi(cc) != 0;
     *out = e;
@@ -2846,8 +2796,8 @@ kg_status kg_snapshot_upsert(kg_engine *e, const int32_t *node_index, const kg_n
     st = ensure_scratch(e, rb + ib + 256);
     if (st) return st;
     char *s = (char *)e->scratch;
-    HIP_TRY(e, hipMemcpyAsync(s, rows, rb, hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(e, hipMemcpyAsync(s + (rb + 255) / 256 * 256, node_index, ib, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, h2d(e, s, rows, rb, e->stream));
+    HIP_TRY(e, h2d(e, s + (rb + 255) / 256 * 256, node_index, ib, e->stream));
     hipLaunchKernelGGL(k_upsert, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->consts, e->pl,
                        (const kg_node_row *)s, (const int32_t *)(s + (rb + 255) / 256 * 256), n);
     HIP_TRY(e, hipGetLastError());
@@ -2952,8 +2902,8 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
         e->hot_bytes = sizeof(kg_pod_hot_t<8>) * (size_t)(n > 0 ? n : 1);
     }
     if (n) {
-        HIP_TRY(e, hipMemcpyAsync(e->pods, dev.data(), sizeof(kg_pod_dev) * (size_t)n, hipMemcpyHostToDevice, e->stream));
-        HIP_TRY(e, hipMemcpyAsync(e->hot, hot.data(), hot.size(), hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(e, h2d(e, e->pods, dev.data(), sizeof(kg_pod_dev) * (size_t)n, e->stream));
+        HIP_TRY(e, h2d(e, e->hot, hot.data(), hot.size(), e->stream));
     }
     // k_eval_numa2 runs a wave's 64 pods in lockstep through the hint enumeration, whose trip counts
     // depend on the pod's hint lists: matrix mode visits the pods grouped by (list count, cpu,
@@ -2971,7 +2921,7 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
                 return dev[x].numa_req[KG_RES_CPU] < dev[y].numa_req[KG_RES_CPU];
             return dev[x].numa_req[KG_RES_MEMORY] < dev[y].numa_req[KG_RES_MEMORY];
         });
-        HIP_TRY(e, hipMemcpyAsync(e->numa_perm, order.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(e, h2d(e, e->numa_perm, order.data(), sizeof(int32_t) * (size_t)n, e->stream));
     }
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     e->nslot = nslot;
@@ -3016,6 +2966,10 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     const bool stage_scores = planes && (!dev || !out->scores);
     const size_t numa_b = (size_t)P * (size_t)((width + 63) / 64 * 64);
     const bool numa_on = (e->consts.plugins & KG_PLUGIN_NUMA) != 0;
+    e->ctr.eval_calls++;
+    e->ctr.evals += (uint64_t)P * (uint64_t)width;
+    e->ctr.out_bytes += (out->mask ? mask_b : 0) + (out->scores ? score_b : 0) + (out->top1 ? top_b : 0) +
+                        (out->numa_scores ? numa_b : 0) + (out->rsv_scores ? numa_b : 0);
     const bool stage_numa = out->numa_scores && !dev;
     const bool stage_rsv = out->rsv_scores && !dev;
     size_t need = up(part_b) + up(top_b) + (stage_mask ? up(mask_b) : 0) + (stage_scores ? up(score_b) : 0) +
@@ -3108,6 +3062,8 @@ namespace {
 kg_status chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev) {
     if (pod_begin < 0 || n < 0 || pod_begin + (int64_t)n > e->n_pods || (n > 0 && !partial_dev))
         return set_err(e, KG_ERR_RANGE, "bad chunk");
+    e->ctr.eval_calls++;
+    e->ctr.evals += (uint64_t)n * (uint64_t)(e->shard_end - e->shard_begin);
     // the top-k kernel writes every slot of every tile of its shard; the NUMA kernel merges with atomics
     // and a shard leaves the other ranks' tiles to the merge: those start from zeros
     const bool whole = e->shard_begin == 0 && e->shard_end == e->n_nodes;
@@ -3133,6 +3089,7 @@ kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t
     if (n == 0) return KG_OK;
     kg_status st = quota_ready(e);
     if (st) return st;
+    e->ctr.resolved += (uint64_t)n;
     RsvArgs ra = rsv_args(e);
     if (ra.rsv) {  // this chunk's entries were written by kg_place_chunk_eval from row 0
         if (n > KG_RSV_POD_CHUNK) return set_err(e, KG_ERR_RANGE, "chunk larger than the reservation entry buffer");
@@ -3199,8 +3156,8 @@ kg_status host_reserve(kg_engine *e, int32_t pod, int32_t node, bool *failed) {
         kg_status st = ensure_scratch(e, kHostReserveHead);
         if (st) return st;
         char *sc = (char *)e->scratch;
-        HIP_TRY(e, hipMemcpyAsync(sc + kHostRowOff, &row, sizeof(row), hipMemcpyHostToDevice, e->stream));
-        HIP_TRY(e, hipMemcpyAsync(sc + kHostNodeOff, &node, 4, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(e, h2d(e, sc + kHostRowOff, &row, sizeof(row), e->stream));
+        HIP_TRY(e, h2d(e, sc + kHostNodeOff, &node, 4, e->stream));
         hipLaunchKernelGGL(k_upsert, dim3(1), dim3(256), 0, e->stream, e->consts, e->pl, (const kg_node_row *)(sc + kHostRowOff),
                            (const int32_t *)(sc + kHostNodeOff), 1);
         HIP_TRY(e, hipGetLastError());
@@ -3220,7 +3177,32 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
     if (st) return st;
     st = bind_ready(e, true);
     if (st) return st;
-    return chunk_eval(e, now_ns, pod_begin, n, partial_dev);
+    hipStream_t main_s = e->stream;
+    if (e->eval_stream) e->stream = e->eval_stream;   // chunk_eval launches on e->stream
+    st = chunk_eval(e, now_ns, pod_begin, n, partial_dev);
+    e->stream = main_s;
+    return st;
+}
+
+kg_status kg_set_eval_stream(kg_engine *e, void *s) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    e->eval_stream = (hipStream_t)s;
+    return KG_OK;
+}
+
+kg_status kg_place_chunk_resolve_prev(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n,
+                                      const uint32_t *partial_dev, int32_t *out_node_dev, int64_t *out_score_dev,
+                                      const int32_t *prev_nodes_dev, int32_t n_prev) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    st = bind_ready(e, true);
+    if (st) return st;
+    if (n_prev < 0 || n_prev > KG_MAX_CHUNK || (n_prev > 0 && !prev_nodes_dev))
+        return set_err(e, KG_ERR_RANGE, "bad previous-chunk node list");
+    if (n_prev > 0 && rsv_args(e).rsv)
+        return set_err(e, KG_ERR_UNSUPPORTED, "pipelined resolve with reservations (chunk_eval writes their entries)");
+    return chunk_resolve(e, now_ns, pod_begin, n, partial_dev, out_node_dev, out_score_dev, false, prev_nodes_dev, n_prev);
 }
 
 kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, const uint32_t *partial_dev,
@@ -3291,7 +3273,19 @@ kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64
 
 extern "C" {
 
+kg_status place_impl(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score);
+
 kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score) {
+    const uint64_t resolved0 = e ? e->ctr.resolved : 0;
+    const kg_status st = place_impl(e, now_ns, out_node, out_score);
+    if (st == KG_OK) {
+        e->ctr.resolved = resolved0 + (uint64_t)e->n_pods;   // (the chunk resolves inside counted the same pods)
+        for (int32_t p = 0; p < e->n_pods; p++) e->ctr.placed += out_node[p] >= 0 ? 1u : 0u;
+    }
+    return st;
+}
+
+kg_status place_impl(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score) {
     kg_status st = check_engine(e);
     if (st) return st;
     if (!out_node || !out_score) return set_err(e, KG_ERR_INVALID_ARG, "null outputs");
@@ -3320,7 +3314,8 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
     const uint8_t may_mask = e->n_node_bind_nodes > 0 ? 3 : 1;
     // the pipeline pays two cross-stream event hops per chunk: it wins where the chunk evaluation is long
     // (NodeNUMAResource: config 3 5.0k → 6.1k pods/s) and loses where it is short (config 2: 82k → 61k)
-    if (!bind_mode && !rsv_args(e).rsv && e->place_pipeline && (e->consts.plugins & KG_PLUGIN_NUMA))
+    if (!bind_mode && !rsv_args(e).rsv &&
+        (e->place_pipeline == 2 || (e->place_pipeline == 1 && (e->consts.plugins & KG_PLUGIN_NUMA))))
         return place_pipelined(e, now_ns, out_node, out_score, chunk);
     // the placement kernels answer cpusets on NUMA-policy nodes for this batch (kg_consts.numa_bz)
     struct BzScope {
@@ -3354,8 +3349,8 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
                 if (failed) {   // the Reserve failed: the pod is not placed
                     const int32_t no = -1;
                     const int64_t ns = -1;
-                    HIP_TRY(e, hipMemcpyAsync(dnode + j, &no, 4, hipMemcpyHostToDevice, e->stream));
-                    HIP_TRY(e, hipMemcpyAsync(dscore + j, &ns, 8, hipMemcpyHostToDevice, e->stream));
+                    HIP_TRY(e, h2d(e, dnode + j, &no, 4, e->stream));
+                    HIP_TRY(e, h2d(e, dscore + j, &ns, 8, e->stream));
                     HIP_TRY(e, hipStreamSynchronize(e->stream));
                 }
             }
@@ -3425,6 +3420,35 @@ kg_status kg_set_profiling(kg_engine *e, int32_t on) {
     }
     e->profiling = on != 0;
     e->ev_count = 0;
+    e->ev_acc = 0;
+    return KG_OK;
+}
+
+kg_status kg_counters_get(kg_engine *e, kg_counters *out) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (!out) return set_err(e, KG_ERR_INVALID_ARG, "null output");
+    if (e->profiling) {   // the timed launches not summed yet (the ring keeps the last kRing)
+        const int64_t from = std::max(e->ev_acc, e->ev_count - (int64_t)kg_engine::kRing);
+        for (int64_t k = from; k < e->ev_count; k++) {
+            const int64_t slot = k % kg_engine::kRing;
+            float ms = 0.f;
+            HIP_TRY(e, hipEventSynchronize(e->ev1[slot]));
+            HIP_TRY(e, hipEventElapsedTime(&ms, e->ev0[slot], e->ev1[slot]));
+            e->ctr.kernel_ns += (uint64_t)((double)ms * 1e6);
+            e->ctr.timed_launches++;
+        }
+        e->ev_acc = e->ev_count;
+    }
+    *out = e->ctr;
+    return KG_OK;
+}
+
+kg_status kg_counters_reset(kg_engine *e) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    e->ctr = kg_counters{};
+    e->ev_acc = e->ev_count;
     return KG_OK;
 }
 
@@ -3487,10 +3511,10 @@ kg_status kg_rsv_set(kg_engine *e, const kg_reservation *rsv, int32_t n) {
     e->rnode = (int32_t *)(m + sb + fb);
     e->rsv_e = (unsigned long long *)(m + sb + fb + nb);
     e->rsv_o = (int64_t *)(m + sb + fb + nb + eb);
-    if (n) HIP_TRY(e, hipMemcpyAsync(e->rsv, slots.data(), sizeof(kg_reservation) * (size_t)n, hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(e, hipMemcpyAsync(e->rfirst, rfirst.data(), 4 * rfirst.size(), hipMemcpyHostToDevice, e->stream));
-    if (n_rn) HIP_TRY(e, hipMemcpyAsync(e->rnode, rnode.data(), 4 * (size_t)n_rn, hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(e, hipMemcpyAsync(e->pl.rsv_of, rsv_of.data(), 4 * rsv_of.size(), hipMemcpyHostToDevice, e->stream));
+    if (n) HIP_TRY(e, h2d(e, e->rsv, slots.data(), sizeof(kg_reservation) * (size_t)n, e->stream));
+    HIP_TRY(e, h2d(e, e->rfirst, rfirst.data(), 4 * rfirst.size(), e->stream));
+    if (n_rn) HIP_TRY(e, h2d(e, e->rnode, rnode.data(), 4 * (size_t)n_rn, e->stream));
+    HIP_TRY(e, h2d(e, e->pl.rsv_of, rsv_of.data(), 4 * rsv_of.size(), e->stream));
     e->n_rsv = n;
     e->n_rn = n_rn;
     e->rsv_perm = order;
@@ -3534,7 +3558,7 @@ kg_status kg_quota_set(kg_engine *e, const kg_quota *q, int32_t n) {
     if (e->quota) HIP_TRY(e, hipFree(e->quota));
     e->quota = nullptr;
     HIP_TRY(e, hipMalloc(&e->quota, sizeof(kg_quota) * (size_t)(n > 0 ? n : 1)));
-    if (n) HIP_TRY(e, hipMemcpyAsync(e->quota, q, sizeof(kg_quota) * (size_t)n, hipMemcpyHostToDevice, e->stream));
+    if (n) HIP_TRY(e, h2d(e, e->quota, q, sizeof(kg_quota) * (size_t)n, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     e->n_quota = n;
     return KG_OK;
@@ -3562,6 +3586,7 @@ kg_status kg_commit(kg_engine *e, int32_t pod, int32_t node) {
     st = host_reserve(e, pod, node, &failed);
     if (st) return st;
     if (failed) return set_err(e, KG_NOT_FOUND, "pod %d on node %d: not enough cpus available to satisfy request", pod, node);
+    e->ctr.placed++;
     return KG_OK;
 }
 

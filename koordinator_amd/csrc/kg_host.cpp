@@ -335,6 +335,7 @@ int64_t kg_struct_size(int32_t sid) {
         case KG_SID_QUOTA: return sizeof(kg_quota);
         case KG_SID_RSV_RESTORED: return sizeof(kg_rsv_restored);
         case KG_SID_CPU_INFO: return sizeof(kg_cpu_info);
+        case KG_SID_COUNTERS: return sizeof(kg_counters);
     }
     return -1;
 }

@@ -74,31 +74,79 @@ class ChunkBackend(Protocol):
 
 
 def place_sharded(backend: ChunkBackend, now_ns: int, device: torch.device, chunk: int = 8,
-                  group=None) -> Tuple[np.ndarray, np.ndarray]:
+                  group=None, pipeline: Optional[bool] = None,
+                  collective: Optional[bool] = None) -> Tuple[np.ndarray, np.ndarray]:
     """Sequential-cycle placement of the backend's pod batch, node-sharded across the group.
 
     The backend must hold the full (replicated) snapshot with its evaluation restricted to this
-    rank's `shard_range`. Returns (node or −1, total or −1) per pod, identical on every rank."""
+    rank's `shard_range`. Returns (node or −1, total or −1) per pod, identical on every rank.
+
+    pipeline (default: when the backend offers it, ``backend.eval_torch_stream``): chunk i + 1 is evaluated and
+    its partials merged on the eval stream while chunk i is resolved on the backend's stream; the resolve of
+    chunk i + 1 re-scores the nodes chunk i placed (``kg_place_chunk_resolve_prev``), as the one-GPU kg_place
+    pipeline does.  collective (default: world size > 1) runs the partial-key merge even on one rank (the RCCL
+    path exercised alone)."""
     if chunk < 1 or chunk > nat.PLACE_CHUNK_MAX:
         raise ValueError(f"chunk {chunk} outside 1..{nat.PLACE_CHUNK_MAX}")
     world = dist.get_world_size(group) if dist.is_initialized() else 1
+    merge = world > 1 if collective is None else collective
     P, tiles = backend.n_pods, backend.num_tiles
     stream = getattr(backend, "torch_stream", None)
-    with torch.cuda.stream(stream) if stream is not None else _nullctx():
-        slots = getattr(backend, "partial_slots", 1)
-        partial = torch.zeros((max(chunk, 1), tiles, slots), dtype=torch.int32, device=device)
+    eval_stream = getattr(backend, "eval_torch_stream", None)
+    if pipeline is None:
+        pipeline = eval_stream is not None
+    if pipeline and (eval_stream is None or stream is None):
+        raise ValueError("the pipelined placement needs the backend's eval and resolve streams")
+    slots = getattr(backend, "partial_slots", 1)
+    if not pipeline:
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():
+            partial = torch.zeros((max(chunk, 1), tiles, slots), dtype=torch.int32, device=device)
+            nodes = torch.full((max(P, 1),), -1, dtype=torch.int32, device=device)
+            scores = torch.full((max(P, 1),), -1, dtype=torch.int64, device=device)
+            for b in range(0, P, chunk):
+                n = min(chunk, P - b)
+                if eval_stream is not None:   # the engine evaluates on its eval stream: order it in
+                    eval_stream.wait_stream(stream)
+                backend.chunk_eval(now_ns, b, n, partial.data_ptr())
+                if eval_stream is not None:
+                    stream.wait_stream(eval_stream)
+                if merge:
+                    merge_partials_(partial[:n], group)
+                backend.chunk_resolve(now_ns, b, n, partial.data_ptr(), nodes.data_ptr() + 4 * b,
+                                      scores.data_ptr() + 8 * b)
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            return nodes[:P].cpu().numpy(), scores[:P].cpu().numpy()
+    # pipelined: eval(i) + merge(i) on eval_stream, resolve(i) on stream; eval(i) waits for resolve(i − 2) (its
+    # partial buffer, and the snapshot older than one chunk), resolve(i) for eval(i) + merge(i)
+    with torch.cuda.stream(stream):
         nodes = torch.full((max(P, 1),), -1, dtype=torch.int32, device=device)
         scores = torch.full((max(P, 1),), -1, dtype=torch.int64, device=device)
-        for b in range(0, P, chunk):
-            n = min(chunk, P - b)
-            backend.chunk_eval(now_ns, b, n, partial.data_ptr())
-            if world > 1:
-                merge_partials_(partial[:n], group)
-            backend.chunk_resolve(now_ns, b, n, partial.data_ptr(), nodes.data_ptr() + 4 * b,
-                                  scores.data_ptr() + 8 * b)
-        if device.type == "cuda":
-            torch.cuda.synchronize(device)
-        return nodes[:P].cpu().numpy(), scores[:P].cpu().numpy()
+    eval_stream.wait_stream(stream)
+    with torch.cuda.stream(eval_stream):
+        partial = [torch.zeros((max(chunk, 1), tiles, slots), dtype=torch.int32, device=device) for _ in range(2)]
+    stream.wait_stream(eval_stream)
+    ev_eval = [torch.cuda.Event() for _ in range(2)]
+    ev_res = [torch.cuda.Event() for _ in range(3)]
+    prev_b = prev_n = 0
+    for i, b in enumerate(range(0, P, chunk)):
+        n = min(chunk, P - b)
+        part = partial[i & 1]
+        if i >= 2:
+            eval_stream.wait_event(ev_res[(i - 2) % 3])
+        with torch.cuda.stream(eval_stream):
+            backend.chunk_eval(now_ns, b, n, part.data_ptr())
+            if merge:
+                merge_partials_(part[:n], group)
+            ev_eval[i & 1].record(eval_stream)
+        stream.wait_event(ev_eval[i & 1])
+        with torch.cuda.stream(stream):
+            backend.chunk_resolve(now_ns, b, n, part.data_ptr(), nodes.data_ptr() + 4 * b, scores.data_ptr() + 8 * b,
+                                  nodes.data_ptr() + 4 * prev_b if i else 0, prev_n if i else 0)
+            ev_res[i % 3].record(stream)
+        prev_b, prev_n = b, n
+    torch.cuda.synchronize(device)
+    return nodes[:P].cpu().numpy(), scores[:P].cpu().numpy()
 
 
 class _nullctx:
@@ -137,6 +185,9 @@ def sharded_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray,
     eng = Engine(cfg)
     eng.torch_stream = torch.cuda.Stream(device)
     eng.set_stream(eng.torch_stream.cuda_stream)
+    if reservations is None:   # the pipelined placement (reservation entries are written by chunk_eval)
+        eng.eval_torch_stream = torch.cuda.Stream(device)
+        eng.set_eval_stream(eng.eval_torch_stream.cuda_stream)
     eng.load_snapshot(node_rows)
     if reservations is not None:
         eng.set_reservations(reservations)

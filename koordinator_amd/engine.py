@@ -251,10 +251,31 @@ class Engine:
                "kg_place_chunk_eval")
 
     def chunk_resolve(self, now_ns: int, pod_begin: int, n: int, partial_ptr: int, node_ptr: int,
-                      score_ptr: int) -> None:
+                      score_ptr: int, prev_ptr: int = 0, n_prev: int = 0) -> None:
+        """kg_place_chunk_resolve; with prev_ptr / n_prev the pipelined form kg_place_chunk_resolve_prev (the
+        previous chunk's placements, device int32, re-scored like touched nodes)."""
+        if n_prev:
+            _check(nat.lib().kg_place_chunk_resolve_prev(self._h, int(now_ns), pod_begin, n, ctypes.c_void_p(partial_ptr),
+                                                         ctypes.c_void_p(node_ptr), ctypes.c_void_p(score_ptr),
+                                                         ctypes.c_void_p(prev_ptr), n_prev), self,
+                   "kg_place_chunk_resolve_prev")
+            return
         _check(nat.lib().kg_place_chunk_resolve(self._h, int(now_ns), pod_begin, n, ctypes.c_void_p(partial_ptr),
                                                 ctypes.c_void_p(node_ptr), ctypes.c_void_p(score_ptr)), self,
                "kg_place_chunk_resolve")
+
+    def set_eval_stream(self, hip_stream: int) -> None:
+        """kg_set_eval_stream: chunk evaluations launch on this stream (0 ⇒ the engine stream)."""
+        _check(nat.lib().kg_set_eval_stream(self._h, ctypes.c_void_p(hip_stream or None)), self, "kg_set_eval_stream")
+
+    def counters(self) -> dict:
+        """kg_counters_get as a dict (evals, out_bytes, resolved, placed, h2d_bytes, kernel_ns, ...)."""
+        out = np.zeros(1, dtype=nat.COUNTERS)
+        _check(nat.lib().kg_counters_get(self._h, nat.ptr(out)), self, "kg_counters_get")
+        return {k: int(out[k][0]) for k in nat.COUNTERS.names}
+
+    def reset_counters(self) -> None:
+        _check(nat.lib().kg_counters_reset(self._h), self, "kg_counters_reset")
 
     def commit(self, pod: int, node: int) -> bool:
         """kg_commit; False ⇔ the Reserve failed (a cpuset the accumulator cannot take; nothing changed)."""
