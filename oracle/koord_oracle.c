@@ -1724,52 +1724,96 @@ static void rsv_index_free(rsv_index *ri) { free(ri->states); free(ri->of); free
  * Score / NormalizeScore (Reservation), weights.  Optional per-node outputs.  Returns the best
  * node (lowest index on ties) or −1; *best_total its weighted total, *best_nom the nominated
  * reservation (index into that node's list) or −1. */
-static int32_t oracle_pod(const kg_config *c, kg_cluster_view *vv, node_state *st, const rsv_index *ri, int32_t N,
-                          const kg_pod_spec *pod, int64_t now_ns, const kg_quota *quotas, uint8_t *mask,
-                          uint8_t *fitp, uint8_t *lap, uint8_t *numap, uint8_t *rsvp, int64_t *best_total,
-                          int *best_nom) {
-    const int rsv_on = (c->enabled_plugins & KG_PLUGIN_RESERVATION) != 0;
+/* One pod's evaluation, node by node (the body of findNodesThatPassFilters + prioritizeNodes for one
+ * node): Filter of every plugin on the (reservation-restored) NodeInfo, the plugins' scores, Reservation
+ * PreScore.  Nodes are independent, so the parallel cycle (kgo_schedule2_parallel) runs this per node on
+ * worker threads exactly as the sequential one does. */
+typedef struct {
+    const kg_config *c;
+    kg_cluster_view *vv;
+    node_state *st;
+    const rsv_index *ri;
+    const kg_pod_spec *pod;
+    int64_t now_ns;
+    int gate, rsv_on;
     kg_resource_list preq;
-    numa_pod_requests(vv, pod, &preq);
-    const int gate = !(c->enabled_plugins & KG_PLUGIN_ELASTICQUOTA) || quota_prefilter(c, pod, &preq, quotas);
-    int64_t *base = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
-    int64_t *raw = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
-    int64_t *ord = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
-    int *nom = (int *)malloc(sizeof(int) * (size_t)(N + 1));
-    uint8_t *feas = (uint8_t *)malloc((size_t)(N + 1));
-    for (int32_t j = 0; j < N; j++) {
-        kg_node_spec n = st[j].spec;
-        rsv_node_state rst;
-        memset(&rst, 0, sizeof(rst));
-        if (rsv_on && ri->n_of[j]) rsv_restore(pod, ri->of[j], ri->n_of[j], &n, &rst);
-        int ok = gate;
-        int64_t numa_score = 0;
-        if (c->enabled_plugins & KG_PLUGIN_NUMA) {
-            numa_hint h;
-            if (!numa_pair(c, vv, pod, &n, st[j].has_numa ? &st[j].numa : NULL, &numa_score, &h)) ok = 0;
-        }
-        if ((c->enabled_plugins & KG_PLUGIN_FIT) && kgo_fit_filter(vv, pod, &n) != KG_CODE_SUCCESS) ok = 0;
-        if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && kgo_loadaware_filter(c, vv, pod, &n, now_ns) != KG_CODE_SUCCESS)
-            ok = 0;
-        if (rsv_on && !rsv_filter(pod, &preq, &n, &rst, ri->of[j])) ok = 0;
-        int64_t fit = (c->enabled_plugins & KG_PLUGIN_FIT) ? kgo_fit_score(c, vv, pod, &n) : 0;
-        int64_t la = (c->enabled_plugins & KG_PLUGIN_LOADAWARE)
-                         ? loadaware_score_impl(c, vv, pod, &n, st[j].assigned, st[j].n_assigned, now_ns) : 0;
-        feas[j] = (uint8_t)ok;
-        base[j] = c->weight_fit * fit + c->weight_loadaware * la + c->weight_numa * numa_score;
-        if (mask) mask[j] = (uint8_t)ok;
-        if (fitp) fitp[j] = (uint8_t)fit;
-        if (lap) lap[j] = (uint8_t)la;
-        if (numap) numap[j] = (uint8_t)numa_score;
-        raw[j] = 0;
-        nom[j] = -1;
-        ord[j] = INT64_MAX;
-        if (rsv_on && ok && rst.n_matched > 0) { /* PreScore (scoring.go:42-101) */
-            rsv_most_preferred(ri->of[j], rst.matched, rst.n_matched, &ord[j]);
-            nom[j] = rsv_nominate(&preq, &n, &rst, ri->of[j]);
-            if (nom[j] >= 0) raw[j] = rsv_score_reservation(&preq, &ri->of[j][nom[j]]->r);
-        }
+    int64_t *base, *raw, *ord;
+    int *nom;
+    uint8_t *feas, *mask, *fitp, *lap, *numap;
+} pod_ctx;
+
+static void oracle_node(const pod_ctx *x, int32_t j) {
+    const kg_config *c = x->c;
+    const kg_pod_spec *pod = x->pod;
+    const rsv_index *ri = x->ri;
+    node_state *st = x->st;
+    kg_node_spec n = st[j].spec;
+    rsv_node_state rst;
+    memset(&rst, 0, sizeof(rst));
+    if (x->rsv_on && ri->n_of[j]) rsv_restore(pod, ri->of[j], ri->n_of[j], &n, &rst);
+    int ok = x->gate;
+    int64_t numa_score = 0;
+    if (c->enabled_plugins & KG_PLUGIN_NUMA) {
+        numa_hint h;
+        if (!numa_pair(c, x->vv, pod, &n, st[j].has_numa ? &st[j].numa : NULL, &numa_score, &h)) ok = 0;
     }
+    if ((c->enabled_plugins & KG_PLUGIN_FIT) && kgo_fit_filter(x->vv, pod, &n) != KG_CODE_SUCCESS) ok = 0;
+    if ((c->enabled_plugins & KG_PLUGIN_LOADAWARE) && kgo_loadaware_filter(c, x->vv, pod, &n, x->now_ns) != KG_CODE_SUCCESS)
+        ok = 0;
+    if (x->rsv_on && !rsv_filter(pod, &x->preq, &n, &rst, ri->of[j])) ok = 0;
+    int64_t fit = (c->enabled_plugins & KG_PLUGIN_FIT) ? kgo_fit_score(c, x->vv, pod, &n) : 0;
+    int64_t la = (c->enabled_plugins & KG_PLUGIN_LOADAWARE)
+                     ? loadaware_score_impl(c, x->vv, pod, &n, st[j].assigned, st[j].n_assigned, x->now_ns) : 0;
+    x->feas[j] = (uint8_t)ok;
+    x->base[j] = c->weight_fit * fit + c->weight_loadaware * la + c->weight_numa * numa_score;
+    if (x->mask) x->mask[j] = (uint8_t)ok;
+    if (x->fitp) x->fitp[j] = (uint8_t)fit;
+    if (x->lap) x->lap[j] = (uint8_t)la;
+    if (x->numap) x->numap[j] = (uint8_t)numa_score;
+    x->raw[j] = 0;
+    x->nom[j] = -1;
+    x->ord[j] = INT64_MAX;
+    if (x->rsv_on && ok && rst.n_matched > 0) { /* PreScore (scoring.go:42-101) */
+        rsv_most_preferred(ri->of[j], rst.matched, rst.n_matched, &x->ord[j]);
+        x->nom[j] = rsv_nominate(&x->preq, &n, &rst, ri->of[j]);
+        if (x->nom[j] >= 0) x->raw[j] = rsv_score_reservation(&x->preq, &ri->of[j][x->nom[j]]->r);
+    }
+}
+
+typedef struct node_pool node_pool;
+static void node_pool_run(node_pool *pool, const pod_ctx *x, int32_t N);
+
+static int32_t oracle_pod_x(const kg_config *c, kg_cluster_view *vv, node_state *st, const rsv_index *ri, int32_t N,
+                            const kg_pod_spec *pod, int64_t now_ns, const kg_quota *quotas, uint8_t *mask,
+                            uint8_t *fitp, uint8_t *lap, uint8_t *numap, uint8_t *rsvp, int64_t *best_total,
+                            int *best_nom, node_pool *pool) {
+    pod_ctx x;
+    memset(&x, 0, sizeof(x));
+    x.c = c;
+    x.vv = vv;
+    x.st = st;
+    x.ri = ri;
+    x.pod = pod;
+    x.now_ns = now_ns;
+    x.rsv_on = (c->enabled_plugins & KG_PLUGIN_RESERVATION) != 0;
+    numa_pod_requests(vv, pod, &x.preq);
+    x.gate = !(c->enabled_plugins & KG_PLUGIN_ELASTICQUOTA) || quota_prefilter(c, pod, &x.preq, quotas);
+    x.base = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
+    x.raw = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
+    x.ord = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
+    x.nom = (int *)malloc(sizeof(int) * (size_t)(N + 1));
+    x.feas = (uint8_t *)malloc((size_t)(N + 1));
+    x.mask = mask;
+    x.fitp = fitp;
+    x.lap = lap;
+    x.numap = numap;
+    if (pool) node_pool_run(pool, &x, N);
+    else
+        for (int32_t j = 0; j < N; j++) oracle_node(&x, j);
+    const int rsv_on = x.rsv_on;
+    int64_t *base = x.base, *raw = x.raw, *ord = x.ord;
+    int *nom = x.nom;
+    uint8_t *feas = x.feas;
     int32_t pref = -1;
     int64_t sel = INT64_MAX;
     for (int32_t j = 0; j < N; j++)
@@ -1791,6 +1835,13 @@ static int32_t oracle_pod(const kg_config *c, kg_cluster_view *vv, node_state *s
     *best_nom = best_n >= 0 ? nom[best_n] : -1;
     free(base); free(raw); free(ord); free(nom); free(feas);
     return best_n;
+}
+
+static int32_t oracle_pod(const kg_config *c, kg_cluster_view *vv, node_state *st, const rsv_index *ri, int32_t N,
+                          const kg_pod_spec *pod, int64_t now_ns, const kg_quota *quotas, uint8_t *mask,
+                          uint8_t *fitp, uint8_t *lap, uint8_t *numap, uint8_t *rsvp, int64_t *best_total,
+                          int *best_nom) {
+    return oracle_pod_x(c, vv, st, ri, N, pod, now_ns, quotas, mask, fitp, lap, numap, rsvp, best_total, best_nom, NULL);
 }
 
 static node_state *states_build(const kg_cluster_view *v, int32_t N) {
@@ -2228,6 +2279,97 @@ int kgo_schedule_parallel(const kg_config *c, const kg_cluster_view *v, const in
     free(args);
     free(pl.best);
     free(cpus);
+    rsv_index_free(&ri);
+    states_free(st, N);
+    return 0;
+}
+
+/* ---------------------------------------------------------------- */
+/* The sequential cycle with every pod's node loop on worker threads */
+/* (the Parallelizer fan-out, parallelism.go:27-49), all plugins      */
+/* including Reservation and ElasticQuota: the same per-node code     */
+/* (oracle_node) and the same sequential reductions and Reserve, so   */
+/* outputs equal kgo_schedule2's (the full config-5 burst check).     */
+/* ---------------------------------------------------------------- */
+struct node_pool {
+    pthread_t *th;
+    int workers, stop;
+    pthread_barrier_t start, done;
+    const pod_ctx *x;
+    int32_t n, chunk, next;
+};
+
+static void *node_pool_worker(void *arg) {
+    node_pool *p = (node_pool *)arg;
+    for (;;) {
+        pthread_barrier_wait(&p->start);
+        if (p->stop) break;
+        for (;;) {
+            int32_t s = __atomic_fetch_add(&p->next, p->chunk, __ATOMIC_RELAXED);
+            if (s >= p->n) break;
+            int32_t e = s + p->chunk < p->n ? s + p->chunk : p->n;
+            for (int32_t j = s; j < e; j++) oracle_node(p->x, j);
+        }
+        pthread_barrier_wait(&p->done);
+    }
+    return NULL;
+}
+
+static void node_pool_run(node_pool *pool, const pod_ctx *x, int32_t N) {
+    pool->x = x;
+    pool->n = N;
+    pool->next = 0;
+    pool->chunk = (int32_t)sqrt((double)N);   /* parallelize.chunkSizeFor */
+    if (N / pool->workers + 1 < pool->chunk) pool->chunk = N / pool->workers + 1;
+    if (pool->chunk < 1) pool->chunk = 1;
+    pthread_barrier_wait(&pool->start);
+    pthread_barrier_wait(&pool->done);
+}
+
+int kgo_schedule2_parallel(const kg_config *c, const kg_cluster_view *v, const int32_t *pod_index, int32_t P,
+                           int64_t now_ns, int32_t workers, int32_t *out_node, int64_t *out_score,
+                           kg_reservation *out_rsv, kg_quota *out_quota) {
+    int32_t N = v->n_nodes;
+    if (workers < 1) workers = 1;
+    if (quota_inputs_valid(c, v, pod_index, P) != 0) return -2;
+    node_state *st = states_build(v, N);
+    kg_cluster_view vv = *v;
+    kg_cpu_info *cpus = (kg_cpu_info *)malloc(sizeof(kg_cpu_info) * (size_t)(v->n_cpus > 0 ? v->n_cpus : 1));
+    if (v->n_cpus > 0) memcpy(cpus, v->cpus, sizeof(kg_cpu_info) * (size_t)v->n_cpus);
+    vv.cpus = cpus;
+    rsv_index ri;
+    if (rsv_index_build(v, N, &ri) != 0) { rsv_index_free(&ri); states_free(st, N); free(cpus); return -1; }
+    kg_quota *quotas = (kg_quota *)calloc((size_t)(v->n_quotas > 0 ? v->n_quotas : 1), sizeof(kg_quota));
+    if (v->n_quotas > 0) memcpy(quotas, v->quotas, sizeof(kg_quota) * (size_t)v->n_quotas);
+    node_pool pool;
+    memset(&pool, 0, sizeof(pool));
+    pool.workers = workers;
+    pthread_barrier_init(&pool.start, NULL, (unsigned)workers + 1);
+    pthread_barrier_init(&pool.done, NULL, (unsigned)workers + 1);
+    pool.th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)workers);
+    for (int w = 0; w < workers; w++) pthread_create(&pool.th[w], NULL, node_pool_worker, &pool);
+    for (int32_t p = 0; p < P; p++) {
+        const kg_pod_spec *pod = &v->pods[pod_index[p]];
+        int64_t best;
+        int nom;
+        int32_t best_n = oracle_pod_x(c, &vv, st, &ri, N, pod, now_ns, quotas, NULL, NULL, NULL, NULL, NULL, &best, &nom,
+                                      &pool);
+        out_node[p] = best_n;
+        out_score[p] = best_n < 0 ? -1 : best;
+        if (best_n < 0) continue;
+        if (!reserve_pod(c, &vv, v, st, &ri, quotas, pod, best_n, nom, now_ns)) out_node[p] = -1, out_score[p] = -1;
+    }
+    pool.stop = 1;
+    pthread_barrier_wait(&pool.start);
+    for (int w = 0; w < workers; w++) pthread_join(pool.th[w], NULL);
+    pthread_barrier_destroy(&pool.start);
+    pthread_barrier_destroy(&pool.done);
+    free(pool.th);
+    if (out_rsv)
+        for (int32_t i = 0; i < v->n_reservations; i++) out_rsv[i] = ri.states[i].r;
+    if (out_quota && v->n_quotas > 0) memcpy(out_quota, quotas, sizeof(kg_quota) * (size_t)v->n_quotas);
+    free(cpus);
+    free(quotas);
     rsv_index_free(&ri);
     states_free(st, N);
     return 0;

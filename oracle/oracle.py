@@ -242,8 +242,10 @@ def eval_matrix5(cfg, view, pod_index, now_ns):
     return mask.astype(bool), fit, la, numa, rsv, top1
 
 
-def schedule2(cfg, view, pod_index, now_ns):
-    """Sequential cycle; also returns the reservation and quota states after the last Reserve."""
+def schedule2(cfg, view, pod_index, now_ns, workers=0):
+    """Sequential cycle; also returns the reservation and quota states after the last Reserve.  workers > 0:
+    each pod's node loop on that many threads (kgo_schedule2_parallel: the same per-node code, reductions and
+    Reserve, so the same outputs)."""
     from koordinator_amd import _native as nat
     idx = np.ascontiguousarray(pod_index, dtype=np.int32)
     nodes = np.zeros(len(idx), np.int32)
@@ -251,11 +253,18 @@ def schedule2(cfg, view, pod_index, now_ns):
     rsv = np.zeros(view.c_view.n_reservations, dtype=nat.RESERVATION)
     quota = np.zeros(view.c_view.n_quotas, dtype=nat.QUOTA)
     L = lib()
-    L.kgo_schedule2.restype = ctypes.c_int
-    L.kgo_schedule2.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32, ctypes.c_int64] + [ctypes.c_void_p] * 4
-    st = L.kgo_schedule2(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, len(idx), now_ns, nodes.ctypes.data,
-                         scores.ctypes.data, rsv.ctypes.data if len(rsv) else None,
-                         quota.ctypes.data if len(quota) else None)
+    outs = [nodes.ctypes.data, scores.ctypes.data, rsv.ctypes.data if len(rsv) else None,
+            quota.ctypes.data if len(quota) else None]
+    if workers > 0:
+        L.kgo_schedule2_parallel.restype = ctypes.c_int
+        L.kgo_schedule2_parallel.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32] + \
+            [ctypes.c_void_p] * 4
+        st = L.kgo_schedule2_parallel(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, len(idx), now_ns, workers,
+                                      *outs)
+    else:
+        L.kgo_schedule2.restype = ctypes.c_int
+        L.kgo_schedule2.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32, ctypes.c_int64] + [ctypes.c_void_p] * 4
+        st = L.kgo_schedule2(_cfg(cfg), ctypes.byref(view.c_view), idx.ctypes.data, len(idx), now_ns, *outs)
     if st != 0:
         raise RuntimeError("kgo_schedule2 failed")
     return nodes, scores, rsv, quota

@@ -6,15 +6,22 @@
   cycle (98 tiles, every top-16 list exhausted many times over, slow nodes crossing bounds mid-run), node
   rows afterwards against a host replay of the Reserve deltas;
 * config 3 — NodeNUMAResource: a 32-pod plane sample of the 10k-pod matrix run (the pod-grouping
-  permutation of kg_pods_set depends on the batch), and kg_place of the first 256 pods at 100k nodes;
+  permutation of kg_pods_set depends on the batch), and kg_place of all 1,000 bench pods at 100k nodes
+  (the first 256 against the live oracle, all against the fixture);
 * config 5 — a 100k-node seed-5 variant whose quota and allocate-once rejections start inside a
-  1.5k-pod prefix, checked pod by pod against the oracle; and the bench's full 100k-pod burst, checked
-  by invariants (no quota group or ancestor above its runtime or min, no reservation above its
-  allocatable, reservation and quota deltas equal to what the placed pods request, rows equal the replay).
+  1.5k-pod prefix, checked pod by pod against the oracle; and the bench's full 100k-pod burst: the first
+  3k placements against the live oracle, every placement and the reservation / quota states after the
+  burst against the fixture, plus invariants (no quota group or ancestor above its runtime or min, no
+  reservation above its allocatable, reservation and quota deltas equal to what the placed pods request,
+  rows equal the replay).
 
-The oracle runs on WORKERS host threads (ctypes releases the GIL).
+The live oracle runs on WORKERS host threads (ctypes releases the GIL).  The fixture
+(tests/golden/fullsize_placements.npz, made by tests/golden/make_fullsize_placements.py — the same oracle
+over the whole bursts, ≈ 35 min of host time) carries a digest of the engine inputs it was computed from;
+a stale one fails the test rather than being compared.
 """
 import os
+import sys
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -24,6 +31,9 @@ from koordinator_amd import _native as nat
 from koordinator_amd import engine, synth
 from koordinator_amd.config import shipped_profile
 from oracle import oracle
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+import make_fullsize_placements as fullsize  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -123,20 +133,32 @@ def test_config3_large_batch_plane_sample():
     np.testing.assert_array_equal(best, tot.max(axis=1))
 
 
-def test_config3_placement_first_pods():
-    N, P, K = 100_000, 1_000, 256
-    cl = synth.make_numa_cluster(N, P, seed=3)
-    cfg = _numa_cfg()
-    idx = np.arange(K)
+def _fixture(key, dig):
+    """The fixture's arrays of one case, after checking they were computed from these inputs."""
+    fx = np.load(fullsize.OUT)
+    assert str(fx[f"{key}_digest"]) == dig, f"{fullsize.OUT} is stale: rerun tests/golden/make_fullsize_placements.py"
+    return fx
+
+
+def test_config3_bench_placement():
+    """kg_place of the bench's 1,000 NodeNUMAResource pods (pipelined chunks, the default with NUMA): the first
+    256 against the live oracle, all 1,000 against the fixture, node rows against the replay."""
+    cfg, cl, nrows, prows = fullsize.c3_case()
+    P, K = len(prows), 256
+    dig = fullsize.c3_digest(nrows, prows)
     with engine.Engine(cfg) as eng:
-        eng.load_snapshot(engine.build_node_rows(cfg, cl))
-        eng.set_pods(engine.build_pod_rows(cfg, cl, idx))
+        eng.load_snapshot(nrows)
+        eng.set_pods(prows)
         nodes, scores = eng.place(cl.now_ns)
         after = eng.download()
-    ref_nodes, ref_scores = oracle.schedule_parallel(cfg, cl, idx, cl.now_ns, WORKERS)
-    np.testing.assert_array_equal(nodes, ref_nodes)
-    np.testing.assert_array_equal(scores, ref_scores)
-    np.testing.assert_array_equal(after, _replay(cfg, cl, idx, nodes))
+    ref_nodes, ref_scores = oracle.schedule_parallel(cfg, cl, np.arange(K), cl.now_ns, WORKERS)
+    np.testing.assert_array_equal(nodes[:K], ref_nodes)
+    np.testing.assert_array_equal(scores[:K], ref_scores)
+    fx = _fixture("c3", dig)
+    np.testing.assert_array_equal(fx["c3_nodes"][:K], ref_nodes)   # the fixture agrees with the live oracle
+    np.testing.assert_array_equal(nodes, fx["c3_nodes"])
+    np.testing.assert_array_equal(scores, fx["c3_scores"])
+    np.testing.assert_array_equal(after, _replay(cfg, cl, np.arange(P), nodes))
 
 
 def _quota_invariants(q_after, q0):
@@ -184,16 +206,16 @@ def test_config5_rejections_inside_checked_prefix():
     np.testing.assert_array_equal(after, _replay(cfg, cl, idx, nodes))
 
 
-def test_config5_full_burst_invariants():
-    """The bench's own burst (100k batch pods × 100k nodes, seed 5) end to end: the first 1k placements
-    against the oracle, then invariants over the whole run."""
-    N, P = 100_000, 100_000
-    cl = synth.make_rsv_cluster(N, P, seed=5)
-    cfg = shipped_profile(plugins=RSV_EQ)
+def test_config5_full_burst():
+    """The bench's own burst (100k batch pods × 100k nodes, seed 5) end to end: the first 3k placements against
+    the oracle's cycle on WORKERS threads (kgo_schedule2_parallel), all 100k and the reservation and quota
+    states after the burst against the fixture, then invariants over the whole run."""
+    cfg, cl, nrows, prow = fullsize.c5_case()
+    N, P = len(nrows), len(prow)
     idx = np.arange(P)
-    prow = engine.build_pod_rows(cfg, cl, idx)
+    dig = fullsize.c5_digest(cl, nrows, prow)
     with engine.Engine(cfg) as eng:
-        eng.load_snapshot(engine.build_node_rows(cfg, cl))
+        eng.load_snapshot(nrows)
         eng.set_reservations(cl.rsv_arr)
         eng.set_quotas(cl.quota_arr)
         eng.set_pods(prow)
@@ -203,9 +225,18 @@ def test_config5_full_burst_invariants():
         q_after = eng.download_quotas()
     placed = nodes >= 0
     assert 0.5 < placed.mean() < 0.95                      # the quota runtimes reject part of the burst
-    ref_nodes, ref_scores, _, _ = oracle.schedule2(cfg, cl, idx[:1_000], cl.now_ns)
-    np.testing.assert_array_equal(nodes[:1_000], ref_nodes)
-    np.testing.assert_array_equal(scores[:1_000], ref_scores)
+    K = 3_000
+    ref_nodes, ref_scores, _, _ = oracle.schedule2(cfg, cl, idx[:K], cl.now_ns, workers=WORKERS)
+    np.testing.assert_array_equal(nodes[:K], ref_nodes)
+    np.testing.assert_array_equal(scores[:K], ref_scores)
+    fx = _fixture("c5", dig)
+    np.testing.assert_array_equal(fx["c5_nodes"][:K], ref_nodes)   # the fixture agrees with the live oracle
+    np.testing.assert_array_equal(nodes, fx["c5_nodes"])
+    np.testing.assert_array_equal(scores, fx["c5_scores"])
+    np.testing.assert_array_equal(rsv_after["n_assigned"], fx["c5_rsv_n_assigned"])
+    np.testing.assert_array_equal(rsv_after["allocated"]["v"], fx["c5_rsv_allocated"])
+    np.testing.assert_array_equal(q_after["used"]["v"], fx["c5_quota_used"])
+    np.testing.assert_array_equal(q_after["non_preemptible_used"]["v"], fx["c5_quota_np_used"])
     _quota_invariants(q_after, cl.quota_arr)
     # quota usage = Σ requests of the placed pods of each group (ElasticQuota.Reserve, plugin.go:323-337)
     q = cl.pods["quota"][:P]

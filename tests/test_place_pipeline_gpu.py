@@ -67,3 +67,43 @@ def test_fit_loadaware_place_pipeline_on_off(pipeline, monkeypatch):
     ref_n, ref_s = oracle.schedule(cfg, cl, idx, cl.now_ns)
     np.testing.assert_array_equal(nodes, ref_n)
     np.testing.assert_array_equal(scores, ref_s)
+
+
+@pytest.mark.parametrize("kind", ["fit_la", "numa", "quota"])
+def test_resolve_small_clusters(kind):
+    """k_resolve against the oracle's cycle on small clusters, so pods keep landing on nodes the previous pod
+    took (the touched-node re-score right after a Reserve); an ElasticQuota tree without Reservation (the gate
+    after each Reserve)."""
+    from rsv_cases import rsv_cluster
+    P = 300
+    if kind == "fit_la":
+        cl = synth.make_cluster(1024, P, seed=95)
+        cfg = shipped_profile(place_chunk=16)
+    elif kind == "numa":
+        cl = synth.make_numa_cluster(1500, P, seed=96)
+        cfg = shipped_profile()
+        cfg["enabled_plugins"] |= nat.PLUGIN_NUMA
+    else:
+        cl = rsv_cluster(2000, P, seed=97, n_quotas=15, quota_ratio=0.5, quota_tree=True)
+        cfg = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "ElasticQuota"),
+                              eq_check_parent_quota=1)
+    idx = np.arange(P)
+    with engine.Engine(cfg) as eng:
+        eng.load_snapshot(engine.build_node_rows(cfg, cl))
+        if kind == "quota":
+            eng.set_quotas(cl.quota_arr)
+        eng.set_pods(engine.build_pod_rows(cfg, cl, idx))
+        nodes, scores = eng.place(cl.now_ns)
+        after = eng.download()
+        q_after = eng.download_quotas() if kind == "quota" else None
+    if kind == "quota":
+        ref_n, ref_s, _, ref_q = oracle.schedule2(cfg, cl, idx, cl.now_ns)
+        assert (ref_n == -1).any() and (ref_n >= 0).any()
+        np.testing.assert_array_equal(q_after["used"]["v"], ref_q["used"]["v"])
+    else:
+        ref_n, ref_s = oracle.schedule(cfg, cl, idx, cl.now_ns)
+    np.testing.assert_array_equal(nodes, ref_n)
+    np.testing.assert_array_equal(scores, ref_s)
+    if kind == "fit_la":
+        assert (np.diff(nodes[nodes >= 0]) == 0).any()   # back-to-back pods on one node
+    np.testing.assert_array_equal(after, _replay(cfg, cl, idx, nodes))
