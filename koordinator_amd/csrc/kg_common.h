@@ -1207,7 +1207,7 @@ KG_HD int64_t kg_rl_get(const kg_resource_list &l, int r) { return ((l.present >
 struct kg_rsv_view {
     bool has_state;                        // nodeReservationStates[node] exists
     int32_t n_matched;
-    int32_t matched[KG_MAX_RSV_PER_NODE];  // slot indices of the node
+    uint32_t matched;                      // bit i ⇔ slot i of the node matches (ascending = the slot order)
     int64_t requested[KG_NUM_RES];         // NodeInfo.Requested after the restore
     int64_t nonzero[2];                    // NodeInfo.NonZeroRequested after the restore
     int64_t pod_count;                     // len(NodeInfo.Pods) after the restore
@@ -1239,6 +1239,7 @@ KG_HD int64_t kg_rsv_remained(const kg_reservation &r, int q) {
 KG_HD void kg_rsv_restore(const kg_node_row &row, const kg_reservation *rs, int nr, const kg_pod_dev &p, kg_rsv_view &v) {
     v.has_state = false;
     v.n_matched = 0;
+    v.matched = 0;
     for (int r = 0; r < KG_NUM_RES; r++) {
         v.requested[r] = row.requested[r];
         v.pod_requested[r] = row.requested[r];
@@ -1247,19 +1248,22 @@ KG_HD void kg_rsv_restore(const kg_node_row &row, const kg_reservation *rs, int 
     v.nonzero[0] = row.nonzero_requested[0];
     v.nonzero[1] = row.nonzero_requested[1];
     v.pod_count = row.pod_count;
-    int32_t unm[KG_MAX_RSV_PER_NODE];
-    int nu = 0;
+    // slot sets as bitmasks (KG_MAX_RSV_PER_NODE ≤ 32), walked in ascending slot order: no per-lane arrays at
+    // run-time indices (on the device those live in scratch memory)
+    static_assert(KG_MAX_RSV_PER_NODE <= 32, "slot sets are 32-bit masks");
+    uint32_t unm = 0;
     for (int i = 0; i < nr; i++) {
         const kg_reservation &r = rs[i];
         if (!kg_rsv_usable(r)) continue;
-        if (!(r.flags & KG_RSV_UNSCHEDULABLE) && kg_rsv_match(p, r)) v.matched[v.n_matched++] = i;
-        else if (r.n_assigned > 0) unm[nu++] = i;
+        if (!(r.flags & KG_RSV_UNSCHEDULABLE) && kg_rsv_match(p, r)) v.matched |= 1u << i;
+        else if (r.n_assigned > 0) unm |= 1u << i;
     }
-    if (v.n_matched == 0 && nu == 0) return;
+    v.n_matched = __builtin_popcount(v.matched);
+    if (v.n_matched == 0 && unm == 0) return;
     if (p.rsv_aff >= 0 && v.n_matched == 0) return;  // the affinity needs a match: node left alone
     v.has_state = true;
-    for (int k = 0; k < nu; k++) {  // restoreUnmatchedReservations
-        const kg_reservation &r = rs[unm[k]];
+    for (uint32_t m = unm; m; m &= m - 1u) {  // restoreUnmatchedReservations
+        const kg_reservation &r = rs[__builtin_ctz(m)];
         kg_rsv_update(v, r.allocatable, -1);
         kg_resource_list rem;
         rem.present = r.allocatable.present | r.allocated.present;
@@ -1272,8 +1276,8 @@ KG_HD void kg_rsv_restore(const kg_node_row &row, const kg_reservation *rs, int 
         if (!zero) kg_rsv_update(v, rem, +1);
     }
     for (int q = 0; q < KG_NUM_RES; q++) v.pod_requested[q] = v.requested[q];
-    for (int k = 0; k < v.n_matched; k++) {  // restoreMatchedReservation → RemovePod(reserve pod)
-        const kg_reservation &r = rs[v.matched[k]];
+    for (uint32_t m = v.matched; m; m &= m - 1u) {  // restoreMatchedReservation → RemovePod(reserve pod)
+        const kg_reservation &r = rs[__builtin_ctz(m)];
         kg_rsv_update(v, r.allocatable, -1);
         v.pod_count -= 1;
         for (int q = 0; q < KG_NUM_RES; q++) v.r_allocated[q] += kg_rl_get(r.allocated, q);
@@ -1293,12 +1297,12 @@ KG_HD bool kg_rsv_fits_node(const kg_node_row &row, const kg_rsv_view &v, const 
     return true;
 }
 
-// filterWithReservations over the slots `list` (plugin.go:377-425)
-KG_HD bool kg_rsv_filter_with(const kg_node_row &row, const kg_rsv_view &v, const kg_reservation *rs,
-                              const int32_t *list, int nl, bool required, const kg_pod_dev &p) {
+// filterWithReservations over the slots of `set` (bit i ⇔ slot i, ascending) (plugin.go:377-425)
+KG_HD bool kg_rsv_filter_with(const kg_node_row &row, const kg_rsv_view &v, const kg_reservation *rs, uint32_t set,
+                              bool required, const kg_pod_dev &p) {
     bool ok = false;
-    for (int k = 0; k < nl && !ok; k++) {
-        const kg_reservation &r = rs[list[k]];
+    for (uint32_t m = set; m && !ok; m &= m - 1u) {
+        const kg_reservation &r = rs[__builtin_ctz(m)];
         if ((r.allocatable.present & p.numa_present) == 0) continue;
         const bool node_fits = kg_rsv_fits_node(row, v, r, p);
         if (r.policy == KG_RSV_POLICY_DEFAULT || r.policy == KG_RSV_POLICY_ALIGNED) {
@@ -1316,15 +1320,17 @@ KG_HD bool kg_rsv_filter_with(const kg_node_row &row, const kg_rsv_view &v, cons
     return ok || !required;
 }
 
-// findMostPreferredReservationByOrder (scoring.go:162-181): position in `list` or −1; *order
-KG_HD int kg_rsv_most_preferred(const kg_reservation *rs, const int32_t *list, int nl, int64_t &order) {
+// findMostPreferredReservationByOrder (scoring.go:162-181) over the slots of `set` (ascending): the slot or −1;
+// *order
+KG_HD int kg_rsv_most_preferred(const kg_reservation *rs, uint32_t set, int64_t &order) {
     order = INT64_MAX;
     int hi = -1;
-    for (int k = 0; k < nl; k++) {
-        const int64_t o = rs[list[k]].order;
+    for (uint32_t m = set; m; m &= m - 1u) {
+        const int i = __builtin_ctz(m);
+        const int64_t o = rs[i].order;
         if (o != 0 && order > o) {
             order = o;
-            hi = k;
+            hi = i;
         }
     }
     return hi;
@@ -1346,21 +1352,23 @@ KG_HD uint32_t kg_rsv_score(const kg_reservation &r, const kg_pod_dev &p) {
 
 // NominateReservation (nominator.go:76-135): slot index or −1
 KG_HD int kg_rsv_nominate(const kg_node_row &row, const kg_rsv_view &v, const kg_reservation *rs, const kg_pod_dev &p) {
-    int32_t cand[KG_MAX_RSV_PER_NODE];
-    int nc = 0;
-    for (int k = 0; k < v.n_matched; k++)
-        if (kg_rsv_filter_with(row, v, rs, &v.matched[k], 1, true, p)) cand[nc++] = v.matched[k];
-    if (nc == 0) return -1;
+    uint32_t cand = 0;
+    for (uint32_t m = v.matched; m; m &= m - 1u) {
+        const uint32_t bit = m & (~m + 1u);
+        if (kg_rsv_filter_with(row, v, rs, bit, true, p)) cand |= bit;
+    }
+    if (cand == 0) return -1;
     int64_t order;
-    const int hi = kg_rsv_most_preferred(rs, cand, nc, order);
-    if (hi >= 0) return cand[hi];
-    int best = cand[0];  // sort.Slice by score descending: insertion sort (≤ 12 items) keeps the first
-    uint32_t bs = kg_rsv_score(rs[cand[0]], p);
-    for (int k = 1; k < nc; k++) {
-        const uint32_t sc = kg_rsv_score(rs[cand[k]], p);
-        if (sc > bs) {
+    const int hi = kg_rsv_most_preferred(rs, cand, order);
+    if (hi >= 0) return hi;
+    int best = -1;  // sort.Slice by score descending: insertion sort (≤ 12 items) keeps the first
+    uint32_t bs = 0;
+    for (uint32_t m = cand; m; m &= m - 1u) {
+        const int i = __builtin_ctz(m);
+        const uint32_t sc = kg_rsv_score(rs[i], p);
+        if (best < 0 || sc > bs) {
             bs = sc;
-            best = cand[k];
+            best = i;
         }
     }
     return best;
@@ -1391,13 +1399,13 @@ KG_HD void kg_rsv_pair(const kg_consts &c, const kg_node_row &row, uint32_t df, 
         o.numa = no.score;
     }
     if (v.n_matched == 0) feas = feas && p.rsv_aff < 0;  // Reservation.Filter (plugin.go:351-369)
-    else feas = feas && kg_rsv_filter_with(row, v, rs, v.matched, v.n_matched, p.rsv_aff >= 0, p);
+    else feas = feas && kg_rsv_filter_with(row, v, rs, v.matched, p.rsv_aff >= 0, p);
     o.feasible = feas;
     o.raw = 0;
     o.order = INT64_MAX;
     o.nominated = -1;
     if (feas && v.n_matched > 0) {
-        kg_rsv_most_preferred(rs, v.matched, v.n_matched, o.order);
+        kg_rsv_most_preferred(rs, v.matched, o.order);
         o.nominated = kg_rsv_nominate(row, v, rs, p);
         if (o.nominated >= 0) o.raw = kg_rsv_score(rs[o.nominated], p);
     }

@@ -1350,14 +1350,31 @@ struct RsvArgs {
     unsigned long long *E;      // [pods][n_rn]
     int64_t *O;                 // [pods][n_rn]
     kg_quota *quota;            // ElasticQuota groups (nullptr: ElasticQuota off)
+    // placement chunks (nullptr in matrix mode, or more groups than the resolve tracks): the entries split for
+    // the resolve's reduction, written by k_rsv_eval beside E / O (rsv_best_resolve)
+    int32_t *M;                 // [pods][n_rn] the entries that can take the preferred node or a raw score
+    int32_t *Mn;                // [pods] their count
+    unsigned long long *G;      // [pods][ngroups] per 64-entry group: the best key of its other feasible entries
+    int32_t ngroups;
 };
+#define KG_RSV_GROUP 64
+#define KG_RSV_MAX_GROUPS 2048   // the resolve's touched-group flags (LDS): up to 131072 reservation nodes
 
-__device__ __forceinline__ void rsv_entry(const kg_consts &c, const kg_planes &pl, const RsvArgs &ra,
+// an entry whose key depends on PreScore / NormalizeScore: a nominated reservation (raw score) or a
+// reservation order (preferred-node candidate); every other feasible entry keys on its base total alone
+__device__ __forceinline__ bool rsv_entry_scored(unsigned long long e, int64_t o) {
+    return (e & 0xFFFFull) != 0 || (o != 0 && o != INT64_MAX);
+}
+__device__ __forceinline__ unsigned long long rsv_base_key(unsigned long long e, int32_t node) {
+    return ((e >> 32) << 32) | (0xFFFFFFFFull - (unsigned long long)(uint32_t)node);
+}
+
+// `row` / `df`: the node's canonical row and dflags (global, or the resolve's LDS copies)
+__device__ __forceinline__ void rsv_entry(const kg_consts &c, const kg_node_row &row, uint32_t df, const RsvArgs &ra,
                                           const kg_pod_dev &p, int32_t k, int64_t now_ns, kg_rsv_out *keep,
                                           unsigned long long &e, int64_t &o) {
-    const int32_t node = ra.rnode[k];
     kg_rsv_out r;
-    kg_rsv_pair(c, pl.rows[node], pl.dflags[node], ra.rsv + ra.rfirst[k], ra.rfirst[k + 1] - ra.rfirst[k], p, now_ns, r);
+    kg_rsv_pair(c, row, df, ra.rsv + ra.rfirst[k], ra.rfirst[k + 1] - ra.rfirst[k], p, now_ns, r);
     const uint32_t base = total_of(c, r.fit, r.la, r.numa);
     e = r.feasible ? ((unsigned long long)(base + 1u) << 32) | ((unsigned long long)r.raw << 16) |
                          (unsigned long long)(uint32_t)(r.nominated + 1)
@@ -1369,20 +1386,41 @@ __device__ __forceinline__ void rsv_entry(const kg_consts &c, const kg_planes &p
 // PreScore / Score / NormalizeScore of one pod over its reservation-node entries, by a whole
 // workgroup of NT threads; returns the best key (total + 1) << 32 | (0xFFFFFFFF − node) (all threads).
 // `plane` (optional) receives the normalized Reservation score of columns [col_begin, col_end).
+// Two passes: (1) the preferred node (the smallest non-zero order among feasible nodes, lowest node on ties)
+// and the largest raw score; (2) totals and the best key.  DefaultNormalizeScore's maximum follows from pass 1:
+// a raw score is ≤ 100 (kg_rsv_score: a mean of terms ≤ 100) and the preferred node scores 1000, so the
+// maximum is 1000 when a preferred node exists and the largest raw score otherwise.  Entries are read
+// RSV_UNR at a time (independent loads in flight: the passes are latency-bound at one workgroup per pod).
+#ifndef KG_RSV_UNR
+#define KG_RSV_UNR 8
+#endif
 template <int NT>
 __device__ unsigned long long rsv_best_block(const kg_consts &c, const unsigned long long *E, const int64_t *O,
                                              const int32_t *rnode, int32_t n_rn, uint8_t *plane, int64_t col_begin,
                                              int64_t col_end, unsigned long long *red, int64_t *redo) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     constexpr int NW = NT / 64;
-    // 1. preferred node: the smallest non-zero order among feasible nodes, lowest node on ties
     int64_t bo = INT64_MAX;
     int32_t bk = INT32_MAX;
-    for (int32_t k = tid; k < n_rn; k += NT) {
-        const int64_t o = O[k];
-        if (E[k] && o != 0 && o != INT64_MAX && o < bo) {
-            bo = o;
-            bk = k;
+    uint32_t mraw = 0;
+    for (int32_t k0 = tid; k0 < n_rn; k0 += NT * KG_RSV_UNR) {
+        unsigned long long e[KG_RSV_UNR];
+        int64_t o[KG_RSV_UNR];
+#pragma unroll
+        for (int u = 0; u < KG_RSV_UNR; u++) {
+            const int32_t k = k0 + u * NT;
+            e[u] = k < n_rn ? E[k] : 0ull;
+            o[u] = k < n_rn ? O[k] : INT64_MAX;
+        }
+#pragma unroll
+        for (int u = 0; u < KG_RSV_UNR; u++) {
+            if (!e[u]) continue;
+            const uint32_t raw = (uint32_t)((e[u] >> 16) & 0xFFFFull);
+            mraw = mraw > raw ? mraw : raw;
+            if (o[u] != 0 && o[u] != INT64_MAX && o[u] < bo) {   // k ascends with u: the first of equal orders
+                bo = o[u];
+                bk = k0 + u * NT;
+            }
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -1392,51 +1430,171 @@ __device__ unsigned long long rsv_best_block(const kg_consts &c, const unsigned 
             bo = o2;
             bk = k2;
         }
+        const uint32_t m2 = __shfl_xor(mraw, off, 64);
+        mraw = mraw > m2 ? mraw : m2;
     }
     if (lane == 0) {
         redo[wv] = bo;
-        red[wv] = (unsigned long long)(uint32_t)bk;
+        red[wv] = (unsigned long long)(uint32_t)bk | ((unsigned long long)mraw << 32);
     }
     __syncthreads();
     bo = redo[0];
     bk = (int32_t)(uint32_t)red[0];
+    mraw = (uint32_t)(red[0] >> 32);
     for (int w = 1; w < NW; w++) {
         const int32_t k2 = (int32_t)(uint32_t)red[w];
         if (redo[w] < bo || (redo[w] == bo && k2 < bk)) {
             bo = redo[w];
             bk = k2;
         }
+        const uint32_t m2 = (uint32_t)(red[w] >> 32);
+        mraw = mraw > m2 ? mraw : m2;
     }
     const int32_t pref = bo == INT64_MAX ? -1 : bk;
+    const unsigned long long mx = pref >= 0 ? 1000ull : mraw;
     __syncthreads();
-    // 2. DefaultNormalizeScore max over feasible nodes (the preferred node scores 1000)
-    unsigned long long mx = 0;
-    for (int32_t k = tid; k < n_rn; k += NT) {
-        const unsigned long long e = E[k];
-        if (!e) continue;
-        const unsigned long long raw = k == pref ? 1000ull : ((e >> 16) & 0xFFFFull);
-        mx = mx > raw ? mx : raw;
-    }
-    mx = wave_max_u64(mx);
-    if (lane == 0) red[wv] = mx;
-    __syncthreads();
-    mx = 0;
-    for (int w = 0; w < NW; w++) mx = mx > red[w] ? mx : red[w];
-    __syncthreads();
-    // 3. totals and the best key
     unsigned long long best = 0;
-    for (int32_t k = tid; k < n_rn; k += NT) {
-        const unsigned long long e = E[k];
-        const int64_t node = rnode[k];
-        uint32_t sn = 0;
-        if (e) {
-            const unsigned long long raw = k == pref ? 1000ull : ((e >> 16) & 0xFFFFull);
-            sn = mx ? (uint32_t)(100ull * raw / mx) : 0u;
-            const unsigned long long total = (e >> 32) - 1ull + (unsigned long long)c.weight_rsv * sn;
-            const unsigned long long key = ((total + 1ull) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
+    for (int32_t k0 = tid; k0 < n_rn; k0 += NT * KG_RSV_UNR) {
+        unsigned long long e[KG_RSV_UNR];
+        int32_t nd[KG_RSV_UNR];
+#pragma unroll
+        for (int u = 0; u < KG_RSV_UNR; u++) {
+            const int32_t k = k0 + u * NT;
+            e[u] = k < n_rn ? E[k] : 0ull;
+            nd[u] = k < n_rn ? rnode[k] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < KG_RSV_UNR; u++) {
+            const int32_t k = k0 + u * NT;
+            if (k >= n_rn) continue;
+            const int64_t node = nd[u];
+            uint32_t sn = 0;
+            if (e[u]) {
+                const unsigned long long raw = k == pref ? 1000ull : ((e[u] >> 16) & 0xFFFFull);
+                sn = mx ? (uint32_t)(100ull * raw / mx) : 0u;
+                const unsigned long long total = (e[u] >> 32) - 1ull + (unsigned long long)c.weight_rsv * sn;
+                const unsigned long long key = ((total + 1ull) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
+                best = best > key ? best : key;
+            }
+            if (plane && node >= col_begin && node < col_end) plane[node - col_begin] = (uint8_t)sn;
+        }
+    }
+    best = wave_max_u64(best);
+    if (lane == 0) red[wv] = best;
+    __syncthreads();
+    best = 0;
+    for (int w = 0; w < NW; w++) best = best > red[w] ? best : red[w];
+    __syncthreads();
+    return best;
+}
+
+// rsv_best_block for pod j of a placement chunk, over the split k_rsv_eval wrote: pass 1 (preferred node,
+// largest raw score) and the scored part of pass 2 walk only the scored entries M and the reservation nodes
+// earlier pods of the chunk touched (their refreshed entries; duplicates are harmless under min / max); the
+// other feasible entries key on their base total whatever NormalizeScore's maximum, so their best is the
+// max of the per-group keys G — except in groups holding a touched node (`gflag`, listed in `glist`), which
+// are rescanned from the refreshed entries.  The same keys as rsv_best_block over every entry.
+template <int NT>
+__device__ unsigned long long rsv_best_resolve(const kg_consts &c, const kg_planes &pl, const RsvArgs &ra, int32_t j,
+                                               const int32_t *touched, int nt, const uint8_t *gflag,
+                                               const int32_t *glist, int ng, unsigned long long *red, int64_t *redo) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    constexpr int NW = NT / 64;
+    const unsigned long long *E = ra.E + (int64_t)j * ra.n_rn;
+    const int64_t *O = ra.O + (int64_t)j * ra.n_rn;
+    const int32_t *M = ra.M + (int64_t)j * ra.n_rn;
+    const int32_t nm = ra.Mn[j];
+    const int nq = nm + nt;
+    auto entry_k = [&](int q) -> int32_t { return q < nm ? M[q] : pl.rsv_of[touched[q - nm]]; };
+    int64_t bo = INT64_MAX;
+    int32_t bk = INT32_MAX;
+    uint32_t mraw = 0;
+    for (int q0 = tid; q0 < nq; q0 += NT * KG_RSV_UNR) {
+        int32_t k[KG_RSV_UNR];
+        unsigned long long e[KG_RSV_UNR];
+        int64_t o[KG_RSV_UNR];
+#pragma unroll
+        for (int u = 0; u < KG_RSV_UNR; u++) k[u] = q0 + u * NT < nq ? entry_k(q0 + u * NT) : -1;
+#pragma unroll
+        for (int u = 0; u < KG_RSV_UNR; u++) {
+            e[u] = k[u] >= 0 ? E[k[u]] : 0ull;
+            o[u] = k[u] >= 0 ? O[k[u]] : INT64_MAX;
+        }
+#pragma unroll
+        for (int u = 0; u < KG_RSV_UNR; u++) {
+            if (!e[u]) continue;
+            const uint32_t raw = (uint32_t)((e[u] >> 16) & 0xFFFFull);
+            mraw = mraw > raw ? mraw : raw;
+            if (o[u] != 0 && o[u] != INT64_MAX && (o[u] < bo || (o[u] == bo && k[u] < bk))) {
+                bo = o[u];
+                bk = k[u];
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const int64_t o2 = __shfl_xor(bo, off, 64);
+        const int32_t k2 = __shfl_xor(bk, off, 64);
+        if (o2 < bo || (o2 == bo && k2 < bk)) {
+            bo = o2;
+            bk = k2;
+        }
+        const uint32_t m2 = __shfl_xor(mraw, off, 64);
+        mraw = mraw > m2 ? mraw : m2;
+    }
+    if (lane == 0) {
+        redo[wv] = bo;
+        red[wv] = (unsigned long long)(uint32_t)bk | ((unsigned long long)mraw << 32);
+    }
+    __syncthreads();
+    bo = redo[0];
+    bk = (int32_t)(uint32_t)red[0];
+    mraw = (uint32_t)(red[0] >> 32);
+    for (int w = 1; w < NW; w++) {
+        const int32_t k2 = (int32_t)(uint32_t)red[w];
+        if (redo[w] < bo || (redo[w] == bo && k2 < bk)) {
+            bo = redo[w];
+            bk = k2;
+        }
+        const uint32_t m2 = (uint32_t)(red[w] >> 32);
+        mraw = mraw > m2 ? mraw : m2;
+    }
+    const int32_t pref = bo == INT64_MAX ? -1 : bk;
+    const unsigned long long mx = pref >= 0 ? 1000ull : mraw;
+    __syncthreads();
+    unsigned long long best = 0;
+    for (int q0 = tid; q0 < nq; q0 += NT * KG_RSV_UNR) {   // the scored entries and the touched nodes
+        int32_t k[KG_RSV_UNR];
+        unsigned long long e[KG_RSV_UNR];
+        int32_t nd[KG_RSV_UNR];
+#pragma unroll
+        for (int u = 0; u < KG_RSV_UNR; u++) k[u] = q0 + u * NT < nq ? entry_k(q0 + u * NT) : -1;
+#pragma unroll
+        for (int u = 0; u < KG_RSV_UNR; u++) {
+            e[u] = k[u] >= 0 ? E[k[u]] : 0ull;
+            nd[u] = k[u] >= 0 ? ra.rnode[k[u]] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < KG_RSV_UNR; u++) {
+            if (!e[u]) continue;
+            const unsigned long long raw = k[u] == pref ? 1000ull : ((e[u] >> 16) & 0xFFFFull);
+            const uint32_t sn = mx ? (uint32_t)(100ull * raw / mx) : 0u;
+            const unsigned long long total = (e[u] >> 32) - 1ull + (unsigned long long)c.weight_rsv * sn;
+            const unsigned long long key = ((total + 1ull) << 32) | (0xFFFFFFFFull - (unsigned long long)(uint32_t)nd[u]);
             best = best > key ? best : key;
         }
-        if (plane && node >= col_begin && node < col_end) plane[node - col_begin] = (uint8_t)sn;
+    }
+    const unsigned long long *G = ra.G + (int64_t)j * ra.ngroups;
+    for (int g = tid; g < ra.ngroups; g += NT) {   // groups without a touched node: their best base key stands
+        const unsigned long long key = gflag[g] ? 0ull : G[g];
+        best = best > key ? best : key;
+    }
+    for (int q = tid; q < ng * KG_RSV_GROUP; q += NT) {   // the others, from the refreshed entries
+        const int32_t k = glist[q / KG_RSV_GROUP] * KG_RSV_GROUP + q % KG_RSV_GROUP;
+        if (k >= ra.n_rn) continue;
+        const unsigned long long e = E[k];
+        if (!e || rsv_entry_scored(e, O[k])) continue;
+        const unsigned long long key = rsv_base_key(e, ra.rnode[k]);
+        best = best > key ? best : key;
     }
     best = wave_max_u64(best);
     if (lane == 0) red[wv] = best;
@@ -1454,14 +1612,32 @@ __global__ __launch_bounds__(256) void k_rsv_eval(kg_consts c, kg_planes pl, Rsv
                                                   int64_t col_end, int32_t mask_words, int64_t score_stride) {
     const int32_t k = blockIdx.x * 256 + threadIdx.x;
     const int32_t p = blockIdx.y;
-    if (k >= ra.n_rn || p >= P) return;
+    if (p >= P) return;   // workgroup-uniform
     kg_rsv_out r;
-    unsigned long long e;
-    int64_t o;
-    rsv_entry(c, pl, ra, pods[p], k, now_ns, &r, e, o);
-    ra.E[(int64_t)p * ra.n_rn + k] = e;
-    ra.O[(int64_t)p * ra.n_rn + k] = o;
-    const int64_t node = ra.rnode[k];
+    unsigned long long e = 0;
+    int64_t o = INT64_MAX;
+    const bool live = k < ra.n_rn;
+    const int32_t nd = live ? ra.rnode[k] : 0;
+    if (live) {
+        rsv_entry(c, pl.rows[nd], pl.dflags[nd], ra, pods[p], k, now_ns, &r, e, o);
+        ra.E[(int64_t)p * ra.n_rn + k] = e;
+        ra.O[(int64_t)p * ra.n_rn + k] = o;
+    }
+    if (ra.M) {   // placement: the split for rsv_best_resolve (a wave is one 64-entry group)
+        const bool scored = e && rsv_entry_scored(e, o);
+        const unsigned long long bk = wave_max_u64(e && !scored ? rsv_base_key(e, nd) : 0ull);
+        const unsigned long long bal = __ballot(scored);
+        const int lane = threadIdx.x & 63;
+        int32_t base = 0;
+        if (lane == 0 && (k >> 6) < ra.ngroups) {   // (a wave past the last entry has no group)
+            ra.G[(int64_t)p * ra.ngroups + (k >> 6)] = bk;
+            if (bal) base = atomicAdd(&ra.Mn[p], (int32_t)__popcll(bal));
+        }
+        base = __shfl(base, 0, 64);
+        if (scored) ra.M[(int64_t)p * ra.n_rn + base + (int32_t)__popcll(bal & ((1ull << lane) - 1ull))] = k;
+    }
+    if (!live) return;
+    const int64_t node = nd;
     if (scores && node >= col_begin && node < col_end) {
         const int64_t col = node - col_begin;
         scores[(int64_t)p * score_stride + col] = (uint16_t)(r.fit | (r.la << 8));
@@ -1511,21 +1687,23 @@ __global__ void k_quota_apply(const uint8_t *__restrict__ gate, int32_t P, unsig
 // Reservation.Reserve takes the nomination of PreScore, or runs NominateReservation itself when
 // scheduleOne skipped scoring (plugin.go:525-560): on a feasible node both are kg_rsv_nominate
 // over the same restored state (the pre-Reserve row: call before the AssumePod delta).
-__device__ __forceinline__ void rsv_commit(const kg_planes &pl, const RsvArgs &ra, const kg_pod_dev &p, int32_t node) {
+// `row`: the node's pre-Reserve canonical row (global, or a copy in LDS)
+__device__ __forceinline__ void rsv_commit(const kg_planes &pl, const RsvArgs &ra, const kg_pod_dev &p, int32_t node,
+                                           const kg_node_row &row) {
     if (ra.rsv && pl.rsv_of) {
         const int32_t k = pl.rsv_of[node];
         if (k >= 0) {
             const kg_reservation *rs = ra.rsv + ra.rfirst[k];
             kg_rsv_view v;
-            kg_rsv_restore(pl.rows[node], rs, ra.rfirst[k + 1] - ra.rfirst[k], p, v);
-            const int nom = kg_rsv_nominate(pl.rows[node], v, rs, p);
+            kg_rsv_restore(row, rs, ra.rfirst[k + 1] - ra.rfirst[k], p, v);
+            const int nom = kg_rsv_nominate(row, v, rs, p);
             if (nom >= 0) kg_rsv_commit(ra.rsv[ra.rfirst[k] + nom], p);
         }
     }
 }
 __device__ __forceinline__ void rsv_quota_commit(const kg_planes &pl, const RsvArgs &ra, const kg_pod_dev &p,
                                                  int32_t node) {
-    rsv_commit(pl, ra, p, node);
+    rsv_commit(pl, ra, p, node, pl.rows[node]);
     if (ra.quota && p.quota >= 0) kg_quota_commit(ra.quota, p.quota, p);
 }
 
@@ -1561,6 +1739,8 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
 // block max; (B) Reserve, one thread per part, and the committed node's planes.  The next pod's row
 // and tile keys are prefetched while the current pod is resolved.
 
+// RSV: the batch has reservation nodes (a separate instantiation: the plain path keeps its register budget)
+template <bool RSV>
 __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_planes pl,
                                                                 const kg_pod_dev *__restrict__ pods, int32_t pod_begin,
                                                                 int32_t n, const uint32_t *partials, int32_t tiles_total,
@@ -1592,11 +1772,17 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     __shared__ NodeCacheEntry ncache[KG_NCACHE];
     // NodeNUMAResource: canonical rows of the cached nodes (the hint enumeration of a re-score reads
     // LDS, not a chain of dependent global loads) and the committed node's row for the zone commit
-    __shared__ __attribute__((aligned(16))) kg_node_row nrow[KG_NCACHE + 1];
+    // (+ its pre-Reserve copy, which the Reservation nomination reads beside the Reserve parts)
+    __shared__ __attribute__((aligned(16))) kg_node_row nrow[KG_NCACHE + 2];
     constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16);
     static_assert(sizeof(kg_node_row) % 16 == 0 && ROW_U4 <= 64, "rows are staged as 16-byte words by one wave");
     const bool numa_on = (c.plugins & KG_PLUGIN_NUMA) != 0;
+    const bool rsv_on = RSV && ra.rsv && ra.n_rn > 0;
     __shared__ int32_t n_slow;
+    // Reservation split (ra.M): the entry groups holding a touched reservation node (rsv_best_resolve)
+    __shared__ uint8_t gflag[KG_RSV_MAX_GROUPS];
+    __shared__ int32_t glist[KG_MAX_CHUNK];
+    __shared__ int32_t n_glist;
     const int tid = threadIdx.x;
     // tile keys of the next pod, prefetched into registers by the thread owning the tile
     const bool key_prefetch = tiles_total <= KG_RESOLVE_THREADS;
@@ -1623,8 +1809,11 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         n_rescan[0] = n_rescan[1] = 0;
         n_slow = *slow_count;
         n_prevt = 0;
+        n_glist = 0;
     }
     for (int t = tid; t < tiles_total; t += KG_RESOLVE_THREADS) ttile[t] = 0;
+    if (rsv_on && ra.M)
+        for (int g = tid; g < ra.ngroups; g += KG_RESOLVE_THREADS) gflag[g] = 0;
     if (tid < POD_DW && n > 0) reinterpret_cast<uint32_t *>(&lpod[0])[tid] = reinterpret_cast<const uint32_t *>(pods + pod_begin)[tid];
     load_keys(0, kcur);
     __syncthreads();
@@ -1651,6 +1840,21 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         load_keys(j + 1, knxt);
         unsigned long long best = 0;
         const int nt = n_touched;
+        if (rsv_on) {
+            // nodes with reservations: this pod's entries of the nodes earlier pods of the chunk touched, refreshed
+            // by the upper waves while the lower ones scan the tiles (the scan leaves them idle: ≤ 256 tiles)
+            unsigned long long *E = ra.E + (int64_t)j * ra.n_rn;
+            int64_t *O = ra.O + (int64_t)j * ra.n_rn;
+            for (int q = tid - KG_RESOLVE_THREADS / 2; q >= 0 && q < nt; q += KG_RESOLVE_THREADS / 2) {
+                const int32_t nd = touched[q];
+                const int32_t k = pl.rsv_of[nd];
+                if (k < 0) continue;
+                if (q < KG_NCACHE)   // the committed row and flags cached in LDS
+                    rsv_entry(c, nrow[q], ncache[q].n.df, ra, pd, k, now_ns, nullptr, E[k], O[k]);
+                else
+                    rsv_entry(c, pl.rows[nd], pl.dflags[nd], ra, pd, k, now_ns, nullptr, E[k], O[k]);
+            }
+        }
         // a pod that requires a reservation can only land on reservation nodes (rsv part below)
         const bool plain_ok = !(pd.flags & KGP_RSV_REQUIRED);
         for (int t = tid; t < tiles_total; t += KG_RESOLVE_THREADS) {
@@ -1737,19 +1941,15 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         if (tid == 0) n_rescan[par] = 0;   // pod j + 2's counter: every reader of it is past the sync above
 #pragma unroll
         for (int q = 0; q < KG_PARTIAL_SLOTS; q++) kcur[q] = knxt[q];
-        if (ra.rsv && ra.n_rn > 0) {
+        if (rsv_on) {
             __syncthreads();
-            // nodes with reservations: refresh this pod's entries of the nodes earlier pods touched,
-            // then PreScore / Score / NormalizeScore over every reservation node
-            unsigned long long *E = ra.E + (int64_t)j * ra.n_rn;
-            int64_t *O = ra.O + (int64_t)j * ra.n_rn;
-            for (int q = tid; q < nt; q += KG_RESOLVE_THREADS) {
-                const int32_t k = pl.rsv_of[touched[q]];
-                if (k >= 0) rsv_entry(c, pl, ra, pd, k, now_ns, nullptr, E[k], O[k]);
-            }
-            __syncthreads();
+            // PreScore / Score / NormalizeScore over every reservation node (the refreshed entries are ordered
+            // by the barriers above)
+            const unsigned long long *E = ra.E + (int64_t)j * ra.n_rn;
+            const int64_t *O = ra.O + (int64_t)j * ra.n_rn;
             const unsigned long long rk =
-                rsv_best_block<KG_RESOLVE_THREADS>(c, E, O, ra.rnode, ra.n_rn, nullptr, 0, 0, red, redo);
+                ra.M ? rsv_best_resolve<KG_RESOLVE_THREADS>(c, pl, ra, j, touched, nt, gflag, glist, n_glist, red, redo)
+                     : rsv_best_block<KG_RESOLVE_THREADS>(c, E, O, ra.rnode, ra.n_rn, nullptr, 0, 0, red, redo);
             wb = wb > rk ? wb : rk;
         }
         const unsigned long long w = gate_ok[par] ? wb : 0ull;   // a pod failing the quota gate is unschedulable
@@ -1764,25 +1964,26 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             continue;   // nothing changed: the next pod's first barrier orders the outputs
         }
         // Reserve.  The Reservation nomination (restore) and NodeNUMAResource's zone commit (its
-        // amplified-cpu filter) read the pre-Reserve node, so they go first when enabled.
+        // amplified-cpu filter) read the pre-Reserve node: the zone commit goes first when enabled, the
+        // nomination reads a pre-Reserve copy of the row beside the parts.
         // the node's canonical row, staged into LDS by one wave (a single coalesced round trip): the
         // Reserve parts below update and re-derive from this copy and store their fields back
         kg_node_row &srow = nrow[KG_NCACHE];
+        kg_node_row &srow0 = nrow[KG_NCACHE + 1];
         uint32_t old_df = 0;
         int64_t old_metric = 0;
         if (tid == 0) {   // the planes tid 0 needs, in flight with the row
             old_df = pl.dflags[node];
             old_metric = pl.metric_ns[node];
         }
-        if (tid < ROW_U4) reinterpret_cast<uint4 *>(&srow)[tid] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
+        if (tid < ROW_U4)
+            reinterpret_cast<uint4 *>(&srow)[tid] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
+        else if (rsv_on && tid >= 64 && tid < 64 + ROW_U4)
+            reinterpret_cast<uint4 *>(&srow0)[tid - 64] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid - 64];
         __syncthreads();
-        if ((ra.rsv && ra.n_rn > 0) || numa_on) {
-            if (tid == 0) {
-                rsv_commit(pl, ra, pd, node);
-                kg_numa_commit(c, srow, pd);
-            }
-            // the parts below read only srow (LDS); tid 0's global writes are ordered for the next pod by
-            // the full barrier that ends this pod
+        if (numa_on) {
+            if (tid == 0) kg_numa_commit(c, srow, pd);
+            // the parts below read only srow (LDS)
             __syncthreads();
         }
         // the node's slot in the touched list (and node cache): its position, or the next one
@@ -1792,7 +1993,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         NodeCacheEntry *ce = slot < KG_NCACHE ? &ncache[slot] : nullptr;
         // AssumePod / LoadAware deltas and the committed node's derived planes, one thread per part:
         // thread 64 + r owns resource r's fields of the row and its Fit planes, 64 + 8 + r the LoadAware
-        // terms of r; thread 0 the reservation / quota Reserve, the pod count and the outputs
+        // terms of r; thread 192 the reservation nomination; thread 0 the quota Reserve, the pod count and the outputs
         kg_node_row &row = pl.rows[node];
         if (tid >= 64 && tid < 64 + KG_NUM_RES) {
             const int r = tid - 64;
@@ -1843,6 +2044,8 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             row.zone_allocated[zi][0] = srow.zone_allocated[zi][0];
             row.zone_allocated[zi][1] = srow.zone_allocated[zi][1];
             if (zi == 0) row.zone_alloc_keys = srow.zone_alloc_keys;
+        } else if (rsv_on && tid == 192) {   // Reservation.Reserve on the pre-Reserve row (its global writes are
+            rsv_commit(pl, ra, pd, node, srow0);   // ordered for the next pod by the barrier that ends this one)
         } else if (tid == 0) {
             if (ra.quota && pd.quota >= 0) kg_quota_commit(ra.quota, pd.quota, pd);
             const int32_t pc = srow.pod_count + 1;
@@ -1854,6 +2057,11 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             if (slot == nt) {
                 touched[n_touched++] = node;
                 ttile[node / KG_TILE] = 1;
+                const int32_t rk = rsv_on && ra.M ? pl.rsv_of[node] : -1;
+                if (rk >= 0 && !gflag[rk / KG_RSV_GROUP]) {   // its entry group: rescanned by later pods
+                    gflag[rk / KG_RSV_GROUP] = 1;
+                    glist[n_glist++] = rk / KG_RSV_GROUP;
+                }
             }
             out_node[j] = node;
             out_score[j] = (int64_t)(w >> 32) - 1;
@@ -1861,7 +2069,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         // the flags step reads the parts' LDS results only: their global stores (row, planes) complete under
         // the full barrier that ends this pod, before the next pod reads them
         __syncthreads();
-        if (numa_on && ce && tid >= 128 && tid < 128 + ROW_U4)   // the committed row into the node cache
+        if ((numa_on || rsv_on) && ce && tid >= 128 && tid < 128 + ROW_U4)   // the committed row into the node cache
             reinterpret_cast<uint4 *>(&nrow[slot])[tid - 128] = reinterpret_cast<const uint4 *>(&srow)[tid - 128];
         if (tid == 0) {   // kg_finalize_flags from the parts (metric and the static bits are unchanged)
             bool slow = false;
@@ -1978,7 +2186,7 @@ struct kg_engine {
                                         // NodeNUMAResource batches, 2 for every batch, 0 never (KG_PLACE_PIPELINE)
     hipEvent_t ev_res[3] = {};          // (KG_PLACE_PIPELINE=0 turns it off)
     // Reservation / ElasticQuota (config 5)
-    void *rsv_mem = nullptr;            // slots | rfirst | rnode | E | O
+    void *rsv_mem = nullptr;            // slots | rfirst | rnode | E | O | M | Mn | G
     kg_reservation *rsv = nullptr;      // slots grouped by node (stable)
     std::vector<int32_t> rsv_perm;      // device slot → caller index
     int32_t n_rsv = 0;
@@ -1986,6 +2194,8 @@ struct kg_engine {
     int32_t n_rn = 0;
     unsigned long long *rsv_e = nullptr;
     int64_t *rsv_o = nullptr;
+    int32_t *rsv_m = nullptr, *rsv_mn = nullptr;   // the placement split of the entries (RsvArgs::M / Mn / G)
+    unsigned long long *rsv_g = nullptr;
     kg_quota *quota = nullptr;
     int32_t n_quota = 0;
     int32_t max_pod_quota = -1;         // largest quota index of the batch
@@ -2533,6 +2743,13 @@ RsvArgs rsv_args(const kg_engine *e) {
         ra.n_rn = e->n_rn;
         ra.E = e->rsv_e;
         ra.O = e->rsv_o;
+        const int32_t ng = (e->n_rn + KG_RSV_GROUP - 1) / KG_RSV_GROUP;
+        if (ng <= KG_RSV_MAX_GROUPS) {   // else the resolve reduces over every entry (rsv_best_block)
+            ra.M = e->rsv_m;
+            ra.Mn = e->rsv_mn;
+            ra.G = e->rsv_g;
+            ra.ngroups = ng;
+        }
     }
     if (e->consts.plugins & KG_PLUGIN_ELASTICQUOTA) ra.quota = e->quota;
     ra.quota_parent = e->cfg.eq_check_parent_quota != 0;
@@ -2574,10 +2791,13 @@ kg_status quota_ready(kg_engine *e) {
 }
 
 // entries of pods [pod_begin, pod_begin + n) (n ≤ KG_RSV_POD_CHUNK) for every reservation node
+// split: also the placement split of the entries (RsvArgs::M / Mn / G) for the resolve
 kg_status rsv_eval_chunk(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
-                         uint8_t *numa_scores, int32_t mask_words, int64_t score_stride) {
-    const RsvArgs ra = rsv_args(e);
+                         uint8_t *numa_scores, int32_t mask_words, int64_t score_stride, bool split = false) {
+    RsvArgs ra = rsv_args(e);
     if (!ra.rsv || n <= 0) return KG_OK;
+    if (!split) ra.M = nullptr;
+    if (ra.M) HIP_TRY(e, hipMemsetAsync(ra.Mn, 0, 4 * (size_t)n, e->stream));
     dim3 grid((unsigned)((ra.n_rn + 255) / 256), (unsigned)n);
     hipLaunchKernelGGL(k_rsv_eval, grid, dim3(256), 0, e->stream, e->consts, e->pl, ra, e->pods + pod_begin, n, now_ns,
                        (unsigned long long *)mask, scores, numa_scores, e->shard_begin, e->shard_end, mask_words,
@@ -2734,6 +2954,8 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
     e->rfirst = e->rnode = nullptr;
     e->rsv_e = nullptr;
     e->rsv_o = nullptr;
+    e->rsv_m = e->rsv_mn = nullptr;
+    e->rsv_g = nullptr;
     e->n_rsv = e->n_rn = 0;
     e->rsv_perm.clear();
     e->pl.cap = cap;
@@ -3075,7 +3297,7 @@ kg_status chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n,
     // ranks in the multi-GPU placement, so each rank holds all of them), rows 0..n of E / O
     if (rsv_args(e).rsv) {
         if (n > KG_RSV_POD_CHUNK) return set_err(e, KG_ERR_RANGE, "chunk larger than the reservation entry buffer");
-        return rsv_eval_chunk(e, now_ns, pod_begin, n, nullptr, nullptr, nullptr, 0, 0);
+        return rsv_eval_chunk(e, now_ns, pod_begin, n, nullptr, nullptr, nullptr, 0, 0, true);
     }
     return KG_OK;
 }
@@ -3097,7 +3319,8 @@ kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t
     st = slow_refresh(e);
     if (st) return st;
     const bool numa = (e->consts.plugins & KG_PLUGIN_NUMA) != 0;
-    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream, e->consts, e->pl, e->pods, pod_begin, n,
+    hipLaunchKernelGGL(ra.rsv ? k_resolve<true> : k_resolve<false>, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream,
+                       e->consts, e->pl, e->pods, pod_begin, n,
                        partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev, ra,
                        numa && n > e->numa_chunk_pods ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count,
                        numa ? 0 : 1,   // the NUMA chunk kernels list slow nodes themselves (exact pair path)
@@ -3501,16 +3724,22 @@ kg_status kg_rsv_set(kg_engine *e, const kg_reservation *rsv, int32_t n) {
     const size_t sb = up(sizeof(kg_reservation) * (size_t)(n > 0 ? n : 1)), fb = up(4 * rfirst.size()),
                  nb = up(4 * (size_t)(n_rn > 0 ? n_rn : 1)),
                  eb = up(8 * (size_t)KG_RSV_POD_CHUNK * (size_t)(n_rn > 0 ? n_rn : 1));
+    // the placement split: scored-entry lists [chunk][n_rn], their counts, per-group keys [chunk][groups]
+    const size_t mb = up(4 * (size_t)KG_RSV_POD_CHUNK * (size_t)(n_rn > 0 ? n_rn : 1)), cb = up(4 * (size_t)KG_RSV_POD_CHUNK),
+                 gb = up(8 * (size_t)KG_RSV_POD_CHUNK * (size_t)((n_rn + KG_RSV_GROUP - 1) / KG_RSV_GROUP + 1));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     if (e->rsv_mem) HIP_TRY(e, hipFree(e->rsv_mem));
     e->rsv_mem = nullptr;
-    HIP_TRY(e, hipMalloc(&e->rsv_mem, sb + fb + nb + 2 * eb));
+    HIP_TRY(e, hipMalloc(&e->rsv_mem, sb + fb + nb + 2 * eb + mb + cb + gb));
     char *m = (char *)e->rsv_mem;
     e->rsv = (kg_reservation *)m;
     e->rfirst = (int32_t *)(m + sb);
     e->rnode = (int32_t *)(m + sb + fb);
     e->rsv_e = (unsigned long long *)(m + sb + fb + nb);
     e->rsv_o = (int64_t *)(m + sb + fb + nb + eb);
+    e->rsv_m = (int32_t *)(m + sb + fb + nb + 2 * eb);
+    e->rsv_mn = (int32_t *)(m + sb + fb + nb + 2 * eb + mb);
+    e->rsv_g = (unsigned long long *)(m + sb + fb + nb + 2 * eb + mb + cb);
     if (n) HIP_TRY(e, h2d(e, e->rsv, slots.data(), sizeof(kg_reservation) * (size_t)n, e->stream));
     HIP_TRY(e, h2d(e, e->rfirst, rfirst.data(), 4 * rfirst.size(), e->stream));
     if (n_rn) HIP_TRY(e, h2d(e, e->rnode, rnode.data(), 4 * (size_t)n_rn, e->stream));
