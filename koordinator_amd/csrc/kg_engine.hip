@@ -1341,6 +1341,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_CHUNK_WP
 //   O = PreScore order of the node (INT64_MAX: none or infeasible)
 // The per-pod PreScore preferred node, Score override (1000) and DefaultNormalizeScore max
 // are block reductions over the pod's entries (rsv_best_block).
+struct kg_rsv_ment {   // one scored entry of a pod, as k_rsv_eval computed it
+    int32_t k, node;
+    unsigned long long e;
+    int64_t o;
+};
 struct RsvArgs {
     kg_reservation *rsv;        // slots, grouped by node (nullptr: Reservation off)
     const int32_t *rfirst;      // [n_rn + 1] first slot of each reservation node
@@ -1352,7 +1357,7 @@ struct RsvArgs {
     kg_quota *quota;            // ElasticQuota groups (nullptr: ElasticQuota off)
     // placement chunks (nullptr in matrix mode, or more groups than the resolve tracks): the entries split for
     // the resolve's reduction, written by k_rsv_eval beside E / O (rsv_best_resolve)
-    int32_t *M;                 // [pods][n_rn] the entries that can take the preferred node or a raw score
+    struct kg_rsv_ment *M;      // [pods][n_rn] the entries that can take the preferred node or a raw score
     int32_t *Mn;                // [pods] their count
     unsigned long long *G;      // [pods][ngroups] per 64-entry group: the best key of its other feasible entries
     int32_t ngroups;
@@ -1488,47 +1493,94 @@ __device__ unsigned long long rsv_best_block(const kg_consts &c, const unsigned 
     return best;
 }
 
-// rsv_best_block for pod j of a placement chunk, over the split k_rsv_eval wrote: pass 1 (preferred node,
-// largest raw score) and the scored part of pass 2 walk only the scored entries M and the reservation nodes
-// earlier pods of the chunk touched (their refreshed entries; duplicates are harmless under min / max); the
-// other feasible entries key on their base total whatever NormalizeScore's maximum, so their best is the
-// max of the per-group keys G — except in groups holding a touched node (`gflag`, listed in `glist`), which
-// are rescanned from the refreshed entries.  The same keys as rsv_best_block over every entry.
+// The first KG_RSV_PF scored entries and the group keys of the resolve's next pod, loaded into LDS by the
+// waves a Reserve leaves idle (rsv_prefetch) while the current pod is reserved.
+#define KG_RSV_PF 1024
+struct RsvPrefetch {
+    int32_t k[KG_RSV_PF], node[KG_RSV_PF];
+    unsigned long long e[KG_RSV_PF];
+    int64_t o[KG_RSV_PF];
+    unsigned long long g[KG_RSV_MAX_GROUPS];
+    int32_t n, nm;   // entries held (≤ KG_RSV_PF), scored entries of the pod
+};
+// pod j's split into `pf` by threads [t0, t0 + nt) (the caller orders it against the readers with barriers)
+__device__ __forceinline__ void rsv_prefetch(const RsvArgs &ra, int32_t j, RsvPrefetch &pf, int t, int nthr) {
+    const int32_t nm = ra.Mn[j];
+    const int32_t n = nm < KG_RSV_PF ? nm : KG_RSV_PF;
+    const kg_rsv_ment *M = ra.M + (int64_t)j * ra.n_rn;
+    for (int q = t; q < n; q += nthr) {
+        const kg_rsv_ment m = M[q];
+        pf.k[q] = m.k;
+        pf.node[q] = m.node;
+        pf.e[q] = m.e;
+        pf.o[q] = m.o;
+    }
+    const unsigned long long *G = ra.G + (int64_t)j * ra.ngroups;
+    for (int g = t; g < ra.ngroups; g += nthr) pf.g[g] = G[g];
+    if (t == 0) {
+        pf.n = n;
+        pf.nm = nm;
+    }
+}
+
+// rsv_best_block for pod j of a placement chunk, over the split k_rsv_eval wrote (prefetched into `pf`): pass 1
+// (preferred node, largest raw score) and the scored part of pass 2 walk only the scored entries and the
+// reservation nodes earlier pods of the chunk touched (their refreshed entries; duplicates are harmless under
+// min / max); a scored entry in a group holding a touched node (`gflag`) is re-read from the refreshed E / O.
+// The other feasible entries key on their base total whatever NormalizeScore's maximum, so their best is the
+// max of the per-group keys — except in touched groups (listed in `glist`), which are rescanned from the
+// refreshed entries.  The same keys as rsv_best_block over every entry.
 template <int NT>
 __device__ unsigned long long rsv_best_resolve(const kg_consts &c, const kg_planes &pl, const RsvArgs &ra, int32_t j,
-                                               const int32_t *touched, int nt, const uint8_t *gflag,
-                                               const int32_t *glist, int ng, unsigned long long *red, int64_t *redo) {
+                                               const RsvPrefetch &pf, const int32_t *touched, int nt,
+                                               const uint8_t *gflag, const int32_t *glist, int ng,
+                                               unsigned long long *red, int64_t *redo) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     constexpr int NW = NT / 64;
     const unsigned long long *E = ra.E + (int64_t)j * ra.n_rn;
     const int64_t *O = ra.O + (int64_t)j * ra.n_rn;
-    const int32_t *M = ra.M + (int64_t)j * ra.n_rn;
-    const int32_t nm = ra.Mn[j];
-    const int nq = nm + nt;
-    auto entry_k = [&](int q) -> int32_t { return q < nm ? M[q] : pl.rsv_of[touched[q - nm]]; };
+    const kg_rsv_ment *M = ra.M + (int64_t)j * ra.n_rn;
+    const int nm = pf.nm, nq = nm + nt;
+    // entry q: a scored entry (prefetched, or from the list), else touched node q − nm; e = 0 ⇒ none
+    auto get = [&](int q, int32_t &k, int32_t &node, unsigned long long &e, int64_t &o) {
+        if (q < nm) {
+            if (q < pf.n) {
+                k = pf.k[q];
+                node = pf.node[q];
+                e = pf.e[q];
+                o = pf.o[q];
+            } else {
+                const kg_rsv_ment m = M[q];
+                k = m.k;
+                node = m.node;
+                e = m.e;
+                o = m.o;
+            }
+            if (gflag[k / KG_RSV_GROUP]) {   // its group holds a touched node: the refreshed entry
+                e = E[k];
+                o = O[k];
+            }
+        } else {
+            node = touched[q - nm];
+            k = pl.rsv_of[node];
+            e = k >= 0 ? E[k] : 0ull;
+            o = k >= 0 ? O[k] : INT64_MAX;
+        }
+    };
     int64_t bo = INT64_MAX;
     int32_t bk = INT32_MAX;
     uint32_t mraw = 0;
-    for (int q0 = tid; q0 < nq; q0 += NT * KG_RSV_UNR) {
-        int32_t k[KG_RSV_UNR];
-        unsigned long long e[KG_RSV_UNR];
-        int64_t o[KG_RSV_UNR];
-#pragma unroll
-        for (int u = 0; u < KG_RSV_UNR; u++) k[u] = q0 + u * NT < nq ? entry_k(q0 + u * NT) : -1;
-#pragma unroll
-        for (int u = 0; u < KG_RSV_UNR; u++) {
-            e[u] = k[u] >= 0 ? E[k[u]] : 0ull;
-            o[u] = k[u] >= 0 ? O[k[u]] : INT64_MAX;
-        }
-#pragma unroll
-        for (int u = 0; u < KG_RSV_UNR; u++) {
-            if (!e[u]) continue;
-            const uint32_t raw = (uint32_t)((e[u] >> 16) & 0xFFFFull);
-            mraw = mraw > raw ? mraw : raw;
-            if (o[u] != 0 && o[u] != INT64_MAX && (o[u] < bo || (o[u] == bo && k[u] < bk))) {
-                bo = o[u];
-                bk = k[u];
-            }
+    for (int q = tid; q < nq; q += NT) {
+        int32_t k, node;
+        unsigned long long e;
+        int64_t o;
+        get(q, k, node, e, o);
+        if (!e) continue;
+        const uint32_t raw = (uint32_t)((e >> 16) & 0xFFFFull);
+        mraw = mraw > raw ? mraw : raw;
+        if (o != 0 && o != INT64_MAX && (o < bo || (o == bo && k < bk))) {
+            bo = o;
+            bk = k;
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -1562,30 +1614,20 @@ __device__ unsigned long long rsv_best_resolve(const kg_consts &c, const kg_plan
     const unsigned long long mx = pref >= 0 ? 1000ull : mraw;
     __syncthreads();
     unsigned long long best = 0;
-    for (int q0 = tid; q0 < nq; q0 += NT * KG_RSV_UNR) {   // the scored entries and the touched nodes
-        int32_t k[KG_RSV_UNR];
-        unsigned long long e[KG_RSV_UNR];
-        int32_t nd[KG_RSV_UNR];
-#pragma unroll
-        for (int u = 0; u < KG_RSV_UNR; u++) k[u] = q0 + u * NT < nq ? entry_k(q0 + u * NT) : -1;
-#pragma unroll
-        for (int u = 0; u < KG_RSV_UNR; u++) {
-            e[u] = k[u] >= 0 ? E[k[u]] : 0ull;
-            nd[u] = k[u] >= 0 ? ra.rnode[k[u]] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < KG_RSV_UNR; u++) {
-            if (!e[u]) continue;
-            const unsigned long long raw = k[u] == pref ? 1000ull : ((e[u] >> 16) & 0xFFFFull);
-            const uint32_t sn = mx ? (uint32_t)(100ull * raw / mx) : 0u;
-            const unsigned long long total = (e[u] >> 32) - 1ull + (unsigned long long)c.weight_rsv * sn;
-            const unsigned long long key = ((total + 1ull) << 32) | (0xFFFFFFFFull - (unsigned long long)(uint32_t)nd[u]);
-            best = best > key ? best : key;
-        }
+    for (int q = tid; q < nq; q += NT) {   // the scored entries and the touched nodes
+        int32_t k, node;
+        unsigned long long e;
+        int64_t o;
+        get(q, k, node, e, o);
+        if (!e) continue;
+        const unsigned long long raw = k == pref ? 1000ull : ((e >> 16) & 0xFFFFull);
+        const uint32_t sn = mx ? (uint32_t)(100ull * raw / mx) : 0u;
+        const unsigned long long total = (e >> 32) - 1ull + (unsigned long long)c.weight_rsv * sn;
+        const unsigned long long key = ((total + 1ull) << 32) | (0xFFFFFFFFull - (unsigned long long)(uint32_t)node);
+        best = best > key ? best : key;
     }
-    const unsigned long long *G = ra.G + (int64_t)j * ra.ngroups;
     for (int g = tid; g < ra.ngroups; g += NT) {   // groups without a touched node: their best base key stands
-        const unsigned long long key = gflag[g] ? 0ull : G[g];
+        const unsigned long long key = gflag[g] ? 0ull : pf.g[g];
         best = best > key ? best : key;
     }
     for (int q = tid; q < ng * KG_RSV_GROUP; q += NT) {   // the others, from the refreshed entries
@@ -1634,7 +1676,7 @@ __global__ __launch_bounds__(256) void k_rsv_eval(kg_consts c, kg_planes pl, Rsv
             if (bal) base = atomicAdd(&ra.Mn[p], (int32_t)__popcll(bal));
         }
         base = __shfl(base, 0, 64);
-        if (scored) ra.M[(int64_t)p * ra.n_rn + base + (int32_t)__popcll(bal & ((1ull << lane) - 1ull))] = k;
+        if (scored) ra.M[(int64_t)p * ra.n_rn + base + (int32_t)__popcll(bal & ((1ull << lane) - 1ull))] = kg_rsv_ment{k, nd, e, o};
     }
     if (!live) return;
     const int64_t node = nd;
@@ -1700,6 +1742,16 @@ __device__ __forceinline__ void rsv_commit(const kg_planes &pl, const RsvArgs &r
             if (nom >= 0) kg_rsv_commit(ra.rsv[ra.rfirst[k] + nom], p);
         }
     }
+}
+// rsv_commit in the resolve: the pod's entry of the node (E, refreshed when an earlier pod of the chunk touched
+// it) holds the nomination PreScore made on the same restored state — Reserve's own NominateReservation
+// (plugin.go:525-560) would recompute the same slot
+__device__ __forceinline__ void rsv_commit_entry(const kg_planes &pl, const RsvArgs &ra, const kg_pod_dev &p,
+                                                 int32_t node, const unsigned long long *E) {
+    const int32_t k = pl.rsv_of[node];
+    if (k < 0) return;
+    const int nom = (int)(E[k] & 0xFFFFull) - 1;
+    if (nom >= 0) kg_rsv_commit(ra.rsv[ra.rfirst[k] + nom], p);
 }
 __device__ __forceinline__ void rsv_quota_commit(const kg_planes &pl, const RsvArgs &ra, const kg_pod_dev &p,
                                                  int32_t node) {
@@ -1772,8 +1824,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     __shared__ NodeCacheEntry ncache[KG_NCACHE];
     // NodeNUMAResource: canonical rows of the cached nodes (the hint enumeration of a re-score reads
     // LDS, not a chain of dependent global loads) and the committed node's row for the zone commit
-    // (+ its pre-Reserve copy, which the Reservation nomination reads beside the Reserve parts)
-    __shared__ __attribute__((aligned(16))) kg_node_row nrow[KG_NCACHE + 2];
+    __shared__ __attribute__((aligned(16))) kg_node_row nrow[KG_NCACHE + 1];
     constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16);
     static_assert(sizeof(kg_node_row) % 16 == 0 && ROW_U4 <= 64, "rows are staged as 16-byte words by one wave");
     const bool numa_on = (c.plugins & KG_PLUGIN_NUMA) != 0;
@@ -1783,6 +1834,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     __shared__ uint8_t gflag[KG_RSV_MAX_GROUPS];
     __shared__ int32_t glist[KG_MAX_CHUNK];
     __shared__ int32_t n_glist;
+    __shared__ RsvPrefetch rpf;   // the split of the pod whose reduction is next (rsv_prefetch)
     const int tid = threadIdx.x;
     // tile keys of the next pod, prefetched into registers by the thread owning the tile
     const bool key_prefetch = tiles_total <= KG_RESOLVE_THREADS;
@@ -1812,8 +1864,10 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         n_glist = 0;
     }
     for (int t = tid; t < tiles_total; t += KG_RESOLVE_THREADS) ttile[t] = 0;
-    if (rsv_on && ra.M)
+    if (rsv_on && ra.M) {
         for (int g = tid; g < ra.ngroups; g += KG_RESOLVE_THREADS) gflag[g] = 0;
+        if (n > 0) rsv_prefetch(ra, 0, rpf, tid, KG_RESOLVE_THREADS);
+    }
     if (tid < POD_DW && n > 0) reinterpret_cast<uint32_t *>(&lpod[0])[tid] = reinterpret_cast<const uint32_t *>(pods + pod_begin)[tid];
     load_keys(0, kcur);
     __syncthreads();
@@ -1948,7 +2002,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             const unsigned long long *E = ra.E + (int64_t)j * ra.n_rn;
             const int64_t *O = ra.O + (int64_t)j * ra.n_rn;
             const unsigned long long rk =
-                ra.M ? rsv_best_resolve<KG_RESOLVE_THREADS>(c, pl, ra, j, touched, nt, gflag, glist, n_glist, red, redo)
+                ra.M ? rsv_best_resolve<KG_RESOLVE_THREADS>(c, pl, ra, j, rpf, touched, nt, gflag, glist, n_glist, red, redo)
                      : rsv_best_block<KG_RESOLVE_THREADS>(c, E, O, ra.rnode, ra.n_rn, nullptr, 0, 0, red, redo);
             wb = wb > rk ? wb : rk;
         }
@@ -1961,25 +2015,22 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 out_node[j] = node;
                 out_score[j] = w ? (int64_t)(w >> 32) - 1 : -1;
             }
+            if (rsv_on && ra.M && j + 1 < n && tid >= KG_RESOLVE_THREADS / 2)   // (the reduction's reads are done)
+                rsv_prefetch(ra, j + 1, rpf, tid - KG_RESOLVE_THREADS / 2, KG_RESOLVE_THREADS / 2);
             continue;   // nothing changed: the next pod's first barrier orders the outputs
         }
-        // Reserve.  The Reservation nomination (restore) and NodeNUMAResource's zone commit (its
-        // amplified-cpu filter) read the pre-Reserve node: the zone commit goes first when enabled, the
-        // nomination reads a pre-Reserve copy of the row beside the parts.
+        // Reserve.  NodeNUMAResource's zone commit (its amplified-cpu filter) reads the pre-Reserve node, so it
+        // goes first when enabled; the Reservation commit takes the nomination from the pod's entry.
         // the node's canonical row, staged into LDS by one wave (a single coalesced round trip): the
         // Reserve parts below update and re-derive from this copy and store their fields back
         kg_node_row &srow = nrow[KG_NCACHE];
-        kg_node_row &srow0 = nrow[KG_NCACHE + 1];
         uint32_t old_df = 0;
         int64_t old_metric = 0;
         if (tid == 0) {   // the planes tid 0 needs, in flight with the row
             old_df = pl.dflags[node];
             old_metric = pl.metric_ns[node];
         }
-        if (tid < ROW_U4)
-            reinterpret_cast<uint4 *>(&srow)[tid] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
-        else if (rsv_on && tid >= 64 && tid < 64 + ROW_U4)
-            reinterpret_cast<uint4 *>(&srow0)[tid - 64] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid - 64];
+        if (tid < ROW_U4) reinterpret_cast<uint4 *>(&srow)[tid] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
         __syncthreads();
         if (numa_on) {
             if (tid == 0) kg_numa_commit(c, srow, pd);
@@ -2044,8 +2095,10 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             row.zone_allocated[zi][0] = srow.zone_allocated[zi][0];
             row.zone_allocated[zi][1] = srow.zone_allocated[zi][1];
             if (zi == 0) row.zone_alloc_keys = srow.zone_alloc_keys;
-        } else if (rsv_on && tid == 192) {   // Reservation.Reserve on the pre-Reserve row (its global writes are
-            rsv_commit(pl, ra, pd, node, srow0);   // ordered for the next pod by the barrier that ends this one)
+        } else if (rsv_on && tid == 192) {   // Reservation.Reserve (its global writes are ordered for the next pod
+            rsv_commit_entry(pl, ra, pd, node, ra.E + (int64_t)j * ra.n_rn);   // by the barrier that ends this one)
+        } else if (rsv_on && ra.M && tid >= KG_RESOLVE_THREADS / 2) {   // the idle upper waves: the next pod's split
+            if (j + 1 < n) rsv_prefetch(ra, j + 1, rpf, tid - KG_RESOLVE_THREADS / 2, KG_RESOLVE_THREADS / 2);
         } else if (tid == 0) {
             if (ra.quota && pd.quota >= 0) kg_quota_commit(ra.quota, pd.quota, pd);
             const int32_t pc = srow.pod_count + 1;
@@ -2194,7 +2247,8 @@ struct kg_engine {
     int32_t n_rn = 0;
     unsigned long long *rsv_e = nullptr;
     int64_t *rsv_o = nullptr;
-    int32_t *rsv_m = nullptr, *rsv_mn = nullptr;   // the placement split of the entries (RsvArgs::M / Mn / G)
+    kg_rsv_ment *rsv_m = nullptr;                  // the placement split of the entries (RsvArgs::M / Mn / G)
+    int32_t *rsv_mn = nullptr;
     unsigned long long *rsv_g = nullptr;
     kg_quota *quota = nullptr;
     int32_t n_quota = 0;
@@ -2954,7 +3008,8 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
     e->rfirst = e->rnode = nullptr;
     e->rsv_e = nullptr;
     e->rsv_o = nullptr;
-    e->rsv_m = e->rsv_mn = nullptr;
+    e->rsv_m = nullptr;
+    e->rsv_mn = nullptr;
     e->rsv_g = nullptr;
     e->n_rsv = e->n_rn = 0;
     e->rsv_perm.clear();
@@ -3725,7 +3780,8 @@ kg_status kg_rsv_set(kg_engine *e, const kg_reservation *rsv, int32_t n) {
                  nb = up(4 * (size_t)(n_rn > 0 ? n_rn : 1)),
                  eb = up(8 * (size_t)KG_RSV_POD_CHUNK * (size_t)(n_rn > 0 ? n_rn : 1));
     // the placement split: scored-entry lists [chunk][n_rn], their counts, per-group keys [chunk][groups]
-    const size_t mb = up(4 * (size_t)KG_RSV_POD_CHUNK * (size_t)(n_rn > 0 ? n_rn : 1)), cb = up(4 * (size_t)KG_RSV_POD_CHUNK),
+    const size_t mb = up(sizeof(kg_rsv_ment) * (size_t)KG_RSV_POD_CHUNK * (size_t)(n_rn > 0 ? n_rn : 1)),
+                 cb = up(4 * (size_t)KG_RSV_POD_CHUNK),
                  gb = up(8 * (size_t)KG_RSV_POD_CHUNK * (size_t)((n_rn + KG_RSV_GROUP - 1) / KG_RSV_GROUP + 1));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     if (e->rsv_mem) HIP_TRY(e, hipFree(e->rsv_mem));
@@ -3737,7 +3793,7 @@ kg_status kg_rsv_set(kg_engine *e, const kg_reservation *rsv, int32_t n) {
     e->rnode = (int32_t *)(m + sb + fb);
     e->rsv_e = (unsigned long long *)(m + sb + fb + nb);
     e->rsv_o = (int64_t *)(m + sb + fb + nb + eb);
-    e->rsv_m = (int32_t *)(m + sb + fb + nb + 2 * eb);
+    e->rsv_m = (kg_rsv_ment *)(m + sb + fb + nb + 2 * eb);
     e->rsv_mn = (int32_t *)(m + sb + fb + nb + 2 * eb + mb);
     e->rsv_g = (unsigned long long *)(m + sb + fb + nb + 2 * eb + mb + cb);
     if (n) HIP_TRY(e, h2d(e, e->rsv, slots.data(), sizeof(kg_reservation) * (size_t)n, e->stream));
