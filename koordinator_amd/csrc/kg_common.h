@@ -1083,6 +1083,19 @@ KG_HD bool kg_numa_binds(const kg_node_row &row, const kg_pod_dev &p, int &requi
     return true;
 }
 
+// the zone allocations of a feasible Reserve hint into the row
+KG_HD void kg_numa_apply(kg_node_row &row, const kg_numa_out &o) {
+    if (!o.feasible) return;
+    for (int j = 0; j < o.n_alloc; j++) {
+        const int zi = o.zone[j];
+        for (int r = 0; r < 2; r++) {
+            if (o.alloc[j][r] == 0) continue;
+            row.zone_allocated[zi][r] += o.alloc[j][r];
+            row.zone_alloc_keys |= 1u << (2 * zi + r);
+        }
+    }
+}
+
 // Reserve of NodeNUMAResource (plugin.go:375-419): record the zone allocations of the chosen node — the
 // hint of its Filter (for a cpuset, the trimmed hint of FilterByNUMANode with the cpuset options) and
 // allocateResourcesByHint on the original requests.  The cpuset itself is taken on the host (kg_cpuset.cpp).
@@ -1103,15 +1116,30 @@ KG_HD void kg_numa_commit(const kg_consts &c, kg_node_row &row, const kg_pod_dev
     } else {
         kg_numa_pair(c, row, p, o, nullptr, true);
     }
-    if (!o.feasible) return;
-    for (int j = 0; j < o.n_alloc; j++) {
-        const int zi = o.zone[j];
-        for (int r = 0; r < 2; r++) {
-            if (o.alloc[j][r] == 0) continue;
-            row.zone_allocated[zi][r] += o.alloc[j][r];
-            row.zone_alloc_keys |= 1u << (2 * zi + r);
-        }
+    kg_numa_apply(row, o);
+}
+
+// kg_numa_commit over a prebuilt zone table of the (pre-commit) row (k_resolve: built by one wave in LDS, so the
+// hint enumeration of the Reserve does table lookups instead of summing zones per mask); the cpuset path keeps
+// its trimmed provider.  Same allocation as kg_numa_commit.  Out of line on the device (the resolve keeps its
+// register budget).
+#if defined(__HIPCC__)
+static __host__ __device__ __noinline__
+#else
+inline
+#endif
+void kg_numa_commit_tab(const kg_consts &c, kg_node_row &row, const kg_pod_dev &p, const kg_zone_tab_data &zt) {
+    if (!(c.plugins & KG_PLUGIN_NUMA) || !(row.flags & KG_NODE_NUMA_OPTIONS) || row.numa_policy == KG_NUMA_NONE ||
+        !(row.flags & KG_NODE_NUMA_TOPO_VALID))
+        return;
+    int required, take;
+    if (kg_numa_binds(row, p, required, take)) {
+        kg_numa_commit(c, row, p);
+        return;
     }
+    kg_numa_out o;
+    kg_numa_pair_z<kg_zone_tab, false, true>(c, row, p, o, kg_zone_tab{zt}, nullptr, true);
+    kg_numa_apply(row, o);
 }
 
 // Exact int64 evaluation of one (pod, node) pair from the canonical row with NodeInfo's Requested /

@@ -1257,6 +1257,8 @@ __global__ void k_top1(const uint32_t *__restrict__ partials, int32_t tiles, int
     if (lane == 0) out[wave] = best;
 }
 
+// NUMA: the resolve instantiation may meet NodeNUMAResource (the plain one carries no NUMA code)
+template <bool NUMA>
 __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, const kg_pod_dev &p, int64_t node,
                                        int64_t n_nodes, int64_t now_ns) {
     if (node < 0 || node >= n_nodes) return 0ull;
@@ -1265,7 +1267,7 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
     load_node(c, pl, node, true, bm, now_ns, n);
     uint32_t fit, la, numa = 0;
     if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
-    if (c.plugins & KG_PLUGIN_NUMA) {
+    if (NUMA && (c.plugins & KG_PLUGIN_NUMA)) {
         const uint64_t ns = kg_numa_eval_any(c, pl.rows[node], p);
         if (!(ns >> 32)) return 0ull;
         numa = (uint32_t)ns;
@@ -1769,6 +1771,7 @@ struct NodeCacheEntry {
     int64_t metric_ns;
 };
 
+template <bool NUMA>
 __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c, const kg_planes &pl, const kg_pod_dev &p,
                                                               const NodeCacheEntry &ce, const kg_node_row &crow,
                                                               int64_t node, int64_t now_ns) {
@@ -1777,7 +1780,7 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
     node_regs_status(c, n.df, expired, n);
     uint32_t fit, la, numa = 0;
     if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
-    if (c.plugins & KG_PLUGIN_NUMA) {
+    if (NUMA && (c.plugins & KG_PLUGIN_NUMA)) {
         const uint64_t ns = kg_numa_eval_any(c, crow, p);   // the LDS copy of the canonical row
         if (!(ns >> 32)) return 0ull;
         numa = (uint32_t)ns;
@@ -1791,8 +1794,9 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
 // block max; (B) Reserve, one thread per part, and the committed node's planes.  The next pod's row
 // and tile keys are prefetched while the current pod is resolved.
 
-// RSV: the batch has reservation nodes (a separate instantiation: the plain path keeps its register budget)
-template <bool RSV>
+// RSV: the batch has reservation nodes; NUMA: NodeNUMAResource is enabled (separate instantiations: the plain
+// path keeps its register budget)
+template <bool RSV, bool NUMA>
 __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_planes pl,
                                                                 const kg_pod_dev *__restrict__ pods, int32_t pod_begin,
                                                                 int32_t n, const uint32_t *partials, int32_t tiles_total,
@@ -1827,7 +1831,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     __shared__ __attribute__((aligned(16))) kg_node_row nrow[KG_NCACHE + 1];
     constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16);
     static_assert(sizeof(kg_node_row) % 16 == 0 && ROW_U4 <= 64, "rows are staged as 16-byte words by one wave");
-    const bool numa_on = (c.plugins & KG_PLUGIN_NUMA) != 0;
+    const bool numa_on = NUMA && (c.plugins & KG_PLUGIN_NUMA) != 0;
     const bool rsv_on = RSV && ra.rsv && ra.n_rn > 0;
     __shared__ int32_t n_slow;
     // Reservation split (ra.M): the entry groups holding a touched reservation node (rsv_best_resolve)
@@ -1835,6 +1839,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     __shared__ int32_t glist[KG_MAX_CHUNK];
     __shared__ int32_t n_glist;
     __shared__ RsvPrefetch rpf;   // the split of the pod whose reduction is next (rsv_prefetch)
+    __shared__ kg_zone_tab_data czt;   // NodeNUMAResource: the zone table of the row being committed
     const int tid = threadIdx.x;
     // tile keys of the next pod, prefetched into registers by the thread owning the tile
     const bool key_prefetch = tiles_total <= KG_RESOLVE_THREADS;
@@ -1881,6 +1886,12 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         __syncthreads();
     }
     const int np_prev = n_prevt;
+#ifdef KG_RES_PROF
+    uint64_t PT[4] = {0, 0, 0, 0}, pt_last = __builtin_amdgcn_s_memtime();
+#define PTICK(i) do { if (tid == 0) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); PT[i] += t_ - pt_last; pt_last = t_; } } while (0)
+#else
+#define PTICK(i) do {} while (0)
+#endif
     for (int j = 0; j < n; j++) {
         const int par = j & 1;
         const kg_pod_dev &pd = lpod[par];
@@ -1965,25 +1976,25 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         }
         if (!plain_ok) best = 0;
         for (int q = tid; q < nt && plain_ok; q += KG_RESOLVE_THREADS) {
-            const unsigned long long k = q < KG_NCACHE ? pair_key_cached(c, pl, pd, ncache[q], nrow[q], touched[q], now_ns)
-                                                       : pair_key(c, pl, pd, touched[q], n_nodes, now_ns);
+            const unsigned long long k = q < KG_NCACHE ? pair_key_cached<NUMA>(c, pl, pd, ncache[q], nrow[q], touched[q], now_ns)
+                                                       : pair_key<NUMA>(c, pl, pd, touched[q], n_nodes, now_ns);
             best = best > k ? best : k;
         }
         for (int q = tid; q < np_prev && plain_ok; q += KG_RESOLVE_THREADS) {   // the previous chunk's nodes
-            const unsigned long long k = pair_key(c, pl, pd, prevt[q], n_nodes, now_ns);
+            const unsigned long long k = pair_key<NUMA>(c, pl, pd, prevt[q], n_nodes, now_ns);
             best = best > k ? best : k;
         }
         // nodes outside the fp64 bounds are not in the lists: re-scored exactly, every pod
         const int ns = (!rescore_slow || !plain_ok) ? 0 : n_slow;
         for (int q = tid; q < ns; q += KG_RESOLVE_THREADS) {
-            const unsigned long long k = pair_key(c, pl, pd, slow_list[q], n_nodes, now_ns);
+            const unsigned long long k = pair_key<NUMA>(c, pl, pd, slow_list[q], n_nodes, now_ns);
             best = best > k ? best : k;
         }
         __syncthreads();
         const int nr = plain_ok ? n_rescan[par] : 0;
         for (int q = tid; q < nr * KG_TILE; q += KG_RESOLVE_THREADS) {
             const int64_t node = (int64_t)rescan[q / KG_TILE] * KG_TILE + (q % KG_TILE);
-            const unsigned long long k = pair_key(c, pl, pd, node, n_nodes, now_ns);
+            const unsigned long long k = pair_key<NUMA>(c, pl, pd, node, n_nodes, now_ns);
             best = best > k ? best : k;
         }
         best = wave_max_u64(best);
@@ -2007,6 +2018,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             wb = wb > rk ? wb : rk;
         }
         const unsigned long long w = gate_ok[par] ? wb : 0ull;   // a pod failing the quota gate is unschedulable
+        PTICK(0);
         const int32_t node = w ? (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull)) : -1;
         if (!w || (defer_last && j == n - 1)) {
             // no feasible node; or the chunk's last pod may bind a cpuset: it is selected here and reserved by
@@ -2033,9 +2045,24 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         if (tid < ROW_U4) reinterpret_cast<uint4 *>(&srow)[tid] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
         __syncthreads();
         if (numa_on) {
-            if (tid == 0) kg_numa_commit(c, srow, pd);
+            // the zone table of the staged row (wave 0), then the zone commit's hint enumeration over it (tid 0)
+            const bool zoned = (srow.flags & KG_NODE_NUMA_OPTIONS) && srow.numa_policy != KG_NUMA_NONE &&
+                               srow.n_zones > 0;   // n_zones ≤ KG_MAX_ZONES (kg_build_node_rows)
+            if (zoned && tid < 64) {
+                kg_zone_tab_fill(srow, tid, 64, czt, [] {
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                });
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+            }
+            if (tid == 0) {
+                if (zoned) kg_numa_commit_tab(c, srow, pd, czt);
+                else kg_numa_commit(c, srow, pd);
+            }
             // the parts below read only srow (LDS)
             __syncthreads();
+            PTICK(1);
         }
         // the node's slot in the touched list (and node cache): its position, or the next one
         int slot = nt;
@@ -2147,7 +2174,11 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             }
         }
         __syncthreads();
+        PTICK(2);
     }
+#ifdef KG_RES_PROF
+    if (tid == 0 && pod_begin == 320) printf("resolve n=%d scan+max %llu stage+numa %llu parts+flags %llu\n", n, (unsigned long long)PT[0], (unsigned long long)PT[1], (unsigned long long)PT[2]);
+#endif
 }
 
 __global__ void k_commit_one(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t pod, int32_t node,
@@ -3374,7 +3405,9 @@ kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t
     st = slow_refresh(e);
     if (st) return st;
     const bool numa = (e->consts.plugins & KG_PLUGIN_NUMA) != 0;
-    hipLaunchKernelGGL(ra.rsv ? k_resolve<true> : k_resolve<false>, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream,
+    auto *kres = ra.rsv ? (numa ? k_resolve<true, true> : k_resolve<true, false>)
+                        : (numa ? k_resolve<false, true> : k_resolve<false, false>);
+    hipLaunchKernelGGL(kres, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream,
                        e->consts, e->pl, e->pods, pod_begin, n,
                        partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev, ra,
                        numa && n > e->numa_chunk_pods ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count,
