@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--c5-pods", type=int, default=100_000,
                     help="config-5 (Reservation + ElasticQuota) pods placed in sequence; 0 skips it")
     ap.add_argument("--c5-matrix-pods", type=int, default=1_000, help="config-5 matrix-mode pods")
+    ap.add_argument("--la-extra-pods", type=int, default=1_000,
+                    help="matrix-mode pods with LoadAware resourceWeights beyond cpu / memory (k_eval_exact); 0 skips")
     return ap.parse_args()
 
 
@@ -211,6 +213,43 @@ def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
                       f"fan-out over nodes per pod (kgo_schedule_parallel); median of {len(t2s)} runs",
             "runs_s": t2s}
     return out
+
+
+def bench_la_extra(args, engine, synth, shipped_profile, dev, stream):
+    """Matrix mode with LoadAware resourceWeights beyond cpu / memory (ephemeral-storage, an extended resource,
+    batch-cpu; estimatedScalingFactors for the first two): the fp64 fast-path planes carry cpu / memory only, so
+    every pair runs the exact int64 path (k_eval_exact, kg_pair_exact).  Config-2-shaped cluster with those
+    resources (synth.make_la_extra_cluster, seed 2), shipped profile."""
+    import torch
+
+    P, N = args.la_extra_pods, args.nodes
+    weights = {"cpu": 1, "memory": 1, "ephemeral-storage": 1, "example.com/gpu": 2, "kubernetes.io/batch-cpu": 1}
+    cl = synth.make_la_extra_cluster(N, P, seed=2)
+    cfg = shipped_profile(resource_weights=weights,
+                          estimated_scaling_factors={"ephemeral-storage": 60, "example.com/gpu": 100})
+    eng = engine.Engine(cfg)
+    eng.set_stream(stream.cuda_stream)
+    eng.load_snapshot(engine.build_node_rows(cfg, cl))
+    eng.set_pods(engine.build_pod_rows(cfg, cl, np.arange(P)))
+    W = eng.mask_words
+    mask = torch.empty((P, W), dtype=torch.int64, device=dev)
+    scores = torch.empty((P, W * 64, 2), dtype=torch.uint8, device=dev)
+    top1 = torch.zeros(P, dtype=torch.int64, device=dev)
+    step = lambda: eng.eval_device(cl.now_ns, mask.data_ptr(), scores.data_ptr(), top1.data_ptr())
+    step()
+    torch.cuda.synchronize(dev)
+    steps = 3
+    eng.set_profiling(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / steps
+    k_ms = float(np.mean(eng.eval_kernel_times(steps)))
+    eng.close()
+    return {"workload": f"{P} pods x {N} nodes, shipped profile, LoadAware resourceWeights {weights}",
+            "kernel": "k_eval_exact", "evals_per_s": round(P * N / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+            "kernel_ms": round(k_ms, 3)}
 
 
 def bench_config5(args, engine, synth, shipped_profile, dev, stream, cpu_model):
@@ -488,6 +527,10 @@ def main():
     if args.c5_pods > 0 and world == 1:
         config5 = bench_config5(args, engine, synth, shipped_profile, dev, stream, cpu_model)
 
+    la_extra = None
+    if args.la_extra_pods > 0 and world == 1:
+        la_extra = bench_la_extra(args, engine, synth, shipped_profile, dev, stream)
+
     # the committed PMC passes profile the default workload (tools/profile.sh: config 2, one GPU)
     profiled = world == 1 and args.scaling == "strong" and P == 10_000 and total == 100_000
     traffic, prof_ms, traffic_src = pmc_traffic() if profiled else (None, None, None)
@@ -527,6 +570,7 @@ def main():
             "placement": placement,
             "config3": config3,
             "config5": config5,
+            "la_extra": la_extra,
             "pods_with_feasible_node": feasible_pods,
             "engine_counters": {**ctr, "source": "kg_counters_get over the timed steps of rank 0",
                                 "evals_per_kernel_s": round(ctr["evals"] / (ctr["kernel_ns"] * 1e-9), 1)

@@ -25,7 +25,7 @@ if has prof; then
 fi
 if has sq; then
   bash tools/sqprof.sh ${TAG}_eval3 k_eval3 > gpurun_out/sq_${TAG}_eval3.txt 2>&1 || { tail -20 gpurun_out/sq_${TAG}_eval3.txt; exit 4; }
-  SQPROF_BENCH="python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-placement --c3-pods 1000 --c5-pods 0" \
+  SQPROF_BENCH="python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-placement --c3-pods 1000 --c5-pods 0 --la-extra-pods 0" \
     bash tools/sqprof.sh ${TAG}_numa2 k_eval_numa2 > gpurun_out/sq_${TAG}_numa2.txt 2>&1 \
     || { tail -20 gpurun_out/sq_${TAG}_numa2.txt; exit 5; }
 fi

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 P=${PODS:-2000}
-timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --c3-pods 0 --c5-pods 0 --pods $P \
+timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --c3-pods 0 --c5-pods 0 --la-extra-pods 0 --pods $P \
   > gpurun_out/dist1.json 2> gpurun_out/dist1.err || { tail -30 gpurun_out/dist1.err; exit 1; }
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29517 bench.py --gpus 2 --backend gloo --steps 3 --warmup 1 --no-cpu-baseline --c3-pods 0 \
@@ -18,6 +18,6 @@ for f in ("gpurun_out/dist1.json", "gpurun_out/dist2.json"):
 PY
 if [ "${C4:-0}" = 1 ]; then
   timeout -k 10 300 python bench.py --scaling config4 --steps 3 --warmup 1 --no-cpu-baseline --no-placement \
-    --c3-pods 0 --c5-pods 0 > gpurun_out/c4.json 2> gpurun_out/c4.err || { tail -30 gpurun_out/c4.err; exit 3; }
+    --c3-pods 0 --c5-pods 0 --la-extra-pods 0 > gpurun_out/c4.json 2> gpurun_out/c4.err || { tail -30 gpurun_out/c4.err; exit 3; }
   tail -c 1500 gpurun_out/c4.json
 fi

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_parity_gpu.py -x -q --timeout 200 --timeout-method thread "$@" \
   > gpurun_out/${TAG}_parity.log 2>&1 || { tail -30 gpurun_out/${TAG}_parity.log; exit 1; }
 tail -2 gpurun_out/${TAG}_parity.log
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --c3-pods 0 --c5-pods 0 > gpurun_out/${TAG}_bench.json \
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --c3-pods 0 --c5-pods 0 --la-extra-pods 0 > gpurun_out/${TAG}_bench.json \
   2> gpurun_out/${TAG}_bench.err || { tail -30 gpurun_out/${TAG}_bench.err; exit 2; }
 python - gpurun_out/${TAG}_bench.json <<'PY'
 import json, sys

@@ -7,7 +7,7 @@ KNAME=${2:-k_eval}
 OUT=gpurun_out/sq_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH=${SQPROF_BENCH:-"python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-placement --c3-pods 0 --c5-pods 0"}
+BENCH=${SQPROF_BENCH:-"python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-placement --c3-pods 0 --c5-pods 0 --la-extra-pods 0"}
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- $BENCH > $OUT/trace.log 2>&1 || { tail -5 $OUT/trace.log; exit 9; }
 P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM"
 P2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INST_CYCLES_SALU SQ_INST_CYCLES_SMEM SQ_INST_CYCLES_VMEM_WR"
