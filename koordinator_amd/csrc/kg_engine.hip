@@ -1886,12 +1886,6 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         __syncthreads();
     }
     const int np_prev = n_prevt;
-#ifdef KG_RES_PROF
-    uint64_t PT[4] = {0, 0, 0, 0}, pt_last = __builtin_amdgcn_s_memtime();
-#define PTICK(i) do { if (tid == 0) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); PT[i] += t_ - pt_last; pt_last = t_; } } while (0)
-#else
-#define PTICK(i) do {} while (0)
-#endif
     for (int j = 0; j < n; j++) {
         const int par = j & 1;
         const kg_pod_dev &pd = lpod[par];
@@ -2018,7 +2012,6 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             wb = wb > rk ? wb : rk;
         }
         const unsigned long long w = gate_ok[par] ? wb : 0ull;   // a pod failing the quota gate is unschedulable
-        PTICK(0);
         const int32_t node = w ? (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull)) : -1;
         if (!w || (defer_last && j == n - 1)) {
             // no feasible node; or the chunk's last pod may bind a cpuset: it is selected here and reserved by
@@ -2062,7 +2055,6 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             }
             // the parts below read only srow (LDS)
             __syncthreads();
-            PTICK(1);
         }
         // the node's slot in the touched list (and node cache): its position, or the next one
         int slot = nt;
@@ -2174,11 +2166,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             }
         }
         __syncthreads();
-        PTICK(2);
     }
-#ifdef KG_RES_PROF
-    if (tid == 0 && pod_begin == 320) printf("resolve n=%d scan+max %llu stage+numa %llu parts+flags %llu\n", n, (unsigned long long)PT[0], (unsigned long long)PT[1], (unsigned long long)PT[2]);
-#endif
 }
 
 __global__ void k_commit_one(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t pod, int32_t node,
