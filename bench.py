@@ -501,7 +501,11 @@ def main():
                         "sample": f"first {k} pods x {N} nodes of the same config-2 cluster, Filter+Score of every pair, "
                                   f"Parallelizer-faithful {workers}-thread node fan-out (oracle/koord_oracle.c "
                                   f"kgo_eval_parallel); median of {len(ts)} runs after a warm-up",
-                        "runs_s": ts, "host": host_info()}
+                        "runs_s": ts, "host": host_info(),
+                        "sampling_note": "every node scored (percentageOfNodesToScore 100, INTEGRATION.md §2); "
+                                         "the upstream default (adaptive: max(5, 50 - nodes/125) %) would stop "
+                                         f"Filter after {max(100, N * max(5, 50 - N // 125) // 100)} feasible nodes "
+                                         "per pod and Score only those"}
         if placement is not None:
             # placement baselines: the sequential cycle, single-threaded and with the 16-thread
             # Parallelizer fan-out over nodes per pod (kgo_schedule_parallel), on a pod prefix
