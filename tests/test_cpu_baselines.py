@@ -27,3 +27,22 @@ def test_parallel_cycle_matches_sequential_numa():
     np.testing.assert_array_equal(got[0], ref[0])
     np.testing.assert_array_equal(got[1], ref[1])
     assert (ref[0] >= 0).any()
+
+
+@pytest.mark.parametrize("workers", [1, 4, 7])
+def test_parallel_cycle2_matches_sequential(workers):
+    """kgo_schedule2_parallel (the threaded node loop the full-size placement fixture is generated with) against
+    the sequential Reservation + ElasticQuota cycle: placements, scores, and the reservation and quota states."""
+    cl = synth.make_rsv_cluster(1_200, 150, seed=15, rsv_node_frac=0.05, quota_ratio=0.6, affinity_frac=0.5,
+                                quota_tree=True)
+    cfg = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "Reservation", "ElasticQuota"),
+                          eq_check_parent_quota=1)
+    idx = np.arange(150)
+    ref = oracle.schedule2(cfg, cl, idx, cl.now_ns)
+    got = oracle.schedule2(cfg, cl, idx, cl.now_ns, workers=workers)
+    np.testing.assert_array_equal(got[0], ref[0])
+    np.testing.assert_array_equal(got[1], ref[1])
+    np.testing.assert_array_equal(got[2]["n_assigned"], ref[2]["n_assigned"])
+    np.testing.assert_array_equal(got[2]["allocated"]["v"], ref[2]["allocated"]["v"])
+    np.testing.assert_array_equal(got[3]["used"]["v"], ref[3]["used"]["v"])
+    assert (ref[0] >= 0).any() and (ref[0] < 0).any()
