@@ -1,7 +1,9 @@
 """ThreadSanitizer run of the oracle's threaded CPU baselines (the Parallelizer restatements kgo_eval_parallel
-and kgo_schedule_parallel of oracle/koord_oracle.c, which bench.py times as cpu_baseline): tests/tsan_driver.c
+and kgo_schedule_parallel of oracle/koord_oracle.c, which bench.py times as cpu_baseline, and the threaded
+Reservation + ElasticQuota cycle kgo_schedule2_parallel the full-size placement fixture is made with): tests/tsan_driver.c
 and the oracle sources built with -fsanitize=thread into a standalone program (no Python in the instrumented
-process), run on dumped clusters (the default profile and NodeNUMAResource with cpusets), checked against the
+process), run on dumped clusters (the default profile, NodeNUMAResource with cpusets, Reservation + ElasticQuota),
+checked against the
 sequential cycle, and required to finish without a ThreadSanitizer report."""
 import os
 import shutil
@@ -47,7 +49,7 @@ def _dump(path, cfg, view, idx, now):
         put(np.array([now], np.int64), np.dtype(np.int64))
 
 
-@pytest.mark.parametrize("kind", ["default", "numa_cpuset"])
+@pytest.mark.parametrize("kind", ["default", "numa_cpuset", "rsv_quota"])
 def test_oracle_parallel_baselines_under_tsan(kind, tmp_path):
     if shutil.which("gcc") is None:
         pytest.skip("no gcc")
@@ -55,6 +57,12 @@ def test_oracle_parallel_baselines_under_tsan(kind, tmp_path):
     if kind == "default":
         cl = synth.make_cluster(1500, 48, seed=31)
         cfg, view, idx, now = shipped_profile(), cl, np.arange(48), cl.now_ns
+    elif kind == "rsv_quota":
+        cl = synth.make_rsv_cluster(1200, 60, seed=33, rsv_node_frac=0.05, quota_ratio=0.6, affinity_frac=0.5,
+                                    quota_tree=True)
+        cfg = shipped_profile(plugins=("NodeResourcesFit", "LoadAwareScheduling", "Reservation", "ElasticQuota"),
+                              eq_check_parent_quota=1)
+        view, idx, now = cl, np.arange(60), cl.now_ns
     else:
         cl, view, idx = make_bind_cluster(200, 40, 32)
         cfg = shipped_profile()
