@@ -1974,7 +1974,9 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                                                        : pair_key<NUMA>(c, pl, pd, touched[q], n_nodes, now_ns);
             best = best > k ? best : k;
         }
-        for (int q = tid; q < np_prev && plain_ok; q += KG_RESOLVE_THREADS) {   // the previous chunk's nodes
+        // the previous chunk's nodes, on the upper half of the workgroup (the tile scan and the touched re-scores
+        // run on the lower threads: each NodeNUMAResource re-score is a long single-lane chain)
+        for (int q = tid - KG_RESOLVE_THREADS / 2; q >= 0 && q < np_prev && plain_ok; q += KG_RESOLVE_THREADS / 2) {
             const unsigned long long k = pair_key<NUMA>(c, pl, pd, prevt[q], n_nodes, now_ns);
             best = best > k ? best : k;
         }
