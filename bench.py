@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: CPU rehearsal of N > 1)")
     ap.add_argument("--no-placement", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-distinct", action="store_true", help="skip the config2_distinct section")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0,
                     help="CPU-baseline budget per baseline: one timed run ≈ budget / 6 (warm-up + median of 5)")
     ap.add_argument("--c3-pods", type=int, default=1_000, help="config-3 (NodeNUMAResource) pods; 0 skips it")
@@ -213,6 +214,45 @@ def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
                       f"fan-out over nodes per pod (kgo_schedule_parallel); median of {len(t2s)} runs",
             "runs_s": t2s}
     return out
+
+
+def bench_config2_distinct(args, engine, synth, cfg, node_rows, N, now, dev, stream):
+    """Config 2's shape with pairwise distinct pod rows (synth distinct_pods: cpu / memory requests drawn from
+    continuous ranges), so no two pods share an evaluation and every pair runs the per-pair kernel (k_eval3's
+    plain part): the per-pair rate beside the headline, whose synthetic batch repeats ~105 request shapes and
+    goes through the duplicate-row form (k_eval3_dup)."""
+    import torch
+
+    P = args.pods
+    pods_cl = synth.make_cluster(1, P, seed=2, distinct_pods=True)
+    rows = engine.build_pod_rows(cfg, pods_cl, np.arange(P))
+    eng = engine.Engine(cfg)
+    eng.set_stream(stream.cuda_stream)
+    eng.load_snapshot(node_rows)
+    eng.set_pods(rows)
+    W = eng.mask_words
+    mask = torch.empty((P, W), dtype=torch.int64, device=dev)
+    scores = torch.empty((P, W * 64, 2), dtype=torch.uint8, device=dev)
+    top1 = torch.zeros(P, dtype=torch.int64, device=dev)
+    step = lambda: eng.eval_device(now, mask.data_ptr(), scores.data_ptr(), top1.data_ptr())
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize(dev)
+    steps = max(3, args.steps // 2)
+    eng.set_profiling(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / steps
+    k_ms = float(np.mean(eng.eval_kernel_times(steps)))
+    eng.close()
+    algo = P * N * BYTES_PER_PAIR + N * BYTES_PER_NODE + P * BYTES_PER_POD
+    distinct = len(np.unique(rows[["request", "fit_score_request", "la_estimate", "flags", "request_present"]]))
+    return {"workload": f"config2 shape, {P} pods with pairwise distinct rows ({distinct} distinct) x {N} nodes, "
+                        "shipped profile", "kernel": "k_eval3 (plain part)",
+            "evals_per_s": round(P * N / dt, 1), "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(k_ms, 4),
+            "roofline_frac": round(algo / (k_ms * 1e-3) / HBM_PEAK, 4)}
 
 
 def bench_la_extra(args, engine, synth, shipped_profile, dev, stream):
@@ -523,6 +563,10 @@ def main():
                              "runs_s": t2s},
                 "host": host_info()}
 
+    distinct = None
+    if not args.no_distinct and world == 1:
+        distinct = bench_config2_distinct(args, engine, synth, cfg, node_rows, N, now, dev, stream)
+
     config3 = None
     if args.c3_pods > 0 and world == 1:
         config3 = bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model)
@@ -565,13 +609,15 @@ def main():
                          "frac_rocprof": None if prof_ms is None else round(algo_bytes / (prof_ms * 1e-3) / HBM_PEAK, 4),
                          "traffic": None if traffic is None else int(traffic), "traffic_unit": "bytes per launch (PMC)",
                          "traffic_source": traffic_src,
-                         "kernel": "k_eval3", "kernel_ms": round(k_ms, 4),
+                         "kernel": "k_eval3_dup (duplicate-row form of k_eval3: ~105 distinct pod rows over the 10k pods)",
+                         "kernel_ms": round(k_ms, 4),
                          "kernel_ms_source": "HIP events on the engine stream around the k_eval3 launches of each "
                                              "timed step (kg_set_profiling), this run; rocprofv3 summaries of the "
                                              "same command are under profiles/",
                          "algorithmic_bytes_per_launch": int(algo_bytes)},
             "cpu_baseline": cpu_baseline,
             "placement": placement,
+            "config2_distinct": distinct,
             "config3": config3,
             "config5": config5,
             "la_extra": la_extra,

@@ -129,7 +129,7 @@ struct alignas(64) kg_pod_hot_t {
 // class every per-pair branch is a compile-time constant: NC compared resources (int64), NF scored
 // resources (fp64 fma), padded to 2 or 4.  Rows are stored class after class (queue order inside a
 // class); the output row of each is in a parallel int32 array (kg_cls_desc::ids_first).
-#define KG_CLS_MAX 16                // classes per batch on the specialised path
+#define KG_CLS_MAX 32                // class parts per batch on the specialised path (a class: plain + duplicate-row part)
 template <int NC, int NF>
 struct alignas(16) kg_pod_cls_t {
     int64_t req[NC];       // Fit filter request of the compared resources (INT64_MIN pads)
@@ -158,15 +158,18 @@ struct kg_cls_desc {
     double uni_pr[4];      // its request, signed like kg_pod_cls_t::pr
     // pods [0, la_uni_end) of the class come in whole k_eval3 chunks of one EstimatePod each (cls_order_la)
     int32_t la_uni_end;
-    int32_t _pad0;
+    // duplicate-row part of a class (k_eval3<DUP>): the rows are the distinct rows of the class's pods whose row
+    // occurs more than once, `count` counts their pods, whose output rows (ids_first) are grouped by row and
+    // whose row indices are at ux_first in the same int32 array; −1 for the plain part
+    int32_t ux_first;
 };
 
 // one workgroup row of the launch grid: a pod range of one class
 struct kg_cls_work {
     int32_t cls;
-    int32_t begin;         // [begin, end) within the class
+    int32_t begin;         // [begin, end) within the class (a duplicate-row part: its pods, grouped by row)
     int32_t end;
-    int32_t _pad;
+    int32_t tile;          // duplicate-row part: the item's tile (its 1-D grid is ordered XCD by XCD); else 0
 };
 
 struct kg_planes {

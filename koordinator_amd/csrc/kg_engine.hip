@@ -41,6 +41,7 @@
 #define KG_CLS_ITEM_MAX 512         // pods per k_eval3 work item (one output-row entry per thread)
 #define KG_MAX_CHUNK KG_PLACE_CHUNK_MAX   // max pods per resolve call (touched-list capacity)
 #define KG_MAX_TILES 4096        // max tiles per snapshot in k_resolve (2M nodes)
+#define KG_XCDS 8                // workgroup b of a 1-D grid runs on XCD b % 8 (each XCD has its own L2)
 
 // ---------------------------------------------------------------------------------------
 // wave reductions
@@ -956,6 +957,172 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
     }
 }
 
+// The duplicate-row part of a class (the equivalence-class idea of the old kube-scheduler equivalence cache): pods
+// whose class rows are equal have equal output rows on every node, so a work item evaluates each distinct row
+// once against its tile and writes the result to every pod of that row.  One workgroup = one 1024-node tile ×
+// a run of the part's pods, grouped by row (w.begin..w.end); its distinct rows are walked in chunks of
+// KG_EVAL3_CC through cls_pods' mixed form, then each wave writes its 128-column score segment of every pod of
+// the chunk's rows from the LDS stage (16 lanes × 16 B per pod, 4 pods per wave store), the feasibility words by
+// lane permutes of the rows' ballot words, and the reducing wave the (pod, tile) key of every pod.  The work is
+// store-bound: per pod and tile 2 KiB of scores + 128 B of mask + 4 B of key against ~1/60 of a pod's compute.
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1>
+__device__ __forceinline__ void cls_block_dup(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
+                                              const kg_cls_work &w, const char *__restrict__ rows_base,
+                                              const int32_t *__restrict__ ids, uint64_t *__restrict__ mask,
+                                              uint16_t *__restrict__ scores, uint32_t *__restrict__ partials,
+                                              uint32_t *kbuf, int32_t *lid, uint16_t *lux, int32_t *cst, uint16_t *sstage) {
+    constexpr int CC = KG_EVAL3_CC;
+    constexpr int BT = KG_TILE / 2;
+    constexpr int SEGW = 128;
+    static_assert(CC == 8 && BT == 512, "the key reduction maps one wave's lanes to 8 rows × 8 lanes");
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tile = a.tile_begin + w.tile;
+    const int64_t wave_base = (int64_t)tile * KG_TILE + wave * SEGW;
+    ClsNode<NC, NF> n[2];
+    ClsLa la[2];
+    unsigned long long okm[2];
+    bool full_l = true;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        load_cls_node<NC, NF, MOST, FIT_ON, LA_ON>(c, pl, d, wave_base + 64 * j + lane, a.node_end, a.now_ns, n[j]);
+        load_cls_la<LA_ON>(pl, d, wave_base + 64 * j + lane, n[j].la_use, la[j]);
+        okm[j] = __builtin_amdgcn_ballot_w64(n[j].ok);
+        full_l = full_l && (n[j].w == (1u << d.fit_shift) || wave_base + 64 * j + lane >= a.node_end);
+    }
+    const bool full = !FIT_ON || __all(full_l);
+    const int64_t col0 = wave_base - a.col_begin;
+    bool seg[2];
+    uint32_t kb[2];
+    const uint32_t local0 = (uint32_t)(wave * SEGW + lane);
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        seg[j] = col0 + 64 * j < a.score_stride;
+        kb[j] = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0 - 64u * j;
+    }
+    // the item's pods (output rows) and their row indices relative to the item's first row go to LDS
+    const int nm = w.end - w.begin;
+    const int32_t *uxs = ids + d.ux_first + w.begin;
+    const int32_t u_first = uxs[0];
+    if (tid < nm) {
+        lid[tid] = ids[d.ids_first + w.begin + tid];
+        lux[tid] = (uint16_t)(uxs[tid] - u_first);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the pod loops then never wait on vector memory
+    __syncthreads();
+    const int nu = lux[nm - 1] + 1;   // distinct rows of the item
+    // cst[k]: the item's first pod whose row is in chunk k (pods are grouped by row, so chunks are pod runs)
+    if (tid < nm) {
+        const int ch = lux[tid] / CC;
+        if (tid == 0 || lux[tid - 1] / CC != ch) cst[ch] = tid;
+    }
+    if (tid == 0) cst[(nu + CC - 1) / CC] = nm;
+    __syncthreads();
+    const kg_pod_cls_t<NC, NF> *grows = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(rows_base + d.rows_offset) + u_first;
+    uint16_t *sst = sstage + wave * (CC * SEGW);
+    const uint32_t lsum[2] = {0u, 0u};
+    int ci = 0;
+    for (int u0 = 0; u0 < nu; u0 += CC, ci++) {
+        const int np = min(CC, nu - u0);
+        uint32_t *kcur = kbuf + (ci & 1) * KG_KBUF_DW;
+        unsigned long long mb[2] = {0ull, 0ull};
+#define KG_CLS_PODS(FULL_, UNR_)                                                                                \
+    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, UNR_, false>(c, d, n, la, okm, lsum, np, kb, kcur, mb, sst, \
+                                                                       grows + u0)
+        if (full && np == CC) KG_CLS_PODS(true, true);
+        else if (full) KG_CLS_PODS(true, false);
+        else KG_CLS_PODS(false, false);
+#undef KG_CLS_PODS
+        const int m0 = cst[ci], m1 = cst[ci + 1];
+        if (OUT) {
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const int s8 = lane & 15;
+            const bool segs = s8 < 8 ? seg[0] : seg[1];
+            // 16 lanes × 16 B = one pod's 128 columns: 4 pods per wave store
+            for (int m = m0; m < m1; m += 4) {
+                const int mm = m + (lane >> 4);
+                if (mm < m1 && segs) {
+                    const int u = lux[mm] - u0;
+                    const uint4 v = *reinterpret_cast<const uint4 *>(sst + u * SEGW + s8 * 8);
+                    const int64_t off = (int64_t)lid[mm] * a.score_stride;
+                    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(scores + off + col0 + s8 * 8));
+                }
+            }
+            // lane l writes the two feasibility words of pod m + l, its row's words taken from lane u (ds_bpermute
+            // with every lane active)
+            for (int m = m0; m < m1; m += 64) {
+                const int mm = m + lane;
+                const int u = mm < m1 ? lux[mm] - u0 : 0;
+                const int src = u << 2;
+                const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)mb[0]);
+                const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(mb[0] >> 32));
+                const uint32_t b0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)mb[1]);
+                const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(mb[1] >> 32));
+                if (mm < m1 && seg[0]) {
+                    uint64_t *mw = mask + (int64_t)lid[mm] * a.mask_words + (col0 >> 6);
+                    mw[0] = (uint64_t)a0 | ((uint64_t)a1 << 32);
+                    if (seg[1]) mw[1] = (uint64_t)b0 | ((uint64_t)b1 << 32);
+                }
+            }
+        }
+        // as cls_block: one barrier per chunk, a rotating reducer wave, double-buffered keys
+        lds_barrier();
+        if (wave == ci % (BT / 64)) {
+            const int p = lane >> 3, q = lane & 7;
+            const uint4 *src = reinterpret_cast<const uint4 *>(kcur + kg_kofs(p)) + q;
+            uint32_t mx = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const uint4 v = src[8 * k];
+                mx = max(mx, max(max(v.x, v.y), max(v.z, v.w)));
+            }
+            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x141, 0xf, 0xf, false));  // row_half_mirror
+            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
+            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+            // every lane of row p's group holds its key; pod m + l takes lane 8u's
+            for (int m = m0; m < m1; m += 64) {
+                const int mm = m + lane;
+                const int u = mm < m1 ? lux[mm] - u0 : 0;
+                const uint32_t k = (uint32_t)__builtin_amdgcn_ds_bpermute(u << 5, (int)mx);
+                if (mm < m1) partials[(int64_t)lid[mm] * a.tiles_total + tile] = k;
+            }
+        }
+    }
+}
+
+// k_eval3's duplicate-row form: one launch per class kind over a 1-D grid of (tile, pod run) items ordered tile by
+// tile, dealt to the XCDs in contiguous ranges (workgroup b runs on XCD b % 8 and takes item (b % 8) · per + b / 8),
+// so the items of one tile run on one XCD and its L2 serves the tile's node planes to all of them.
+template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int KIND>
+__global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? KG_EVAL3_WPE0 : KIND == 2 ? 5 : 4))) void k_eval3_dup(kg_consts c, kg_planes pl, HotArgs a,
+                                                        const kg_cls_desc *__restrict__ descs,
+                                                        const kg_cls_work *__restrict__ work, int32_t n_items,
+                                                        const char *__restrict__ rows, const int32_t *__restrict__ ids,
+                                                        uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
+                                                        uint32_t *__restrict__ partials) {
+    constexpr int CC = KG_EVAL3_CC, BT = KG_TILE / 2;
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[2 * KG_KBUF_DW];
+    static_assert(CC * BT <= 4096, "a chunk's keys fit the key buffer");
+    __shared__ int32_t lid[KG_CLS_ITEM_MAX];
+    __shared__ uint16_t lux[KG_CLS_ITEM_MAX];
+    __shared__ int32_t cst[KG_CLS_ITEM_MAX / CC + 1];
+    __shared__ __attribute__((aligned(16))) uint16_t sstage[OUT ? (BT / 64) * CC * 128 : 8];
+    const int per = (int)(gridDim.x / KG_XCDS);
+    const int item = (int)(blockIdx.x % KG_XCDS) * per + (int)(blockIdx.x / KG_XCDS);
+    if (item >= n_items) return;   // grid padded to a multiple of 8; block-uniform
+    const kg_cls_work w = work[item];
+    const kg_cls_desc d = descs[w.cls];
+#define KG_CLS_ARGS c, pl, a, d, w, rows, ids, mask, scores, partials, kbuf, lid, lux, cst, sstage
+    if constexpr (KIND == 0) cls_block_dup<2, 2, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
+    else if constexpr (KIND == 1) cls_block_dup<2, 4, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
+    else if constexpr (KIND == 2) cls_block_dup<4, 2, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
+    else cls_block_dup<4, 4, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
+#undef KG_CLS_ARGS
+}
+
 // One launch per (class kind, LAU) (the work table is grouped that way): each kernel is register-allocated for
 // its own kind.  OUT: the feasibility words and score planes are written (else per-(pod, tile) keys only).
 template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int KIND, bool LAU>
@@ -978,6 +1145,21 @@ __global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIN
     else if constexpr (KIND == 2) cls_block<4, 2, MOST, FIT_ON, LA_ON, OUT, W1, LAU>(KG_CLS_ARGS);
     else cls_block<4, 4, MOST, FIT_ON, LA_ON, OUT, W1, LAU>(KG_CLS_ARGS);
 #undef KG_CLS_ARGS
+}
+
+// Pod equivalence (kg_engine::eq_on): row p of an output plane := row of[p] of the distinct batch's plane.  VB-byte
+// vectors, non-temporal stores (a write-once stream); the distinct rows stay in L2 / MALL across their pods.
+template <int VB>
+__global__ __launch_bounds__(256) void k_eq_rows(const int32_t *__restrict__ of, int32_t P, const char *__restrict__ src,
+                                                 char *__restrict__ dst, int64_t row_bytes) {
+    typedef uint32_t vec_t __attribute__((ext_vector_type(VB / 4)));
+    const int64_t nv = row_bytes / VB;
+    for (int32_t p = blockIdx.y; p < P; p += gridDim.y) {
+        const vec_t *s = reinterpret_cast<const vec_t *>(src + (int64_t)of[p] * row_bytes);
+        vec_t *d = reinterpret_cast<vec_t *>(dst + (int64_t)p * row_bytes);
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x)
+            __builtin_nontemporal_store(s[i], d + i);
+    }
 }
 
 // Slow nodes (outside the fp64 exactness bounds) come out of k_eval2 as infeasible with
@@ -1283,7 +1465,6 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
 // workgroup b to XCD b % 8, so the n pods of one tile are consecutive workgroups of ONE XCD and its
 // L2 serves the tile's rows to all of them.
 #define KG_NUMA_CHUNK_PODS 16
-#define KG_XCDS 8
 // BZ (kg_consts.numa_bz): the launch answers cpusets on NUMA-policy nodes (a call into the cpuset path); the
 // common BZ = false form inlines the whole pair and carries no call, so its register budget is its own
 // (a call would charge it the callee's full-ABI budget: 254 VGPRs + 132 AGPRs, one wave per SIMD)
@@ -2200,6 +2381,17 @@ struct kg_engine {
     size_t hot_bytes = 0;
     int32_t *numa_perm = nullptr;   // NodeNUMAResource matrix mode: pod rows grouped by hint-list shape
     bool numa_perm_on = false;
+    // pod equivalence in matrix mode off the class path (NodeNUMAResource, LoadAware extra weights): every output
+    // of a pod is a function of its device row, so kg_eval evaluates each distinct row once (a batch of the
+    // distinct rows) and copies the rows of the planes to every pod of it (k_eq_rows)
+    bool eq_on = false;
+    int32_t eq_n = 0;                  // distinct rows
+    kg_pod_dev *eq_pods = nullptr;     // [eq_n]
+    int32_t *eq_perm = nullptr;        // [eq_n] their NodeNUMAResource visiting order (as numa_perm)
+    bool eq_perm_on = false;
+    int32_t *eq_of = nullptr;          // [n_pods] the distinct row of each pod
+    void *eq_mem = nullptr;            // the distinct batch's outputs, then the staging of host outputs
+    size_t eq_mem_bytes = 0;
     BatchMasks bm{0, 0};
     int numa_queue_mode = 1;        // k_eval_numa2's form: 1 queued for large launches, 0 grid (KG_NUMA_QUEUE=0,
                                     // measurement), 2 queued for every launch (KG_NUMA_QUEUE=2, tests)
@@ -2214,13 +2406,16 @@ struct kg_engine {
     bool cls_ok = false;                    // every pod of the batch belongs to a specialisable class
     bool cls_dirty = true;
     int64_t cls_width = -1, cls_tiles = -1;
-    std::vector<kg_cls_desc> cls_desc;      // host copies
-    std::vector<std::vector<int32_t>> cls_members;   // pod indices (queue order) per class
+    std::vector<kg_cls_desc> cls_desc;      // host copies, one per class part (plain / duplicate-row)
+    std::vector<std::vector<int32_t>> cls_members;   // pod indices per class part (a duplicate-row part: grouped by row)
+    std::vector<std::vector<int32_t>> cls_ux;        // duplicate-row part: each member's row index (else empty)
+    std::vector<std::vector<int32_t>> cls_reps;      // duplicate-row part: a pod of each distinct row (else empty)
     std::vector<kg_pod_row> pod_rows_h;
     void *cls_mem = nullptr;                // device: descs | work | rows
     size_t cls_mem_bytes = 0;
     int32_t cls_nwork = 0;
-    int32_t cls_kind_work[8][2] = {};   // [2 · kind + LoadAware-uniform] = (first work item, count)
+    int32_t cls_kind_work[12][2] = {};  // [3 · kind + form] = (first work item, count); form 0 mixed, 1 LoadAware-
+                                        // uniform, 2 duplicate-row (its items carry their tile)
     size_t cls_work_off = 0, cls_rows_off = 0, cls_ids_off = 0;
     int32_t *slow_list = nullptr;   // [cap] nodes outside the fast-path bounds, whole snapshot
     int32_t *slow_count = nullptr;
@@ -2248,12 +2443,9 @@ struct kg_engine {
     std::unordered_map<int32_t, CpuTable> cpu_tab;
     std::vector<uint8_t> pod_may_bind;   // bit 0: binds by its own PreFilter; bit 1: a cpu request (node policy)
     bool profiling = false;
-    bool cls_fold_uniform = true;       // class-uniform scored slots folded per node (KG_CLS_FOLD_UNIFORM=0: off)
-    bool cls_fold_la = true;            // LoadAware-uniform chunks (KG_CLS_FOLD_LA=0: off; parity tests of both forms)
-    int64_t cls_target_blocks = 2048;   // k_eval3 work items per class ≈ this / tiles (KG_CLS_TARGET_BLOCKS)
-    // the class kinds' launches on two streams (kinds 1 / 3 on stream2), so one kind's grid tail is filled by
-    // the other's workgroups (KG_CLS_CONCURRENT)
-    bool cls_concurrent = true;
+    int64_t cls_target_blocks = 2048;   // k_eval3 work items per class part ≈ this / tiles (r03 A/B: 1024-6144)
+    // the class kinds' launches on two streams (the mixed form on stream2), so one grid's tail is filled by the
+    // other's workgroups (r03 A/B: 0.84 vs 0.87 ms per config-2 pass)
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int place_pipeline = 1;             // kg_place overlaps chunk i + 1's evaluation with chunk i's resolve: 1 for
@@ -2409,7 +2601,7 @@ bool pod_class(const kg_config &cfg, const kg_pod_row &row, ClsKey &key) {
 // order within a class is free.  Returns the end of the uniform region.
 int32_t cls_order_la(const kg_engine *e, std::vector<int32_t> &mem) {
     const bool la_on = (e->cfg.enabled_plugins & KG_PLUGIN_LOADAWARE) != 0;
-    if (!la_on || !e->cls_fold_la) return 0;
+    if (!la_on) return 0;
     auto est = [&](int32_t i) { return std::make_pair(e->pod_rows_h[i].la_estimate[0], e->pod_rows_h[i].la_estimate[1]); };
     std::vector<int32_t> s = mem;
     std::stable_sort(s.begin(), s.end(), [&](int32_t x, int32_t y) { return est(x) < est(y); });
@@ -2429,39 +2621,66 @@ int32_t cls_order_la(const kg_engine *e, std::vector<int32_t> &mem) {
     return end;
 }
 
+template <int NC, int NF>
+void cls_fill_row(const kg_engine *e, const kg_cls_desc &d, const kg_pod_row &r, char *dst) {
+    kg_pod_cls_t<NC, NF> h;
+    memset(&h, 0, sizeof(h));
+    const bool most = e->cfg.fit_strategy == KG_STRATEGY_MOST_ALLOCATED;
+    for (int k = 0; k < NC; k++) h.req[k] = d.cmp_res[k] >= 0 ? r.request[d.cmp_res[k]] : KG_NEUTRAL_REQ;
+    for (int f = 0; f < NF; f++) {
+        const double pr = d.fit_res[f] >= 0 ? (double)r.fit_score_request[d.fit_res[f]] : 0.0;
+        h.pr[f] = most ? pr : -pr;
+    }
+    h.la[0] = -(double)r.la_estimate[0];
+    h.la[1] = -(double)r.la_estimate[1];
+    memcpy(dst, &h, sizeof(h));
+}
+
+void cls_fill_any(const kg_engine *e, const kg_cls_desc &d, const kg_pod_row &r, char *dst) {
+    if (d.kind == 0) cls_fill_row<2, 2>(e, d, r, dst);
+    else if (d.kind == 1) cls_fill_row<2, 4>(e, d, r, dst);
+    else if (d.kind == 2) cls_fill_row<4, 2>(e, d, r, dst);
+    else cls_fill_row<4, 4>(e, d, r, dst);
+}
+
+// Classes of the batch, each split in two parts: the pods whose class row (the only per-pod input of k_eval3)
+// occurs more than once in the class form its duplicate-row part (evaluated once per distinct row, written to
+// every pod of it: k_eval3_dup), the rest its plain part.
 void cls_prepare(kg_engine *e) {
     e->cls_ok = false;
     e->cls_dirty = true;
     e->cls_desc.clear();
     e->cls_members.clear();
+    e->cls_ux.clear();
+    e->cls_reps.clear();
     const bool la_on = (e->cfg.enabled_plugins & KG_PLUGIN_LOADAWARE) != 0;
     if (la_on && e->consts.la_shift == 0xFF) return;
     std::map<ClsKey, int> index;
     std::vector<ClsKey> keys;
+    std::vector<std::vector<int32_t>> members;
     for (int32_t i = 0; i < (int32_t)e->pod_rows_h.size(); i++) {
         ClsKey k;
         if (!pod_class(e->cfg, e->pod_rows_h[i], k)) return;
         auto it = index.find(k);
         int c;
         if (it == index.end()) {
-            if ((int)keys.size() == KG_CLS_MAX) return;
+            if (2 * (int)keys.size() == KG_CLS_MAX) return;
             c = (int)keys.size();
             index.emplace(k, c);
             keys.push_back(k);
-            e->cls_members.emplace_back();
+            members.emplace_back();
         } else {
             c = it->second;
         }
-        e->cls_members[c].push_back(i);
+        members[c].push_back(i);
     }
     for (size_t c = 0; c < keys.size(); c++) {
         const ClsKey &k = keys[c];
         kg_cls_desc d;
         memset(&d, 0, sizeof(d));
-        d.la_uni_end = cls_order_la(e, e->cls_members[c]);
         // scored resources whose request is one value over the whole class fold into a per-node term when
         // that leaves at most two per-pod slots (a four-slot class then runs as a two-slot kind)
-        const std::vector<int32_t> &mem = e->cls_members[c];
+        const std::vector<int32_t> &mem = members[c];
         uint32_t unim = 0;
         for (int r = 0; r < KG_NUM_RES; r++) {
             if (!((k.fitm >> r) & 1u)) continue;
@@ -2470,11 +2689,10 @@ void cls_prepare(kg_engine *e) {
             for (size_t j = 1; j < mem.size() && same; j++) same = e->pod_rows_h[mem[j]].fit_score_request[r] == v0;
             if (same) unim |= 1u << r;
         }
-        if (__builtin_popcount(k.fitm) <= 2 || __builtin_popcount(k.fitm & ~unim) > 2 || !e->cls_fold_uniform) unim = 0;
+        if (__builtin_popcount(k.fitm) <= 2 || __builtin_popcount(k.fitm & ~unim) > 2) unim = 0;
         const uint32_t varm = k.fitm & ~unim;
         const int nc = __builtin_popcount(k.nzc) <= 2 ? 2 : 4, nf = __builtin_popcount(varm) <= 2 ? 2 : 4;
         d.kind = (nc == 2 ? 0 : 2) + (nf == 2 ? 0 : 1);
-        d.count = (int32_t)e->cls_members[c].size();
         int a = 0, b = 0, u = 0;
         uint32_t w = 0;
         const bool most = e->cfg.fit_strategy == KG_STRATEGY_MOST_ALLOCATED;
@@ -2500,24 +2718,50 @@ void cls_prepare(kg_engine *e) {
         d.over_mask = k.zc;
         d.row_bytes = d.kind == 0 ? (int64_t)sizeof(kg_pod_cls_t<2, 2>) : d.kind == 1 ? (int64_t)sizeof(kg_pod_cls_t<2, 4>)
                       : d.kind == 2 ? (int64_t)sizeof(kg_pod_cls_t<4, 2>) : (int64_t)sizeof(kg_pod_cls_t<4, 4>);
-        e->cls_desc.push_back(d);
+        // the class rows, grouped: distinct rows in order of first occurrence, each with its pods in queue order
+        std::map<std::string, int32_t> row_id;
+        std::vector<std::vector<int32_t>> by_row;
+        std::string buf((size_t)d.row_bytes, '\0');
+        for (int32_t i : mem) {
+            cls_fill_any(e, d, e->pod_rows_h[i], &buf[0]);
+            auto it = row_id.emplace(buf, (int32_t)by_row.size());
+            if (it.second) by_row.emplace_back();
+            by_row[it.first->second].push_back(i);
+        }
+        std::vector<int32_t> plain, dup, ux, reps;
+        for (const std::vector<int32_t> &g : by_row) {
+            if (g.size() == 1) {
+                plain.push_back(g[0]);
+                continue;
+            }
+            reps.push_back(g[0]);
+            for (int32_t i : g) {
+                dup.push_back(i);
+                ux.push_back((int32_t)reps.size() - 1);
+            }
+        }
+        if (!plain.empty()) {
+            kg_cls_desc dp = d;
+            dp.la_uni_end = cls_order_la(e, plain);
+            dp.count = (int32_t)plain.size();
+            dp.ux_first = -1;
+            e->cls_desc.push_back(dp);
+            e->cls_members.push_back(std::move(plain));
+            e->cls_ux.emplace_back();
+            e->cls_reps.emplace_back();
+        }
+        if (!dup.empty()) {
+            kg_cls_desc dd = d;
+            dd.la_uni_end = 0;
+            dd.count = (int32_t)dup.size();
+            dd.ux_first = 0;   // laid out by cls_layout
+            e->cls_desc.push_back(dd);
+            e->cls_members.push_back(std::move(dup));
+            e->cls_ux.push_back(std::move(ux));
+            e->cls_reps.push_back(std::move(reps));
+        }
     }
     e->cls_ok = true;
-}
-
-template <int NC, int NF>
-void cls_fill_row(const kg_engine *e, const kg_cls_desc &d, const kg_pod_row &r, char *dst) {
-    kg_pod_cls_t<NC, NF> h;
-    memset(&h, 0, sizeof(h));
-    const bool most = e->cfg.fit_strategy == KG_STRATEGY_MOST_ALLOCATED;
-    for (int k = 0; k < NC; k++) h.req[k] = d.cmp_res[k] >= 0 ? r.request[d.cmp_res[k]] : KG_NEUTRAL_REQ;
-    for (int f = 0; f < NF; f++) {
-        const double pr = d.fit_res[f] >= 0 ? (double)r.fit_score_request[d.fit_res[f]] : 0.0;
-        h.pr[f] = most ? pr : -pr;
-    }
-    h.la[0] = -(double)r.la_estimate[0];
-    h.la[1] = -(double)r.la_estimate[1];
-    memcpy(dst, &h, sizeof(h));
 }
 
 // Lay the class rows out for the shard width (output offsets) and the work table for its tiles.
@@ -2530,23 +2774,46 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
     size_t rows_bytes = 0;
     int32_t n_ids = 0;
     for (size_t c = 0; c < descs.size(); c++) {
+        const bool dup = !e->cls_reps[c].empty();
         descs[c].rows_offset = (int64_t)rows_bytes;
-        rows_bytes += (size_t)descs[c].row_bytes * (size_t)descs[c].count;
+        rows_bytes += (size_t)descs[c].row_bytes * (dup ? e->cls_reps[c].size() : (size_t)descs[c].count);
         descs[c].ids_first = n_ids;
         n_ids += descs[c].count;
+        if (dup) {
+            descs[c].ux_first = n_ids;
+            n_ids += descs[c].count;
+        }
     }
-    // the work table grouped by (kind, LoadAware-uniform): one launch each; a class's LoadAware-uniform region
-    // [0, la_uni_end) and its tail are split into work items separately
-    for (int g = 0; g < 8; g++) {
-        const int kind = g >> 1;
-        const bool lau = (g & 1) != 0;
+    // the work table grouped by (kind, form): one launch each; a plain part's LoadAware-uniform region
+    // [0, la_uni_end) and its tail are split into work items separately; a duplicate-row part is split into pod runs
+    // of equal length per tile, tile by tile (k_eval3_dup's XCD order)
+    for (int g = 0; g < 12; g++) {
+        const int kind = g / 3, form = g % 3;
         e->cls_kind_work[g][0] = (int32_t)work.size();
-        for (size_t c = 0; c < descs.size(); c++) {
-            if (descs[c].kind != kind) continue;
-            const int32_t b0 = lau ? 0 : descs[c].la_uni_end, b1 = lau ? descs[c].la_uni_end : descs[c].count;
-            if (b1 <= b0) continue;
-            const int32_t ppb = pods_per_block_for(b1 - b0, shard_tiles, e->cls_target_blocks);
-            for (int32_t b = b0; b < b1; b += ppb) work.push_back(kg_cls_work{(int32_t)c, b, b + ppb < b1 ? b + ppb : b1, 0});
+        if (form < 2) {
+            const bool lau = form == 1;
+            for (size_t c = 0; c < descs.size(); c++) {
+                if (descs[c].kind != kind || !e->cls_reps[c].empty()) continue;
+                const int32_t b0 = lau ? 0 : descs[c].la_uni_end, b1 = lau ? descs[c].la_uni_end : descs[c].count;
+                if (b1 <= b0) continue;
+                const int32_t ppb = pods_per_block_for(b1 - b0, shard_tiles, e->cls_target_blocks);
+                for (int32_t b = b0; b < b1; b += ppb) work.push_back(kg_cls_work{(int32_t)c, b, b + ppb < b1 ? b + ppb : b1, 0});
+            }
+        } else {
+            std::vector<std::pair<int32_t, int32_t>> runs;   // (part, run length) of one tile
+            for (size_t c = 0; c < descs.size(); c++) {
+                if (descs[c].kind != kind || e->cls_reps[c].empty()) continue;
+                const int32_t cnt = descs[c].count;
+                const int32_t ppb = pods_per_block_for(cnt, shard_tiles, e->cls_target_blocks);
+                const int32_t n_it = (cnt + ppb - 1) / ppb;
+                runs.emplace_back((int32_t)c, (cnt + n_it - 1) / n_it);
+            }
+            for (int32_t t = 0; t < (int32_t)shard_tiles; t++)
+                for (const auto &r : runs) {
+                    const int32_t cnt = descs[r.first].count;
+                    for (int32_t b = 0; b < cnt; b += r.second)
+                        work.push_back(kg_cls_work{r.first, b, b + r.second < cnt ? b + r.second : cnt, t});
+                }
         }
         e->cls_kind_work[g][1] = (int32_t)work.size() - e->cls_kind_work[g][0];
     }
@@ -2554,16 +2821,14 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
     std::vector<int32_t> ids((size_t)n_ids + 1, 0);
     for (size_t c = 0; c < descs.size(); c++) {
         const kg_cls_desc &d = descs[c];
-        for (int32_t j = 0; j < d.count; j++) {
-            const int32_t i = e->cls_members[c][j];
-            ids[(size_t)d.ids_first + (size_t)j] = i;
-            char *dst = rows.data() + d.rows_offset + (size_t)j * (size_t)d.row_bytes;
-            const kg_pod_row &r = e->pod_rows_h[i];
-            if (d.kind == 0) cls_fill_row<2, 2>(e, d, r, dst);
-            else if (d.kind == 1) cls_fill_row<2, 4>(e, d, r, dst);
-            else if (d.kind == 2) cls_fill_row<4, 2>(e, d, r, dst);
-            else cls_fill_row<4, 4>(e, d, r, dst);
-        }
+        const std::vector<int32_t> &mem = e->cls_members[c];
+        for (int32_t j = 0; j < d.count; j++) ids[(size_t)d.ids_first + (size_t)j] = mem[(size_t)j];
+        const bool dup = !e->cls_reps[c].empty();
+        if (dup)
+            for (int32_t j = 0; j < d.count; j++) ids[(size_t)d.ux_first + (size_t)j] = e->cls_ux[c][(size_t)j];
+        const std::vector<int32_t> &src = dup ? e->cls_reps[c] : mem;
+        for (size_t j = 0; j < src.size(); j++)
+            cls_fill_any(e, d, e->pod_rows_h[src[j]], rows.data() + d.rows_offset + j * (size_t)d.row_bytes);
     }
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t desc_b = sizeof(kg_cls_desc) * KG_CLS_MAX, work_b = sizeof(kg_cls_work) * (work.size() + 1);
@@ -2592,14 +2857,23 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
     return KG_OK;
 }
 
-template <bool MOST, bool FIT_ON, bool LA_ON, bool W1, int KIND, bool LAU>
+template <bool MOST, bool FIT_ON, bool LA_ON, bool W1, int KIND, int FORM>
 void launch_cls_kind(kg_engine *e, dim3 grid, const HotArgs &a, const kg_cls_desc *descs, const kg_cls_work *work,
                      const char *rows, const int32_t *ids, uint64_t *mask, uint16_t *scores, uint32_t *partials,
                      hipStream_t stream) {
-    const int32_t first = e->cls_kind_work[2 * KIND + LAU][0], count = e->cls_kind_work[2 * KIND + LAU][1];
+    constexpr bool LAU = FORM == 1;
+    const int32_t first = e->cls_kind_work[3 * KIND + FORM][0], count = e->cls_kind_work[3 * KIND + FORM][1];
     if (count == 0) return;
     if constexpr (LAU && !LA_ON) return;   // (no such work items: cls_order_la)
-    else {
+    else if constexpr (FORM == 2) {
+        const dim3 g1((unsigned)((count + KG_XCDS - 1) / KG_XCDS * KG_XCDS));
+        if (mask)
+            hipLaunchKernelGGL((k_eval3_dup<MOST, FIT_ON, LA_ON, true, W1, KIND>), g1, dim3(KG_TILE / 2), 0, stream,
+                               e->consts, e->pl, a, descs, work + first, count, rows, ids, mask, scores, partials);
+        else
+            hipLaunchKernelGGL((k_eval3_dup<MOST, FIT_ON, LA_ON, false, W1, KIND>), g1, dim3(KG_TILE / 2), 0, stream,
+                               e->consts, e->pl, a, descs, work + first, count, rows, ids, mask, scores, partials);
+    } else {
         grid.y = (unsigned)count;
         // matrix mode: 8-pod chunks, score segments staged in LDS and written as 1 KiB wave stores; two nodes per
         // lane (four: 92 VGPRs, 5 waves per SIMD, 1.98 vs 0.88 ms per config-2 pass, round 2)
@@ -2619,30 +2893,29 @@ void launch_cls4(kg_engine *e, dim3 grid, const HotArgs &a, uint64_t *mask, uint
     const kg_cls_work *work = (const kg_cls_work *)(m + e->cls_work_off);
     const char *rows = m + e->cls_rows_off;
     const int32_t *ids = (const int32_t *)(m + e->cls_ids_off);
-    hipStream_t s2 = e->stream;
-    if (e->cls_concurrent) {   // fork: stream2 starts after everything already queued on the engine stream
-        if (!e->stream2) {
-            (void)hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking);
-            (void)hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
-            (void)hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
-        }
-        (void)hipEventRecord(e->ev_fork, e->stream);
-        (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
-        s2 = e->stream2;
+    // fork: stream2 starts after everything already queued on the engine stream
+    if (!e->stream2) {
+        (void)hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking);
+        (void)hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
     }
-    // LoadAware-uniform work on the engine stream, the rest on stream2: one grid's tail is filled by the other's
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 0, true>(e, grid, a, descs, work, rows, ids, mask, scores, partials, e->stream);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 0, false>(e, grid, a, descs, work, rows, ids, mask, scores, partials, s2);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 1, true>(e, grid, a, descs, work, rows, ids, mask, scores, partials, e->stream);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 1, false>(e, grid, a, descs, work, rows, ids, mask, scores, partials, s2);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 2, true>(e, grid, a, descs, work, rows, ids, mask, scores, partials, e->stream);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 2, false>(e, grid, a, descs, work, rows, ids, mask, scores, partials, s2);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 3, true>(e, grid, a, descs, work, rows, ids, mask, scores, partials, e->stream);
-    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, 3, false>(e, grid, a, descs, work, rows, ids, mask, scores, partials, s2);
-    if (e->cls_concurrent) {   // join: the engine stream continues after both kinds
-        (void)hipEventRecord(e->ev_join, s2);
-        (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
-    }
+    (void)hipEventRecord(e->ev_fork, e->stream);
+    (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
+    hipStream_t s2 = e->stream2;
+    // duplicate-row and LoadAware-uniform work on the engine stream, the mixed rest on stream2: one grid's tail is
+    // filled by the other's workgroups
+#define KG_LAUNCH_KIND(K)                                                                                              \
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, K, 2>(e, grid, a, descs, work, rows, ids, mask, scores, partials, e->stream); \
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, K, 1>(e, grid, a, descs, work, rows, ids, mask, scores, partials, e->stream); \
+    launch_cls_kind<MOST, FIT_ON, LA_ON, W1, K, 0>(e, grid, a, descs, work, rows, ids, mask, scores, partials, s2)
+    KG_LAUNCH_KIND(0);
+    KG_LAUNCH_KIND(1);
+    KG_LAUNCH_KIND(2);
+    KG_LAUNCH_KIND(3);
+#undef KG_LAUNCH_KIND
+    // join: the engine stream continues after every kind
+    (void)hipEventRecord(e->ev_join, s2);
+    (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
 }
 
 template <bool MOST, bool FIT_ON, bool LA_ON>
@@ -2892,6 +3165,10 @@ kg_status check_engine(kg_engine *e, bool reloading = false) {
 
 }  // namespace
 
+namespace {
+kg_status eval_eq(kg_engine *e, int64_t now_ns, const kg_eval_out *out);
+}
+
 extern "C" {
 
 kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
@@ -2918,20 +3195,12 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
         return KG_ERR_HIP;
     }
     e->own_stream = true;
-    const char *tb = getenv("KG_CLS_TARGET_BLOCKS");   // measurement switches (tools/ab_cls.sh)
-    if (tb && atoll(tb) > 0) e->cls_target_blocks = atoll(tb);
-    const char *fu = getenv("KG_CLS_FOLD_UNIFORM");
-    e->cls_fold_uniform = !(fu && atoi(fu) == 0);
-    const char *fl = getenv("KG_CLS_FOLD_LA");
-    e->cls_fold_la = !(fl && atoi(fl) == 0);
     const char *ncp = getenv("KG_NUMA_CHUNK_PODS");
     if (ncp) e->numa_chunk_pods = std::min(atoi(ncp), KG_NUMA_CHUNK_PODS);
     const char *nq = getenv("KG_NUMA_QUEUE");
     e->numa_queue_mode = nq ? atoi(nq) : 1;
     const char *pp = getenv("KG_PLACE_PIPELINE");
     e->place_pipeline = pp ? atoi(pp) : 1;
-    const char *cc = getenv("KG_CLS_CONCURRENT");   // default on: 0.84 vs 0.87 ms per config-2 pass (r03 A/B)
-    e->cls_concurrent = !cc || atoi(cc) != 0;
     *out = e;
     return KG_OK;
 }
@@ -2950,6 +3219,10 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->gate) (void)hipFree(e->gate);
     if (e->numa_perm) (void)hipFree(e->numa_perm);
     if (e->numa_queue) (void)hipFree(e->numa_queue);
+    if (e->eq_pods) (void)hipFree(e->eq_pods);
+    if (e->eq_perm) (void)hipFree(e->eq_perm);
+    if (e->eq_of) (void)hipFree(e->eq_of);
+    if (e->eq_mem) (void)hipFree(e->eq_mem);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
@@ -3206,20 +3479,63 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     // k_eval_numa2 runs a wave's 64 pods in lockstep through the hint enumeration, whose trip counts
     // depend on the pod's hint lists: matrix mode visits the pods grouped by (list count, cpu,
     // memory request), so a wave's lanes mostly share one loop shape (outputs stay in pod-row order)
-    std::vector<int32_t> order;
-    e->numa_perm_on = (e->cfg.enabled_plugins & KG_PLUGIN_NUMA) && n > 64;
-    if (e->numa_perm_on) {
-        order.resize((size_t)n);
-        for (int32_t i = 0; i < n; i++) order[i] = i;
+    // (of the pods `ids`, as positions into ids)
+    auto numa_order = [&](const std::vector<int32_t> &ids) {
+        std::vector<int32_t> order(ids.size());
+        for (size_t i = 0; i < ids.size(); i++) order[i] = (int32_t)i;
         auto lists = [&](int32_t i) { return (rows[i].flags & KG_POD_NUMA_SKIP) ? 0 : kg_numa_list_count(rows[i]); };
-        std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+            const int32_t x = ids[(size_t)a], y = ids[(size_t)b];
             const int lx = lists(x), ly = lists(y);
             if (lx != ly) return lx < ly;
             if (dev[x].numa_req[KG_RES_CPU] != dev[y].numa_req[KG_RES_CPU])
                 return dev[x].numa_req[KG_RES_CPU] < dev[y].numa_req[KG_RES_CPU];
             return dev[x].numa_req[KG_RES_MEMORY] < dev[y].numa_req[KG_RES_MEMORY];
         });
+        return order;
+    };
+    std::vector<int32_t> all((size_t)n);
+    for (int32_t i = 0; i < n; i++) all[(size_t)i] = i;
+    e->numa_perm_on = (e->cfg.enabled_plugins & KG_PLUGIN_NUMA) && n > 64;
+    if (e->numa_perm_on) {
+        const std::vector<int32_t> order = numa_order(all);
         HIP_TRY(e, h2d(e, e->numa_perm, order.data(), sizeof(int32_t) * (size_t)n, e->stream));
+    }
+    // distinct device rows (pod equivalence, matrix mode off the class path): on when they are at most 3/4 of the
+    // batch
+    e->eq_on = false;
+    if (((e->cfg.enabled_plugins & KG_PLUGIN_NUMA) || e->consts.la_extra) && n >= 64) {
+        std::unordered_map<std::string, int32_t> seen;
+        std::vector<int32_t> of((size_t)n), reps;
+        for (int32_t i = 0; i < n; i++) {
+            auto it = seen.emplace(std::string(reinterpret_cast<const char *>(&dev[(size_t)i]), sizeof(kg_pod_dev)),
+                                   (int32_t)reps.size());
+            if (it.second) reps.push_back(i);
+            of[(size_t)i] = it.first->second;
+        }
+        const int32_t u = (int32_t)reps.size();
+        if (4 * (int64_t)u <= 3 * (int64_t)n) {
+            if (e->eq_pods) HIP_TRY(e, hipFree(e->eq_pods));
+            if (e->eq_perm) HIP_TRY(e, hipFree(e->eq_perm));
+            if (e->eq_of) HIP_TRY(e, hipFree(e->eq_of));
+            e->eq_pods = nullptr;
+            e->eq_perm = nullptr;
+            e->eq_of = nullptr;
+            HIP_TRY(e, hipMalloc(&e->eq_pods, sizeof(kg_pod_dev) * (size_t)u));
+            HIP_TRY(e, hipMalloc(&e->eq_perm, sizeof(int32_t) * (size_t)u));
+            HIP_TRY(e, hipMalloc(&e->eq_of, sizeof(int32_t) * (size_t)n));
+            std::vector<kg_pod_dev> udev((size_t)u);
+            for (int32_t k = 0; k < u; k++) udev[(size_t)k] = dev[(size_t)reps[(size_t)k]];
+            HIP_TRY(e, h2d(e, e->eq_pods, udev.data(), sizeof(kg_pod_dev) * (size_t)u, e->stream));
+            HIP_TRY(e, h2d(e, e->eq_of, of.data(), sizeof(int32_t) * (size_t)n, e->stream));
+            e->eq_perm_on = (e->cfg.enabled_plugins & KG_PLUGIN_NUMA) && u > 64;
+            if (e->eq_perm_on) {
+                const std::vector<int32_t> order = numa_order(reps);
+                HIP_TRY(e, h2d(e, e->eq_perm, order.data(), sizeof(int32_t) * (size_t)u, e->stream));
+            }
+            e->eq_n = u;
+            e->eq_on = true;
+        }
     }
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     e->nslot = nslot;
@@ -3249,6 +3565,7 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     if (st) return st;
     if (!out) return set_err(e, KG_ERR_INVALID_ARG, "null output");
     if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised");
+    if (e->eq_on && e->n_pods > 0) return eval_eq(e, now_ns, out);
     const int32_t P = e->n_pods;
     const int64_t T = tiles_total(e);
     const int64_t width = e->shard_end - e->shard_begin;
@@ -3356,6 +3673,78 @@ kg_status kg_eval(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
 }  // extern "C"
 
 namespace {
+
+// Matrix mode over the distinct rows of the batch (kg_engine::eq_on): the batch is swapped for its distinct rows,
+// evaluated by kg_eval into device buffers, and every output row is copied to each pod of its distinct row.
+kg_status eval_eq(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
+    const int32_t P = e->n_pods, U = e->eq_n;
+    const int64_t width = e->shard_end - e->shard_begin;
+    const int64_t words = (width + 63) / 64, stride = words * 64;
+    const size_t rb[5] = {(size_t)words * 8, (size_t)stride * 2, 8, (size_t)stride, (size_t)stride};   // mask scores top1 numa rsv
+    void *const want[5] = {out->mask, out->scores, out->top1, out->numa_scores, out->rsv_scores};
+    const bool dev = out->out_on_device != 0;
+    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+    size_t need = 0, off_c[5] = {}, off_s[5] = {};
+    for (int k = 0; k < 5; k++)
+        if (want[k]) { off_c[k] = need; need += up(rb[k] * (size_t)U); }
+    for (int k = 0; k < 5; k++)
+        if (want[k] && !dev) { off_s[k] = need; need += up(rb[k] * (size_t)P); }
+    if (need > e->eq_mem_bytes) {
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+        if (e->eq_mem) HIP_TRY(e, hipFree(e->eq_mem));
+        e->eq_mem = nullptr;
+        e->eq_mem_bytes = 0;
+        HIP_TRY(e, hipMalloc(&e->eq_mem, need));
+        e->eq_mem_bytes = need;
+    }
+    char *m = (char *)e->eq_mem;
+    kg_eval_out cout;
+    memset(&cout, 0, sizeof(cout));
+    void **cptr[5] = {(void **)&cout.mask, (void **)&cout.scores, (void **)&cout.top1, (void **)&cout.numa_scores,
+                      (void **)&cout.rsv_scores};
+    for (int k = 0; k < 5; k++)
+        if (want[k]) *cptr[k] = m + off_c[k];
+    cout.out_on_device = 1;
+    // the distinct batch in place of the batch for the inner call (restored on every path)
+    const kg_counters ctr0 = e->ctr;
+    std::swap(e->pods, e->eq_pods);
+    std::swap(e->numa_perm, e->eq_perm);
+    std::swap(e->numa_perm_on, e->eq_perm_on);
+    e->n_pods = U;
+    e->eq_on = false;
+    kg_status st = kg_eval(e, now_ns, &cout);
+    e->eq_on = true;
+    e->n_pods = P;
+    std::swap(e->pods, e->eq_pods);
+    std::swap(e->numa_perm, e->eq_perm);
+    std::swap(e->numa_perm_on, e->eq_perm_on);
+    e->ctr = ctr0;   // counted as the whole batch below
+    if (st) return st;
+    e->ctr.eval_calls++;
+    e->ctr.evals += (uint64_t)P * (uint64_t)width;
+    for (int k = 0; k < 5; k++)
+        if (want[k]) e->ctr.out_bytes += rb[k] * (size_t)P;
+    for (int k = 0; k < 5; k++) {
+        if (!want[k]) continue;
+        char *dst = dev ? (char *)want[k] : m + off_s[k];
+        const int64_t nvec = (int64_t)rb[k] / 8;
+        const unsigned gx = (unsigned)std::min<int64_t>((nvec + 511) / 512, 1024);
+        const dim3 grid(gx > 0 ? gx : 1, (unsigned)std::min<int32_t>(P, 65535));
+        if (rb[k] % 16 == 0)
+            hipLaunchKernelGGL(k_eq_rows<16>, grid, dim3(256), 0, e->stream, e->eq_of, P, (const char *)(m + off_c[k]), dst,
+                               (int64_t)rb[k]);
+        else
+            hipLaunchKernelGGL(k_eq_rows<8>, grid, dim3(256), 0, e->stream, e->eq_of, P, (const char *)(m + off_c[k]), dst,
+                               (int64_t)rb[k]);
+        HIP_TRY(e, hipGetLastError());
+    }
+    if (!dev) {
+        for (int k = 0; k < 5; k++)
+            if (want[k]) HIP_TRY(e, hipMemcpyAsync(want[k], m + off_s[k], rb[k] * (size_t)P, hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+    }
+    return KG_OK;
+}
 
 kg_status chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint32_t *partial_dev) {
     if (pod_begin < 0 || n < 0 || pod_begin + (int64_t)n > e->n_pods || (n > 0 && !partial_dev))

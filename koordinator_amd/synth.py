@@ -114,12 +114,19 @@ def make_nodes(n: int, seed: int, now_ns: int = NOW_NS, no_metric_frac: float = 
     return nodes
 
 
-def make_pods(p: int, seed: int):
+def make_pods(p: int, seed: int, distinct: bool = False):
+    """Pending pods of the config-1/2 distribution.  distinct: cpu uniform in [100, 4000] m and memory uniform
+    in [128 Mi, 16 Gi] bytes instead of the 5 × 7 request shapes, so (almost) every pod's row is its own
+    (the bench's config2_distinct section: no two pods share an evaluation)."""
     rng = np.random.default_rng(seed + 1_000_003)
     pods = np.zeros(p, dtype=nat.POD_SPEC)
     cont = np.zeros(p, dtype=nat.CONTAINER)
-    cpu = rng.choice(np.array([250, 500, 1000, 2000, 4000], np.int64), p)
-    mem = rng.choice(np.array([256, 512, 1024, 2048, 4096, 8192, 16384], np.int64), p) * MI
+    if distinct:
+        cpu = rng.integers(100, 4001, p).astype(np.int64)
+        mem = rng.integers(128 * MI, 16 * GI + 1, p).astype(np.int64)
+    else:
+        cpu = rng.choice(np.array([250, 500, 1000, 2000, 4000], np.int64), p)
+        mem = rng.choice(np.array([256, 512, 1024, 2048, 4096, 8192, 16384], np.int64), p) * MI
     kind = rng.random(p)
     guaranteed = kind < 0.5
     burstable = (kind >= 0.5) & (kind < 0.8)
@@ -248,9 +255,9 @@ def decorate(nodes: np.ndarray, pods: np.ndarray, cont: np.ndarray, seed: int, a
 
 
 def make_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, decorated: bool = True,
-                 **kw) -> SynthView:
+                 distinct_pods: bool = False, **kw) -> SynthView:
     nodes = make_nodes(n_nodes, seed, now_ns, **kw)
-    pods, cont = make_pods(n_pods, seed)
+    pods, cont = make_pods(n_pods, seed, distinct=distinct_pods)
     if not decorated:
         return SynthView(pods, cont, nodes, now_ns)
     pods, cont, agg, pm, asg = decorate(nodes, pods, cont, seed)

@@ -42,6 +42,25 @@ def test_la_extra_matrix_parity(shipped):
     assert m.any()
 
 
+def test_la_extra_matrix_equivalent_pods():
+    """Pod equivalence on the exact path: 600 pods over 40 distinct rows, evaluated once per row."""
+    cl = synth.make_la_extra_cluster(2_600, 40, seed=44)
+    cfg = shipped_profile(resource_weights=W, estimated_scaling_factors=SF)
+    N = len(cl.nodes)
+    idx = np.random.default_rng(44).integers(0, 40, 600)
+    with _engine(cfg, cl, idx) as eng:
+        res = eng.eval(cl.now_ns)
+    u, inv = np.unique(idx, return_inverse=True)
+    m, f, l = oracle.eval_matrix(cfg, cl, u, cl.now_ns)
+    np.testing.assert_array_equal(engine.unpack_mask(res["mask"], N), m[inv])
+    np.testing.assert_array_equal(res["scores"][:, :N, 0], f[inv])
+    np.testing.assert_array_equal(res["scores"][:, :N, 1], l[inv])
+    tot = np.where(m, int(cfg["weight_fit"]) * f.astype(np.int64) + int(cfg["weight_loadaware"]) * l, -1)[inv]
+    node, best = engine.decode_top1(res["top1"])
+    np.testing.assert_array_equal(node, np.where(tot.max(axis=1) >= 0, tot.argmax(axis=1), -1))
+    np.testing.assert_array_equal(best, tot.max(axis=1))
+
+
 def test_la_extra_matrix_shard():
     cl = synth.make_la_extra_cluster(2_500, 24, seed=42)
     cfg = make_config(plugins=("NodeResourcesFit", "LoadAwareScheduling"), resource_weights=W,

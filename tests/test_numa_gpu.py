@@ -31,10 +31,10 @@ def _weights(cfg):
     return int(cfg["weight_fit"]), int(cfg["weight_loadaware"]), int(cfg["weight_numa"])
 
 
-def _check_matrix3(cfg, cl, P, begin=0, end=None):
+def _check_matrix3(cfg, cl, P, begin=0, end=None, idx=None):
     N = len(cl.nodes)
     end = N if end is None else end
-    idx = np.arange(P)
+    idx = np.arange(P) if idx is None else idx
     with _engine_for(cfg, cl, idx) as eng:
         if (begin, end) != (0, N):
             eng.set_shard(begin, end)
@@ -74,6 +74,40 @@ def test_matrix_numa_grouped_pods(seed, pods):
     _check_matrix3(numa_config(), cl, pods)
     cl3 = synth.make_numa_cluster(2_000, pods, seed=seed)
     _check_matrix3(numa_config(), cl3, pods)
+
+
+@pytest.mark.parametrize("begin,end", [(0, None), (1024, 2300)])
+def test_matrix_numa_equivalent_pods(begin, end):
+    """Pod equivalence (kg_engine::eq_on): a batch of 700 pods over 120 distinct rows is evaluated as its distinct
+    rows, whose output rows are copied to every pod of each; planes and top-1 against the oracle, also on a
+    shard, and a device-output pass equal to the host-output one."""
+    cl = make_numa_edge_cluster(2_300, 120, seed=51)
+    idx = np.random.default_rng(51).integers(0, 120, 700)
+    _check_matrix3(numa_config(), cl, len(idx), begin=begin, end=end, idx=idx)
+
+
+def test_matrix_numa_equivalent_pods_device_outputs():
+    import torch
+    cl = synth.make_numa_cluster(2_000, 600, seed=52)
+    cfg = numa_config()
+    idx = np.arange(600)
+    # torch's HIP context first (it does not initialise beside a live engine)
+    dev = torch.device("cuda", 0)
+    W = (len(cl.nodes) + 63) // 64
+    mask = torch.zeros((600, W), dtype=torch.int64, device=dev)
+    scores = torch.zeros((600, W * 64, 2), dtype=torch.uint8, device=dev)
+    numa = torch.zeros((600, W * 64), dtype=torch.uint8, device=dev)
+    top1 = torch.zeros(600, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    with _engine_for(cfg, cl, idx) as eng:
+        host = eng.eval(cl.now_ns)
+        assert eng.mask_words == W
+        eng.eval_device(cl.now_ns, mask.data_ptr(), scores.data_ptr(), top1.data_ptr(), numa.data_ptr())
+        eng.sync()
+    np.testing.assert_array_equal(mask.cpu().numpy().view(np.uint64), host["mask"])
+    np.testing.assert_array_equal(scores.cpu().numpy(), host["scores"])
+    np.testing.assert_array_equal(numa.cpu().numpy(), host["numa_scores"])
+    np.testing.assert_array_equal(top1.cpu().numpy().view(np.uint64), host["top1"])
 
 
 def test_matrix_numa_shard():

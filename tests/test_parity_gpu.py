@@ -3,6 +3,7 @@ import numpy as np
 import pytest
 
 from kat import case_cluster, load
+from koordinator_amd import _native as nat
 from koordinator_amd import engine, synth
 from koordinator_amd.config import make_config, shipped_profile
 from oracle import oracle
@@ -64,13 +65,11 @@ def test_matrix_parity_config1_shape(profile):
     _check_matrix(cfg, cl, np.arange(96), cl.now_ns)
 
 
-@pytest.mark.parametrize("fold", ["1", "0"])
 @pytest.mark.parametrize("profile", ["least4", "most4", "w2"])
-def test_matrix_parity_uniform_slot_fold(profile, fold, monkeypatch):
+def test_matrix_parity_uniform_slot_fold(profile):
     """Batch pods score cpu / memory at the NonZero defaults (one value for the whole class): the class
-    path folds those slots into a per-node term (kg_cls_desc::uni_res), KG_CLS_FOLD_UNIFORM=0 keeps them
-    per pair; both must equal the oracle under LeastAllocated / MostAllocated and non-unit weights."""
-    monkeypatch.setenv("KG_CLS_FOLD_UNIFORM", fold)
+    path folds those slots into a per-node term (kg_cls_desc::uni_res); it must equal the oracle under
+    LeastAllocated / MostAllocated and non-unit weights."""
     four = ("cpu", "memory", "kubernetes.io/batch-cpu", "kubernetes.io/batch-memory")
     cfg = {"least4": lambda: make_config(fit_resources={r: 1 for r in four}),
            "most4": lambda: make_config(fit_strategy="MostAllocated", fit_resources={r: 1 for r in four}),
@@ -79,22 +78,68 @@ def test_matrix_parity_uniform_slot_fold(profile, fold, monkeypatch):
     _check_matrix(cfg, cl, np.arange(160), cl.now_ns)
 
 
-@pytest.mark.parametrize("fold", ["1", "0"])
+def _distinct_rows(cl, n_pods, seed):
+    """Every pending pod gets its own ephemeral-storage request (and every node room for it): the class rows
+    are then pairwise distinct while the ~105 cpu / memory shapes still share EstimatePods."""
+    rng = np.random.default_rng(seed)
+    cont = cl.containers
+    eph = rng.permutation(n_pods).astype(np.int64) * 4096 + (1 << 30)
+    first = cl.pods["first_container"][:n_pods]
+    cont["requests"]["v"][first, nat.RES_EPHEMERAL_STORAGE] = eph
+    cont["requests"]["present"][first] |= np.uint32(1 << nat.RES_EPHEMERAL_STORAGE)
+    nodes = cl.nodes
+    nodes["allocatable"]["v"][:, nat.RES_EPHEMERAL_STORAGE] = rng.integers(1 << 30, 1 << 40, len(nodes))
+    nodes["allocatable"]["present"] |= np.uint32(1 << nat.RES_EPHEMERAL_STORAGE)
+    nodes["requested"]["v"][:, nat.RES_EPHEMERAL_STORAGE] = rng.integers(0, 1 << 39, len(nodes))
+    return cl.with_nodes(nodes)
+
+
 @pytest.mark.parametrize("profile", ["shipped", "default", "prod_usage", "most_w"])
-def test_matrix_parity_la_uniform_chunks(profile, fold, monkeypatch):
-    """k_eval3 groups a class's pods by EstimatePod and evaluates the LoadAware sums of a whole chunk of one
-    estimate once per node (kg_cls_desc::la_uni_end); KG_CLS_FOLD_LA=0 evaluates them per pair.  1,600 pods
-    of ~105 request shapes give both uniform chunks and a mixed tail per class; some nodes are beyond the fp64
-    bounds and the node count is ragged."""
-    monkeypatch.setenv("KG_CLS_FOLD_LA", fold)
+def test_matrix_parity_la_uniform_chunks(profile):
+    """k_eval3's plain part groups a class's pods by EstimatePod and evaluates the LoadAware sums of a whole
+    chunk of one estimate once per node (kg_cls_desc::la_uni_end).  1,600 pods with pairwise distinct class
+    rows (each its own ephemeral-storage request) over ~105 request shapes give both uniform chunks and a
+    mixed tail per class; some nodes are beyond the fp64 bounds and the node count is ragged."""
     cfg = {"shipped": shipped_profile, "default": make_config,
            "prod_usage": lambda: shipped_profile(score_according_prod_usage=True),
            "most_w": lambda: make_config(fit_strategy="MostAllocated", fit_resources={"cpu": 2, "memory": 1})}[profile]()
     cl = synth.make_cluster(1_100, 1_600, seed=31)
     big = np.arange(3, 1_100, 97)
     cl.nodes["allocatable"]["v"][big, 1] = (1 << 43) + 99
-    cl = cl.with_nodes(cl.nodes)
+    cl = _distinct_rows(cl.with_nodes(cl.nodes), 1_600, 31)
     _check_matrix(cfg, cl, np.arange(1_600), cl.now_ns)
+
+
+def _dup_batch(n_nodes, seed, mult=(1, 2, 3, 9, 40, 700, 1300)):
+    """A pod batch of repeated rows: shapes of the config-2 distribution, each repeated `mult` times in a
+    shuffled queue (a row of 1,300 pods spans several k_eval3_dup work items), plus distinct singles."""
+    rng = np.random.default_rng(seed)
+    base = synth.make_cluster(n_nodes, 400, seed=seed)
+    picks = [rng.integers(0, 400) for _ in mult for _ in range(3)]
+    reps = np.repeat(picks, [m for m in mult for _ in range(3)])
+    order = np.concatenate([reps, np.arange(400)])   # the 400 originals: mostly singles or small groups
+    rng.shuffle(order)
+    pods = base.pods.copy()
+    view = base.with_nodes(base.nodes, pods)
+    return view, order
+
+
+@pytest.mark.parametrize("profile", ["shipped", "most_w", "prod_usage"])
+def test_matrix_parity_duplicate_rows(profile):
+    """k_eval3_dup: pods whose class rows repeat are evaluated once per distinct row and written to every pod
+    of the row (multiplicities 2 to 1,300, work items split inside a row, singles on the plain path); planes,
+    top-1 and a top-1-only pass against the oracle on a ragged cluster with slow nodes."""
+    cfg = {"shipped": shipped_profile, "prod_usage": lambda: shipped_profile(score_according_prod_usage=True),
+           "most_w": lambda: make_config(fit_strategy="MostAllocated", fit_resources={"cpu": 2, "memory": 1})}[profile]()
+    cl, order = _dup_batch(2_500, 41)
+    big = np.arange(5, 2_500, 83)
+    cl.nodes["allocatable"]["v"][big, 1] = (1 << 43) + 99
+    cl = cl.with_nodes(cl.nodes)
+    _check_matrix(cfg, cl, order, cl.now_ns)
+    with _engine_for(cfg, cl, order) as eng:
+        full = eng.eval(cl.now_ns)
+        keys = eng.eval(cl.now_ns, mask=False, scores=False)
+    np.testing.assert_array_equal(keys["top1"], full["top1"])
 
 
 @pytest.mark.parametrize("n_nodes", [1, 63, 64, 511, 513, 1500])
