@@ -750,7 +750,8 @@ __device__ __forceinline__ int kg_kofs(int i) { return (i >> 1) * 512 + (i & 1) 
 // 128-column segment).  Pod rows are wave-uniform scalar loads.  UNR: a whole chunk, unrolled, so every
 // LDS address and lane select is an immediate.  LAU: the chunk's pods share one EstimatePod, whose LoadAware
 // sums are lsum[] (per node); otherwise they are evaluated per pair from la[].
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool UNR, bool LAU>
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool UNR, bool LAU,
+          bool WMAX = false>
 __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> (&n)[2],
                                          const ClsLa (&la)[2], const unsigned long long (&okm)[2],
                                          const uint32_t (&lsum)[2], int np_rt, const uint32_t (&kb)[2], uint32_t *kbuf,
@@ -806,7 +807,12 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
             s01 = s[0] | (s[1] << 16);
             if (OUT) put_lane2(mb[0], mb[1], 1ull << i, m[0], m[1]);
         }
-        kbuf[kg_kofs(i) + tid] = kmax;
+        if constexpr (WMAX) {   // the wave's key of the pod (kbuf: the wave's 8 slots)
+            const uint32_t wm = wave_max_u32(kmax);
+            if (lane == 0) kbuf[i] = wm;
+        } else {
+            kbuf[kg_kofs(i) + tid] = kmax;
+        }
         if (OUT) {
             // the wave's 128-column score segment of this pod, written out per chunk
             sst[i * 128 + lane] = (uint16_t)s01;
@@ -961,25 +967,30 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
 // whose class rows are equal have equal output rows on every node, so a work item evaluates each distinct row
 // once against its tile and writes the result to every pod of that row.  One workgroup = one 1024-node tile ×
 // a run of the part's pods, grouped by row (w.begin..w.end); its distinct rows are walked in chunks of
-// KG_EVAL3_CC through cls_pods' mixed form, then each wave writes its 128-column score segment of every pod of
-// the chunk's rows from the LDS stage (16 lanes × 16 B per pod, 4 pods per wave store), the feasibility words by
-// lane permutes of the rows' ballot words, and the reducing wave the (pod, tile) key of every pod.  The work is
-// store-bound: per pod and tile 2 KiB of scores + 128 B of mask + 4 B of key against ~1/60 of a pod's compute.
+// KG_EVAL3_CC through cls_pods' mixed form (each wave stages its 128-column score segments, ballot words and
+// wave-max keys of the chunk's rows in LDS), one barrier, then the pods of the chunk's rows are dealt to the
+// waves: per pod the tile's 2 KiB score row as two contiguous 1 KiB wave stores assembled from the 8 waves'
+// segments, its 128-B feasibility row by 8 lanes, its (pod, tile) key by one.  The stage is double-buffered,
+// so chunk c + 1 is evaluated while other waves still store chunk c.  The work is store-bound: per pod and tile
+// 2 KiB + 128 B + 4 B against ~1/60 of a pod's evaluation.
+#define KG_DUP_STAGE_DW ((KG_TILE / 128) * KG_EVAL3_CC * 128 / 2)   // one buffer: [wave][row][128 u16]
 template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1>
 __device__ __forceinline__ void cls_block_dup(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
                                               const kg_cls_work &w, const char *__restrict__ rows_base,
                                               const int32_t *__restrict__ ids, uint64_t *__restrict__ mask,
                                               uint16_t *__restrict__ scores, uint32_t *__restrict__ partials,
-                                              uint32_t *kbuf, int32_t *lid, uint16_t *lux, int32_t *cst, uint16_t *sstage) {
+                                              uint32_t *stage, uint4 *mstage, uint32_t *kw, int32_t *lid, uint16_t *lux,
+                                              int32_t *cst) {
     constexpr int CC = KG_EVAL3_CC;
-    constexpr int BT = KG_TILE / 2;
+    constexpr int NW = KG_TILE / 128;     // waves of the workgroup (128 columns each)
     constexpr int SEGW = 128;
-    static_assert(CC == 8 && BT == 512, "the key reduction maps one wave's lanes to 8 rows × 8 lanes");
+    static_assert(CC == 8 && NW == 8, "8 rows per chunk, 8 waves");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tile = a.tile_begin + w.tile;
-    const int64_t wave_base = (int64_t)tile * KG_TILE + wave * SEGW;
+    const int64_t tile_base = (int64_t)tile * KG_TILE;
+    const int64_t wave_base = tile_base + wave * SEGW;
     ClsNode<NC, NF> n[2];
     ClsLa la[2];
     unsigned long long okm[2];
@@ -992,15 +1003,11 @@ __device__ __forceinline__ void cls_block_dup(const kg_consts &c, const kg_plane
         full_l = full_l && (n[j].w == (1u << d.fit_shift) || wave_base + 64 * j + lane >= a.node_end);
     }
     const bool full = !FIT_ON || __all(full_l);
-    const int64_t col0 = wave_base - a.col_begin;
-    bool seg[2];
+    const int64_t tcol0 = tile_base - a.col_begin;   // the tile's first output column
     uint32_t kb[2];
     const uint32_t local0 = (uint32_t)(wave * SEGW + lane);
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-        seg[j] = col0 + 64 * j < a.score_stride;
-        kb[j] = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0 - 64u * j;
-    }
+    for (int j = 0; j < 2; j++) kb[j] = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0 - 64u * j;
     // the item's pods (output rows) and their row indices relative to the item's first row go to LDS
     const int nm = w.end - w.begin;
     const int32_t *uxs = ids + d.ux_first + w.begin;
@@ -1020,75 +1027,61 @@ __device__ __forceinline__ void cls_block_dup(const kg_consts &c, const kg_plane
     if (tid == 0) cst[(nu + CC - 1) / CC] = nm;
     __syncthreads();
     const kg_pod_cls_t<NC, NF> *grows = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(rows_base + d.rows_offset) + u_first;
-    uint16_t *sst = sstage + wave * (CC * SEGW);
     const uint32_t lsum[2] = {0u, 0u};
+    // this lane's part of a 1 KiB half of a score row: wave segment sw (+ 4 for the second half), 16 B s16
+    const int sw = lane >> 4, s16 = lane & 15;
     int ci = 0;
     for (int u0 = 0; u0 < nu; u0 += CC, ci++) {
         const int np = min(CC, nu - u0);
-        uint32_t *kcur = kbuf + (ci & 1) * KG_KBUF_DW;
+        const int buf = ci & 1;
+        uint16_t *sst = reinterpret_cast<uint16_t *>(stage + buf * KG_DUP_STAGE_DW) + wave * (CC * SEGW);
+        uint32_t *kcur = kw + (buf * NW + wave) * CC;
         unsigned long long mb[2] = {0ull, 0ull};
 #define KG_CLS_PODS(FULL_, UNR_)                                                                                \
-    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, UNR_, false>(c, d, n, la, okm, lsum, np, kb, kcur, mb, sst, \
-                                                                       grows + u0)
+    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, UNR_, false, true>(c, d, n, la, okm, lsum, np, kb, kcur, mb, \
+                                                                             sst, grows + u0)
         if (full && np == CC) KG_CLS_PODS(true, true);
         else if (full) KG_CLS_PODS(true, false);
         else KG_CLS_PODS(false, false);
 #undef KG_CLS_PODS
-        const int m0 = cst[ci], m1 = cst[ci + 1];
-        if (OUT) {
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("" ::: "memory");
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            const int s8 = lane & 15;
-            const bool segs = s8 < 8 ? seg[0] : seg[1];
-            // 16 lanes × 16 B = one pod's 128 columns: 4 pods per wave store
-            for (int m = m0; m < m1; m += 4) {
-                const int mm = m + (lane >> 4);
-                if (mm < m1 && segs) {
-                    const int u = lux[mm] - u0;
-                    const uint4 v = *reinterpret_cast<const uint4 *>(sst + u * SEGW + s8 * 8);
-                    const int64_t off = (int64_t)lid[mm] * a.score_stride;
-                    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(scores + off + col0 + s8 * 8));
-                }
-            }
-            // lane l writes the two feasibility words of pod m + l, its row's words taken from lane u (ds_bpermute
-            // with every lane active)
-            for (int m = m0; m < m1; m += 64) {
-                const int mm = m + lane;
-                const int u = mm < m1 ? lux[mm] - u0 : 0;
-                const int src = u << 2;
-                const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)mb[0]);
-                const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(mb[0] >> 32));
-                const uint32_t b0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)mb[1]);
-                const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(mb[1] >> 32));
-                if (mm < m1 && seg[0]) {
-                    uint64_t *mw = mask + (int64_t)lid[mm] * a.mask_words + (col0 >> 6);
-                    mw[0] = (uint64_t)a0 | ((uint64_t)a1 << 32);
-                    if (seg[1]) mw[1] = (uint64_t)b0 | ((uint64_t)b1 << 32);
-                }
-            }
-        }
-        // as cls_block: one barrier per chunk, a rotating reducer wave, double-buffered keys
+        if (OUT && lane < CC) mstage[(buf * CC + lane) * NW + wave] = uint4{(uint32_t)mb[0], (uint32_t)(mb[0] >> 32),
+                                                                           (uint32_t)mb[1], (uint32_t)(mb[1] >> 32)};
         lds_barrier();
-        if (wave == ci % (BT / 64)) {
-            const int p = lane >> 3, q = lane & 7;
-            const uint4 *src = reinterpret_cast<const uint4 *>(kcur + kg_kofs(p)) + q;
-            uint32_t mx = 0;
+        // the chunk's keys: lane u < np takes row u's max over the waves
+        uint32_t rk = 0;
+        if (lane < CC) {
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const uint4 v = src[8 * k];
-                mx = max(mx, max(max(v.x, v.y), max(v.z, v.w)));
+            for (int v = 0; v < NW; v++) rk = max(rk, kw[(buf * NW + v) * CC + lane]);
+        }
+        const int m0 = cst[ci], m1 = cst[ci + 1];
+        const uint4 *st4 = reinterpret_cast<const uint4 *>(stage + buf * KG_DUP_STAGE_DW);
+        for (int m = m0 + wave; m < m1; m += NW) {
+            const int u = __builtin_amdgcn_readfirstlane(lux[m] - u0);
+            const int32_t row = __builtin_amdgcn_readfirstlane(lid[m]);
+            if (OUT) {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                uint16_t *srow = scores + (int64_t)row * a.score_stride + tcol0;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int seg = 4 * h + sw;   // wave segment of 128 columns
+                    const int64_t col = seg * SEGW + s16 * 8;
+                    if (tcol0 + col < a.score_stride) {   // ragged shard end: whole 64-column halves only
+                        const uint4 v = st4[(seg * CC + u) * (SEGW / 8) + s16];
+                        __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(srow + col));
+                    }
+                }
+                if (lane < NW) {   // words 2·lane, 2·lane + 1 of the tile's 16
+                    const int64_t c0 = tcol0 + lane * SEGW;
+                    if (c0 < a.score_stride) {
+                        const uint4 v = mstage[(buf * CC + u) * NW + lane];
+                        uint64_t *mw = mask + (int64_t)row * a.mask_words + (c0 >> 6);
+                        mw[0] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                        if (c0 + 64 < a.score_stride) mw[1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+                    }
+                }
             }
-            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x141, 0xf, 0xf, false));  // row_half_mirror
-            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
-            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
-            // every lane of row p's group holds its key; pod m + l takes lane 8u's
-            for (int m = m0; m < m1; m += 64) {
-                const int mm = m + lane;
-                const int u = mm < m1 ? lux[mm] - u0 : 0;
-                const uint32_t k = (uint32_t)__builtin_amdgcn_ds_bpermute(u << 5, (int)mx);
-                if (mm < m1) partials[(int64_t)lid[mm] * a.tiles_total + tile] = k;
-            }
+            const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)rk, u);
+            if (lane == 0) partials[(int64_t)row * a.tiles_total + tile] = k;
         }
     }
 }
@@ -1097,25 +1090,25 @@ __device__ __forceinline__ void cls_block_dup(const kg_consts &c, const kg_plane
 // tile, dealt to the XCDs in contiguous ranges (workgroup b runs on XCD b % 8 and takes item (b % 8) · per + b / 8),
 // so the items of one tile run on one XCD and its L2 serves the tile's node planes to all of them.
 template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int KIND>
-__global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? KG_EVAL3_WPE0 : KIND == 2 ? 5 : 4))) void k_eval3_dup(kg_consts c, kg_planes pl, HotArgs a,
+__global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? 8 : KIND == 2 ? 5 : 4))) void k_eval3_dup(kg_consts c, kg_planes pl, HotArgs a,
                                                         const kg_cls_desc *__restrict__ descs,
                                                         const kg_cls_work *__restrict__ work, int32_t n_items,
                                                         const char *__restrict__ rows, const int32_t *__restrict__ ids,
                                                         uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
                                                         uint32_t *__restrict__ partials) {
-    constexpr int CC = KG_EVAL3_CC, BT = KG_TILE / 2;
-    __shared__ __attribute__((aligned(16))) uint32_t kbuf[2 * KG_KBUF_DW];
-    static_assert(CC * BT <= 4096, "a chunk's keys fit the key buffer");
+    constexpr int CC = KG_EVAL3_CC, NW = KG_TILE / 128;
+    __shared__ __attribute__((aligned(16))) uint32_t stage[OUT ? 2 * KG_DUP_STAGE_DW : 4];
+    __shared__ uint4 mstage[OUT ? 2 * CC * NW : 1];
+    __shared__ uint32_t kw[2 * NW * CC];
     __shared__ int32_t lid[KG_CLS_ITEM_MAX];
     __shared__ uint16_t lux[KG_CLS_ITEM_MAX];
     __shared__ int32_t cst[KG_CLS_ITEM_MAX / CC + 1];
-    __shared__ __attribute__((aligned(16))) uint16_t sstage[OUT ? (BT / 64) * CC * 128 : 8];
     const int per = (int)(gridDim.x / KG_XCDS);
     const int item = (int)(blockIdx.x % KG_XCDS) * per + (int)(blockIdx.x / KG_XCDS);
     if (item >= n_items) return;   // grid padded to a multiple of 8; block-uniform
     const kg_cls_work w = work[item];
     const kg_cls_desc d = descs[w.cls];
-#define KG_CLS_ARGS c, pl, a, d, w, rows, ids, mask, scores, partials, kbuf, lid, lux, cst, sstage
+#define KG_CLS_ARGS c, pl, a, d, w, rows, ids, mask, scores, partials, stage, mstage, kw, lid, lux, cst
     if constexpr (KIND == 0) cls_block_dup<2, 2, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
     else if constexpr (KIND == 1) cls_block_dup<2, 4, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
     else if constexpr (KIND == 2) cls_block_dup<4, 2, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
@@ -2470,6 +2463,8 @@ struct kg_engine {
     kg_counters ctr{};                  // kg_counters_get
     int64_t ev_acc = 0;                 // profiled launches already summed into ctr.kernel_ns
     hipStream_t eval_stream = nullptr;  // kg_set_eval_stream (kg_place_chunk_eval), nullptr ⇒ stream
+    hipEvent_t ev_eval = nullptr;       // recorded on eval_stream after each kg_place_chunk_eval; the chunk resolve
+                                        // entries make the engine stream wait on its latest record
     static constexpr int kRing = 256;   // event pairs: one per profiled k_eval launch
     hipEvent_t ev0[kRing] = {}, ev1[kRing] = {};
     int64_t ev_count = 0;               // launches recorded since kg_set_profiling
@@ -2501,6 +2496,32 @@ kg_status set_err(kg_engine *e, kg_status code, const char *fmt, ...) {
 hipError_t h2d(kg_engine *e, void *dst, const void *src, size_t bytes, hipStream_t s) {
     e->ctr.h2d_bytes += bytes;
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+}
+
+// Profiled launches (kg_set_profiling): an event pair per launch in a ring of kRing; a slot about to be reused is
+// summed into the counters first, so kg_counters_get's kernel_ns covers every timed launch
+hipError_t prof_sum(kg_engine *e, int64_t k) {
+    const int64_t slot = k % kg_engine::kRing;
+    float ms = 0.f;
+    hipError_t st = hipEventSynchronize(e->ev1[slot]);
+    if (st == hipSuccess) st = hipEventElapsedTime(&ms, e->ev0[slot], e->ev1[slot]);
+    if (st != hipSuccess) return st;
+    e->ctr.kernel_ns += (uint64_t)((double)ms * 1e6);
+    e->ctr.timed_launches++;
+    return hipSuccess;
+}
+hipError_t prof_begin(kg_engine *e) {
+    if (e->ev_count - e->ev_acc >= kg_engine::kRing) {
+        const hipError_t st = prof_sum(e, e->ev_acc);
+        if (st != hipSuccess) return st;
+        e->ev_acc++;
+    }
+    return hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream);
+}
+hipError_t prof_end(kg_engine *e) {
+    const hipError_t st = hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream);
+    e->ev_count++;
+    return st;
 }
 
 kg_status ensure_scratch(kg_engine *e, size_t bytes) {
@@ -2974,7 +2995,7 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     for (int s = 0; s < 8; s++) a.slot_res[s] = s < e->nslot ? e->slot_res[s] : -1;
     a.now_ns = now_ns;
     if ((e->consts.plugins & KG_PLUGIN_NUMA) && topk && n <= e->numa_chunk_pods) {
-        if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
+        if (e->profiling) HIP_TRY(e, prof_begin(e));
         const unsigned blocks = (unsigned)((shard_tiles + KG_XCDS - 1) / KG_XCDS * KG_XCDS * n);
         if (e->consts.numa_bz)
             hipLaunchKernelGGL(k_eval_numa_chunk<true>, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
@@ -2983,14 +3004,11 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
             hipLaunchKernelGGL(k_eval_numa_chunk<false>, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
                                e->pods + pod_begin, (int32_t)shard_tiles, partials);
         HIP_TRY(e, hipGetLastError());
-        if (e->profiling) {
-            HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
-            e->ev_count++;
-        }
+        if (e->profiling) HIP_TRY(e, prof_end(e));
         return KG_OK;
     }
     if (e->consts.plugins & KG_PLUGIN_NUMA) {
-        if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
+        if (e->profiling) HIP_TRY(e, prof_begin(e));
         {  // pod per lane; queued 32-node items when they fill every resident wave slot several times over,
            // else a grid where a single pod block splits each wave's node run 4 ways
             // segment: 32 nodes (half mask words); 8 for a placement chunk's keys-only launch
@@ -3030,24 +3048,18 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
                                (unsigned long long *)mask, scores, numa_scores, partials);
             HIP_TRY(e, hipGetLastError());
         }
-        if (e->profiling) {
-            HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
-            e->ev_count++;
-        }
+        if (e->profiling) HIP_TRY(e, prof_end(e));
         return KG_OK;
     }
     if (e->consts.la_extra && !topk) {   // every node is on the exact path: no fast kernel, no slow list
-        if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
+        if (e->profiling) HIP_TRY(e, prof_begin(e));
         const int64_t width = e->shard_end - e->shard_begin;
         dim3 grid((unsigned)((width + 255) / 256), (unsigned)(n < 65535 ? n : 65535));
         hipLaunchKernelGGL(k_eval_exact, grid, dim3(256), 0, e->stream, e->consts, e->pl, e->pods + pod_begin, n,
                            e->shard_begin, e->shard_end, a.mask_words, a.score_stride, a.tiles_total, now_ns,
                            (unsigned long long *)mask, scores, partials);
         HIP_TRY(e, hipGetLastError());
-        if (e->profiling) {
-            HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
-            e->ev_count++;
-        }
+        if (e->profiling) HIP_TRY(e, prof_end(e));
         return KG_OK;
     }
     use_cls = use_cls && e->cls_ok && pod_begin == 0 && n == e->n_pods;
@@ -3056,16 +3068,13 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
         if (st) return st;
     }
     dim3 grid((unsigned)shard_tiles, use_cls ? (unsigned)e->cls_nwork : (unsigned)((n + a.pods_per_block - 1) / a.pods_per_block));
-    if (e->profiling) HIP_TRY(e, hipEventRecord(e->ev0[e->ev_count % kg_engine::kRing], e->stream));
+    if (e->profiling) HIP_TRY(e, prof_begin(e));
     if (use_cls) launch_cls(e, grid, a, mask, scores, partials);
     else if (e->nslot == 2) launch_hot<2>(e, grid, a, pod_begin, mask, scores, partials, topk);
     else if (e->nslot == 4) launch_hot<4>(e, grid, a, pod_begin, mask, scores, partials, topk);
     else launch_hot<8>(e, grid, a, pod_begin, mask, scores, partials, topk);
     HIP_TRY(e, hipGetLastError());
-    if (e->profiling) {
-        HIP_TRY(e, hipEventRecord(e->ev1[e->ev_count % kg_engine::kRing], e->stream));
-        e->ev_count++;
-    }
+    if (e->profiling) HIP_TRY(e, prof_end(e));
     // exact re-evaluation of the (rare) nodes outside the fp64 fast-path bounds; a placement chunk
     // leaves them to the resolve, which re-scores the slow-node list itself
     kg_status st = slow_refresh(e);
@@ -3226,6 +3235,7 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_eval) (void)hipEventDestroy(e->ev_eval);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     for (int k = 0; k < 3; k++)
         if (e->ev_res[k]) (void)hipEventDestroy(e->ev_res[k]);
@@ -3871,8 +3881,26 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
     if (e->eval_stream) e->stream = e->eval_stream;   // chunk_eval launches on e->stream
     st = chunk_eval(e, now_ns, pod_begin, n, partial_dev);
     e->stream = main_s;
-    return st;
+    if (st) return st;
+    if (e->eval_stream) {   // the resolve that reads these partials waits for them (eval_join)
+        if (!e->ev_eval) HIP_TRY(e, hipEventCreateWithFlags(&e->ev_eval, hipEventDisableTiming));
+        HIP_TRY(e, hipEventRecord(e->ev_eval, e->eval_stream));
+    }
+    return KG_OK;
 }
+
+}  // extern "C"
+
+namespace {
+// a chunk resolve after kg_place_chunk_eval on the eval stream: the engine stream waits for the latest such eval
+// (in the pipelined order resolve(i) is enqueued before eval(i + 1), so that is the chunk's own)
+kg_status eval_join(kg_engine *e) {
+    if (e->eval_stream && e->ev_eval) HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev_eval, 0));
+    return KG_OK;
+}
+}  // namespace
+
+extern "C" {
 
 kg_status kg_set_eval_stream(kg_engine *e, void *s) {
     kg_status st = check_engine(e);
@@ -3892,6 +3920,8 @@ kg_status kg_place_chunk_resolve_prev(kg_engine *e, int64_t now_ns, int32_t pod_
         return set_err(e, KG_ERR_RANGE, "bad previous-chunk node list");
     if (n_prev > 0 && rsv_args(e).rsv)
         return set_err(e, KG_ERR_UNSUPPORTED, "pipelined resolve with reservations (chunk_eval writes their entries)");
+    st = eval_join(e);
+    if (st) return st;
     return chunk_resolve(e, now_ns, pod_begin, n, partial_dev, out_node_dev, out_score_dev, false, prev_nodes_dev, n_prev);
 }
 
@@ -3900,6 +3930,8 @@ kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin
     kg_status st = check_engine(e);
     if (st) return st;
     st = bind_ready(e, true);
+    if (st) return st;
+    st = eval_join(e);
     if (st) return st;
     return chunk_resolve(e, now_ns, pod_begin, n, partial_dev, out_node_dev, out_score_dev, false);
 }
@@ -3934,6 +3966,12 @@ kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64
     hipStream_t main_s = e->stream, eval_s = e->stream2;
     HIP_TRY(e, hipEventRecord(e->ev_fork, main_s));   // the eval stream starts after everything queued so far
     HIP_TRY(e, hipStreamWaitEvent(eval_s, e->ev_fork, 0));
+    // an error return leaves no evaluation in flight behind the engine stream (it may write the scratch buffer)
+    auto fail = [&](kg_status code) {
+        (void)hipEventRecord(e->ev_join, eval_s);
+        (void)hipStreamWaitEvent(main_s, e->ev_join, 0);
+        return code;
+    };
     int32_t prev_b = 0, prev_n = 0;
     int32_t i = 0;
     for (int32_t b = 0; b < P; b += chunk, i++) {
@@ -3942,12 +3980,12 @@ kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64
         e->stream = eval_s;   // chunk_eval launches on e->stream
         st = chunk_eval(e, now_ns, b, n, part[i & 1]);
         e->stream = main_s;
-        if (st) return st;
+        if (st) return fail(st);
         HIP_TRY(e, hipEventRecord(e->ev_join, eval_s));
         HIP_TRY(e, hipStreamWaitEvent(main_s, e->ev_join, 0));
         st = chunk_resolve(e, now_ns, b, n, part[i & 1], dnode + b, dscore + b, false, i ? dnode + prev_b : nullptr,
                            i ? prev_n : 0);
-        if (st) return st;
+        if (st) return fail(st);
         HIP_TRY(e, hipEventRecord(e->ev_res[i % 3], main_s));
         prev_b = b;
         prev_n = n;
@@ -4004,6 +4042,8 @@ kg_status place_impl(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *o
     const uint8_t may_mask = e->n_node_bind_nodes > 0 ? 3 : 1;
     // the pipeline pays two cross-stream event hops per chunk: it wins where the chunk evaluation is long
     // (NodeNUMAResource: config 3 5.0k → 6.1k pods/s) and loses where it is short (config 2: 82k → 61k)
+    st = quota_ready(e);   // (before the pipeline: chunk_resolve checks it too, with an evaluation in flight)
+    if (st) return st;
     if (!bind_mode && !rsv_args(e).rsv &&
         (e->place_pipeline == 2 || (e->place_pipeline == 1 && (e->consts.plugins & KG_PLUGIN_NUMA))))
         return place_pipelined(e, now_ns, out_node, out_score, chunk);
@@ -4118,17 +4158,8 @@ kg_status kg_counters_get(kg_engine *e, kg_counters *out) {
     kg_status st = check_engine(e);
     if (st) return st;
     if (!out) return set_err(e, KG_ERR_INVALID_ARG, "null output");
-    if (e->profiling) {   // the timed launches not summed yet (the ring keeps the last kRing)
-        const int64_t from = std::max(e->ev_acc, e->ev_count - (int64_t)kg_engine::kRing);
-        for (int64_t k = from; k < e->ev_count; k++) {
-            const int64_t slot = k % kg_engine::kRing;
-            float ms = 0.f;
-            HIP_TRY(e, hipEventSynchronize(e->ev1[slot]));
-            HIP_TRY(e, hipEventElapsedTime(&ms, e->ev0[slot], e->ev1[slot]));
-            e->ctr.kernel_ns += (uint64_t)((double)ms * 1e6);
-            e->ctr.timed_launches++;
-        }
-        e->ev_acc = e->ev_count;
+    if (e->profiling) {   // the timed launches not summed yet (prof_begin sums a ring slot before reusing it)
+        for (; e->ev_acc < e->ev_count; e->ev_acc++) HIP_TRY(e, prof_sum(e, e->ev_acc));
     }
     *out = e->ctr;
     return KG_OK;
@@ -4191,10 +4222,12 @@ kg_status kg_rsv_set(kg_engine *e, const kg_reservation *rsv, int32_t n) {
     const size_t sb = up(sizeof(kg_reservation) * (size_t)(n > 0 ? n : 1)), fb = up(4 * rfirst.size()),
                  nb = up(4 * (size_t)(n_rn > 0 ? n_rn : 1)),
                  eb = up(8 * (size_t)KG_RSV_POD_CHUNK * (size_t)(n_rn > 0 ? n_rn : 1));
-    // the placement split: scored-entry lists [chunk][n_rn], their counts, per-group keys [chunk][groups]
-    const size_t mb = up(sizeof(kg_rsv_ment) * (size_t)KG_RSV_POD_CHUNK * (size_t)(n_rn > 0 ? n_rn : 1)),
-                 cb = up(4 * (size_t)KG_RSV_POD_CHUNK),
-                 gb = up(8 * (size_t)KG_RSV_POD_CHUNK * (size_t)((n_rn + KG_RSV_GROUP - 1) / KG_RSV_GROUP + 1));
+    // the placement split: scored-entry lists [chunk][n_rn], their counts, per-group keys [chunk][groups]; only
+    // when the resolve's touched-group flags cover the groups (rsv_args), else nothing reads it
+    const bool split = (n_rn + KG_RSV_GROUP - 1) / KG_RSV_GROUP <= KG_RSV_MAX_GROUPS;
+    const size_t mb = split ? up(sizeof(kg_rsv_ment) * (size_t)KG_RSV_POD_CHUNK * (size_t)(n_rn > 0 ? n_rn : 1)) : 0,
+                 cb = split ? up(4 * (size_t)KG_RSV_POD_CHUNK) : 0,
+                 gb = split ? up(8 * (size_t)KG_RSV_POD_CHUNK * (size_t)((n_rn + KG_RSV_GROUP - 1) / KG_RSV_GROUP + 1)) : 0;
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     if (e->rsv_mem) HIP_TRY(e, hipFree(e->rsv_mem));
     e->rsv_mem = nullptr;
@@ -4205,9 +4238,9 @@ kg_status kg_rsv_set(kg_engine *e, const kg_reservation *rsv, int32_t n) {
     e->rnode = (int32_t *)(m + sb + fb);
     e->rsv_e = (unsigned long long *)(m + sb + fb + nb);
     e->rsv_o = (int64_t *)(m + sb + fb + nb + eb);
-    e->rsv_m = (kg_rsv_ment *)(m + sb + fb + nb + 2 * eb);
-    e->rsv_mn = (int32_t *)(m + sb + fb + nb + 2 * eb + mb);
-    e->rsv_g = (unsigned long long *)(m + sb + fb + nb + 2 * eb + mb + cb);
+    e->rsv_m = split ? (kg_rsv_ment *)(m + sb + fb + nb + 2 * eb) : nullptr;
+    e->rsv_mn = split ? (int32_t *)(m + sb + fb + nb + 2 * eb + mb) : nullptr;
+    e->rsv_g = split ? (unsigned long long *)(m + sb + fb + nb + 2 * eb + mb + cb) : nullptr;
     if (n) HIP_TRY(e, h2d(e, e->rsv, slots.data(), sizeof(kg_reservation) * (size_t)n, e->stream));
     HIP_TRY(e, h2d(e, e->rfirst, rfirst.data(), 4 * rfirst.size(), e->stream));
     if (n_rn) HIP_TRY(e, h2d(e, e->rnode, rnode.data(), 4 * (size_t)n_rn, e->stream));

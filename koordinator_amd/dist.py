@@ -61,7 +61,12 @@ def merge_top1_(keys: torch.Tensor, group=None) -> None:
 
 
 class ChunkBackend(Protocol):
-    """What `place_sharded` needs from an engine (the HIP engine implements it through the C-ABI)."""
+    """What `place_sharded` needs from an engine (the HIP engine implements it through the C-ABI).
+
+    Optional attributes: ``torch_stream`` (the torch stream the engine launches on; the merge runs on it) and
+    ``eval_torch_stream`` (a second stream for ``chunk_eval``: its presence turns the pipelined order on, and
+    ``chunk_resolve`` is then called with the previous chunk's placed nodes, ``prev_ptr`` / ``n_prev``, to
+    re-score)."""
 
     n_pods: int
     num_tiles: int
@@ -70,7 +75,7 @@ class ChunkBackend(Protocol):
     def chunk_eval(self, now_ns: int, pod_begin: int, n: int, partial_ptr: int) -> None: ...
 
     def chunk_resolve(self, now_ns: int, pod_begin: int, n: int, partial_ptr: int, node_ptr: int,
-                      score_ptr: int) -> None: ...
+                      score_ptr: int, prev_ptr: int = 0, n_prev: int = 0) -> None: ...
 
 
 def place_sharded(backend: ChunkBackend, now_ns: int, device: torch.device, chunk: int = 8,

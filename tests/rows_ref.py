@@ -126,13 +126,14 @@ class RowsBackend:
         ok, tot = pair_totals(self.cfg, self.nodes[node:node + 1], pod, now_ns)
         return ((int(tot[0]) + 1) << 32) | (0xFFFFFFFF - node) if ok[0] else 0
 
-    def chunk_resolve(self, now_ns, b, n, partial_ptr, node_ptr, score_ptr):
+    def chunk_resolve(self, now_ns, b, n, partial_ptr, node_ptr, score_ptr, prev_ptr=0, n_prev=0):
         T = self.num_tiles
         part = self._view(partial_ptr, n * T, ctypes.c_uint32).reshape(n, T)
         out_node = self._view(node_ptr, n, ctypes.c_int32)
         out_score = self._view(score_ptr, n, ctypes.c_int64)
         N = len(self.nodes)
-        touched = []
+        # the previous chunk's placements (pipelined order): their keys may predate those commits, so re-score
+        touched = [int(x) for x in self._view(prev_ptr, n_prev, ctypes.c_int32) if x >= 0] if n_prev else []
         for j in range(n):
             pod = self.pods[b + j]
             best, rescan = 0, []

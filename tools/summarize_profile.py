@@ -45,7 +45,7 @@ def main(src: str, dst: str) -> None:
         hot = {"name": " + ".join(k["name"].split("(")[0] for k in parts), "calls": calls,
                "avg_ns": sum(k["avg_ns"] for k in parts), "percent": sum(k["percent"] for k in parts),
                "parts": parts}
-    # the kinds run on two streams (KG_CLS_CONCURRENT): their durations overlap, so the pass time is the
+    # the forms / kinds run on two streams: their durations overlap, so the pass time is the
     # wall span from the first kind's start to the last kind's end, taken per pass from the kernel trace
     trace = os.path.join(src, "trace", "trace_kernel_trace.csv")
     if hot and os.path.exists(trace):
@@ -81,7 +81,9 @@ def main(src: str, dst: str) -> None:
         traffic = {"fetch_bytes": 2 * pmc["FETCH_SIZE"] * 1024, "write_bytes": pmc["WRITE_SIZE"] * 1024}
         traffic["total_bytes"] = traffic["fetch_bytes"] + traffic["write_bytes"]
     summary = {"hot_kernel": hot, "kernels": kernels, "pmc_per_dispatch": pmc, "hbm_traffic_per_launch": traffic}
-    if hot and "GRBM_GUI_ACTIVE" in pmc:
+    if hot and "GRBM_GUI_ACTIVE" in pmc and len(hot["parts"]) == 1:
+        # GRBM_GUI_ACTIVE counts GPU-busy cycles of each of the 8 XCDs over the dispatch; with more than one
+        # concurrent launch per pass (two streams) the per-dispatch counts overlap in time and no clock follows
         summary["effective_clock_ghz"] = pmc["GRBM_GUI_ACTIVE"] / 8 / hot["avg_ns"]
     with open(os.path.join(dst, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
