@@ -750,8 +750,7 @@ __device__ __forceinline__ int kg_kofs(int i) { return (i >> 1) * 512 + (i & 1) 
 // 128-column segment).  Pod rows are wave-uniform scalar loads.  UNR: a whole chunk, unrolled, so every
 // LDS address and lane select is an immediate.  LAU: the chunk's pods share one EstimatePod, whose LoadAware
 // sums are lsum[] (per node); otherwise they are evaluated per pair from la[].
-template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool UNR, bool LAU,
-          bool WMAX = false>
+template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool FULL, bool W1, bool UNR, bool LAU>
 __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &d, const ClsNode<NC, NF> (&n)[2],
                                          const ClsLa (&la)[2], const unsigned long long (&okm)[2],
                                          const uint32_t (&lsum)[2], int np_rt, const uint32_t (&kb)[2], uint32_t *kbuf,
@@ -807,12 +806,7 @@ __device__ __forceinline__ void cls_pods(const kg_consts &c, const kg_cls_desc &
             s01 = s[0] | (s[1] << 16);
             if (OUT) put_lane2(mb[0], mb[1], 1ull << i, m[0], m[1]);
         }
-        if constexpr (WMAX) {   // the wave's key of the pod (kbuf: the wave's 8 slots)
-            const uint32_t wm = wave_max_u32(kmax);
-            if (lane == 0) kbuf[i] = wm;
-        } else {
-            kbuf[kg_kofs(i) + tid] = kmax;
-        }
+        kbuf[kg_kofs(i) + tid] = kmax;
         if (OUT) {
             // the wave's 128-column score segment of this pod, written out per chunk
             sst[i * 128 + lane] = (uint16_t)s01;
@@ -967,30 +961,26 @@ __device__ __forceinline__ void cls_block(const kg_consts &c, const kg_planes &p
 // whose class rows are equal have equal output rows on every node, so a work item evaluates each distinct row
 // once against its tile and writes the result to every pod of that row.  One workgroup = one 1024-node tile ×
 // a run of the part's pods, grouped by row (w.begin..w.end); its distinct rows are walked in chunks of
-// KG_EVAL3_CC through cls_pods' mixed form (each wave stages its 128-column score segments, ballot words and
-// wave-max keys of the chunk's rows in LDS), one barrier, then the pods of the chunk's rows are dealt to the
-// waves: per pod the tile's 2 KiB score row as two contiguous 1 KiB wave stores assembled from the 8 waves'
-// segments, its 128-B feasibility row by 8 lanes, its (pod, tile) key by one.  The stage is double-buffered,
-// so chunk c + 1 is evaluated while other waves still store chunk c.  The work is store-bound: per pod and tile
-// 2 KiB + 128 B + 4 B against ~1/60 of a pod's evaluation.
-#define KG_DUP_STAGE_DW ((KG_TILE / 128) * KG_EVAL3_CC * 128 / 2)   // one buffer: [wave][row][128 u16]
+// KG_EVAL3_CC through cls_pods' mixed form, then each wave writes its 128-column score segment of every pod of
+// the chunk's rows from the LDS stage (16 lanes × 16 B per pod, 4 pods per wave store), the feasibility words by
+// lane permutes of the rows' ballot words, and the reducing wave the (pod, tile) key of every pod.  The work is
+// store-bound: per pod and tile 2 KiB of scores + 128 B of mask + 4 B of key against ~1/60 of a pod's compute.
 template <int NC, int NF, bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1>
 __device__ __forceinline__ void cls_block_dup(const kg_consts &c, const kg_planes &pl, const HotArgs &a, const kg_cls_desc &d,
                                               const kg_cls_work &w, const char *__restrict__ rows_base,
                                               const int32_t *__restrict__ ids, uint64_t *__restrict__ mask,
                                               uint16_t *__restrict__ scores, uint32_t *__restrict__ partials,
-                                              uint32_t *stage, uint4 *mstage, uint32_t *kw, int32_t *lid, uint16_t *lux,
-                                              int32_t *cst) {
+                                              uint32_t *kbuf, int32_t *lid, uint16_t *lux, int32_t *cst, uint16_t *sstage,
+                                              uint4 *mstage) {
     constexpr int CC = KG_EVAL3_CC;
-    constexpr int NW = KG_TILE / 128;     // waves of the workgroup (128 columns each)
+    constexpr int BT = KG_TILE / 2;
     constexpr int SEGW = 128;
-    static_assert(CC == 8 && NW == 8, "8 rows per chunk, 8 waves");
+    static_assert(CC == 8 && BT == 512, "the key reduction maps one wave's lanes to 8 rows × 8 lanes");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tile = a.tile_begin + w.tile;
-    const int64_t tile_base = (int64_t)tile * KG_TILE;
-    const int64_t wave_base = tile_base + wave * SEGW;
+    const int64_t wave_base = (int64_t)tile * KG_TILE + wave * SEGW;
     ClsNode<NC, NF> n[2];
     ClsLa la[2];
     unsigned long long okm[2];
@@ -1003,11 +993,15 @@ __device__ __forceinline__ void cls_block_dup(const kg_consts &c, const kg_plane
         full_l = full_l && (n[j].w == (1u << d.fit_shift) || wave_base + 64 * j + lane >= a.node_end);
     }
     const bool full = !FIT_ON || __all(full_l);
-    const int64_t tcol0 = tile_base - a.col_begin;   // the tile's first output column
+    const int64_t col0 = wave_base - a.col_begin;
+    bool seg[2];
     uint32_t kb[2];
     const uint32_t local0 = (uint32_t)(wave * SEGW + lane);
 #pragma unroll
-    for (int j = 0; j < 2; j++) kb[j] = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0 - 64u * j;
+    for (int j = 0; j < 2; j++) {
+        seg[j] = col0 + 64 * j < a.score_stride;
+        kb[j] = (1u << KG_TILE_SHIFT) + (KG_TILE - 1) - local0 - 64u * j;
+    }
     // the item's pods (output rows) and their row indices relative to the item's first row go to LDS
     const int nm = w.end - w.begin;
     const int32_t *uxs = ids + d.ux_first + w.begin;
@@ -1027,61 +1021,83 @@ __device__ __forceinline__ void cls_block_dup(const kg_consts &c, const kg_plane
     if (tid == 0) cst[(nu + CC - 1) / CC] = nm;
     __syncthreads();
     const kg_pod_cls_t<NC, NF> *grows = reinterpret_cast<const kg_pod_cls_t<NC, NF> *>(rows_base + d.rows_offset) + u_first;
+    uint16_t *sst = sstage + wave * (CC * SEGW);
     const uint32_t lsum[2] = {0u, 0u};
-    // this lane's part of a 1 KiB half of a score row: wave segment sw (+ 4 for the second half), 16 B s16
-    const int sw = lane >> 4, s16 = lane & 15;
     int ci = 0;
     for (int u0 = 0; u0 < nu; u0 += CC, ci++) {
         const int np = min(CC, nu - u0);
-        const int buf = ci & 1;
-        uint16_t *sst = reinterpret_cast<uint16_t *>(stage + buf * KG_DUP_STAGE_DW) + wave * (CC * SEGW);
-        uint32_t *kcur = kw + (buf * NW + wave) * CC;
+        uint32_t *kcur = kbuf + (ci & 1) * KG_KBUF_DW;
         unsigned long long mb[2] = {0ull, 0ull};
 #define KG_CLS_PODS(FULL_, UNR_)                                                                                \
-    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, UNR_, false, true>(c, d, n, la, okm, lsum, np, kb, kcur, mb, \
-                                                                             sst, grows + u0)
+    cls_pods<NC, NF, MOST, FIT_ON, LA_ON, OUT, FULL_, W1, UNR_, false>(c, d, n, la, okm, lsum, np, kb, kcur, mb, sst, \
+                                                                       grows + u0)
         if (full && np == CC) KG_CLS_PODS(true, true);
         else if (full) KG_CLS_PODS(true, false);
         else KG_CLS_PODS(false, false);
 #undef KG_CLS_PODS
-        if (OUT && lane < CC) mstage[(buf * CC + lane) * NW + wave] = uint4{(uint32_t)mb[0], (uint32_t)(mb[0] >> 32),
-                                                                           (uint32_t)mb[1], (uint32_t)(mb[1] >> 32)};
-        lds_barrier();
-        // the chunk's keys: lane u < np takes row u's max over the waves
-        uint32_t rk = 0;
-        if (lane < CC) {
-#pragma unroll
-            for (int v = 0; v < NW; v++) rk = max(rk, kw[(buf * NW + v) * CC + lane]);
-        }
         const int m0 = cst[ci], m1 = cst[ci + 1];
-        const uint4 *st4 = reinterpret_cast<const uint4 *>(stage + buf * KG_DUP_STAGE_DW);
-        for (int m = m0 + wave; m < m1; m += NW) {
-            const int u = __builtin_amdgcn_readfirstlane(lux[m] - u0);
-            const int32_t row = __builtin_amdgcn_readfirstlane(lid[m]);
-            if (OUT) {
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                uint16_t *srow = scores + (int64_t)row * a.score_stride + tcol0;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int seg = 4 * h + sw;   // wave segment of 128 columns
-                    const int64_t col = seg * SEGW + s16 * 8;
-                    if (tcol0 + col < a.score_stride) {   // ragged shard end: whole 64-column halves only
-                        const uint4 v = st4[(seg * CC + u) * (SEGW / 8) + s16];
-                        __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(srow + col));
-                    }
+        if (OUT) {
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const int s8 = lane & 15;
+            const bool segs = s8 < 8 ? seg[0] : seg[1];
+            // 16 lanes × 16 B = one pod's 128 columns: 4 pods per wave store
+            for (int m = m0; m < m1; m += 4) {
+                const int mm = m + (lane >> 4);
+                if (mm < m1 && segs) {
+                    const int u = lux[mm] - u0;
+                    const uint4 v = *reinterpret_cast<const uint4 *>(sst + u * SEGW + s8 * 8);
+                    const int64_t off = (int64_t)lid[mm] * a.score_stride;
+                    // non-temporal: whole 256-B segments stream past L2 (plain stores: 0.65 vs 0.42 ms per pass, r05)
+                    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(scores + off + col0 + s8 * 8));
                 }
-                if (lane < NW) {   // words 2·lane, 2·lane + 1 of the tile's 16
-                    const int64_t c0 = tcol0 + lane * SEGW;
-                    if (c0 < a.score_stride) {
-                        const uint4 v = mstage[(buf * CC + u) * NW + lane];
-                        uint64_t *mw = mask + (int64_t)row * a.mask_words + (c0 >> 6);
+            }
+            // the chunk rows' ballot words, [buffer][row][wave]: each pod's 128-B feasibility line is written whole
+            // after the barrier
+            if (lane < CC) mstage[((ci & 1) * CC + lane) * 8 + wave] = uint4{(uint32_t)mb[0], (uint32_t)(mb[0] >> 32),
+                                                                            (uint32_t)mb[1], (uint32_t)(mb[1] >> 32)};
+        }
+        // as cls_block: one barrier per chunk, a rotating reducer wave, double-buffered keys
+        lds_barrier();
+        if (OUT) {
+            // each pod's 128-B feasibility line of the tile (8 lanes × 16 B), 8 pods per wave store, the groups of 8
+            // pods dealt to the waves; plain stores: the lines merge in L2 (non-temporal 128-B lines: 0.57 vs 0.41 ms
+            // per pass, r05; 16-B pieces per wave and pod: 0.41 vs 0.407 ms)
+            const int sub = lane >> 3, wl = lane & 7;   // pod of the group, wave segment of the line
+            const int64_t c0 = (wave_base - wave * SEGW - a.col_begin) + wl * SEGW;   // tile column of segment wl
+            for (int m = m0 + wave * 8; m < m1; m += 64) {
+                const int mm = m + sub;
+                if (mm < m1 && c0 < a.score_stride) {
+                    const uint4 v = mstage[((ci & 1) * CC + (lux[mm] - u0)) * 8 + wl];
+                    uint64_t *mw = mask + (int64_t)lid[mm] * a.mask_words + (c0 >> 6);
+                    if (c0 + 64 < a.score_stride) {
+                        *reinterpret_cast<uint4 *>(mw) = v;
+                    } else {
                         mw[0] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-                        if (c0 + 64 < a.score_stride) mw[1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
                     }
                 }
             }
-            const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)rk, u);
-            if (lane == 0) partials[(int64_t)row * a.tiles_total + tile] = k;
+        }
+        if (wave == ci % (BT / 64)) {
+            const int p = lane >> 3, q = lane & 7;
+            const uint4 *src = reinterpret_cast<const uint4 *>(kcur + kg_kofs(p)) + q;
+            uint32_t mx = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const uint4 v = src[8 * k];
+                mx = max(mx, max(max(v.x, v.y), max(v.z, v.w)));
+            }
+            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x141, 0xf, 0xf, false));  // row_half_mirror
+            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
+            mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+            // every lane of row p's group holds its key; pod m + l takes lane 8u's
+            for (int m = m0; m < m1; m += 64) {
+                const int mm = m + lane;
+                const int u = mm < m1 ? lux[mm] - u0 : 0;
+                const uint32_t k = (uint32_t)__builtin_amdgcn_ds_bpermute(u << 5, (int)mx);
+                if (mm < m1) partials[(int64_t)lid[mm] * a.tiles_total + tile] = k;
+            }
         }
     }
 }
@@ -1090,25 +1106,26 @@ __device__ __forceinline__ void cls_block_dup(const kg_consts &c, const kg_plane
 // tile, dealt to the XCDs in contiguous ranges (workgroup b runs on XCD b % 8 and takes item (b % 8) · per + b / 8),
 // so the items of one tile run on one XCD and its L2 serves the tile's node planes to all of them.
 template <bool MOST, bool FIT_ON, bool LA_ON, bool OUT, bool W1, int KIND>
-__global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? 8 : KIND == 2 ? 5 : 4))) void k_eval3_dup(kg_consts c, kg_planes pl, HotArgs a,
+__global__ __launch_bounds__(KG_TILE / 2) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? KG_EVAL3_WPE0 : KIND == 2 ? 5 : 4))) void k_eval3_dup(kg_consts c, kg_planes pl, HotArgs a,
                                                         const kg_cls_desc *__restrict__ descs,
                                                         const kg_cls_work *__restrict__ work, int32_t n_items,
                                                         const char *__restrict__ rows, const int32_t *__restrict__ ids,
                                                         uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
                                                         uint32_t *__restrict__ partials) {
-    constexpr int CC = KG_EVAL3_CC, NW = KG_TILE / 128;
-    __shared__ __attribute__((aligned(16))) uint32_t stage[OUT ? 2 * KG_DUP_STAGE_DW : 4];
-    __shared__ uint4 mstage[OUT ? 2 * CC * NW : 1];
-    __shared__ uint32_t kw[2 * NW * CC];
+    constexpr int CC = KG_EVAL3_CC, BT = KG_TILE / 2;
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[2 * KG_KBUF_DW];
+    static_assert(CC * BT <= 4096, "a chunk's keys fit the key buffer");
     __shared__ int32_t lid[KG_CLS_ITEM_MAX];
     __shared__ uint16_t lux[KG_CLS_ITEM_MAX];
     __shared__ int32_t cst[KG_CLS_ITEM_MAX / CC + 1];
+    __shared__ __attribute__((aligned(16))) uint16_t sstage[OUT ? (BT / 64) * CC * 128 : 8];
+    __shared__ uint4 mstage[2 * CC * 8];
     const int per = (int)(gridDim.x / KG_XCDS);
     const int item = (int)(blockIdx.x % KG_XCDS) * per + (int)(blockIdx.x / KG_XCDS);
     if (item >= n_items) return;   // grid padded to a multiple of 8; block-uniform
     const kg_cls_work w = work[item];
     const kg_cls_desc d = descs[w.cls];
-#define KG_CLS_ARGS c, pl, a, d, w, rows, ids, mask, scores, partials, stage, mstage, kw, lid, lux, cst
+#define KG_CLS_ARGS c, pl, a, d, w, rows, ids, mask, scores, partials, kbuf, lid, lux, cst, sstage, mstage
     if constexpr (KIND == 0) cls_block_dup<2, 2, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
     else if constexpr (KIND == 1) cls_block_dup<2, 4, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
     else if constexpr (KIND == 2) cls_block_dup<4, 2, MOST, FIT_ON, LA_ON, OUT, W1>(KG_CLS_ARGS);
@@ -2436,7 +2453,9 @@ struct kg_engine {
     std::unordered_map<int32_t, CpuTable> cpu_tab;
     std::vector<uint8_t> pod_may_bind;   // bit 0: binds by its own PreFilter; bit 1: a cpu request (node policy)
     bool profiling = false;
-    int64_t cls_target_blocks = 2048;   // k_eval3 work items per class part ≈ this / tiles (r03 A/B: 1024-6144)
+    // k_eval3 work items per class part ≈ these / tiles: the plain form (r03 A/B: 1024 / 2048 / 3072 0.78 ms,
+    // 4096 / 6144 0.80 ms), the duplicate-row form (r05 A/B: 4096 / 8192 0.407 ms, 2048 0.424, 1024 0.427)
+    int64_t cls_target_blocks = 2048, cls_dup_target_blocks = 4096;
     // the class kinds' launches on two streams (the mixed form on stream2), so one grid's tail is filled by the
     // other's workgroups (r03 A/B: 0.84 vs 0.87 ms per config-2 pass)
     hipStream_t stream2 = nullptr;
@@ -2825,7 +2844,7 @@ kg_status cls_layout(kg_engine *e, int64_t width, int64_t shard_tiles) {
             for (size_t c = 0; c < descs.size(); c++) {
                 if (descs[c].kind != kind || e->cls_reps[c].empty()) continue;
                 const int32_t cnt = descs[c].count;
-                const int32_t ppb = pods_per_block_for(cnt, shard_tiles, e->cls_target_blocks);
+                const int32_t ppb = pods_per_block_for(cnt, shard_tiles, e->cls_dup_target_blocks);
                 const int32_t n_it = (cnt + ppb - 1) / ppb;
                 runs.emplace_back((int32_t)c, (cnt + n_it - 1) / n_it);
             }
@@ -3023,8 +3042,11 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
                 e->numa_resident_wgs = (int64_t)dev_cus * (per_cu > 0 ? per_cu : 1);
                 HIP_TRY(e, hipMalloc(&e->numa_queue, sizeof(int32_t)));
             }
+            // queued when the items give every resident wave one at least; else the grid, each wave's 256-node run
+            // split z ways so that the grid covers the resident slots twice (a 70-row distinct batch of config 3:
+            // 98 tiles × 2 pod blocks would otherwise be 196 workgroups for 768 slots)
             const bool queued = e->numa_queue_mode == 2 ||
-                                (e->numa_queue_mode == 1 && (topk || n_items >= 4 * 4 * e->numa_resident_wgs));
+                                (e->numa_queue_mode == 1 && (topk || n_items >= 4 * e->numa_resident_wgs));
             if (queued && n_items < INT32_MAX) {
                 HIP_TRY(e, hipMemsetAsync(e->numa_queue, 0, sizeof(int32_t), e->stream));
                 const int64_t wgs = std::min<int64_t>(e->numa_resident_wgs, (n_items + 3) / 4);
@@ -3032,7 +3054,10 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
                                    e->pods + pod_begin, e->pl.rows, (unsigned long long *)mask, scores, numa_scores,
                                    partials, perm, bm, e->numa_queue, (int32_t)n_items, seg);
             } else {
-                dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), n <= 64 ? 4u : 1u);
+                const int64_t blocks = shard_tiles * ((n + 63) / 64);
+                unsigned z = 1;
+                while (z < KG_NUMA2_NODES / 32 && blocks * z < 2 * e->numa_resident_wgs) z *= 2;
+                dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), z);
                 hipLaunchKernelGGL(k_eval_numa2, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
                                    e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials, perm, bm,
                                    (int32_t *)nullptr, 0, 0);

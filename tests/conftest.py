@@ -20,6 +20,14 @@ def _built():
     """Build the in-tree engine and oracle libraries once (fast no-op when up to date)."""
     from koordinator_amd.build import build_all
     build_all()
+    # torch's HIP runtime (its own copy) first: it does not initialise once the engine library has created a
+    # context in this process, and some GPU tests hand torch tensors to the engine
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
 
 
 def gpu_available() -> bool:
