@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--no-placement", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-distinct", action="store_true", help="skip the config2_distinct section")
+    ap.add_argument("--no-host-outputs", action="store_true", help="skip the host_outputs (pinned, PCIe) section")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0,
                     help="CPU-baseline budget per baseline: one timed run ≈ budget / 6 (warm-up + median of 5)")
     ap.add_argument("--c3-pods", type=int, default=1_000, help="config-3 (NodeNUMAResource) pods; 0 skips it")
@@ -253,6 +254,36 @@ def bench_config2_distinct(args, engine, synth, cfg, node_rows, N, now, dev, str
                         "shipped profile", "kernel": "k_eval3 (plain part)",
             "evals_per_s": round(P * N / dt, 1), "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(k_ms, 4),
             "roofline_frac": round(algo / (k_ms * 1e-3) / HBM_PEAK, 4)}
+
+
+def bench_host_outputs(args, engine, eng, P, N, now, dev):
+    """The drop-in boundary's rate (INTEGRATION.md `Eval`): the config-2 pass with the planes delivered to
+    pinned host memory, the PCIe copy back included — what the Go plugins' PreFilter hook waits for."""
+    import torch
+
+    W = eng.mask_words
+    mask = torch.empty((P, W), dtype=torch.int64, pin_memory=True)
+    scores = torch.empty((P, W * 64, 2), dtype=torch.uint8, pin_memory=True)
+    top1 = torch.empty(P, dtype=torch.int64, pin_memory=True)
+    step = lambda: eng.eval_host(now, mask.data_ptr(), scores.data_ptr(), top1.data_ptr())
+    step()
+    steps = 3
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = (time.perf_counter() - t0) / steps
+    nbytes = mask.numel() * 8 + scores.numel() + top1.numel() * 8
+    step2 = lambda: eng.eval_host(now, 0, 0, top1.data_ptr())
+    step2()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        step2()
+    dt2 = (time.perf_counter() - t1) / steps
+    del mask, scores, top1
+    return {"workload": f"config2: {P} pods x {N} nodes, kg_eval into pinned host buffers (out_on_device = 0)",
+            "planes": {"evals_per_s": round(P * N / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+                       "host_bytes": int(nbytes), "d2h_GB_per_s": round(nbytes / dt / 1e9, 1)},
+            "top1_only": {"evals_per_s": round(P * N / dt2, 1), "ms_per_step": round(dt2 * 1e3, 3)}}
 
 
 def bench_la_extra(args, engine, synth, shipped_profile, dev, stream):
@@ -503,6 +534,10 @@ def main():
     achieved = algo_bytes / (k_ms * 1e-3)
     feasible_pods = int((merged != 0).sum().item())
 
+    host_out = None   # before placement: the same snapshot as the timed steps
+    if not args.no_host_outputs and world == 1:
+        host_out = bench_host_outputs(args, engine, eng, P, N, now, dev)
+
     placement = None
     if not args.no_placement and world == 1:
         eng.load_snapshot(node_rows)
@@ -617,6 +652,7 @@ def main():
                          "algorithmic_bytes_per_launch": int(algo_bytes)},
             "cpu_baseline": cpu_baseline,
             "placement": placement,
+            "host_outputs": host_out,
             "config2_distinct": distinct,
             "config3": config3,
             "config5": config5,

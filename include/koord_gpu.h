@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 9
+#define KG_ABI_VERSION 10
 #define KG_QUOTA_MAX_DEPTH 64 /* longest kg_quota parent chain (cycles are rejected) */
 
 /* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
@@ -679,6 +679,21 @@ kg_status kg_place_chunk_resolve_prev(kg_engine *eng, int64_t now_ns, int32_t po
                                       const uint32_t *partial_dev, int32_t *out_node_dev, int64_t *out_score_dev,
                                       const int32_t *prev_nodes_dev, int32_t n_prev);
 kg_status kg_set_eval_stream(kg_engine *eng, void *hip_stream);
+
+/* Kernel forms the engine picks by batch and snapshot size, forced so that parity tests reach each form on
+ * small clusters (0, the default: chosen by size).  Every form answers identically.
+ *  KG_FORM_PLACE_PIPELINE    kg_place evaluates chunk i + 1 beside chunk i's resolve for every batch (by size:
+ *                            NodeNUMAResource batches, whose chunk evaluation is long)
+ *  KG_FORM_PLACE_SEQUENTIAL  kg_place never pipelines
+ *  KG_FORM_NUMA_QUEUED       NodeNUMAResource matrix launches take the queued work-item form (by size: launches
+ *                            with at least one work item per resident wave, and placement chunks)
+ *  KG_FORM_NUMA_CHUNK_TILE   NodeNUMAResource placement chunks write one key per tile through the matrix kernel
+ *                            (by size: chunks above 16 pods; smaller ones take per-tile top-16 lists) */
+#define KG_FORM_PLACE_PIPELINE 0x1u
+#define KG_FORM_PLACE_SEQUENTIAL 0x2u
+#define KG_FORM_NUMA_QUEUED 0x4u
+#define KG_FORM_NUMA_CHUNK_TILE 0x8u
+kg_status kg_set_forms(kg_engine *eng, uint32_t forms);
 
 /* Reservation cache (KG_PLUGIN_RESERVATION): replaces every reservation slot; a node holds at most
  * KG_MAX_RSV_PER_NODE.  Nodes carrying slots are evaluated on the exact per-pair path with the

@@ -15,7 +15,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
+# kg_set_forms bits (include/koord_gpu.h)
+FORM_PLACE_PIPELINE, FORM_PLACE_SEQUENTIAL, FORM_NUMA_QUEUED, FORM_NUMA_CHUNK_TILE = 0x1, 0x2, 0x4, 0x8
 NUM_RES = 8
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
  RES_EXTENDED) = range(8)
@@ -210,7 +212,7 @@ EXPORTED = [
     "kg_place_chunk_eval", "kg_place_chunk_resolve", "kg_commit", "kg_set_profiling", "kg_eval_kernel_times",
     "kg_rsv_set", "kg_rsv_download", "kg_quota_set", "kg_quota_download", "kg_row_eval_rsv", "kg_row_rsv_restore",
     "kg_snapshot_generation", "kg_cpuset_take", "kg_row_reserve", "kg_cpus_set", "kg_cpus_download",
-    "kg_place_chunk_resolve_prev", "kg_set_eval_stream", "kg_counters_get", "kg_counters_reset",
+    "kg_place_chunk_resolve_prev", "kg_set_eval_stream", "kg_set_forms", "kg_counters_get", "kg_counters_reset",
 ]
 
 _lib = None
@@ -257,7 +259,7 @@ def lib() -> ctypes.CDLL:
         "kg_row_reserve": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
         "kg_cpus_set": (i32, [vp, vp, vp, vp, i32]), "kg_cpus_download": (i32, [vp, i32, vp, i32]),
         "kg_place_chunk_resolve_prev": (i32, [vp, i64, i32, i32, vp, vp, vp, vp, i32]),
-        "kg_set_eval_stream": (i32, [vp, vp]), "kg_counters_get": (i32, [vp, vp]), "kg_counters_reset": (i32, [vp]),
+        "kg_set_eval_stream": (i32, [vp, vp]), "kg_set_forms": (i32, [vp, ctypes.c_uint32]), "kg_counters_get": (i32, [vp, vp]), "kg_counters_reset": (i32, [vp]),
     }
     for name, (res, args) in sig.items():
         if host_only and not hasattr(L, name):

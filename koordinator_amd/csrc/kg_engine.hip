@@ -1281,9 +1281,7 @@ __global__ __launch_bounds__(256) void k_numa_bind_fix(kg_consts c, kg_planes pl
 #define KG_NUMA2_NODES 256
 #define KG_NUMA2_SEG 32   // nodes per work item of the queued form (whole 32-bit halves of the mask words)
 #define KG_NUMA2_SEG_TOPK 8   // ... of a placement chunk (keys only: no mask or score planes)
-#ifndef KG_NUMA2_WPE
-#define KG_NUMA2_WPE 3   // waves per SIMD the register budget is sized for (measurement builds vary it)
-#endif
+#define KG_NUMA2_WPE 3   // waves per SIMD the register budget is sized for (r02 A/B)
 // one wave's run of `npw` nodes from `base` (inside tile `tile`) for the 64 pods of its lanes; npw is a
 // multiple of 32, runs start on a 32-node boundary
 __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &pl, const HotArgs &a,
@@ -1478,9 +1476,7 @@ __device__ unsigned long long pair_key(const kg_consts &c, const kg_planes &pl, 
 // BZ (kg_consts.numa_bz): the launch answers cpusets on NUMA-policy nodes (a call into the cpuset path); the
 // common BZ = false form inlines the whole pair and carries no call, so its register budget is its own
 // (a call would charge it the callee's full-ABI budget: 254 VGPRs + 132 AGPRs, one wave per SIMD)
-#ifndef KG_CHUNK_WPE
 #define KG_CHUNK_WPE 3   // r03 A/B: 9.5k pods/s at 3, 8.5k at 2 (config-3 placement)
-#endif
 template <bool BZ>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_CHUNK_WPE))) void k_eval_numa_chunk(kg_consts c, kg_planes pl, HotArgs a,
                                                          const kg_pod_dev *__restrict__ pods, int32_t shard_tiles,
@@ -1589,9 +1585,7 @@ __device__ __forceinline__ void rsv_entry(const kg_consts &c, const kg_node_row 
 // a raw score is ≤ 100 (kg_rsv_score: a mean of terms ≤ 100) and the preferred node scores 1000, so the
 // maximum is 1000 when a preferred node exists and the largest raw score otherwise.  Entries are read
 // RSV_UNR at a time (independent loads in flight: the passes are latency-bound at one workgroup per pod).
-#ifndef KG_RSV_UNR
 #define KG_RSV_UNR 8
-#endif
 template <int NT>
 __device__ unsigned long long rsv_best_block(const kg_consts &c, const unsigned long long *E, const int64_t *O,
                                              const int32_t *rnode, int32_t n_rn, uint8_t *plane, int64_t col_begin,
@@ -2403,12 +2397,11 @@ struct kg_engine {
     void *eq_mem = nullptr;            // the distinct batch's outputs, then the staging of host outputs
     size_t eq_mem_bytes = 0;
     BatchMasks bm{0, 0};
-    int numa_queue_mode = 1;        // k_eval_numa2's form: 1 queued for large launches, 0 grid (KG_NUMA_QUEUE=0,
-                                    // measurement), 2 queued for every launch (KG_NUMA_QUEUE=2, tests)
+    uint32_t forms = 0;             // kg_set_forms: size-chosen kernel forms forced (KG_FORM_*), 0 = by size
     int64_t numa_resident_wgs = 0;  // resident k_eval_numa2 workgroups of the device (queried at first use)
     int32_t *numa_queue = nullptr;  // its work-item counter
     int32_t numa_chunk_pods = KG_NUMA_CHUNK_PODS;   // placement chunks up to this many pods take k_eval_numa_chunk
-                                                    // (KG_NUMA_CHUNK_PODS=0: k_eval_numa2 for every chunk, measurement)
+                                                    // (0 under KG_FORM_NUMA_CHUNK_TILE: k_eval_numa2 for every chunk)
     bool la_prod = false;           // some pod of the batch scores with the prod-usage variant
     bool pow2 = true;               // every Fit / LoadAware weight sum of the batch is a power of two
     // class-specialised matrix mode (k_eval3): built from the batch in kg_pods_set, laid out for
@@ -2460,9 +2453,7 @@ struct kg_engine {
     // other's workgroups (r03 A/B: 0.84 vs 0.87 ms per config-2 pass)
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int place_pipeline = 1;             // kg_place overlaps chunk i + 1's evaluation with chunk i's resolve: 1 for
-                                        // NodeNUMAResource batches, 2 for every batch, 0 never (KG_PLACE_PIPELINE)
-    hipEvent_t ev_res[3] = {};          // (KG_PLACE_PIPELINE=0 turns it off)
+    hipEvent_t ev_res[3] = {};          // kg_place's pipeline (place_pipelined)
     // Reservation / ElasticQuota (config 5)
     void *rsv_mem = nullptr;            // slots | rfirst | rnode | E | O | M | Mn | G
     kg_reservation *rsv = nullptr;      // slots grouped by node (stable)
@@ -3045,8 +3036,7 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
             // queued when the items give every resident wave one at least; else the grid, each wave's 256-node run
             // split z ways so that the grid covers the resident slots twice (a 70-row distinct batch of config 3:
             // 98 tiles × 2 pod blocks would otherwise be 196 workgroups for 768 slots)
-            const bool queued = e->numa_queue_mode == 2 ||
-                                (e->numa_queue_mode == 1 && (topk || n_items >= 4 * e->numa_resident_wgs));
+            const bool queued = (e->forms & KG_FORM_NUMA_QUEUED) || topk || n_items >= 4 * e->numa_resident_wgs;
             if (queued && n_items < INT32_MAX) {
                 HIP_TRY(e, hipMemsetAsync(e->numa_queue, 0, sizeof(int32_t), e->stream));
                 const int64_t wgs = std::min<int64_t>(e->numa_resident_wgs, (n_items + 3) / 4);
@@ -3229,12 +3219,6 @@ kg_status kg_engine_create(const kg_config *cfg, kg_engine **out) {
         return KG_ERR_HIP;
     }
     e->own_stream = true;
-    const char *ncp = getenv("KG_NUMA_CHUNK_PODS");
-    if (ncp) e->numa_chunk_pods = std::min(atoi(ncp), KG_NUMA_CHUNK_PODS);
-    const char *nq = getenv("KG_NUMA_QUEUE");
-    e->numa_queue_mode = nq ? atoi(nq) : 1;
-    const char *pp = getenv("KG_PLACE_PIPELINE");
-    e->place_pipeline = pp ? atoi(pp) : 1;
     *out = e;
     return KG_OK;
 }
@@ -3927,6 +3911,18 @@ kg_status eval_join(kg_engine *e) {
 
 extern "C" {
 
+kg_status kg_set_forms(kg_engine *e, uint32_t forms) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (forms & ~(KG_FORM_PLACE_PIPELINE | KG_FORM_PLACE_SEQUENTIAL | KG_FORM_NUMA_QUEUED | KG_FORM_NUMA_CHUNK_TILE))
+        return set_err(e, KG_ERR_INVALID_ARG, "unknown kernel form bits 0x%x", forms);
+    if ((forms & KG_FORM_PLACE_PIPELINE) && (forms & KG_FORM_PLACE_SEQUENTIAL))
+        return set_err(e, KG_ERR_INVALID_ARG, "pipelined and sequential placement together");
+    e->forms = forms;
+    e->numa_chunk_pods = (forms & KG_FORM_NUMA_CHUNK_TILE) ? 0 : KG_NUMA_CHUNK_PODS;
+    return KG_OK;
+}
+
 kg_status kg_set_eval_stream(kg_engine *e, void *s) {
     kg_status st = check_engine(e);
     if (st) return st;
@@ -4070,7 +4066,8 @@ kg_status place_impl(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *o
     st = quota_ready(e);   // (before the pipeline: chunk_resolve checks it too, with an evaluation in flight)
     if (st) return st;
     if (!bind_mode && !rsv_args(e).rsv &&
-        (e->place_pipeline == 2 || (e->place_pipeline == 1 && (e->consts.plugins & KG_PLUGIN_NUMA))))
+        !(e->forms & KG_FORM_PLACE_SEQUENTIAL) &&
+        ((e->forms & KG_FORM_PLACE_PIPELINE) || (e->consts.plugins & KG_PLUGIN_NUMA)))
         return place_pipelined(e, now_ns, out_node, out_score, chunk);
     // the placement kernels answer cpusets on NUMA-policy nodes for this batch (kg_consts.numa_bz)
     struct BzScope {

@@ -239,6 +239,19 @@ class Engine:
         out.numa_scores = numa_ptr or None
         _check(nat.lib().kg_eval(self._h, int(now_ns), ctypes.byref(out)), self, "kg_eval")
 
+    def set_forms(self, forms: int) -> None:
+        """Force size-chosen kernel forms (nat.FORM_*; 0 = by size), for parity tests on small clusters."""
+        _check(nat.lib().kg_set_forms(self._h, int(forms)), self, "kg_set_forms")
+
+    def eval_host(self, now_ns: int, mask_ptr: int = 0, scores_ptr: int = 0, top1_ptr: int = 0,
+                  numa_ptr: int = 0, rsv_ptr: int = 0) -> None:
+        """Matrix mode into caller-owned host buffers (e.g. pinned memory): the outputs the Go plugins read
+        (INTEGRATION.md `Eval`), copied back over PCIe before the call returns."""
+        out = nat.EvalOut()
+        out.mask, out.scores, out.top1, out.out_on_device = mask_ptr or None, scores_ptr or None, top1_ptr or None, 0
+        out.numa_scores, out.rsv_scores = numa_ptr or None, rsv_ptr or None
+        _check(nat.lib().kg_eval(self._h, int(now_ns), ctypes.byref(out)), self, "kg_eval")
+
     def place(self, now_ns: int):
         P = self.n_pods
         nodes = np.zeros(P, dtype=np.int32)

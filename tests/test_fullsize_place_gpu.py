@@ -119,6 +119,12 @@ def test_config3_large_batch_plane_sample():
         eng.load_snapshot(engine.build_node_rows(cfg, cl))
         eng.set_pods(engine.build_pod_rows(cfg, cl, np.arange(P)))
         res = eng.eval(cl.now_ns)
+    # every pod through its raw-spec group, then a direct sample
+    from test_fullsize_gpu import _oracle_rows, check_planes_by_group, spec_groups
+    check_planes_by_group(spec_groups(cl, P),
+                          lambda reps: _oracle_rows(lambda i: oracle.eval_matrix3(cfg, cl, i, cl.now_ns), reps), res, N,
+                          [lambda r, q: r["scores"][q, :, 0], lambda r, q: r["scores"][q, :, 1],
+                           lambda r, q: r["numa_scores"][q]])
     pods = np.sort(np.random.default_rng(313).choice(P, 32, replace=False))
     with ThreadPoolExecutor(WORKERS) as ex:
         parts = list(ex.map(lambda p: oracle.eval_matrix3(cfg, cl, np.array([p]), cl.now_ns), pods))

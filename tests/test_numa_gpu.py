@@ -31,11 +31,12 @@ def _weights(cfg):
     return int(cfg["weight_fit"]), int(cfg["weight_loadaware"]), int(cfg["weight_numa"])
 
 
-def _check_matrix3(cfg, cl, P, begin=0, end=None, idx=None):
+def _check_matrix3(cfg, cl, P, begin=0, end=None, idx=None, forms=0):
     N = len(cl.nodes)
     end = N if end is None else end
     idx = np.arange(P) if idx is None else idx
     with _engine_for(cfg, cl, idx) as eng:
+        eng.set_forms(forms)
         if (begin, end) != (0, N):
             eng.set_shard(begin, end)
         res = eng.eval(cl.now_ns)
@@ -130,12 +131,11 @@ def test_matrix_numa_huge_zone_memory():
 
 
 @pytest.mark.parametrize("pods,begin,end", [(40, 0, None), (333, 0, None), (97, 1024, 2500)])
-def test_matrix_numa_queued_form(monkeypatch, pods, begin, end):
-    # KG_NUMA_QUEUE=2: k_eval_numa2's queued form (32-node work items from a device counter, half mask
-    # words) on launches the default keeps on the grid form — the full-size launches take it by default
-    monkeypatch.setenv("KG_NUMA_QUEUE", "2")
-    cl = make_numa_edge_cluster(2_500, pods, seed=21 + pods)
-    _check_matrix3(numa_config(), cl, pods, begin=begin, end=end)
+def test_matrix_numa_queued_form(pods, begin, end):
+    # KG_FORM_NUMA_QUEUED: k_eval_numa2's queued form (32-node work items from a device counter, half mask
+    # words) on launches the size rule keeps on the grid form — the full-size launches take it by default
+    _check_matrix3(numa_config(), make_numa_edge_cluster(2_500, pods, seed=21 + pods), pods, begin=begin, end=end,
+                   forms=nat.FORM_NUMA_QUEUED)
 
 
 @pytest.mark.parametrize("case", SCORE["cases"], ids=lambda c: c["name"])
@@ -170,13 +170,13 @@ def test_kat_amplified_filter(case):
 
 
 @pytest.mark.parametrize("chunk,numa2", [(1, False), (16, False), (64, False), (1, True), (16, True)])
-def test_placement_numa_matches_sequential_cycle(monkeypatch, chunk, numa2):
-    if numa2:   # every chunk through k_eval_numa2's queued form (one key per tile) instead of k_eval_numa_chunk
-        monkeypatch.setenv("KG_NUMA_CHUNK_PODS", "0")
+def test_placement_numa_matches_sequential_cycle(chunk, numa2):
     cl = make_numa_edge_cluster(700, 200, seed=21)
     cfg = numa_config(weight_numa=2, place_chunk=chunk)
     idx = np.arange(200)
     with _engine_for(cfg, cl, idx) as eng:
+        if numa2:   # every chunk through k_eval_numa2's queued form (one key per tile) instead of k_eval_numa_chunk
+            eng.set_forms(nat.FORM_NUMA_CHUNK_TILE)
         nodes, scores = eng.place(cl.now_ns)
         after = eng.download()
     ref_n, ref_s = oracle.schedule(cfg, cl, idx, cl.now_ns)

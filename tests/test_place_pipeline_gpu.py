@@ -1,7 +1,7 @@
 """kg_place's pipeline (chunk i + 1 evaluated while chunk i commits; its resolve re-scores chunk i's nodes)
 forced on and off, on clusters small enough that consecutive chunks keep choosing the same nodes — the case
 where a stale key of a node chunk i committed could win if the re-score were missing.  Both NodeNUMAResource
-chunk forms (k_eval_numa_chunk's top-16 lists and k_eval_numa2's one key per tile, KG_NUMA_CHUNK_PODS=0) and
+chunk forms (k_eval_numa_chunk's top-16 lists and k_eval_numa2's one key per tile, KG_FORM_NUMA_CHUNK_TILE) and
 the Fit + LoadAware chunk kernel; placements and scores against the oracle's sequential cycle, node rows
 against the host replay."""
 import numpy as np
@@ -27,16 +27,15 @@ def _replay(cfg, cl, idx, nodes):
 @pytest.mark.parametrize("chunk_form", ["topk", "tile_key"])
 @pytest.mark.parametrize("pipeline", ["1", "0"])
 @pytest.mark.parametrize("n_nodes", [1024, 2000])
-def test_numa_place_pipeline_on_off(n_nodes, pipeline, chunk_form, monkeypatch):
-    monkeypatch.setenv("KG_PLACE_PIPELINE", pipeline)
-    if chunk_form == "tile_key":
-        monkeypatch.setenv("KG_NUMA_CHUNK_PODS", "0")
+def test_numa_place_pipeline_on_off(n_nodes, pipeline, chunk_form):
+    forms = (0 if pipeline == "1" else nat.FORM_PLACE_SEQUENTIAL) | (nat.FORM_NUMA_CHUNK_TILE if chunk_form == "tile_key" else 0)
     P = 240
     cl = synth.make_numa_cluster(n_nodes, P, seed=91 + n_nodes)
     cfg = shipped_profile()
     cfg["enabled_plugins"] |= nat.PLUGIN_NUMA
     idx = np.arange(P)
     with engine.Engine(cfg) as eng:
+        eng.set_forms(forms)
         eng.load_snapshot(engine.build_node_rows(cfg, cl))
         eng.set_pods(engine.build_pod_rows(cfg, cl, idx))
         nodes, scores = eng.place(cl.now_ns)
@@ -52,15 +51,15 @@ def test_numa_place_pipeline_on_off(n_nodes, pipeline, chunk_form, monkeypatch):
 
 
 @pytest.mark.parametrize("pipeline", ["2", "0"])
-def test_fit_loadaware_place_pipeline_on_off(pipeline, monkeypatch):
-    """The Fit + LoadAware batch takes the sequential form by default; forced on (KG_PLACE_PIPELINE=2), the
+def test_fit_loadaware_place_pipeline_on_off(pipeline):
+    """The Fit + LoadAware batch takes the sequential form by default; forced on (KG_FORM_PLACE_PIPELINE), the
     pipeline must agree."""
-    monkeypatch.setenv("KG_PLACE_PIPELINE", pipeline)
     P = 600
     cl = synth.make_cluster(1024, P, seed=93)
     cfg = shipped_profile()
     idx = np.arange(P)
     with engine.Engine(cfg) as eng:
+        eng.set_forms(nat.FORM_PLACE_PIPELINE if pipeline == "2" else 0)
         eng.load_snapshot(engine.build_node_rows(cfg, cl))
         eng.set_pods(engine.build_pod_rows(cfg, cl, idx))
         nodes, scores = eng.place(cl.now_ns)
