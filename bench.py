@@ -554,17 +554,24 @@ def main():
         from koordinator_amd import dist as kdist
         all_rows = global_rows if global_rows is not None else np.concatenate(
             [engine.build_node_rows(cfg, synth.make_cluster(N, 1, seed=2 + 7919 * r)) for r in range(world)])
-        deng = kdist.sharded_engine(cfg, all_rows, pod_rows, dev)
+        native = args.backend == "nccl"   # kg_place_sharded on the engine's own RCCL communicator
+        deng = (kdist.native_engine(cfg, all_rows, pod_rows, dev, stream=stream) if native
+                else kdist.sharded_engine(cfg, all_rows, pod_rows, dev))
         dist.barrier()
         torch.cuda.synchronize(dev)
         tp0 = time.perf_counter()
-        nodes, tot = kdist.place_sharded(deng, now, dev, chunk=kdist.place_chunk_of(cfg))
+        if native:
+            nodes, tot = deng.place_sharded(now)
+        else:   # gloo rehearsal: the Python chunk loop over torch.distributed
+            nodes, tot = kdist.place_sharded(deng, now, dev, chunk=kdist.place_chunk_of(cfg))
         dist.barrier()
         tp1 = time.perf_counter()
         deng.close()
         placement = {"pods": P, "nodes": total, "seconds": round(tp1 - tp0, 6),
                      "pods_placed_per_s": round(P / (tp1 - tp0), 1), "placed": int((nodes >= 0).sum()),
-                     "chunk": int(cfg["place_chunk"]), "mode": f"dist.place_sharded over {world} ranks"}
+                     "chunk": int(cfg["place_chunk"]),
+                     "mode": (f"kg_place_sharded over {world} ranks (RCCL)" if native
+                              else f"dist.place_sharded over {world} ranks ({args.backend})")}
 
     cpu_baseline = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 10
+#define KG_ABI_VERSION 11
 #define KG_QUOTA_MAX_DEPTH 64 /* longest kg_quota parent chain (cycles are rejected) */
 
 /* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
@@ -657,6 +657,18 @@ kg_status kg_eval(kg_engine *eng, int64_t now_ns, const kg_eval_out *out);
  * Pods that may bind a cpuset end their device chunk; their Reserve takes the CPUs on the host
  * (kg_cpus_set tables) before the next chunk is evaluated. */
 kg_status kg_place(kg_engine *eng, int64_t now_ns, int32_t *out_node, int64_t *out_score);
+
+/* Native multi-GPU placement: one engine per GPU, each holding the whole (replicated) snapshot and
+ * restricted to its node shard (kg_set_shard).  kg_comm_unique_id (one rank) makes the RCCL id every rank passes
+ * to kg_comm_init (librccl is loaded on first use; KG_ERR_UNSUPPORTED without it).  kg_place_sharded is kg_place
+ * over the shards: per chunk each rank evaluates its tiles, the chunk's per-(pod, tile) partial keys are merged
+ * with one ncclAllReduce(max) on the engine stream (beside the resolve in the pipelined form), and every rank runs
+ * the same resolve and host Reserve steps (cpusets included) on identical inputs, so the replicas stay identical
+ * and the placements equal kg_place's.  Every rank calls it with the same batch; outputs as kg_place. */
+#define KG_COMM_ID_BYTES 128
+kg_status kg_comm_unique_id(void *out /* KG_COMM_ID_BYTES */);
+kg_status kg_comm_init(kg_engine *eng, int32_t rank, int32_t world, const void *unique_id);
+kg_status kg_place_sharded(kg_engine *eng, int64_t now_ns, int32_t *out_node, int64_t *out_score);
 
 /* Multi-GPU building blocks of kg_place (see koordinator_amd/dist.py); pods that bind cpusets are refused
  * here (KG_ERR_UNSUPPORTED: the sharded resolve has no host Reserve step):

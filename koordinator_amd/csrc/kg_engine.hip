@@ -21,7 +21,9 @@
 // a tile's partial is still exact if its best node was not touched by an earlier pod of the
 // chunk; touched nodes are re-scored; tiles whose best node was touched are re-scanned; the
 // winner is committed to the canonical row and its planes re-derived on the device.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -2472,6 +2474,8 @@ struct kg_engine {
     uint8_t *gate = nullptr;            // [pods] ElasticQuota PreFilter outcome (matrix mode)
     kg_counters ctr{};                  // kg_counters_get
     int64_t ev_acc = 0;                 // profiled launches already summed into ctr.kernel_ns
+    ncclComm_t comm = nullptr;          // kg_comm_init: this rank's RCCL communicator (kg_place_sharded)
+    int32_t comm_rank = 0, comm_world = 0;
     hipStream_t eval_stream = nullptr;  // kg_set_eval_stream (kg_place_chunk_eval), nullptr ⇒ stream
     hipEvent_t ev_eval = nullptr;       // recorded on eval_stream after each kg_place_chunk_eval; the chunk resolve
                                         // entries make the engine stream wait on its latest record
@@ -2480,6 +2484,39 @@ struct kg_engine {
     int64_t ev_count = 0;               // launches recorded since kg_set_profiling
     std::string err;
 };
+
+// RCCL, loaded on first use (kg_comm_*): the engine library does not depend on it otherwise
+namespace {
+struct Rccl {
+    bool tried = false;
+    void *h = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+};
+Rccl &rccl() {
+    static Rccl r;
+    if (r.tried) return r;
+    r.tried = true;
+    for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+        r.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+        if (r.h) break;
+    }
+    if (!r.h) return r;
+    r.get_unique_id = (decltype(r.get_unique_id))dlsym(r.h, "ncclGetUniqueId");
+    r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(r.h, "ncclCommInitRank");
+    r.all_reduce = (decltype(r.all_reduce))dlsym(r.h, "ncclAllReduce");
+    r.comm_destroy = (decltype(r.comm_destroy))dlsym(r.h, "ncclCommDestroy");
+    r.error_string = (decltype(r.error_string))dlsym(r.h, "ncclGetErrorString");
+    if (!r.get_unique_id || !r.comm_init_rank || !r.all_reduce || !r.comm_destroy || !r.error_string) {
+        dlclose(r.h);
+        r.h = nullptr;
+    }
+    return r;
+}
+}  // namespace
 
 namespace {
 
@@ -3237,6 +3274,7 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->gate) (void)hipFree(e->gate);
     if (e->numa_perm) (void)hipFree(e->numa_perm);
     if (e->numa_queue) (void)hipFree(e->numa_queue);
+    if (e->comm) (void)rccl().comm_destroy(e->comm);
     if (e->eq_pods) (void)hipFree(e->eq_pods);
     if (e->eq_perm) (void)hipFree(e->eq_perm);
     if (e->eq_of) (void)hipFree(e->eq_of);
@@ -3967,7 +4005,10 @@ namespace {
 // skipped and they are re-scored exactly, while every other node's key is exact (its planes did not change).
 // Partial buffers alternate; a buffer is rewritten only after the resolve that read it (eval i + 2 waits for
 // resolve i).  Not used with reservations (one entry buffer) or cpuset pods (host Reserve between chunks).
-kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score, int32_t chunk) {
+kg_status merge_partials(kg_engine *e, uint32_t *part, int32_t n, hipStream_t s);
+
+kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score, int32_t chunk,
+                          bool merge = false) {
     const int32_t P = e->n_pods;
     const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS;
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
@@ -4002,6 +4043,10 @@ kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64
         st = chunk_eval(e, now_ns, b, n, part[i & 1]);
         e->stream = main_s;
         if (st) return fail(st);
+        if (merge) {   // the shards' partials merged beside the resolve (kg_place_sharded)
+            st = merge_partials(e, part[i & 1], n, eval_s);
+            if (st) return fail(st);
+        }
         HIP_TRY(e, hipEventRecord(e->ev_join, eval_s));
         HIP_TRY(e, hipStreamWaitEvent(main_s, e->ev_join, 0));
         st = chunk_resolve(e, now_ns, b, n, part[i & 1], dnode + b, dscore + b, false, i ? dnode + prev_b : nullptr,
@@ -4023,6 +4068,54 @@ kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64
 extern "C" {
 
 kg_status place_impl(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score);
+kg_status place_loop(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score, bool sharded);
+
+kg_status kg_comm_unique_id(void *out) {
+    if (!out) return KG_ERR_INVALID_ARG;
+    Rccl &r = rccl();
+    if (!r.h) return KG_ERR_UNSUPPORTED;
+    ncclUniqueId id;
+    if (r.get_unique_id(&id) != ncclSuccess) return KG_ERR_HIP;
+    memcpy(out, &id, sizeof(id));
+    return KG_OK;
+}
+
+kg_status kg_comm_init(kg_engine *e, int32_t rank, int32_t world, const void *unique_id) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (!unique_id || world < 1 || rank < 0 || rank >= world) return set_err(e, KG_ERR_INVALID_ARG, "bad rank / world");
+    Rccl &r = rccl();
+    if (!r.h) return set_err(e, KG_ERR_UNSUPPORTED, "librccl not found");
+    if (e->comm) {
+        (void)r.comm_destroy(e->comm);
+        e->comm = nullptr;
+    }
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof(id));
+    const ncclResult_t res = r.comm_init_rank(&e->comm, world, id, rank);
+    if (res != ncclSuccess) {
+        e->comm = nullptr;
+        return set_err(e, KG_ERR_HIP, "ncclCommInitRank: %s", r.error_string(res));
+    }
+    e->comm_rank = rank;
+    e->comm_world = world;
+    return KG_OK;
+}
+
+kg_status kg_place_sharded(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score) {
+    const uint64_t resolved0 = e ? e->ctr.resolved : 0;
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (!out_node || !out_score) return set_err(e, KG_ERR_INVALID_ARG, "null outputs");
+    if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised");
+    if (!e->comm) return set_err(e, KG_ERR_STATE, "kg_place_sharded needs kg_comm_init");
+    st = place_loop(e, now_ns, out_node, out_score, true);
+    if (st == KG_OK) {
+        e->ctr.resolved = resolved0 + (uint64_t)e->n_pods;
+        for (int32_t p = 0; p < e->n_pods; p++) e->ctr.placed += out_node[p] >= 0 ? 1u : 0u;
+    }
+    return st;
+}
 
 kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score) {
     const uint64_t resolved0 = e ? e->ctr.resolved : 0;
@@ -4034,14 +4127,37 @@ kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out
     return st;
 }
 
+kg_status place_loop(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score, bool sharded);
+
 kg_status place_impl(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score) {
     kg_status st = check_engine(e);
     if (st) return st;
     if (!out_node || !out_score) return set_err(e, KG_ERR_INVALID_ARG, "null outputs");
     if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised");
     if (e->shard_begin != 0 || e->shard_end != e->n_nodes)
-        return set_err(e, KG_ERR_STATE, "kg_place runs on the whole snapshot; use the chunk API for shards");
-    st = bind_ready(e, true, true);
+        return set_err(e, KG_ERR_STATE, "kg_place runs on the whole snapshot; use kg_place_sharded for shards");
+    return place_loop(e, now_ns, out_node, out_score, false);
+}
+
+}  // extern "C"
+
+namespace {
+// every rank's partial keys of a chunk merged in place (max over ranks: a tile's slots come from one rank, the
+// others hold zeros), on stream s
+kg_status merge_partials(kg_engine *e, uint32_t *part, int32_t n, hipStream_t s) {
+    const size_t count = (size_t)n * (size_t)tiles_total(e) * KG_PARTIAL_SLOTS;
+    const ncclResult_t r = rccl().all_reduce(part, part, count, ncclUint32, ncclMax, e->comm, s);
+    if (r != ncclSuccess) return set_err(e, KG_ERR_HIP, "ncclAllReduce: %s", rccl().error_string(r));
+    return KG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+// kg_place's chunk loop; sharded: this rank evaluates its node shard and the chunk's partial keys are merged over
+// the communicator before the (replicated, identical) resolve and host Reserve steps
+kg_status place_loop(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score, bool sharded) {
+    kg_status st = bind_ready(e, true, true);
     if (st) return st;
     const int32_t P = e->n_pods;
     if (P == 0) return KG_OK;
@@ -4068,7 +4184,7 @@ kg_status place_impl(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *o
     if (!bind_mode && !rsv_args(e).rsv &&
         !(e->forms & KG_FORM_PLACE_SEQUENTIAL) &&
         ((e->forms & KG_FORM_PLACE_PIPELINE) || (e->consts.plugins & KG_PLUGIN_NUMA)))
-        return place_pipelined(e, now_ns, out_node, out_score, chunk);
+        return place_pipelined(e, now_ns, out_node, out_score, chunk, sharded);
     // the placement kernels answer cpusets on NUMA-policy nodes for this batch (kg_consts.numa_bz)
     struct BzScope {
         kg_consts &k;
@@ -4087,6 +4203,10 @@ kg_status place_impl(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *o
                 }
         st = chunk_eval(e, now_ns, b, n, part);
         if (st) return st;
+        if (sharded) {
+            st = merge_partials(e, part, n, e->stream);
+            if (st) return st;
+        }
         st = chunk_resolve(e, now_ns, b, n, part, dnode + b, dscore + b, defer);
         if (st) return st;
         if (defer) {

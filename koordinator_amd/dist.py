@@ -204,6 +204,37 @@ def sharded_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray,
     return eng
 
 
+def native_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, device: torch.device, group=None,
+                  reservations: Optional[np.ndarray] = None, quotas: Optional[np.ndarray] = None,
+                  stream: Optional[torch.cuda.Stream] = None):
+    """A HIP engine holding the full snapshot, restricted to this rank's shard, with its own RCCL communicator
+    over the group (kg_comm_init; rank 0's unique id is broadcast through torch.distributed): the engine then
+    runs the whole sharded placement natively (Engine.place_sharded = kg_place_sharded), the chunk loop, the
+    partial-key ncclAllReduce and the replicated resolve / host Reserve steps in C++."""
+    from .engine import Engine
+
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    cfg = cfg.copy()
+    cfg["device"] = device.index or 0
+    eng = Engine(cfg)
+    if stream is not None:
+        eng.set_stream(stream.cuda_stream)
+    eng.load_snapshot(node_rows)
+    if reservations is not None:
+        eng.set_reservations(reservations)
+    if quotas is not None:
+        eng.set_quotas(quotas)
+    eng.set_pods(pod_rows)
+    begin, end = shard_range(len(node_rows), rank, world)
+    eng.set_shard(begin, end)
+    uid = [Engine.comm_unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0, group=group)
+    eng.comm_init(rank, world, uid[0])
+    return eng
+
+
 def place(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, now_ns: int,
           device: Optional[torch.device] = None, group=None, reservations: Optional[np.ndarray] = None,
           quotas: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:

@@ -239,6 +239,29 @@ class Engine:
         out.numa_scores = numa_ptr or None
         _check(nat.lib().kg_eval(self._h, int(now_ns), ctypes.byref(out)), self, "kg_eval")
 
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """An RCCL unique id for kg_comm_init (one rank makes it, every rank passes it)."""
+        buf = ctypes.create_string_buffer(nat.COMM_ID_BYTES)
+        st = nat.lib().kg_comm_unique_id(buf)
+        if st != 0:
+            raise EngineError(f"kg_comm_unique_id failed ({st})")
+        return buf.raw
+
+    def comm_init(self, rank: int, world: int, unique_id: bytes) -> None:
+        buf = ctypes.create_string_buffer(bytes(unique_id), nat.COMM_ID_BYTES)
+        _check(nat.lib().kg_comm_init(self._h, int(rank), int(world), buf), self, "kg_comm_init")
+
+    def place_sharded(self, now_ns: int):
+        """kg_place over the ranks' node shards (kg_place_sharded): per chunk one ncclAllReduce of the partial
+        keys, the resolve and host Reserve steps replicated.  Same outputs as place()."""
+        P = self.n_pods
+        nodes = np.zeros(P, dtype=np.int32)
+        scores = np.zeros(P, dtype=np.int64)
+        _check(nat.lib().kg_place_sharded(self._h, int(now_ns), nat.ptr(nodes), nat.ptr(scores)), self,
+               "kg_place_sharded")
+        return nodes, scores
+
     def set_forms(self, forms: int) -> None:
         """Force size-chosen kernel forms (nat.FORM_*; 0 = by size), for parity tests on small clusters."""
         _check(nat.lib().kg_set_forms(self._h, int(forms)), self, "kg_set_forms")

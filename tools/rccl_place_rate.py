@@ -1,6 +1,7 @@
-"""Sharded placement over RCCL at world size 1 (GPU box): dist.place_sharded with the partial-key all_reduce
+"""Sharded placement over RCCL at world size 1 (GPU box): the native kg_place_sharded (the chunk loop and the
+partial-key ncclAllReduce in C++, dist.native_engine) and dist.place_sharded with the partial-key all_reduce
 running through the nccl backend (collective=True), pipelined and not, beside kg_place on the same config-2
-batch.  The merge is a real RCCL launch on the eval stream, so the pipelined rate shows what the per-chunk
+batch (a second kg_place run first, for the run-to-run spread).  The merge is a real RCCL launch on the eval stream, so the pipelined rate shows what the per-chunk
 collective costs the sequential cycle when it overlaps the resolve.
 
     python tools/rccl_place_rate.py [pods]
@@ -37,6 +38,22 @@ with engine.Engine(cfg) as eng:
     t_one = time.perf_counter() - t0
 
 out = {"kg_place": P / t_one}
+with engine.Engine(cfg) as eng:
+    eng.load_snapshot(rows)
+    eng.set_pods(pods)
+    eng.sync()
+    t0 = time.perf_counter()
+    eng.place(cl.now_ns)
+    out["kg_place (again)"] = P / (time.perf_counter() - t0)
+for rep in range(2):
+    neng = kdist.native_engine(cfg, rows, pods, dev)
+    neng.sync()
+    t0 = time.perf_counter()
+    nodes, _ = neng.place_sharded(cl.now_ns)
+    dt = time.perf_counter() - t0
+    neng.close()
+    assert np.array_equal(nodes, ref_nodes), "native sharded placements differ from kg_place"
+    out[f"kg_place_sharded (native RCCL, run {rep})"] = P / dt
 for pipeline in (True, False):
     deng = kdist.sharded_engine(cfg, rows, pods, dev)
     kdist.place_sharded(deng, cl.now_ns, dev, chunk=chunk, pipeline=pipeline, collective=True)   # warm-up
