@@ -1981,6 +1981,13 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
 // block max; (B) Reserve, one thread per part, and the committed node's planes.  The next pod's row
 // and tile keys are prefetched while the current pod is resolved.
 
+#ifdef KG_RESOLVE_TIMING   // measurement build: per-pod phase timestamps of k_resolve (thread 0, shader clock)
+__device__ unsigned long long g_rtimes[65536 * 8];
+__device__ int g_rtimes_pod;
+#define KG_RT(k) do { if (threadIdx.x == 0) { const int gp_ = g_rtimes_pod + j; if (gp_ < 65536) g_rtimes[gp_ * 8 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
+#else
+#define KG_RT(k) do { } while (0)
+#endif
 // RSV: the batch has reservation nodes; NUMA: NodeNUMAResource is enabled (separate instantiations: the plain
 // path keeps its register budget)
 template <bool RSV, bool NUMA>
@@ -2074,6 +2081,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     }
     const int np_prev = n_prevt;
     for (int j = 0; j < n; j++) {
+        KG_RT(1);
         const int par = j & 1;
         const kg_pod_dev &pd = lpod[par];
         if (tid == 0)  // ElasticQuota PreFilter on the quota state after every earlier Reserve (read after the sync below)
@@ -2174,6 +2182,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             best = best > k ? best : k;
         }
         __syncthreads();
+        KG_RT(2);
         const int nr = plain_ok ? n_rescan[par] : 0;
         for (int q = tid; q < nr * KG_TILE; q += KG_RESOLVE_THREADS) {
             const int64_t node = (int64_t)rescan[q / KG_TILE] * KG_TILE + (q % KG_TILE);
@@ -2183,6 +2192,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         best = wave_max_u64(best);
         if ((tid & 63) == 0) red[tid >> 6] = best;
         __syncthreads();
+        KG_RT(3);
         // every thread takes the block maximum itself (no broadcast barrier)
         unsigned long long wb = 0;
         for (int q = 0; q < KG_RESOLVE_THREADS / 64; q++) wb = wb > red[q] ? wb : red[q];
@@ -2226,6 +2236,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         }
         if (tid < ROW_U4) reinterpret_cast<uint4 *>(&srow)[tid] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
         __syncthreads();
+        KG_RT(4);
         if (numa_on) {
             // the zone table of the staged row (wave 0), then the zone commit's hint enumeration over it (tid 0)
             const bool zoned = (srow.flags & KG_NODE_NUMA_OPTIONS) && srow.numa_policy != KG_NUMA_NONE &&
@@ -2330,6 +2341,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         // the flags step reads the parts' LDS results only: their global stores (row, planes) complete under
         // the full barrier that ends this pod, before the next pod reads them
         __syncthreads();
+        KG_RT(5);
         if ((numa_on || rsv_on) && ce && tid >= 128 && tid < 128 + ROW_U4)   // the committed row into the node cache
             reinterpret_cast<uint4 *>(&nrow[slot])[tid - 128] = reinterpret_cast<const uint4 *>(&srow)[tid - 128];
         if (tid == 0) {   // kg_finalize_flags from the parts (metric and the static bits are unchanged)
@@ -2355,7 +2367,11 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             }
         }
         __syncthreads();
+        KG_RT(6);
     }
+#ifdef KG_RESOLVE_TIMING
+    if (threadIdx.x == 0) g_rtimes_pod += n;
+#endif
 }
 
 __global__ void k_commit_one(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t pod, int32_t node,
@@ -3948,6 +3964,17 @@ kg_status eval_join(kg_engine *e) {
 }  // namespace
 
 extern "C" {
+
+#ifdef KG_RESOLVE_TIMING
+int32_t kg_debug_resolve_times(unsigned long long *out, int32_t n_pods) {
+    int pods = 0;
+    if (hipMemcpyFromSymbol(&pods, HIP_SYMBOL(g_rtimes_pod), sizeof(int)) != hipSuccess) return -1;
+    if (pods > n_pods) pods = n_pods;
+    if (pods > 65536) pods = 65536;
+    if (pods > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtimes), sizeof(unsigned long long) * 8 * (size_t)pods) != hipSuccess) return -1;
+    return pods;
+}
+#endif
 
 kg_status kg_set_forms(kg_engine *e, uint32_t forms) {
     kg_status st = check_engine(e);
