@@ -189,13 +189,17 @@ struct kg_planes {
 KG_HD int64_t kg_abs64(int64_t x) { return x < 0 ? -x : x; }
 
 // Exact truncating int64 quotient and remainder of n / d (d > 0) — the device has no int64 divide
-// instruction: an fp64 estimate (relative error ≈ 2^-52, so off by ≤ |n/d|·2^-51 + 1) is corrected
-// with exact int64 arithmetic, the residual's own fp64 quotient and a final ±1 step.
-// Valid for |n| < 2^57 and 0 < d < 2^53 (the finalize operands: |100·(a − base)| < 2^57, a < 2^41).
+// instruction: an fp64 estimate n · RN(1/d) (relative error ≤ 3·2^-53, so off by < |n/d|·2^-51.4 + 1 ≤ 49) is
+// corrected with exact int64 arithmetic, the residual's own estimate r0 · RN(1/d) (off from r0/d by < 2^-45.8,
+// less than 1/d: its truncation is exact but at exact integers, where it is low by one) and a final ±1 step.
+// One fp64 division (the reciprocal) instead of two: the placement resolve's Reserve derives its planes through
+// this chain (r05: the LoadAware part 4.0k → Fit part 3.9k cycles per pod were mostly fp64 divisions).
+// Valid for |n| < 2^57 and 0 < d < 2^41 (the finalize operands: |100·(a − base)| < 2^57, a < KG_CAP_LIMIT).
 KG_HD void kg_divmod64_fp(int64_t n, int64_t d, int64_t &q, int64_t &r) {
-    int64_t q0 = (int64_t)((double)n / (double)d);
+    const double inv = 1.0 / (double)d;
+    int64_t q0 = (int64_t)((double)n * inv);
     int64_t r0 = n - q0 * d;
-    const int64_t q1 = (int64_t)((double)r0 / (double)d);
+    const int64_t q1 = (int64_t)((double)r0 * inv);
     q0 += q1;
     r0 -= q1 * d;
     // C truncation: the remainder takes the sign of n and |r| < d

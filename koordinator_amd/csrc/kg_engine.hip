@@ -40,6 +40,7 @@
 
 #define KG_POD_CHUNK 64          // pods between two LDS partial combines in k_eval
 #define KG_RESOLVE_THREADS 512
+#define KG_RESOLVE_LA_T0 448     // k_resolve's LoadAware Reserve threads (wave 7)
 #define KG_CLS_ITEM_MAX 512         // pods per k_eval3 work item (one output-row entry per thread)
 #define KG_MAX_CHUNK KG_PLACE_CHUNK_MAX   // max pods per resolve call (touched-list capacity)
 #define KG_MAX_TILES 4096        // max tiles per snapshot in k_resolve (2M nodes)
@@ -72,12 +73,26 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// the same DPP ladder on 64-bit keys (each half moved by its own v_mov_dpp; old = 0 is the identity of unsigned
+// max): no LDS round trips (the ds_bpermute butterfly it replaces sat on the placement resolve's critical path)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ unsigned long long dpp_max64_step(unsigned long long v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW_MASK, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROW_MASK, 0xf, false);
+    const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+    return v > o ? v : o;
+}
+// max over the 64 lanes, returned wave-uniform
 __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
-    for (int off = 32; off > 0; off >>= 1) {
-        unsigned long long o = __shfl_xor(v, off, 64);
-        v = v > o ? v : o;
-    }
-    return v;
+    v = dpp_max64_step<0x111, 0xf>(v);   // row_shr:1
+    v = dpp_max64_step<0x112, 0xf>(v);   // row_shr:2
+    v = dpp_max64_step<0x114, 0xf>(v);   // row_shr:4
+    v = dpp_max64_step<0x118, 0xf>(v);   // row_shr:8
+    v = dpp_max64_step<0x142, 0xa>(v);   // row_bcast:15
+    v = dpp_max64_step<0x143, 0xc>(v);   // row_bcast:31
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1953,6 +1968,7 @@ __device__ __forceinline__ void rsv_quota_commit(const kg_planes &pl, const RsvA
 // the commit threads themselves, so later pods of the chunk re-score those nodes without a global round
 // trip (the canonical row and the global planes are written as well).
 #define KG_NCACHE 16
+#define KG_TSLOTS 64    // touched tiles with a node bitmask in k_resolve (more: linear compares)
 struct NodeCacheEntry {
     NodeRegs n;          // ok_bits / la_valid are derived at use (they depend on `now`)
     int64_t metric_ns;
@@ -1966,7 +1982,13 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
     const bool expired = (c.plugins & KG_PLUGIN_LOADAWARE) ? kg_metric_expired(c, n.df, ce.metric_ns, now_ns) : false;
     node_regs_status(c, n.df, expired, n);
     uint32_t fit, la, numa = 0;
-    if (!eval_pair(c, pl, p, n, node, now_ns, fit, la)) return 0ull;
+    if (n.df & KGD_SLOW) {   // the exact pair path on the LDS copy of the committed row (its global stores may
+        bool feas;           // still be in flight: the plain resolve orders pods by LDS-only barriers)
+        kg_pair_exact(c, crow, n.df, p, now_ns, feas, fit, la);
+        if (!feas) return 0ull;
+    } else if (!eval_fast(c, p, n, fit, la)) {
+        return 0ull;
+    }
     if (NUMA && (c.plugins & KG_PLUGIN_NUMA)) {
         const uint64_t ns = kg_numa_eval_any(c, crow, p);   // the LDS copy of the canonical row
         if (!(ns >> 32)) return 0ull;
@@ -1982,10 +2004,12 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
 // and tile keys are prefetched while the current pod is resolved.
 
 #ifdef KG_RESOLVE_TIMING   // measurement build: per-pod phase timestamps of k_resolve (thread 0, shader clock)
-__device__ unsigned long long g_rtimes[65536 * 8];
+__device__ unsigned long long g_rtimes[65536 * 16];
 __device__ int g_rtimes_pod;
-#define KG_RT(k) do { if (threadIdx.x == 0) { const int gp_ = g_rtimes_pod + j; if (gp_ < 65536) g_rtimes[gp_ * 8 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
+#define KG_RT_AT(t, k) do { if (threadIdx.x == (t)) { const int gp_ = rt_base + j; if (gp_ < 65536) g_rtimes[gp_ * 16 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
+#define KG_RT(k) KG_RT_AT(0, k)
 #else
+#define KG_RT_AT(t, k) do { } while (0)
 #define KG_RT(k) do { } while (0)
 #endif
 // RSV: the batch has reservation nodes; NUMA: NodeNUMAResource is enabled (separate instantiations: the plain
@@ -2006,14 +2030,18 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     // evaluated — treated as touched (their keys may predate the commit; re-scored like touched nodes)
     __shared__ int32_t prevt[KG_MAX_CHUNK];
     __shared__ int32_t n_prevt;
-    __shared__ uint8_t ttile[KG_MAX_TILES];   // the tile holds a touched node (the key lists of others are exact)
+    // touched tiles (the key lists of the others are exact): ttile[t] = 0 none, s ∈ [1, KG_TSLOTS] the tile's slot in
+    // tbits (a bit per node of the tile: "touched?" is one LDS read), 255 beyond KG_TSLOTS tiles (linear compares)
+    __shared__ uint8_t ttile[KG_MAX_TILES];
+    __shared__ uint32_t tbits[KG_TSLOTS][KG_TILE / 32];
+    __shared__ int32_t n_tslots;
     __shared__ int32_t rescan[KG_MAX_TILES];
     __shared__ unsigned long long red[KG_RESOLVE_THREADS / 64];
     __shared__ int64_t redo[KG_RESOLVE_THREADS / 64];
     // the quota gate and the rescan counter alternate between two slots by pod parity: a pod that
     // commits nothing ends without a barrier, so the next pod must not overwrite what a slower wave of
     // this pod may still read
-    __shared__ int32_t n_touched, n_rescan[2], gate_ok[2];
+    __shared__ int32_t n_touched, n_rescan[2], gate_ok[2], slot_s;
     __shared__ uint32_t fin[KG_NUM_RES + 4];
     __shared__ int32_t fl_pods_full;
     __shared__ uint32_t fl_over[3];
@@ -2027,6 +2055,10 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     static_assert(sizeof(kg_node_row) % 16 == 0 && ROW_U4 <= 64, "rows are staged as 16-byte words by one wave");
     const bool numa_on = NUMA && (c.plugins & KG_PLUGIN_NUMA) != 0;
     const bool rsv_on = RSV && ra.rsv && ra.n_rn > 0;
+    constexpr bool LDSB = !RSV && !NUMA;   // the plain form's pods may end on LDS-only barriers (below)
+#ifdef KG_RESOLVE_TIMING
+    const int rt_base = g_rtimes_pod;
+#endif
     __shared__ int32_t n_slow;
     // Reservation split (ra.M): the entry groups holding a touched reservation node (rsv_best_resolve)
     __shared__ uint8_t gflag[KG_RSV_MAX_GROUPS];
@@ -2060,9 +2092,30 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         n_rescan[0] = n_rescan[1] = 0;
         n_slow = *slow_count;
         n_prevt = 0;
+        n_tslots = 0;
         n_glist = 0;
     }
     for (int t = tid; t < tiles_total; t += KG_RESOLVE_THREADS) ttile[t] = 0;
+    for (int q = tid; q < KG_TSLOTS * (KG_TILE / 32); q += KG_RESOLVE_THREADS) (&tbits[0][0])[q] = 0u;
+    // node marked touched (one thread at a time: the slot allocation is not atomic)
+    auto mark = [&](int32_t node) {
+        const int t = node / KG_TILE;
+        int sl = ttile[t];
+        if (sl == 0) {
+            sl = n_tslots < KG_TSLOTS ? ++n_tslots : 255;
+            ttile[t] = (uint8_t)sl;
+        }
+        if (sl != 255) tbits[sl - 1][(node % KG_TILE) >> 5] |= 1u << (node & 31);
+    };
+    // was `node` (in a tile whose ttile entry is sl) touched by this chunk or the previous one?
+    auto is_touched = [&](int sl, int32_t node, int nt_, int np_) {
+        if (sl == 0) return false;
+        if (sl != 255) return ((tbits[sl - 1][(node % KG_TILE) >> 5] >> (node & 31)) & 1u) != 0;
+        bool hit = false;
+        for (int q = 0; q < nt_; q++) hit |= touched[q] == node;
+        for (int q = 0; q < np_; q++) hit |= prevt[q] == node;
+        return hit;
+    };
     if (rsv_on && ra.M) {
         for (int g = tid; g < ra.ngroups; g += KG_RESOLVE_THREADS) gflag[g] = 0;
         if (n > 0) rsv_prefetch(ra, 0, rpf, tid, KG_RESOLVE_THREADS);
@@ -2075,8 +2128,10 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             const int32_t node = prev_nodes[q];
             if (node < 0) continue;
             prevt[atomicAdd(&n_prevt, 1)] = node;
-            ttile[node / KG_TILE] = 1;
         }
+        __syncthreads();
+        if (tid == 0)
+            for (int q = 0; q < n_prevt; q++) mark(prevt[q]);
         __syncthreads();
     }
     const int np_prev = n_prevt;
@@ -2091,6 +2146,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         if (j + 1 < n && tid >= KG_RESOLVE_THREADS - POD_DW)
             reinterpret_cast<uint32_t *>(&lpod[par ^ 1])[tid - (KG_RESOLVE_THREADS - POD_DW)] =
                 reinterpret_cast<const uint32_t *>(pods + pod_begin + j + 1)[tid - (KG_RESOLVE_THREADS - POD_DW)];
+        KG_RT_AT(KG_RESOLVE_THREADS - 1, 10);
         load_keys(j + 1, knxt);
         unsigned long long best = 0;
         const int nt = n_touched;
@@ -2125,11 +2181,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 const unsigned long long k = decode_partial(kcur[0], t);
                 if (!k) continue;
                 const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
-                bool hit = false;
-                if (ttile[t]) {
-                    for (int q = 0; q < nt; q++) hit |= touched[q] == node;
-                    for (int q = 0; q < np_prev; q++) hit |= prevt[q] == node;
-                }
+                const bool hit = is_touched(ttile[t], node, nt, np_prev);
                 if (hit) rescan[atomicAdd(&n_rescan[par], 1)] = t;
                 else best = best > k ? best : k;
                 continue;
@@ -2139,23 +2191,38 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             // (fully unrolled: the list stays in registers)
             unsigned long long cand = 0;
             bool found = false, ended = false;
-            if (!ttile[t]) {   // no touched node in the tile: its best key stands
+            const int tsl = ttile[t];
+            if (!tsl) {   // no touched node in the tile: its best key stands
                 cand = decode_partial(kcur[0], t);
                 best = best > cand ? best : cand;
                 continue;
             }
+            if (tsl != 255) {
+                // every entry's touched bit read at once (independent LDS reads, one latency), then the first
+                // untouched entry taken; a partial key's low bits are 1023 − the node's tile offset
+                uint32_t tw[KG_TOPK];
 #pragma unroll
-            for (int s = 0; s < KG_TOPK; s++) {
-                const unsigned long long k = decode_partial(kcur[s], t);
-                ended = ended || k == 0;
-                if (!found && !ended) {
-                    const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
-                    bool hit = false;
-                    for (int q = 0; q < nt; q++) hit |= touched[q] == node;
-                    for (int q = 0; q < np_prev; q++) hit |= prevt[q] == node;
-                    if (!hit) {
-                        cand = k;
+                for (int s = 0; s < KG_TOPK; s++) tw[s] = tbits[tsl - 1][(KG_TILE - 1 - (kcur[s] & (KG_TILE - 1))) >> 5];
+#pragma unroll
+                for (int s = 0; s < KG_TOPK; s++) {
+                    const uint32_t loc = KG_TILE - 1 - (kcur[s] & (KG_TILE - 1));
+                    ended = ended || kcur[s] == 0;
+                    if (!found && !ended && !((tw[s] >> (loc & 31)) & 1u)) {
+                        cand = decode_partial(kcur[s], t);
                         found = true;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < KG_TOPK; s++) {
+                    const unsigned long long k = decode_partial(kcur[s], t);
+                    ended = ended || k == 0;
+                    if (!found && !ended) {
+                        const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
+                        if (!is_touched(tsl, node, nt, np_prev)) {
+                            cand = k;
+                            found = true;
+                        }
                     }
                 }
             }
@@ -2163,12 +2230,19 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             if (need) rescan[atomicAdd(&n_rescan[par], 1)] = t;
             else best = best > cand ? best : cand;
         }
+        KG_RT_AT(0, 9);
+        KG_RT_AT(97, 11);
         if (!plain_ok) best = 0;
-        for (int q = tid; q < nt && plain_ok; q += KG_RESOLVE_THREADS) {
-            const unsigned long long k = q < KG_NCACHE ? pair_key_cached<NUMA>(c, pl, pd, ncache[q], nrow[q], touched[q], now_ns)
-                                                       : pair_key<NUMA>(c, pl, pd, touched[q], n_nodes, now_ns);
-            best = best > k ? best : k;
+        // the touched nodes' re-scores on threads 128.. (beside the tile scan of the lower threads, not after it), the
+        // pod row copied to registers first (its fields in LDS would be a chain of dependent reads)
+        if (tid >= 128 && tid - 128 < nt && plain_ok) {
+            for (int q = tid - 128; q < nt; q += KG_RESOLVE_THREADS - 128) {
+                const unsigned long long k = q < KG_NCACHE ? pair_key_cached<NUMA>(c, pl, pd, ncache[q], nrow[q], touched[q], now_ns)
+                                                           : pair_key<NUMA>(c, pl, pd, touched[q], n_nodes, now_ns);
+                best = best > k ? best : k;
+            }
         }
+        KG_RT_AT(128, 8);
         // the previous chunk's nodes, on the upper half of the workgroup (the tile scan and the touched re-scores
         // run on the lower threads: each NodeNUMAResource re-score is a long single-lane chain)
         for (int q = tid - KG_RESOLVE_THREADS / 2; q >= 0 && q < np_prev && plain_ok; q += KG_RESOLVE_THREADS / 2) {
@@ -2178,7 +2252,10 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         // nodes outside the fp64 bounds are not in the lists: re-scored exactly, every pod
         const int ns = (!rescore_slow || !plain_ok) ? 0 : n_slow;
         for (int q = tid; q < ns; q += KG_RESOLVE_THREADS) {
-            const unsigned long long k = pair_key<NUMA>(c, pl, pd, slow_list[q], n_nodes, now_ns);
+            const int32_t sn = slow_list[q];
+            // a slow node the chunk touched is re-scored above (cached: from its LDS row)
+            if (LDSB && sn >= 0 && sn < n_nodes && is_touched(ttile[sn / KG_TILE], sn, nt, 0)) continue;
+            const unsigned long long k = pair_key<NUMA>(c, pl, pd, sn, n_nodes, now_ns);
             best = best > k ? best : k;
         }
         __syncthreads();
@@ -2186,6 +2263,9 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         const int nr = plain_ok ? n_rescan[par] : 0;
         for (int q = tid; q < nr * KG_TILE; q += KG_RESOLVE_THREADS) {
             const int64_t node = (int64_t)rescan[q / KG_TILE] * KG_TILE + (q % KG_TILE);
+            // the chunk's touched nodes are re-scored above (cached: from their LDS rows, whose global stores the
+            // plain form's LDS-only barriers leave unordered)
+            if (LDSB && node < n_nodes && is_touched(ttile[rescan[q / KG_TILE]], (int32_t)node, nt, 0)) continue;
             const unsigned long long k = pair_key<NUMA>(c, pl, pd, node, n_nodes, now_ns);
             best = best > k ? best : k;
         }
@@ -2228,14 +2308,33 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         // the node's canonical row, staged into LDS by one wave (a single coalesced round trip): the
         // Reserve parts below update and re-derive from this copy and store their fields back
         kg_node_row &srow = nrow[KG_NCACHE];
+        // the node's slot in the touched list (and node cache): its position, or the next one — found by wave 0 with
+        // one ballot (a touched list of ≤ 64; longer lists are walked), handed to the other waves through LDS
         uint32_t old_df = 0;
         int64_t old_metric = 0;
-        if (tid == 0) {   // the planes tid 0 needs, in flight with the row
-            old_df = pl.dflags[node];
-            old_metric = pl.metric_ns[node];
+        if (tid < 64) {
+            int sl = nt;
+            if (nt <= 64) {
+                const unsigned long long hit = __ballot(tid < nt && touched[tid] == node);
+                sl = hit ? __builtin_ctzll(hit) : nt;
+            } else {
+                for (int q = 0; q < nt; q++)
+                    if (touched[q] == node) sl = q;
+            }
+            // a node an earlier pod of the chunk committed is staged from its LDS copy (the committed row, flags and
+            // NodeMetric time), the others from global memory
+            const bool cached = sl < nt && sl < KG_NCACHE;
+            if (tid == 0) {   // the planes tid 0 needs, in flight with the row
+                old_df = cached ? ncache[sl].n.df : pl.dflags[node];
+                old_metric = cached ? ncache[sl].metric_ns : pl.metric_ns[node];
+                slot_s = sl;
+            }
+            if (tid < ROW_U4)
+                reinterpret_cast<uint4 *>(&srow)[tid] = cached ? reinterpret_cast<const uint4 *>(&nrow[sl])[tid]
+                                                               : reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
         }
-        if (tid < ROW_U4) reinterpret_cast<uint4 *>(&srow)[tid] = reinterpret_cast<const uint4 *>(pl.rows + node)[tid];
         __syncthreads();
+        const int slot = slot_s;
         KG_RT(4);
         if (numa_on) {
             // the zone table of the staged row (wave 0), then the zone commit's hint enumeration over it (tid 0)
@@ -2256,10 +2355,6 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             // the parts below read only srow (LDS)
             __syncthreads();
         }
-        // the node's slot in the touched list (and node cache): its position, or the next one
-        int slot = nt;
-        for (int q = 0; q < nt; q++)
-            if (touched[q] == node) slot = q;
         NodeCacheEntry *ce = slot < KG_NCACHE ? &ncache[slot] : nullptr;
         // AssumePod / LoadAware deltas and the committed node's derived planes, one thread per part:
         // thread 64 + r owns resource r's fields of the row and its Fit planes, 64 + 8 + r the LoadAware
@@ -2279,35 +2374,59 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             int64_t fr;
             double R, F;
             fin[r] = kg_finalize_fit_r(c, pl, node, srow, r, &fr, &R, &F);
+            KG_RT_AT(64 + 1, 7);
             if (ce) {
                 ce->n.free_[r] = fr;
                 ce->n.fit_R[r] = R;
                 ce->n.fit_F[r] = F;
             }
-        } else if (tid >= 64 + KG_NUM_RES && tid < 64 + KG_NUM_RES + 2) {
-            const int r = tid - 64 - KG_NUM_RES;
-            srow.la_used[0][r] += pd.la_est_i[r];
-            row.la_used[0][r] = srow.la_used[0][r];
-            if (pd.flags & KG_POD_PROD) {
-                srow.la_used[1][r] += pd.la_est_i[r];
-                row.la_used[1][r] = srow.la_used[1][r];
+        } else if (tid >= KG_RESOLVE_LA_T0 && tid < KG_RESOLVE_LA_T0 + 4) {
+            // LoadAware Reserve, one thread per (resource r, usage variant v), on a wave of their own (in the Fit
+            // parts' wave they ran after them: 6.8k → the Fit part's 2.4k cycles per pod, r05): the term and its
+            // planes (kg_finalize_la_r split by variant; the slow test reads both new terms, computed by each)
+            const int r = (tid - KG_RESOLVE_LA_T0) >> 1, v = (tid - KG_RESOLVE_LA_T0) & 1;
+            const int64_t est = pd.la_est_i[r];
+            const bool prod = (pd.flags & KG_POD_PROD) != 0;
+            const int64_t u0 = srow.la_used[0][r] + est, u1 = srow.la_used[1][r] + (prod ? est : 0);
+            if (v == 0) {
+                srow.la_used[0][r] = u0;
+                row.la_used[0][r] = u0;
+            } else if (prod) {
+                srow.la_used[1][r] = u1;
+                row.la_used[1][r] = u1;
             }
-            if (r == 0 && c.la_extra) {   // LoadAware weights beyond cpu / memory
+            if (r == 0 && v == 0 && c.la_extra) {   // LoadAware weights beyond cpu / memory
                 for (int x = 0; x < KG_NUM_RES - 2; x++) {
                     srow.la_used_x[0][x] += pd.la_est_x[x];
                     row.la_used_x[0][x] = srow.la_used_x[0][x];
-                    if (pd.flags & KG_POD_PROD) {
+                    if (prod) {
                         srow.la_used_x[1][x] += pd.la_est_x[x];
                         row.la_used_x[1][x] = srow.la_used_x[1][x];
                     }
                 }
             }
-            double R, F0, F1;
-            fin[KG_NUM_RES + r] = kg_finalize_la_r(c, pl, node, srow, r, &R, &F0, &F1) ? 1u : 0u;
+            const int64_t cap = pl.cap, a = srow.la_alloc[r], uv = v ? u1 : u0;
+            bool slow = c.la_extra != 0;
+            double R = 0.0, F = 0.0;
+            if (a != 0) {
+                if (a < 0 || a >= KG_CAP_LIMIT || kg_abs64(u0) >= KG_VAL_LIMIT || kg_abs64(u1) >= KG_VAL_LIMIT) {
+                    slow = true;
+                } else {
+                    R = 100.0 / (double)a;
+                    F = kg_scaled_ratio(a - uv, a);
+                }
+            }
+            if (v == 0) pl.la_R[r * cap + node] = R;
+            pl.la_F[(v * 2 + r) * cap + node] = F;
+            if (v == 0) fin[KG_NUM_RES + r] = slow ? 1u : 0u;
+            KG_RT_AT(KG_RESOLVE_LA_T0, 0);
             if (ce) {
-                ce->n.la_R[r] = R;
-                ce->n.la_F0[r] = F0;
-                ce->n.la_F1[r] = F1;
+                if (v == 0) {
+                    ce->n.la_R[r] = R;
+                    ce->n.la_F0[r] = F;
+                } else {
+                    ce->n.la_F1[r] = F;
+                }
             }
         } else if (numa_on && tid >= 128 && tid < 128 + KG_MAX_ZONES) {   // the zone commit, back to the row
             const int zi = tid - 128;
@@ -2316,8 +2435,9 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             if (zi == 0) row.zone_alloc_keys = srow.zone_alloc_keys;
         } else if (rsv_on && tid == 192) {   // Reservation.Reserve (its global writes are ordered for the next pod
             rsv_commit_entry(pl, ra, pd, node, ra.E + (int64_t)j * ra.n_rn);   // by the barrier that ends this one)
-        } else if (rsv_on && ra.M && tid >= KG_RESOLVE_THREADS / 2) {   // the idle upper waves: the next pod's split
-            if (j + 1 < n) rsv_prefetch(ra, j + 1, rpf, tid - KG_RESOLVE_THREADS / 2, KG_RESOLVE_THREADS / 2);
+        } else if (rsv_on && ra.M && tid >= KG_RESOLVE_THREADS / 2 && tid < KG_RESOLVE_LA_T0) {   // the idle upper
+            // waves: the next pod's split
+            if (j + 1 < n) rsv_prefetch(ra, j + 1, rpf, tid - KG_RESOLVE_THREADS / 2, KG_RESOLVE_LA_T0 - KG_RESOLVE_THREADS / 2);
         } else if (tid == 0) {
             if (ra.quota && pd.quota >= 0) kg_quota_commit(ra.quota, pd.quota, pd);
             const int32_t pc = srow.pod_count + 1;
@@ -2328,7 +2448,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             if (ce) ce->metric_ns = old_metric;
             if (slot == nt) {
                 touched[n_touched++] = node;
-                ttile[node / KG_TILE] = 1;
+                mark(node);
                 const int32_t rk = rsv_on && ra.M ? pl.rsv_of[node] : -1;
                 if (rk >= 0 && !gflag[rk / KG_RSV_GROUP]) {   // its entry group: rescanned by later pods
                     gflag[rk / KG_RSV_GROUP] = 1;
@@ -2338,11 +2458,15 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             out_node[j] = node;
             out_score[j] = (int64_t)(w >> 32) - 1;
         }
-        // the flags step reads the parts' LDS results only: their global stores (row, planes) complete under
-        // the full barrier that ends this pod, before the next pod reads them
-        __syncthreads();
+        // the flags step reads the parts' LDS results only.  Their global stores (row, planes) need to be complete
+        // only for a later global read of this node in the kernel: with a node-cache slot (the plain resolve) every
+        // later read of it is served from LDS (staging, re-scores, exact pairs) and the barriers order LDS only;
+        // otherwise (no slot, or the Reservation / NodeNUMAResource forms) they are full barriers.
+        const bool lds_only = LDSB && slot < KG_NCACHE;
+        if (lds_only) lds_barrier();
+        else __syncthreads();
         KG_RT(5);
-        if ((numa_on || rsv_on) && ce && tid >= 128 && tid < 128 + ROW_U4)   // the committed row into the node cache
+        if (ce && tid >= 128 && tid < 128 + ROW_U4)   // the committed row into the node cache
             reinterpret_cast<uint4 *>(&nrow[slot])[tid - 128] = reinterpret_cast<const uint4 *>(&srow)[tid - 128];
         if (tid == 0) {   // kg_finalize_flags from the parts (metric and the static bits are unchanged)
             bool slow = false;
@@ -2360,13 +2484,15 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             if ((df & KGD_SLOW) && !(old & KGD_SLOW)) {   // the node left the fast paths: list it
                 slow_list[n_slow++] = node;
                 *slow_count = n_slow;
+                if (lds_only) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the list entry is read next pod
             }
             if (ce) {
                 ce->n.df = df;
                 ce->n.fit_mask = fmask;
             }
         }
-        __syncthreads();
+        if (lds_only) lds_barrier();
+        else __syncthreads();
         KG_RT(6);
     }
 #ifdef KG_RESOLVE_TIMING
@@ -3971,7 +4097,7 @@ int32_t kg_debug_resolve_times(unsigned long long *out, int32_t n_pods) {
     if (hipMemcpyFromSymbol(&pods, HIP_SYMBOL(g_rtimes_pod), sizeof(int)) != hipSuccess) return -1;
     if (pods > n_pods) pods = n_pods;
     if (pods > 65536) pods = 65536;
-    if (pods > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtimes), sizeof(unsigned long long) * 8 * (size_t)pods) != hipSuccess) return -1;
+    if (pods > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtimes), sizeof(unsigned long long) * 16 * (size_t)pods) != hipSuccess) return -1;
     return pods;
 }
 #endif

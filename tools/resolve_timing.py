@@ -33,7 +33,7 @@ L = nat.lib()
 f = L.kg_debug_resolve_times
 f.restype = ctypes.c_int32
 f.argtypes = [ctypes.c_void_p, ctypes.c_int32]
-buf = np.zeros((P, 8), np.uint64)
+buf = np.zeros((P, 16), np.uint64)
 k = f(buf.ctypes.data, P)
 t = buf[:k].astype(np.int64)
 ok = (t[:, 6] > 0) & (t[:, 1] > 0)
@@ -41,6 +41,15 @@ d = np.diff(t[ok][:, 1:7], axis=1)
 print(f"{which}: {P} pods, {P / dt:.0f} pods/s, {int(ok.sum())} timed pods")
 for i, name in enumerate(["scan+rescore", "rescan+wavemax", "blockmax+row", "reserve parts", "flags+sync"]):
     print(f"  {name:16s} median {np.median(d[:, i]):8.0f}  mean {d[:, i].mean():8.0f} cycles")
+tt = t[ok]
+fit1 = tt[:, 7] - tt[:, 4]
+la0 = tt[:, 0] - tt[:, 4]
+print(f"  reserve: Fit part (memory) done after median {np.median(fit1):8.0f}, LoadAware part (cpu) after "
+      f"{np.median(la0):8.0f} cycles")
+for slot, name in ((9, "thread 0 after its tile"), (11, "thread 97 after its tile"), (8, "touched re-score (thread 128)"),
+                   (10, "next pod's row prefetched (thread 511)")):
+    x = tt[:, slot] - tt[:, 1]
+    print(f"  scan: {name:40s} median {np.median(x[tt[:, slot] > 0]) if (tt[:, slot] > 0).any() else float('nan'):8.0f}")
 tot = t[ok][:, 6] - t[ok][:, 1]
 print(f"  total per pod   median {np.median(tot):8.0f}  mean {tot.mean():8.0f}")
 nxt = t[ok][1:, 1] - t[ok][:-1, 6]
