@@ -288,8 +288,8 @@ def bench_host_outputs(args, engine, eng, P, N, now, dev):
 
 def bench_la_extra(args, engine, synth, shipped_profile, dev, stream):
     """Matrix mode with LoadAware resourceWeights beyond cpu / memory (ephemeral-storage, an extended resource,
-    batch-cpu; estimatedScalingFactors for the first two): the fp64 fast-path planes carry cpu / memory only, so
-    every pair runs the exact int64 path (k_eval_exact, kg_pair_exact).  Config-2-shaped cluster with those
+    batch-cpu; estimatedScalingFactors for the first two): k_eval2's LAX form reads fp64 planes of the weighted
+    extra resources beside the cpu / memory ones (up to KG_LAX = 4 of them; more take k_eval_exact).  Config-2-shaped cluster with those
     resources (synth.make_la_extra_cluster, seed 2), shipped profile."""
     import torch
 
@@ -319,7 +319,8 @@ def bench_la_extra(args, engine, synth, shipped_profile, dev, stream):
     k_ms = float(np.mean(eng.eval_kernel_times(steps)))
     eng.close()
     return {"workload": f"{P} pods x {N} nodes, shipped profile, LoadAware resourceWeights {weights}",
-            "kernel": "k_eval_exact", "evals_per_s": round(P * N / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+            "kernel": "k_eval2 LAX form (fp64 planes of the weighted extra resources; exact pair path for nodes "
+                      "outside their bounds)", "evals_per_s": round(P * N / dt, 1), "ms_per_step": round(dt * 1e3, 3),
             "kernel_ms": round(k_ms, 3)}
 
 

@@ -49,6 +49,10 @@
 #define KGD_LA_PASS_NP 0x100u
 #define KGD_LA_PASS_P 0x200u
 #define KGD_RSV 0x400u              // carries reservation slots: only the exact Reservation path evaluates it
+#define KGD_XSLOW 0x800u            // outside the fp64 bounds of a plane the batch reads, LoadAware extra resources
+                                    // included: under LoadAware weights beyond cpu / memory every node carries
+                                    // KGD_SLOW (the paths without extra-resource planes take kg_pair_exact), and the
+                                    // matrix kernel with those planes takes the exact path only for KGD_XSLOW nodes
 
 // engine-internal pod flag: Reservation is enabled and the pod has a required reservation affinity,
 // so every node without a matching reservation fails Reservation.Filter (plugin.go:354-357)
@@ -184,6 +188,8 @@ struct kg_planes {
     uint32_t *fit_mask;  // [cap] resources the node contributes to the Fit score
     int64_t cap;
     int32_t *rsv_of;     // [cap] index of the node in the reservation node list, −1 none (nullptr: no list)
+    double *la_Rx;       // [KG_NUM_RES − 2][cap] LoadAware planes of resources 2..7 (nullptr: not kept)
+    double *la_Fx;       // [2 variants][KG_NUM_RES − 2][cap]
 };
 
 KG_HD int64_t kg_abs64(int64_t x) { return x < 0 ? -x : x; }
@@ -267,16 +273,18 @@ KG_HD uint32_t kg_finalize_fit(const kg_consts &c, const kg_planes &pl, int64_t 
                                double *R_out = nullptr, double *F_out = nullptr) {
     return kg_finalize_fit_r(c, pl, i, pl.rows[i], r, free_out, R_out, F_out);
 }
-KG_HD bool kg_finalize_la_r(const kg_consts &c, const kg_planes &pl, int64_t i, const kg_node_row &row, int r,
-                            double *R_out = nullptr, double *F0_out = nullptr, double *F1_out = nullptr) {
+// bit 0: slow (KGD_SLOW: outside the bounds, or LoadAware weights beyond cpu / memory, whose planes only the
+// matrix kernel's extra-resource form reads); bit 1: outside the bounds (KGD_XSLOW)
+KG_HD uint32_t kg_finalize_la_r(const kg_consts &c, const kg_planes &pl, int64_t i, const kg_node_row &row, int r,
+                                double *R_out = nullptr, double *F0_out = nullptr, double *F1_out = nullptr) {
     const int64_t cap = pl.cap;
-    bool slow = c.la_extra != 0;   // weights beyond cpu / memory: the fp64 planes cover only cpu / memory
+    uint32_t slow = c.la_extra != 0 ? 1u : 0u;
     int64_t a = row.la_alloc[r];
     double R = 0.0, F0 = 0.0, F1 = 0.0;
     if (a != 0) {
         if (a < 0 || a >= KG_CAP_LIMIT || kg_abs64(row.la_used[0][r]) >= KG_VAL_LIMIT ||
             kg_abs64(row.la_used[1][r]) >= KG_VAL_LIMIT) {
-            slow = true;
+            slow = 3u;
         } else {
             R = 100.0 / (double)a;
             F0 = kg_scaled_ratio(a - row.la_used[0][r], a);
@@ -293,17 +301,48 @@ KG_HD bool kg_finalize_la_r(const kg_consts &c, const kg_planes &pl, int64_t i, 
     }
     return slow;
 }
-KG_HD bool kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, int r, double *R_out = nullptr,
-                          double *F0_out = nullptr, double *F1_out = nullptr) {
+KG_HD uint32_t kg_finalize_la(const kg_consts &c, const kg_planes &pl, int64_t i, int r, double *R_out = nullptr,
+                              double *F0_out = nullptr, double *F1_out = nullptr) {
     return kg_finalize_la_r(c, pl, i, pl.rows[i], r, R_out, F0_out, F1_out);
 }
-// the bits of dflags a Reserve can change, from the committed row values
-#define KGD_DYNAMIC (KGD_PODS_FULL | KGD_OVER_CPU | KGD_OVER_MEM | KGD_OVER_EPH | KGD_SLOW)
-KG_HD uint32_t kg_dflags_dynamic(bool pods_full, const bool over[3], bool slow) {
-    return (pods_full ? KGD_PODS_FULL : 0u) | (over[0] ? KGD_OVER_CPU : 0u) | (over[1] ? KGD_OVER_MEM : 0u) |
-           (over[2] ? KGD_OVER_EPH : 0u) | (slow ? KGD_SLOW : 0u);
+// LoadAware planes of extra resource x (resource 2 + x), both usage variants, when LoadAware weighs it; true when
+// outside the fp64 bounds.  The same operands as the cpu / memory planes: R = RN(100/a), F_v = RN(100·(a − used_v)/a
+// + 2^-42), so the pair score cvt_sat(fma(−EstimatePod, R, F_v)) is the exact least-requested integer.
+KG_HD bool kg_finalize_lax_r(const kg_consts &c, const kg_planes &pl, int64_t i, const kg_node_row &row, int x,
+                             double *R_out = nullptr, double *F0_out = nullptr, double *F1_out = nullptr) {
+    const int64_t cap = pl.cap;
+    bool slow = false;
+    const int64_t a = row.la_alloc_x[x];
+    double R = 0.0, F0 = 0.0, F1 = 0.0;
+    if (c.la_wx[x] > 0 && a != 0) {
+        if (a < 0 || a >= KG_CAP_LIMIT || kg_abs64(row.la_used_x[0][x]) >= KG_VAL_LIMIT ||
+            kg_abs64(row.la_used_x[1][x]) >= KG_VAL_LIMIT) {
+            slow = true;
+        } else {
+            R = 100.0 / (double)a;
+            F0 = kg_scaled_ratio(a - row.la_used_x[0][x], a);
+            F1 = kg_scaled_ratio(a - row.la_used_x[1][x], a);
+        }
+    }
+    if (pl.la_Rx) {
+        pl.la_Rx[x * cap + i] = R;
+        pl.la_Fx[(0 * (KG_NUM_RES - 2) + x) * cap + i] = F0;
+        pl.la_Fx[(1 * (KG_NUM_RES - 2) + x) * cap + i] = F1;
+    }
+    if (R_out) {
+        *R_out = R;
+        *F0_out = F0;
+        *F1_out = F1;
+    }
+    return slow;
 }
-KG_HD void kg_finalize_flags(const kg_planes &pl, int64_t i, bool slow, uint32_t fmask) {
+// the bits of dflags a Reserve can change, from the committed row values
+#define KGD_DYNAMIC (KGD_PODS_FULL | KGD_OVER_CPU | KGD_OVER_MEM | KGD_OVER_EPH | KGD_SLOW | KGD_XSLOW)
+KG_HD uint32_t kg_dflags_dynamic(bool pods_full, const bool over[3], bool slow, bool xslow) {
+    return (pods_full ? KGD_PODS_FULL : 0u) | (over[0] ? KGD_OVER_CPU : 0u) | (over[1] ? KGD_OVER_MEM : 0u) |
+           (over[2] ? KGD_OVER_EPH : 0u) | (slow ? KGD_SLOW : 0u) | (xslow ? KGD_XSLOW : 0u);
+}
+KG_HD void kg_finalize_flags(const kg_planes &pl, int64_t i, bool slow, uint32_t fmask, bool xslow = false) {
     const kg_node_row &row = pl.rows[i];
     uint32_t df = 0;
     if (row.flags & KG_NODE_VALID) df |= KGD_VALID;
@@ -312,25 +351,33 @@ KG_HD void kg_finalize_flags(const kg_planes &pl, int64_t i, bool slow, uint32_t
     if (row.alloc[KG_RES_MEMORY] - row.requested[KG_RES_MEMORY] < 0) df |= KGD_OVER_MEM;
     if (row.alloc[KG_RES_EPHEMERAL_STORAGE] - row.requested[KG_RES_EPHEMERAL_STORAGE] < 0) df |= KGD_OVER_EPH;
     if (slow) df |= KGD_SLOW;
+    if (xslow) df |= KGD_XSLOW;
     if (row.flags & KG_NODE_HAS_METRIC) df |= KGD_HAS_METRIC;
     if (row.flags & KG_NODE_HAS_UPDATE_TIME) df |= KGD_HAS_UPDATE;
     if (row.flags & KG_NODE_LA_PASS_NONPROD) df |= KGD_LA_PASS_NP;
     if (row.flags & KG_NODE_LA_PASS_PROD) df |= KGD_LA_PASS_P;
-    if (pl.rsv_of && pl.rsv_of[i] >= 0) df = (df & ~(KGD_VALID | KGD_SLOW)) | KGD_RSV;  // kg_rsv_pair owns it
+    if (pl.rsv_of && pl.rsv_of[i] >= 0) df = (df & ~(KGD_VALID | KGD_SLOW | KGD_XSLOW)) | KGD_RSV;  // kg_rsv_pair owns it
     pl.metric_ns[i] = row.metric_update_ns;
     pl.fit_mask[i] = fmask;
     pl.dflags[i] = df;
 }
 KG_HD void kg_finalize_node(const kg_consts &c, const kg_planes &pl, int64_t i) {
-    bool slow = false;
+    bool slow = false, xslow = false;
     uint32_t fmask = 0;
     for (int r = 0; r < KG_NUM_RES; r++) {
         const uint32_t f = kg_finalize_fit(c, pl, i, r);
         slow = slow || (f & 1u);
         if (f & 2u) fmask |= 1u << r;
     }
-    for (int r = 0; r < 2; r++) slow = kg_finalize_la(c, pl, i, r) || slow;
-    kg_finalize_flags(pl, i, slow, fmask);
+    xslow = slow;
+    for (int r = 0; r < 2; r++) {
+        const uint32_t f = kg_finalize_la(c, pl, i, r);
+        slow = slow || (f & 1u);
+        xslow = xslow || (f & 2u);
+    }
+    if (c.la_extra)
+        for (int x = 0; x < KG_NUM_RES - 2; x++) xslow = kg_finalize_lax_r(c, pl, i, pl.rows[i], x) || xslow;
+    kg_finalize_flags(pl, i, slow, fmask, xslow);
 }
 
 // Reserve delta: NodeInfo.AddPod (requested += request, nonzero += nonzero, pods += 1;

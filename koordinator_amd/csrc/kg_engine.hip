@@ -44,6 +44,7 @@
 #define KG_CLS_ITEM_MAX 512         // pods per k_eval3 work item (one output-row entry per thread)
 #define KG_MAX_CHUNK KG_PLACE_CHUNK_MAX   // max pods per resolve call (touched-list capacity)
 #define KG_MAX_TILES 4096        // max tiles per snapshot in k_resolve (2M nodes)
+#define KG_LAX 4                 // LoadAware extra resources k_eval2's LAX form carries (more: k_eval_exact)
 #define KG_XCDS 8                // workgroup b of a 1-D grid runs on XCD b % 8 (each XCD has its own L2)
 
 // ---------------------------------------------------------------------------------------
@@ -306,28 +307,36 @@ struct HotArgs {
     uint32_t fit_cap;        // 100 for MostAllocated (clamp), 0xFFFFFFFF for LeastAllocated (no-op)
     int32_t slot_res[8];     // resource id of each slot (−1 unused)
     int64_t now_ns;
+    // LoadAware weights beyond cpu / memory (k_eval2's LAX form): the weighted extra resources (index x into the
+    // LoadAware extra planes, resource 2 + x), their weights, and the pods' −EstimatePod of each ([pod][KG_LAX])
+    int32_t lax_n;
+    int32_t lax_x[KG_LAX];
+    uint32_t lax_w[KG_LAX];
+    const double *lax_est;
 };
 
 // ---------------------------------------------------------------------------------------
 // v2: two nodes per lane (a 1024-node tile per 512-thread workgroup)
 // ---------------------------------------------------------------------------------------
 // per-lane registers of one node
-template <int S, bool LA_PROD>
+template <int S, bool LA_PROD, bool LAX = false>
 struct HotNode {
     int64_t fr[S];          // Allocatable − Requested per slot (Fit filter)
     double R[S], F[S];      // Fit least/most-requested fma operands per slot
     double laR[2], laF0[2], laF1[2];
+    double lxR[LAX ? KG_LAX : 1], lxF0[LAX ? KG_LAX : 1], lxF1[LAX ? KG_LAX : 1];   // the LoadAware extra resources
     uint32_t okbits;        // node-only filter outcome per pod variant (bit variant + 3·has_request)
     uint32_t slot_mask;     // slots the node contributes to the Fit score
 };
 
-template <int S, bool LA_PROD>
+template <int S, bool LA_PROD, bool LAX = false>
 __device__ __forceinline__ void load_hot_node(const kg_consts &c, const kg_planes &pl, const HotArgs &a, int64_t node,
-                                              uint32_t slot_natives, HotNode<S, LA_PROD> &n) {
+                                              uint32_t slot_natives, HotNode<S, LA_PROD, LAX> &n) {
     const int64_t cap = pl.cap;
     const bool in_range = node < a.node_end;   // nodes past the shard end are never feasible
     const uint32_t df = in_range ? pl.dflags[node] : 0u;
-    const bool slow = (df & KGD_SLOW) != 0;
+    // LAX: the extra-resource planes are read, so only nodes outside the fp64 bounds are slow
+    const bool slow = (df & (LAX ? KGD_XSLOW : KGD_SLOW)) != 0;
     const uint32_t nfm = in_range ? pl.fit_mask[node] : 0u;
     n.slot_mask = 0;
 #pragma unroll
@@ -359,6 +368,17 @@ __device__ __forceinline__ void load_hot_node(const kg_consts &c, const kg_plane
             }
         }
     }
+    if constexpr (LAX) {
+        const bool use = in_range && !slow && (c.plugins & KG_PLUGIN_LOADAWARE) && kg_la_valid(c, df, expired);
+#pragma unroll
+        for (int k = 0; k < KG_LAX; k++) {
+            const int x = k < a.lax_n ? a.lax_x[k] : 0;
+            const bool on = use && k < a.lax_n;
+            n.lxR[k] = on ? pl.la_Rx[x * cap + node] : 0.0;
+            n.lxF0[k] = on ? pl.la_Fx[(0 * (KG_NUM_RES - 2) + x) * cap + node] : 0.0;
+            n.lxF1[k] = (on && LA_PROD) ? pl.la_Fx[(1 * (KG_NUM_RES - 2) + x) * cap + node] : 0.0;
+        }
+    }
     bool base = (df & KGD_VALID) && !slow;
     if (c.plugins & KG_PLUGIN_FIT) base = base && !(df & KGD_PODS_FULL);
     bool over = false;  // a zero request of a native resource without a slot still fails an overcommitted node
@@ -379,9 +399,10 @@ __device__ __forceinline__ void load_hot_node(const kg_consts &c, const kg_plane
 }
 
 // One (pod, node) pair on the fast path: feasibility, Fit and LoadAware scores.
-template <int S, bool FAST, bool LA_PROD, bool FULL>
+template <int S, bool FAST, bool LA_PROD, bool FULL, bool LAX = false>
 __device__ __forceinline__ bool eval_hot(const kg_consts &c, const HotArgs &a, const kg_pod_hot_t<S> &pd,
-                                         const HotNode<S, LA_PROD> &n, uint32_t &fit, uint32_t &la) {
+                                         const HotNode<S, LA_PROD, LAX> &n, uint32_t &fit, uint32_t &la,
+                                         const double *lax_est = nullptr) {
     bool ok = (n.okbits >> pd.okshift) & 1u;
     fit = 0;
     if (FAST || (c.plugins & KG_PLUGIN_FIT)) {
@@ -413,7 +434,15 @@ __device__ __forceinline__ bool eval_hot(const kg_consts &c, const HotArgs &a, c
         const bool prod = LA_PROD && (pd.flags & KG_HOT_PROD);
         const uint32_t q0 = cvt_u32_sat(__builtin_fma(pd.la_est[0], n.laR[0], prod ? n.laF1[0] : n.laF0[0]));
         const uint32_t q1 = cvt_u32_sat(__builtin_fma(pd.la_est[1], n.laR[1], prod ? n.laF1[1] : n.laF0[1]));
-        const uint32_t sum = __umul24((uint32_t)c.la_w[0], q0) + __umul24((uint32_t)c.la_w[1], q1);
+        uint32_t sum = __umul24((uint32_t)c.la_w[0], q0) + __umul24((uint32_t)c.la_w[1], q1);
+        if constexpr (LAX) {
+#pragma unroll
+            for (int k = 0; k < KG_LAX; k++) {
+                if (k >= a.lax_n) break;   // uniform
+                const uint32_t q = cvt_u32_sat(__builtin_fma(lax_est[k], n.lxR[k], prod ? n.lxF1[k] : n.lxF0[k]));
+                sum = __umul24(a.lax_w[k], q) + sum;
+            }
+        }
         la = FAST ? sum >> c.la_shift : div_w<false>(sum, (uint32_t)c.la_shift, c.la_rcp);
     }
     return ok;
@@ -421,19 +450,24 @@ __device__ __forceinline__ bool eval_hot(const kg_consts &c, const HotArgs &a, c
 
 // Pods [p0, p1) against the lane's two nodes (n0 = wave base + lane, n1 = n0 + 64).
 // seg0 / seg1: the wave's two 64-node segments lie inside the output rows (wave-uniform).
-template <int S, bool FAST, bool LA_PROD, bool FULL, bool OUT, bool TOPK>
+template <int S, bool FAST, bool LA_PROD, bool FULL, bool OUT, bool TOPK, bool LAX = false>
 __device__ __forceinline__ void hot_loop2(const kg_consts &c, const HotArgs &a, const kg_pod_hot_t<S> *__restrict__ pods,
                                           uint64_t *__restrict__ mrow, uint16_t *__restrict__ srow,
-                                          const HotNode<S, LA_PROD> &n0, const HotNode<S, LA_PROD> &n1,
+                                          const HotNode<S, LA_PROD, LAX> &n0, const HotNode<S, LA_PROD, LAX> &n1,
                                           uint32_t kb0, uint32_t kb1, int mask_lanes, bool seg0, bool seg1, int p0,
                                           int p1, uint32_t *kbuf) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     for (int p = p0; p < p1; p++) {
         const kg_pod_hot_t<S> pd = load_pod<S>(pods + p);
+        double lx[LAX ? KG_LAX : 1];
+        if constexpr (LAX) {
+#pragma unroll
+            for (int k = 0; k < KG_LAX; k++) lx[k] = a.lax_est[(int64_t)p * KG_LAX + k];   // scalar loads
+        }
         uint32_t fit0, la0, fit1, la1;
-        const bool ok0 = eval_hot<S, FAST, LA_PROD, FULL>(c, a, pd, n0, fit0, la0);
-        const bool ok1 = eval_hot<S, FAST, LA_PROD, FULL>(c, a, pd, n1, fit1, la1);
+        const bool ok0 = eval_hot<S, FAST, LA_PROD, FULL, LAX>(c, a, pd, n0, fit0, la0, lx);
+        const bool ok1 = eval_hot<S, FAST, LA_PROD, FULL, LAX>(c, a, pd, n1, fit1, la1, lx);
         if (OUT) {
             uint16_t *s = srow + (int64_t)p * a.score_stride;
             if (seg0) s[0] = (uint16_t)(fit0 | (la0 << 8));
@@ -487,7 +521,7 @@ __device__ __forceinline__ uint32_t tile_topk(const uint32_t *keys) {
 #define KG_KCHUNK 16   // pods per LDS key buffer
 
 // TOPK (placement chunks, no planes): the partials hold KG_TOPK best keys per (pod, tile) instead of one
-template <int S, bool FAST, bool LA_PROD, bool OUT, bool TOPK>
+template <int S, bool FAST, bool LA_PROD, bool OUT, bool TOPK, bool LAX = false>
 __global__ __launch_bounds__(KG_BLOCK) void k_eval2(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_pod_hot_t<S> *__restrict__ pods,
                                                     uint64_t *__restrict__ mask, uint16_t *__restrict__ scores,
@@ -507,9 +541,9 @@ __global__ __launch_bounds__(KG_BLOCK) void k_eval2(kg_consts c, kg_planes pl, H
         if (r >= 0 && r < 3) slot_natives |= 1u << r;
         all_slots |= (r >= 0) ? (1u << s) : 0u;
     }
-    HotNode<S, LA_PROD> n0, n1;
-    load_hot_node<S, LA_PROD>(c, pl, a, node0, slot_natives, n0);
-    load_hot_node<S, LA_PROD>(c, pl, a, node1, slot_natives, n1);
+    HotNode<S, LA_PROD, LAX> n0, n1;
+    load_hot_node<S, LA_PROD, LAX>(c, pl, a, node0, slot_natives, n0);
+    load_hot_node<S, LA_PROD, LAX>(c, pl, a, node1, slot_natives, n1);
     const bool full = __all(((n0.slot_mask & all_slots) == all_slots || node0 >= a.node_end) &&
                             ((n1.slot_mask & all_slots) == all_slots || node1 >= a.node_end));
     // output columns: a 64-node segment is written iff it lies inside the padded row (wave-uniform)
@@ -527,11 +561,11 @@ __global__ __launch_bounds__(KG_BLOCK) void k_eval2(kg_consts c, kg_planes pl, H
     for (int p0 = pb; p0 < pe; p0 += KG_KCHUNK) {
         const int p1 = min(p0 + KG_KCHUNK, pe);
         if (full)
-            hot_loop2<S, FAST, LA_PROD, true, OUT, TOPK>(c, a, pods, mrow, srow, n0, n1, kb0, kb1, mask_lanes, seg0,
-                                                         seg1, p0, p1, kbuf);
+            hot_loop2<S, FAST, LA_PROD, true, OUT, TOPK, LAX>(c, a, pods, mrow, srow, n0, n1, kb0, kb1, mask_lanes, seg0,
+                                                              seg1, p0, p1, kbuf);
         else
-            hot_loop2<S, FAST, LA_PROD, false, OUT, TOPK>(c, a, pods, mrow, srow, n0, n1, kb0, kb1, mask_lanes, seg0,
-                                                          seg1, p0, p1, kbuf);
+            hot_loop2<S, FAST, LA_PROD, false, OUT, TOPK, LAX>(c, a, pods, mrow, srow, n0, n1, kb0, kb1, mask_lanes, seg0,
+                                                               seg1, p0, p1, kbuf);
         __syncthreads();
         if (TOPK) {
             for (int pp = wave; pp < p1 - p0; pp += KG_BLOCK / 64) {
@@ -1192,9 +1226,9 @@ __global__ __launch_bounds__(256) void k_eq_rows(const int32_t *__restrict__ of,
 // Slow nodes (outside the fp64 exactness bounds) come out of k_eval2 as infeasible with
 // zero scores; k_slow_list collects them and k_fix_slow re-evaluates those pairs exactly.
 __global__ void k_slow_list(const uint32_t *__restrict__ dflags, int64_t begin, int64_t end, int32_t *__restrict__ list,
-                            int32_t *__restrict__ count) {
+                            int32_t *__restrict__ count, uint32_t bit = KGD_SLOW) {
     const int64_t i = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < end && (dflags[i] & KGD_SLOW) && (dflags[i] & KGD_VALID)) list[atomicAdd(count, 1)] = (int32_t)i;
+    if (i < end && (dflags[i] & bit) && (dflags[i] & KGD_VALID)) list[atomicAdd(count, 1)] = (int32_t)i;
 }
 
 // (the list covers the whole snapshot; columns outside the evaluated range [col_begin, col_end) are skipped)
@@ -2042,7 +2076,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
     // commits nothing ends without a barrier, so the next pod must not overwrite what a slower wave of
     // this pod may still read
     __shared__ int32_t n_touched, n_rescan[2], gate_ok[2], slot_s;
-    __shared__ uint32_t fin[KG_NUM_RES + 4];
+    __shared__ uint32_t fin[KG_NUM_RES + 2 + (KG_NUM_RES - 2)];
     __shared__ int32_t fl_pods_full;
     __shared__ uint32_t fl_over[3];
     __shared__ uint32_t fl_old_df;
@@ -2395,22 +2429,12 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 srow.la_used[1][r] = u1;
                 row.la_used[1][r] = u1;
             }
-            if (r == 0 && v == 0 && c.la_extra) {   // LoadAware weights beyond cpu / memory
-                for (int x = 0; x < KG_NUM_RES - 2; x++) {
-                    srow.la_used_x[0][x] += pd.la_est_x[x];
-                    row.la_used_x[0][x] = srow.la_used_x[0][x];
-                    if (prod) {
-                        srow.la_used_x[1][x] += pd.la_est_x[x];
-                        row.la_used_x[1][x] = srow.la_used_x[1][x];
-                    }
-                }
-            }
             const int64_t cap = pl.cap, a = srow.la_alloc[r], uv = v ? u1 : u0;
-            bool slow = c.la_extra != 0;
+            bool bounds = false;
             double R = 0.0, F = 0.0;
             if (a != 0) {
                 if (a < 0 || a >= KG_CAP_LIMIT || kg_abs64(u0) >= KG_VAL_LIMIT || kg_abs64(u1) >= KG_VAL_LIMIT) {
-                    slow = true;
+                    bounds = true;
                 } else {
                     R = 100.0 / (double)a;
                     F = kg_scaled_ratio(a - uv, a);
@@ -2418,7 +2442,8 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             }
             if (v == 0) pl.la_R[r * cap + node] = R;
             pl.la_F[(v * 2 + r) * cap + node] = F;
-            if (v == 0) fin[KG_NUM_RES + r] = slow ? 1u : 0u;
+            // (kg_finalize_la_r's bits: 1 slow, LoadAware weights beyond cpu / memory included; 2 outside the bounds)
+            if (v == 0) fin[KG_NUM_RES + r] = (bounds || c.la_extra ? 1u : 0u) | (bounds ? 2u : 0u);
             KG_RT_AT(KG_RESOLVE_LA_T0, 0);
             if (ce) {
                 if (v == 0) {
@@ -2428,6 +2453,20 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                     ce->n.la_F1[r] = F;
                 }
             }
+        } else if (tid >= KG_RESOLVE_LA_T0 + 4 && tid < KG_RESOLVE_LA_T0 + 4 + (KG_NUM_RES - 2)) {
+            // LoadAware weights beyond cpu / memory: extra resource x's terms and planes (kg_finalize_lax_r)
+            const int x = tid - KG_RESOLVE_LA_T0 - 4;
+            bool bounds = false;
+            if (c.la_extra) {
+                srow.la_used_x[0][x] += pd.la_est_x[x];
+                row.la_used_x[0][x] = srow.la_used_x[0][x];
+                if (pd.flags & KG_POD_PROD) {
+                    srow.la_used_x[1][x] += pd.la_est_x[x];
+                    row.la_used_x[1][x] = srow.la_used_x[1][x];
+                }
+                bounds = kg_finalize_lax_r(c, pl, node, srow, x);
+            }
+            fin[KG_NUM_RES + 2 + x] = bounds ? 1u : 0u;
         } else if (numa_on && tid >= 128 && tid < 128 + KG_MAX_ZONES) {   // the zone commit, back to the row
             const int zi = tid - 128;
             row.zone_allocated[zi][0] = srow.zone_allocated[zi][0];
@@ -2469,15 +2508,21 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         if (ce && tid >= 128 && tid < 128 + ROW_U4)   // the committed row into the node cache
             reinterpret_cast<uint4 *>(&nrow[slot])[tid - 128] = reinterpret_cast<const uint4 *>(&srow)[tid - 128];
         if (tid == 0) {   // kg_finalize_flags from the parts (metric and the static bits are unchanged)
-            bool slow = false;
+            bool slow = false, xslow = false;
             uint32_t fmask = 0;
-            for (int r = 0; r < KG_NUM_RES + 2; r++) slow = slow || (fin[r] & 1u);
+            for (int r = 0; r < KG_NUM_RES; r++) slow = slow || (fin[r] & 1u);
+            xslow = slow;
+            for (int r = KG_NUM_RES; r < KG_NUM_RES + 2; r++) {
+                slow = slow || (fin[r] & 1u);
+                xslow = xslow || (fin[r] & 2u);
+            }
+            for (int x = 0; x < KG_NUM_RES - 2; x++) xslow = xslow || (fin[KG_NUM_RES + 2 + x] & 1u);
             for (int r = 0; r < KG_NUM_RES; r++)
                 if (fin[r] & 2u) fmask |= 1u << r;
             const bool over[3] = {fl_over[0] != 0, fl_over[1] != 0, fl_over[2] != 0};
             const uint32_t old = fl_old_df;
-            uint32_t dyn = kg_dflags_dynamic(fl_pods_full != 0, over, slow);
-            if (old & KGD_RSV) dyn &= ~KGD_SLOW;   // kg_rsv_pair owns reservation nodes
+            uint32_t dyn = kg_dflags_dynamic(fl_pods_full != 0, over, slow, xslow);
+            if (old & KGD_RSV) dyn &= ~(KGD_SLOW | KGD_XSLOW);   // kg_rsv_pair owns reservation nodes
             const uint32_t df = (old & ~KGD_DYNAMIC) | dyn;
             pl.dflags[node] = df;
             pl.fit_mask[node] = fmask;
@@ -2564,6 +2609,11 @@ struct kg_engine {
     int32_t cls_kind_work[12][2] = {};  // [3 · kind + form] = (first work item, count); form 0 mixed, 1 LoadAware-
                                         // uniform, 2 duplicate-row (its items carry their tile)
     size_t cls_work_off = 0, cls_rows_off = 0, cls_ids_off = 0;
+    int32_t *xslow_list = nullptr;  // [cap] LoadAware-extra batches: nodes outside the bounds of any plane (KGD_XSLOW)
+    int32_t *xslow_count = nullptr;
+    double *hot_lax = nullptr;      // [n_pods][KG_LAX] the pods' −EstimatePod of the weighted extra resources
+    bool lax_ok = false;            // the batch takes k_eval2's LAX form in matrix mode (≤ KG_LAX weighted extras)
+    int32_t lax_n = 0, lax_x[KG_LAX] = {};
     int32_t *slow_list = nullptr;   // [cap] nodes outside the fast-path bounds, whole snapshot
     int32_t *slow_count = nullptr;
     bool slow_valid = false;        // the list matches the planes (rebuilt lazily after host-side changes;
@@ -3245,6 +3295,51 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
         if (e->profiling) HIP_TRY(e, prof_end(e));
         return KG_OK;
     }
+    if (e->consts.la_extra && !topk && e->lax_ok) {
+        // LoadAware weights beyond cpu / memory, at most KG_LAX of them: k_eval2's LAX form reads their planes too;
+        // the nodes outside the fp64 bounds of any plane (KGD_XSLOW) are re-evaluated exactly after it
+        a.lax_n = e->lax_n;
+        for (int k = 0; k < KG_LAX; k++) {
+            a.lax_x[k] = k < e->lax_n ? e->lax_x[k] : 0;
+            a.lax_w[k] = k < e->lax_n ? (uint32_t)e->consts.la_wx[e->lax_x[k]] : 0u;
+        }
+        a.lax_est = e->hot_lax + (int64_t)pod_begin * KG_LAX;
+        if (e->profiling) HIP_TRY(e, prof_begin(e));
+        dim3 grid((unsigned)shard_tiles, (unsigned)((n + a.pods_per_block - 1) / a.pods_per_block));
+        const bool prod = e->la_prod;
+#define KG_LAX_LAUNCH(S_)                                                                                               \
+        do {                                                                                                            \
+            const kg_pod_hot_t<S_> *hp = reinterpret_cast<const kg_pod_hot_t<S_> *>(e->hot) + pod_begin;                \
+            if (mask && prod)                                                                                          \
+                hipLaunchKernelGGL((k_eval2<S_, false, true, true, false, true>), grid, dim3(KG_BLOCK), 0, e->stream,  \
+                                   e->consts, e->pl, a, hp, mask, scores, partials);                                   \
+            else if (mask)                                                                                             \
+                hipLaunchKernelGGL((k_eval2<S_, false, false, true, false, true>), grid, dim3(KG_BLOCK), 0, e->stream, \
+                                   e->consts, e->pl, a, hp, mask, scores, partials);                                   \
+            else if (prod)                                                                                             \
+                hipLaunchKernelGGL((k_eval2<S_, false, true, false, false, true>), grid, dim3(KG_BLOCK), 0, e->stream, \
+                                   e->consts, e->pl, a, hp, mask, scores, partials);                                   \
+            else                                                                                                       \
+                hipLaunchKernelGGL((k_eval2<S_, false, false, false, false, true>), grid, dim3(KG_BLOCK), 0, e->stream,\
+                                   e->consts, e->pl, a, hp, mask, scores, partials);                                   \
+        } while (0)
+        if (e->nslot == 2) KG_LAX_LAUNCH(2);
+        else if (e->nslot == 4) KG_LAX_LAUNCH(4);
+        else KG_LAX_LAUNCH(8);
+#undef KG_LAX_LAUNCH
+        HIP_TRY(e, hipGetLastError());
+        if (e->profiling) HIP_TRY(e, prof_end(e));
+        HIP_TRY(e, hipMemsetAsync(e->xslow_count, 0, sizeof(int32_t), e->stream));
+        if (e->n_nodes > 0)
+            hipLaunchKernelGGL(k_slow_list, dim3((unsigned)((e->n_nodes + 255) / 256)), dim3(256), 0, e->stream, e->pl.dflags,
+                               (int64_t)0, e->n_nodes, e->xslow_list, e->xslow_count, (uint32_t)KGD_XSLOW);
+        hipLaunchKernelGGL(k_fix_slow, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->consts, e->pl,
+                           e->pods + pod_begin, n, e->xslow_list, e->xslow_count, e->shard_begin, e->shard_end,
+                           a.mask_words, a.score_stride, a.tiles_total, now_ns, (unsigned long long *)mask, scores,
+                           partials);
+        HIP_TRY(e, hipGetLastError());
+        return KG_OK;
+    }
     if (e->consts.la_extra && !topk) {   // every node is on the exact path: no fast kernel, no slow list
         if (e->profiling) HIP_TRY(e, prof_begin(e));
         const int64_t width = e->shard_end - e->shard_begin;
@@ -3417,6 +3512,7 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->numa_perm) (void)hipFree(e->numa_perm);
     if (e->numa_queue) (void)hipFree(e->numa_queue);
     if (e->comm) (void)rccl().comm_destroy(e->comm);
+    if (e->hot_lax) (void)hipFree(e->hot_lax);
     if (e->eq_pods) (void)hipFree(e->eq_pods);
     if (e->eq_perm) (void)hipFree(e->eq_perm);
     if (e->eq_of) (void)hipFree(e->eq_of);
@@ -3475,9 +3571,14 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
         return r;
     };
     size_t total = 0;
+    const bool lax = e->consts.la_extra != 0;
     const size_t sizes[] = {sizeof(kg_node_row) * (size_t)cap, (size_t)KG_NUM_RES * 8 * cap, (size_t)KG_NUM_RES * 8 * cap,
                             (size_t)KG_NUM_RES * 8 * cap, 2 * 8 * (size_t)cap, 4 * 8 * (size_t)cap, 8 * (size_t)cap,
-                            4 * (size_t)cap, 4 * (size_t)cap, 4 * (size_t)cap, 256, 4 * (size_t)cap};
+                            4 * (size_t)cap, 4 * (size_t)cap, 4 * (size_t)cap, 256, 4 * (size_t)cap,
+                            // LoadAware weights beyond cpu / memory: their planes and the list of the nodes outside the
+                            // fp64 bounds of any plane (KGD_XSLOW)
+                            lax ? (size_t)(KG_NUM_RES - 2) * 8 * cap : 0, lax ? (size_t)2 * (KG_NUM_RES - 2) * 8 * cap : 0,
+                            lax ? 4 * (size_t)cap : 0, lax ? (size_t)256 : 0};
     for (size_t s : sizes) total += (s + 255) / 256 * 256;
     HIP_TRY(e, hipMalloc(&e->plane_mem, total));
     HIP_TRY(e, hipMemsetAsync(e->plane_mem, 0, total, e->stream));
@@ -3494,6 +3595,10 @@ kg_status kg_snapshot_reset(kg_engine *e, int32_t n_nodes) {
     e->slow_list = (int32_t *)carve(sizes[9]);
     e->slow_count = (int32_t *)carve(sizes[10]);
     e->pl.rsv_of = (int32_t *)carve(sizes[11]);
+    e->pl.la_Rx = lax ? (double *)carve(sizes[12]) : nullptr;
+    e->pl.la_Fx = lax ? (double *)carve(sizes[13]) : nullptr;
+    e->xslow_list = lax ? (int32_t *)carve(sizes[14]) : nullptr;
+    e->xslow_count = lax ? (int32_t *)carve(sizes[15]) : nullptr;
     HIP_TRY(e, hipMemsetAsync(e->pl.rsv_of, 0xFF, sizes[11], e->stream));  // −1: no reservations
     if (e->rsv_mem) HIP_TRY(e, hipFree(e->rsv_mem));  // reservations refer to node indices: dropped
     e->rsv_mem = nullptr;
@@ -3700,10 +3805,33 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
         const std::vector<int32_t> order = numa_order(all);
         HIP_TRY(e, h2d(e, e->numa_perm, order.data(), sizeof(int32_t) * (size_t)n, e->stream));
     }
+    // LoadAware weights beyond cpu / memory: the pods' extra estimates for k_eval2's LAX form (exact in fp64:
+    // within the value bound), when at most KG_LAX extra resources are weighted
+    e->lax_ok = false;
+    if (e->consts.la_extra && (e->cfg.enabled_plugins & KG_PLUGIN_LOADAWARE)) {
+        int32_t nx = 0, xs[KG_NUM_RES - 2];
+        for (int x = 0; x < KG_NUM_RES - 2; x++)
+            if (e->consts.la_wx[x] > 0) xs[nx++] = x;
+        bool ok = nx <= KG_LAX;
+        for (int32_t i = 0; i < n && ok; i++)
+            for (int k = 0; k < nx; k++) ok = ok && kg_abs64(dev[(size_t)i].la_est_x[xs[k]]) < KG_VAL_LIMIT;
+        if (ok) {
+            std::vector<double> est((size_t)(n > 0 ? n : 1) * KG_LAX, 0.0);
+            for (int32_t i = 0; i < n; i++)
+                for (int k = 0; k < nx; k++) est[(size_t)i * KG_LAX + k] = -(double)dev[(size_t)i].la_est_x[xs[k]];
+            if (e->hot_lax) HIP_TRY(e, hipFree(e->hot_lax));
+            e->hot_lax = nullptr;
+            HIP_TRY(e, hipMalloc(&e->hot_lax, sizeof(double) * est.size()));
+            HIP_TRY(e, h2d(e, e->hot_lax, est.data(), sizeof(double) * est.size(), e->stream));
+            e->lax_n = nx;
+            for (int k = 0; k < nx; k++) e->lax_x[k] = xs[k];
+            e->lax_ok = true;
+        }
+    }
     // distinct device rows (pod equivalence, matrix mode off the class path): on when they are at most 3/4 of the
     // batch
     e->eq_on = false;
-    if (((e->cfg.enabled_plugins & KG_PLUGIN_NUMA) || e->consts.la_extra) && n >= 64) {
+    if (((e->cfg.enabled_plugins & KG_PLUGIN_NUMA) || (e->consts.la_extra && !e->lax_ok)) && n >= 64) {
         std::unordered_map<std::string, int32_t> seen;
         std::vector<int32_t> of((size_t)n), reps;
         for (int32_t i = 0; i < n; i++) {

@@ -118,3 +118,35 @@ def test_la_extra_with_numa_and_reservations():
     np.testing.assert_array_equal(res["numa_scores"][:, :N], numa)
     np.testing.assert_array_equal(res["top1"], top1)
     assert nat.PLUGIN_NUMA & int(cfg["enabled_plugins"])
+
+
+@pytest.mark.parametrize("shipped", [False, True], ids=["default", "shipped"])
+def test_la_extra_fast_form_with_out_of_bound_nodes(shipped):
+    """k_eval2's LAX form (the extra resources' fp64 planes): nodes whose extra-resource or native capacity lies
+    outside the fp64 bounds (KGD_XSLOW) go to the exact pair path after it; planes and top-1 against the oracle,
+    on a ragged node count and a shard."""
+    cl = synth.make_la_extra_cluster(2_300, 48, seed=45)
+    nodes = cl.nodes
+    big = np.arange(7, 2_300, 61)
+    nodes["allocatable"]["v"][big, nat.RES_EPHEMERAL_STORAGE] = (1 << 43) + 5
+    huge = np.arange(11, 2_300, 97)
+    nodes["allocatable"]["v"][huge, nat.RES_MEMORY] = (1 << 43) + 99
+    cl = cl.with_nodes(nodes)
+    kw = dict(resource_weights=W, estimated_scaling_factors=SF)
+    cfg = shipped_profile(**kw) if shipped else make_config(plugins=("NodeResourcesFit", "LoadAwareScheduling"), **kw)
+    N, idx = len(cl.nodes), np.arange(48)
+    with _engine(cfg, cl, idx) as eng:
+        res = eng.eval(cl.now_ns)
+        eng.set_shard(1024, 2300)
+        shard = eng.eval(cl.now_ns)
+    m, f, l = oracle.eval_matrix(cfg, cl, idx, cl.now_ns)
+    np.testing.assert_array_equal(engine.unpack_mask(res["mask"], N), m)
+    np.testing.assert_array_equal(res["scores"][:, :N, 0], f)
+    np.testing.assert_array_equal(res["scores"][:, :N, 1], l)
+    tot = np.where(m, int(cfg["weight_fit"]) * f.astype(np.int64) + int(cfg["weight_loadaware"]) * l, -1)
+    node, best = engine.decode_top1(res["top1"])
+    np.testing.assert_array_equal(node, np.where(tot.max(axis=1) >= 0, tot.argmax(axis=1), -1))
+    np.testing.assert_array_equal(best, tot.max(axis=1))
+    np.testing.assert_array_equal(engine.unpack_mask(shard["mask"], N - 1024), m[:, 1024:])
+    np.testing.assert_array_equal(shard["scores"][:, :N - 1024, 1], l[:, 1024:])
+    assert m[:, big].any()
