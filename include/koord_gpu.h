@@ -700,11 +700,15 @@ kg_status kg_set_eval_stream(kg_engine *eng, void *hip_stream);
  *  KG_FORM_NUMA_QUEUED       NodeNUMAResource matrix launches take the queued work-item form (by size: launches
  *                            with at least one work item per resident wave, and placement chunks)
  *  KG_FORM_NUMA_CHUNK_TILE   NodeNUMAResource placement chunks write one key per tile through the matrix kernel
- *                            (by size: chunks above 16 pods; smaller ones take per-tile top-16 lists) */
+ *                            (by size: chunks above 16 pods; smaller ones take per-tile top-16 lists)
+ *  KG_FORM_NUMA_NO_CACHE     pipelined NodeNUMAResource placement evaluates every chunk pair by pair (by size: a
+ *                            batch of repeated pod rows reads the distinct rows' outcomes from a per-node cache,
+ *                            refreshed for each chunk's committed nodes) */
 #define KG_FORM_PLACE_PIPELINE 0x1u
 #define KG_FORM_PLACE_SEQUENTIAL 0x2u
 #define KG_FORM_NUMA_QUEUED 0x4u
 #define KG_FORM_NUMA_CHUNK_TILE 0x8u
+#define KG_FORM_NUMA_NO_CACHE 0x10u
 kg_status kg_set_forms(kg_engine *eng, uint32_t forms);
 
 /* Reservation cache (KG_PLUGIN_RESERVATION): replaces every reservation slot; a node holds at most

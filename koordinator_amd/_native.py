@@ -19,6 +19,7 @@ ABI_VERSION = 11
 COMM_ID_BYTES = 128   # KG_COMM_ID_BYTES
 # kg_set_forms bits (include/koord_gpu.h)
 FORM_PLACE_PIPELINE, FORM_PLACE_SEQUENTIAL, FORM_NUMA_QUEUED, FORM_NUMA_CHUNK_TILE = 0x1, 0x2, 0x4, 0x8
+FORM_NUMA_NO_CACHE = 0x10
 NUM_RES = 8
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
  RES_EXTENDED) = range(8)

@@ -1570,6 +1570,91 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_CHUNK_WP
     }
 }
 
+// NodeNUMAResource results per (distinct pod row, node) for the pipelined placement (kg_engine::ncache): a pod's
+// Filter + NodeNUMAResource outcome on a node depends only on its device row and the node's state, so the batch's
+// distinct rows (pod equivalence, eq_pods / eq_of) are evaluated over the shard once (k_eval_numa2, matrix mode) and
+// each chunk's committed nodes are re-evaluated for every distinct row before the chunk two later is evaluated.
+// One byte per entry: the NUMA score when the pair is feasible (eval_pair and the NUMA Filter), KG_NCACHE_NO else.
+#define KG_NCACHE_NO 255u
+// the matrix mask and NUMA planes of the distinct rows → the cache (one thread per entry)
+__global__ __launch_bounds__(256) void k_ncache_init(const unsigned long long *__restrict__ mask,
+                                                     const uint8_t *__restrict__ numa, int32_t U, int32_t words,
+                                                     int64_t stride, int64_t width, uint8_t *__restrict__ cache) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)U * stride) return;
+    const int64_t u = i / stride, col = i % stride;
+    const bool ok = col < width && ((mask[u * words + (col >> 6)] >> (col & 63)) & 1ull);
+    cache[i] = ok ? numa[i] : (uint8_t)KG_NCACHE_NO;
+}
+
+// the committed nodes of one chunk (nodes[0..n), −1 for an unplaced pod) re-evaluated for every distinct row: one
+// thread per (row, node), the same pair functions as k_eval_numa2 (its zone-table provider derives every value with
+// the functions kg_zone_calc calls, so the results are identical)
+__global__ __launch_bounds__(256) void k_ncache_refresh(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ rows,
+                                                        int32_t U, const int32_t *__restrict__ nodes, int32_t n,
+                                                        int64_t now_ns, uint8_t *__restrict__ cache, int64_t stride,
+                                                        int64_t col_begin, int64_t col_end) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (n <= 0 || i >= (int64_t)U * n) return;
+    const int32_t u = (int32_t)(i / n);
+    const int64_t node = nodes[i % n];
+    if (node < col_begin || node >= col_end) return;
+    const kg_pod_dev pd = rows[u];
+    NodeRegs nr;
+    load_node(c, pl, node, true, BatchMasks{0xFFu, 0xFFu}, now_ns, nr);
+    uint32_t fit, la;
+    bool ok = eval_pair(c, pl, pd, nr, node, now_ns, fit, la);
+    kg_numa_out o;
+    const kg_node_row &row = pl.rows[node];
+    kg_numa_pair_z<kg_zone_calc, false, false>(c, row, pd, o, kg_zone_calc{row});
+    ok = ok && o.feasible;
+    cache[(int64_t)u * stride + (node - col_begin)] = ok ? (uint8_t)o.score : (uint8_t)KG_NCACHE_NO;
+}
+
+// k_eval_numa_chunk with the pair's Filter + NodeNUMAResource outcome read from the cache row of the pod's distinct
+// row (cls_of: the chunk's pods' rows in the cache); Fit / LoadAware scores from the planes as in every fast path.
+// The keys of nodes the previous chunk committed (not yet refreshed) are stale: the resolve re-scores those.
+__global__ __launch_bounds__(256) void k_eval_numa_cached(kg_consts c, kg_planes pl, HotArgs a,
+                                                          const kg_pod_dev *__restrict__ pods, int32_t shard_tiles,
+                                                          uint32_t *__restrict__ partials, const uint8_t *__restrict__ cache,
+                                                          const int32_t *__restrict__ cls_of, int64_t stride) {
+    __shared__ __attribute__((aligned(16))) kg_pod_dev lp;
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_TILE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int n = a.n_pods;   // 1..KG_NUMA_CHUNK_PODS (host-checked)
+    const int b = blockIdx.x, xcd = b % KG_XCDS, r = b / KG_XCDS;
+    const int tile_rel = (r / n) * KG_XCDS + xcd, p = r % n;
+    if (tile_rel >= shard_tiles) return;   // grid padded to a multiple of 8 tiles; block-uniform
+    constexpr int POD_DW = (int)(sizeof(kg_pod_dev) / 4);
+    for (int k = tid; k < POD_DW; k += 256)
+        reinterpret_cast<uint32_t *>(&lp)[k] = reinterpret_cast<const uint32_t *>(pods + p)[k];
+    __syncthreads();
+    const uint8_t *crow = cache + (int64_t)cls_of[p] * stride - a.col_begin;
+    const int tile = a.tile_begin + tile_rel;
+    const BatchMasks bm{0xFFu, 0xFFu};
+#pragma unroll 1
+    for (int v = 0; v < KG_TILE / 256; v++) {
+        const int local = v * 256 + tid;
+        const int64_t node = (int64_t)tile * KG_TILE + local;
+        const bool in_range = node < a.node_end;
+        const uint32_t ns = in_range ? crow[node] : KG_NCACHE_NO;
+        uint32_t key = 0;
+        if (ns != KG_NCACHE_NO) {
+            NodeRegs nr;
+            load_node(c, pl, node, true, bm, a.now_ns, nr);
+            uint32_t fit, la;
+            if (eval_pair(c, pl, lp, nr, node, a.now_ns, fit, la))
+                key = ((total_of(c, fit, la, ns) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local);
+        }
+        kbuf[local] = key;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t t = tile_topk(kbuf);
+        if (lane < KG_TOPK) partials[((int64_t)p * a.tiles_total + tile) * KG_PARTIAL_SLOTS + lane] = t;
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // Reservation + ElasticQuota (BASELINE config 5)
 // ---------------------------------------------------------------------------------------
@@ -2585,6 +2670,13 @@ struct kg_engine {
     int32_t *eq_of = nullptr;          // [n_pods] the distinct row of each pod
     void *eq_mem = nullptr;            // the distinct batch's outputs, then the staging of host outputs
     size_t eq_mem_bytes = 0;
+    // pipelined NodeNUMAResource placement over the distinct rows (k_ncache_*): the cache [eq_n][stride] and the
+    // matrix outputs it is built from, in one buffer; ncache_live while place_pipelined runs on it
+    void *ncache_mem = nullptr;
+    size_t ncache_bytes = 0;
+    uint8_t *ncache = nullptr;
+    int64_t ncache_stride = 0;
+    bool ncache_live = false;
     BatchMasks bm{0, 0};
     uint32_t forms = 0;             // kg_set_forms: size-chosen kernel forms forced (KG_FORM_*), 0 = by size
     int64_t numa_resident_wgs = 0;  // resident k_eval_numa2 workgroups of the device (queried at first use)
@@ -3236,7 +3328,11 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
     if ((e->consts.plugins & KG_PLUGIN_NUMA) && topk && n <= e->numa_chunk_pods) {
         if (e->profiling) HIP_TRY(e, prof_begin(e));
         const unsigned blocks = (unsigned)((shard_tiles + KG_XCDS - 1) / KG_XCDS * KG_XCDS * n);
-        if (e->consts.numa_bz)
+        if (e->ncache_live && !e->consts.numa_bz)
+            hipLaunchKernelGGL(k_eval_numa_cached, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                               e->pods + pod_begin, (int32_t)shard_tiles, partials, e->ncache, e->eq_of + pod_begin,
+                               e->ncache_stride);
+        else if (e->consts.numa_bz)
             hipLaunchKernelGGL(k_eval_numa_chunk<true>, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
                                e->pods + pod_begin, (int32_t)shard_tiles, partials);
         else
@@ -3517,6 +3613,7 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->eq_perm) (void)hipFree(e->eq_perm);
     if (e->eq_of) (void)hipFree(e->eq_of);
     if (e->eq_mem) (void)hipFree(e->eq_mem);
+    if (e->ncache_mem) (void)hipFree(e->ncache_mem);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
@@ -4233,7 +4330,8 @@ int32_t kg_debug_resolve_times(unsigned long long *out, int32_t n_pods) {
 kg_status kg_set_forms(kg_engine *e, uint32_t forms) {
     kg_status st = check_engine(e);
     if (st) return st;
-    if (forms & ~(KG_FORM_PLACE_PIPELINE | KG_FORM_PLACE_SEQUENTIAL | KG_FORM_NUMA_QUEUED | KG_FORM_NUMA_CHUNK_TILE))
+    if (forms & ~(KG_FORM_PLACE_PIPELINE | KG_FORM_PLACE_SEQUENTIAL | KG_FORM_NUMA_QUEUED | KG_FORM_NUMA_CHUNK_TILE |
+                  KG_FORM_NUMA_NO_CACHE))
         return set_err(e, KG_ERR_INVALID_ARG, "unknown kernel form bits 0x%x", forms);
     if ((forms & KG_FORM_PLACE_PIPELINE) && (forms & KG_FORM_PLACE_SEQUENTIAL))
         return set_err(e, KG_ERR_INVALID_ARG, "pipelined and sequential placement together");
@@ -4288,6 +4386,65 @@ namespace {
 // resolve i).  Not used with reservations (one entry buffer) or cpuset pods (host Reserve between chunks).
 kg_status merge_partials(kg_engine *e, uint32_t *part, int32_t n, hipStream_t s);
 
+// the NodeNUMAResource cache of the batch's distinct rows over the shard (kg_engine::ncache), on the engine stream:
+// matrix mode (k_eval_numa2) over eq_pods into the buffer's tail, then k_ncache_init
+kg_status ncache_build(kg_engine *e, int64_t now_ns) {
+    const int32_t U = e->eq_n;
+    const int64_t width = e->shard_end - e->shard_begin;
+    const int64_t words = (width + 63) / 64, stride = words * 64;
+    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t cache_b = up((size_t)U * (size_t)stride), mask_b = up((size_t)U * (size_t)words * 8),
+                 score_b = up((size_t)U * (size_t)stride * 4), numa_b = up((size_t)U * (size_t)stride),
+                 part_b = up((size_t)U * (size_t)tiles_total(e) * 4);
+    const size_t need = cache_b + mask_b + score_b + numa_b + part_b;
+    if (need > e->ncache_bytes) {
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+        if (e->ncache_mem) HIP_TRY(e, hipFree(e->ncache_mem));
+        e->ncache_mem = nullptr;
+        e->ncache_bytes = 0;
+        HIP_TRY(e, hipMalloc(&e->ncache_mem, need));
+        e->ncache_bytes = need;
+    }
+    char *m = (char *)e->ncache_mem;
+    uint8_t *cache = (uint8_t *)m;
+    unsigned long long *mask = (unsigned long long *)(m + cache_b);
+    uint16_t *scores = (uint16_t *)(m + cache_b + mask_b);
+    uint8_t *numa = (uint8_t *)(m + cache_b + mask_b + score_b);
+    uint32_t *part = (uint32_t *)(m + cache_b + mask_b + score_b + numa_b);
+    HIP_TRY(e, hipMemsetAsync(part, 0, part_b, e->stream));
+    // the distinct batch in place of the batch (as eval_eq), restored on every path
+    const kg_counters ctr0 = e->ctr;
+    const int32_t P = e->n_pods;
+    std::swap(e->pods, e->eq_pods);
+    std::swap(e->numa_perm, e->eq_perm);
+    std::swap(e->numa_perm_on, e->eq_perm_on);
+    e->n_pods = U;
+    kg_status st = launch_eval(e, now_ns, 0, U, (uint64_t *)mask, scores, part, false, numa);
+    e->n_pods = P;
+    std::swap(e->pods, e->eq_pods);
+    std::swap(e->numa_perm, e->eq_perm);
+    std::swap(e->numa_perm_on, e->eq_perm_on);
+    e->ctr = ctr0;
+    if (st) return st;
+    const int64_t total = (int64_t)U * stride;
+    hipLaunchKernelGGL(k_ncache_init, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, e->stream, mask, numa, U,
+                       (int32_t)words, stride, width, cache);
+    HIP_TRY(e, hipGetLastError());
+    e->ncache = cache;
+    e->ncache_stride = stride;
+    return KG_OK;
+}
+
+// chunk i − 2's committed nodes re-evaluated in the cache, on stream s (after that chunk's resolve)
+kg_status ncache_refresh(kg_engine *e, int64_t now_ns, const int32_t *nodes, int32_t n, hipStream_t s) {
+    const int64_t total = (int64_t)e->eq_n * n;
+    if (total <= 0) return KG_OK;
+    hipLaunchKernelGGL(k_ncache_refresh, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, e->consts, e->pl,
+                       e->eq_pods, e->eq_n, nodes, n, now_ns, e->ncache, e->ncache_stride, e->shard_begin, e->shard_end);
+    HIP_TRY(e, hipGetLastError());
+    return KG_OK;
+}
+
 kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score, int32_t chunk,
                           bool merge = false) {
     const int32_t P = e->n_pods;
@@ -4315,11 +4472,29 @@ kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64
         (void)hipStreamWaitEvent(main_s, e->ev_join, 0);
         return code;
     };
+    // NodeNUMAResource over a batch of repeated rows: the chunks read the distinct rows' cached outcomes (built on the
+    // engine stream before the fork below; ncache_live off again on every return)
+    struct NcacheScope {
+        kg_engine *e;
+        ~NcacheScope() { e->ncache_live = false; }
+    } ncache_scope{e};
+    if ((e->consts.plugins & KG_PLUGIN_NUMA) && e->eq_on && !e->consts.numa_bz && !(e->forms & KG_FORM_NUMA_NO_CACHE) &&
+        P > 2 * chunk && chunk <= e->numa_chunk_pods) {
+        st = ncache_build(e, now_ns);
+        if (st) return st;
+        e->ncache_live = true;
+        HIP_TRY(e, hipEventRecord(e->ev_fork, main_s));
+        HIP_TRY(e, hipStreamWaitEvent(eval_s, e->ev_fork, 0));
+    }
     int32_t prev_b = 0, prev_n = 0;
     int32_t i = 0;
     for (int32_t b = 0; b < P; b += chunk, i++) {
         const int32_t n = P - b < chunk ? P - b : chunk;
         if (i >= 2) HIP_TRY(e, hipStreamWaitEvent(eval_s, e->ev_res[(i - 2) % 3], 0));
+        if (i >= 2 && e->ncache_live) {   // chunk i − 2 (full-size) resolved: its nodes' cache entries re-evaluated
+            st = ncache_refresh(e, now_ns, dnode + (b - 2 * chunk), chunk, eval_s);
+            if (st) return fail(st);
+        }
         e->stream = eval_s;   // chunk_eval launches on e->stream
         st = chunk_eval(e, now_ns, b, n, part[i & 1]);
         e->stream = main_s;

@@ -24,11 +24,14 @@ def _replay(cfg, cl, idx, nodes):
     return rows
 
 
-@pytest.mark.parametrize("chunk_form", ["topk", "tile_key"])
+@pytest.mark.parametrize("chunk_form", ["topk", "topk_nocache", "tile_key"])
 @pytest.mark.parametrize("pipeline", ["1", "0"])
 @pytest.mark.parametrize("n_nodes", [1024, 2000])
 def test_numa_place_pipeline_on_off(n_nodes, pipeline, chunk_form):
+    """The pipelined "topk" form of a batch of repeated pod rows (~50 distinct of 240) reads the distinct rows'
+    cached NodeNUMAResource outcomes (k_eval_numa_cached, refreshed per chunk); "topk_nocache" evaluates every pair."""
     forms = (0 if pipeline == "1" else nat.FORM_PLACE_SEQUENTIAL) | (nat.FORM_NUMA_CHUNK_TILE if chunk_form == "tile_key" else 0)
+    forms |= nat.FORM_NUMA_NO_CACHE if chunk_form == "topk_nocache" else 0
     P = 240
     cl = synth.make_numa_cluster(n_nodes, P, seed=91 + n_nodes)
     cfg = shipped_profile()
@@ -43,6 +46,9 @@ def test_numa_place_pipeline_on_off(n_nodes, pipeline, chunk_form):
     ref_n, ref_s = oracle.schedule(cfg, cl, idx, cl.now_ns)
     np.testing.assert_array_equal(nodes, ref_n)
     np.testing.assert_array_equal(scores, ref_s)
+    if chunk_form == "topk":   # the cache's precondition: the batch repeats rows (pod equivalence on)
+        rows = engine.build_pod_rows(cfg, cl, idx)
+        assert 4 * len({r.tobytes() for r in rows}) <= 3 * P
     # consecutive chunks (16 pods) land on common nodes: the re-score of the previous chunk's nodes matters
     placed = nodes[nodes >= 0]
     chunks = [set(placed[i:i + 16].tolist()) for i in range(0, len(placed), 16)]
