@@ -1587,28 +1587,42 @@ __global__ __launch_bounds__(256) void k_ncache_init(const unsigned long long *_
     cache[i] = ok ? numa[i] : (uint8_t)KG_NCACHE_NO;
 }
 
-// the committed nodes of one chunk (nodes[0..n), −1 for an unplaced pod) re-evaluated for every distinct row: one
-// thread per (row, node), the same pair functions as k_eval_numa2 (its zone-table provider derives every value with
-// the functions kg_zone_calc calls, so the results are identical)
+// the committed nodes of one chunk (nodes[0..n), −1 for an unplaced pod; host-checked n ≤ KG_NUMA_CHUNK_PODS) re-evaluated
+// for every distinct row: workgroup b takes rows [16b, 16b + 16), a thread per (row, node), both staged in LDS; the same
+// pair functions as k_eval_numa2 (its zone-table provider derives every value with the functions kg_zone_calc calls, so
+// the results are identical)
 __global__ __launch_bounds__(256) void k_ncache_refresh(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ rows,
                                                         int32_t U, const int32_t *__restrict__ nodes, int32_t n,
                                                         int64_t now_ns, uint8_t *__restrict__ cache, int64_t stride,
                                                         int64_t col_begin, int64_t col_end) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (n <= 0 || i >= (int64_t)U * n) return;
-    const int32_t u = (int32_t)(i / n);
-    const int64_t node = nodes[i % n];
+    constexpr int G = KG_NUMA_CHUNK_PODS;
+    static_assert(G * G == 256, "a thread per (row, node) of a 16 × 16 block");
+    __shared__ __attribute__((aligned(16))) kg_node_row lrow[G];
+    __shared__ __attribute__((aligned(16))) kg_pod_dev lpd[G];
+    constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16), POD_DW = (int)(sizeof(kg_pod_dev) / 4);
+    const int tid = threadIdx.x;
+    const int u0 = blockIdx.x * G, nu = U - u0 < G ? U - u0 : G;
+    for (int x = tid; x < n * ROW_U4; x += 256) {
+        const int q = x / ROW_U4, w = x - q * ROW_U4;
+        const int64_t nd = nodes[q];
+        if (nd >= col_begin && nd < col_end) reinterpret_cast<uint4 *>(&lrow[q])[w] = reinterpret_cast<const uint4 *>(pl.rows + nd)[w];
+    }
+    for (int x = tid; x < nu * POD_DW; x += 256)
+        reinterpret_cast<uint32_t *>(lpd)[x] = reinterpret_cast<const uint32_t *>(rows + u0)[x];
+    __syncthreads();
+    const int ul = tid / G, k = tid % G;
+    if (ul >= nu || k >= n) return;
+    const int64_t node = nodes[k];
     if (node < col_begin || node >= col_end) return;
-    const kg_pod_dev pd = rows[u];
+    const kg_pod_dev &pd = lpd[ul];
     NodeRegs nr;
     load_node(c, pl, node, true, BatchMasks{0xFFu, 0xFFu}, now_ns, nr);
     uint32_t fit, la;
     bool ok = eval_pair(c, pl, pd, nr, node, now_ns, fit, la);
     kg_numa_out o;
-    const kg_node_row &row = pl.rows[node];
-    kg_numa_pair_z<kg_zone_calc, false, false>(c, row, pd, o, kg_zone_calc{row});
+    kg_numa_pair_z<kg_zone_calc, false, false>(c, lrow[k], pd, o, kg_zone_calc{lrow[k]});
     ok = ok && o.feasible;
-    cache[(int64_t)u * stride + (node - col_begin)] = ok ? (uint8_t)o.score : (uint8_t)KG_NCACHE_NO;
+    cache[(int64_t)(u0 + ul) * stride + (node - col_begin)] = ok ? (uint8_t)o.score : (uint8_t)KG_NCACHE_NO;
 }
 
 // k_eval_numa_chunk with the pair's Filter + NodeNUMAResource outcome read from the cache row of the pod's distinct
@@ -2116,6 +2130,45 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
     return ((unsigned long long)(total_of(c, fit, la, numa) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
 }
 
+// NodeNUMAResource, pipelined placement: the keys of every (chunk pod j, previous-chunk node q) pair, keys[j · n_prev + q],
+// after the previous chunk's resolve and before this chunk's (k_resolve's pvkeys).  One workgroup, a thread per pair
+// (host-checked: n, n_prev ≤ KG_NUMA_CHUNK_PODS); the nodes' canonical rows and the pods' rows staged in LDS first
+// (the hint enumeration re-reads the zone fields in every loop: from global memory it was a 187k-cycle chain).
+__global__ __launch_bounds__(256) void k_prev_keys(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t n,
+                                                   const int32_t *__restrict__ prev_nodes, int32_t n_prev, int64_t n_nodes,
+                                                   int64_t now_ns, unsigned long long *__restrict__ keys) {
+    __shared__ __attribute__((aligned(16))) kg_node_row lrow[KG_NUMA_CHUNK_PODS];
+    __shared__ __attribute__((aligned(16))) kg_pod_dev lpd[KG_NUMA_CHUNK_PODS];
+    constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16), POD_DW = (int)(sizeof(kg_pod_dev) / 4);
+    const int tid = threadIdx.x;
+    for (int x = tid; x < n_prev * ROW_U4; x += 256) {
+        const int q = x / ROW_U4, w = x - q * ROW_U4;
+        const int64_t node = prev_nodes[q];
+        if (node >= 0 && node < n_nodes) reinterpret_cast<uint4 *>(&lrow[q])[w] = reinterpret_cast<const uint4 *>(pl.rows + node)[w];
+    }
+    for (int x = tid; x < n * POD_DW; x += 256)
+        reinterpret_cast<uint32_t *>(lpd)[x] = reinterpret_cast<const uint32_t *>(pods)[x];
+    __syncthreads();
+    if (tid >= n * n_prev) return;
+    const int j = tid / n_prev, q = tid - j * n_prev;
+    const int64_t node = prev_nodes[q];
+    const kg_pod_dev &pd = lpd[j];
+    unsigned long long key = 0;
+    if (node >= 0 && node < n_nodes && !(pd.flags & KGP_RSV_REQUIRED)) {
+        NodeRegs nr;
+        load_node(c, pl, node, true, BatchMasks{0xFFu, 0xFFu}, now_ns, nr);
+        uint32_t fit, la;
+        if (eval_pair(c, pl, pd, nr, node, now_ns, fit, la)) {
+            // inlined (kg_numa_eval_any is a call: its frame in scratch); placement pipelines carry no cpuset binds
+            kg_numa_out o;
+            kg_numa_pair_z<kg_zone_calc, false, false>(c, lrow[q], pd, o, kg_zone_calc{lrow[q]});
+            if (o.feasible)
+                key = ((unsigned long long)(total_of(c, fit, la, o.score) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
+        }
+    }
+    keys[tid] = key;
+}
+
 // Sequential commit of pods [pod_begin, pod_begin + n) given their per-tile partial keys (kslots per
 // (pod, tile): 1 = the tile's best key, KG_PARTIAL_SLOTS = the top-KG_TOPK list + slow slot).
 // One workgroup; per pod: (A) every tile's best untouched candidate and the re-scored touched nodes →
@@ -2141,13 +2194,15 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                                                                 int64_t *out_score, RsvArgs ra, int32_t kslots,
                                                                 int32_t *slow_list, int32_t *slow_count,
                                                                 int32_t rescore_slow, int32_t defer_last,
-                                                                const int32_t *prev_nodes, int32_t n_prev) {
+                                                                const int32_t *prev_nodes, int32_t n_prev,
+                                                                const unsigned long long *pvkeys) {
     constexpr int POD_DW = (int)(sizeof(kg_pod_dev) / 4);
     static_assert(sizeof(kg_pod_dev) % 4 == 0 && POD_DW <= KG_RESOLVE_THREADS, "pod rows are staged one dword per thread");
     __shared__ int32_t touched[KG_MAX_CHUNK];
     // pipelined placement: the previous chunk's placements, committed while this chunk's keys were being
     // evaluated — treated as touched (their keys may predate the commit; re-scored like touched nodes)
     __shared__ int32_t prevt[KG_MAX_CHUNK];
+    __shared__ int32_t prevq[KG_MAX_CHUNK];   // each one's index in prev_nodes (pvkeys' column)
     __shared__ int32_t n_prevt;
     // touched tiles (the key lists of the others are exact): ttile[t] = 0 none, s ∈ [1, KG_TSLOTS] the tile's slot in
     // tbits (a bit per node of the tile: "touched?" is one LDS read), 255 beyond KG_TSLOTS tiles (linear compares)
@@ -2246,7 +2301,9 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         for (int q = tid; q < n_prev; q += KG_RESOLVE_THREADS) {
             const int32_t node = prev_nodes[q];
             if (node < 0) continue;
-            prevt[atomicAdd(&n_prevt, 1)] = node;
+            const int slot = atomicAdd(&n_prevt, 1);
+            prevt[slot] = node;
+            prevq[slot] = q;
         }
         __syncthreads();
         if (tid == 0)
@@ -2254,6 +2311,10 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         __syncthreads();
     }
     const int np_prev = n_prevt;
+    // NodeNUMAResource: the (pod, previous-chunk node) keys computed beforehand by k_prev_keys, all pairs at once (each
+    // pod re-scored those nodes on its own: one single-lane NUMA pair chain per pod on the critical path); a pod takes
+    // a node's key unless an earlier pod of this chunk touched the node again (the touched re-score then)
+    const bool pv_pre = NUMA && pvkeys != nullptr;
     for (int j = 0; j < n; j++) {
         KG_RT(1);
         const int par = j & 1;
@@ -2365,7 +2426,15 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         // the previous chunk's nodes, on the upper half of the workgroup (the tile scan and the touched re-scores
         // run on the lower threads: each NodeNUMAResource re-score is a long single-lane chain)
         for (int q = tid - KG_RESOLVE_THREADS / 2; q >= 0 && q < np_prev && plain_ok; q += KG_RESOLVE_THREADS / 2) {
-            const unsigned long long k = pair_key<NUMA>(c, pl, pd, prevt[q], n_nodes, now_ns);
+            unsigned long long k;
+            if (pv_pre) {
+                const int32_t nd = prevt[q];
+                bool again = false;
+                for (int z = 0; z < nt; z++) again |= touched[z] == nd;
+                k = again ? 0ull : pvkeys[(int64_t)j * n_prev + prevq[q]];
+            } else {
+                k = pair_key<NUMA>(c, pl, pd, prevt[q], n_nodes, now_ns);
+            }
             best = best > k ? best : k;
         }
         // nodes outside the fp64 bounds are not in the lists: re-scored exactly, every pod
@@ -4194,7 +4263,8 @@ kg_status chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n,
 // defer_last: the chunk's last pod is only selected (out_node / out_score); its Reserve is host_reserve's
 kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, const uint32_t *partial_dev,
                         int32_t *out_node_dev, int64_t *out_score_dev, bool defer_last,
-                        const int32_t *prev_nodes_dev = nullptr, int32_t n_prev = 0) {
+                        const int32_t *prev_nodes_dev = nullptr, int32_t n_prev = 0,
+                        unsigned long long *pvkeys = nullptr) {
     if (pod_begin < 0 || n < 0 || n > KG_MAX_CHUNK || pod_begin + (int64_t)n > e->n_pods)
         return set_err(e, KG_ERR_RANGE, "bad chunk");
     if (n == 0) return KG_OK;
@@ -4208,6 +4278,14 @@ kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t
     st = slow_refresh(e);
     if (st) return st;
     const bool numa = (e->consts.plugins & KG_PLUGIN_NUMA) != 0;
+    // NodeNUMAResource: the previous chunk's nodes keyed for every pod at once (pvkeys: n × n_prev, the caller's)
+    const bool pv = numa && pvkeys && n_prev > 0 && !ra.rsv && n <= KG_NUMA_CHUNK_PODS && n_prev <= KG_NUMA_CHUNK_PODS;
+    if (pv) {
+        static_assert(KG_NUMA_CHUNK_PODS * KG_NUMA_CHUNK_PODS <= 256, "one thread per pair in one workgroup");
+        hipLaunchKernelGGL(k_prev_keys, dim3(1), dim3(256), 0, e->stream, e->consts, e->pl,
+                           e->pods + pod_begin, n, prev_nodes_dev, n_prev, e->n_nodes, now_ns, pvkeys);
+        HIP_TRY(e, hipGetLastError());
+    }
     auto *kres = ra.rsv ? (numa ? k_resolve<true, true> : k_resolve<true, false>)
                         : (numa ? k_resolve<false, true> : k_resolve<false, false>);
     hipLaunchKernelGGL(kres, dim3(1), dim3(KG_RESOLVE_THREADS), 0, e->stream,
@@ -4215,7 +4293,7 @@ kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t
                        partial_dev, (int32_t)tiles_total(e), e->n_nodes, now_ns, out_node_dev, out_score_dev, ra,
                        numa && n > e->numa_chunk_pods ? 1 : KG_PARTIAL_SLOTS, e->slow_list, e->slow_count,
                        numa ? 0 : 1,   // the NUMA chunk kernels list slow nodes themselves (exact pair path)
-                       defer_last ? 1 : 0, prev_nodes_dev, n_prev);
+                       defer_last ? 1 : 0, prev_nodes_dev, n_prev, pv ? pvkeys : nullptr);
     HIP_TRY(e, hipGetLastError());
     e->generation++;   // the resolve commits the chunk's winners to the snapshot
     return KG_OK;
@@ -4439,7 +4517,9 @@ kg_status ncache_build(kg_engine *e, int64_t now_ns) {
 kg_status ncache_refresh(kg_engine *e, int64_t now_ns, const int32_t *nodes, int32_t n, hipStream_t s) {
     const int64_t total = (int64_t)e->eq_n * n;
     if (total <= 0) return KG_OK;
-    hipLaunchKernelGGL(k_ncache_refresh, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, e->consts, e->pl,
+    if (n > KG_NUMA_CHUNK_PODS) return set_err(e, KG_ERR_RANGE, "cache refresh of more than %d nodes", KG_NUMA_CHUNK_PODS);
+    hipLaunchKernelGGL(k_ncache_refresh, dim3((unsigned)((e->eq_n + KG_NUMA_CHUNK_PODS - 1) / KG_NUMA_CHUNK_PODS)), dim3(256), 0, s,
+                       e->consts, e->pl,
                        e->eq_pods, e->eq_n, nodes, n, now_ns, e->ncache, e->ncache_stride, e->shard_begin, e->shard_end);
     HIP_TRY(e, hipGetLastError());
     return KG_OK;
@@ -4450,12 +4530,14 @@ kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64
     const int32_t P = e->n_pods;
     const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS;
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
-    kg_status st = ensure_scratch(e, 2 * up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + 256);
+    const size_t pvk_b = up((size_t)chunk * (size_t)chunk * 8);
+    kg_status st = ensure_scratch(e, 2 * up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + pvk_b + 256);
     if (st) return st;
     char *s = (char *)e->scratch;
     uint32_t *part[2] = {(uint32_t *)s, (uint32_t *)(s + up(part_b))};
     int32_t *dnode = (int32_t *)(s + 2 * up(part_b));
     int64_t *dscore = (int64_t *)(s + 2 * up(part_b) + up((size_t)P * 4));
+    unsigned long long *pvkeys = (unsigned long long *)(s + 2 * up(part_b) + up((size_t)P * 4) + up((size_t)P * 8));
     if (!e->stream2) {
         HIP_TRY(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
         HIP_TRY(e, hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
@@ -4506,7 +4588,7 @@ kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64
         HIP_TRY(e, hipEventRecord(e->ev_join, eval_s));
         HIP_TRY(e, hipStreamWaitEvent(main_s, e->ev_join, 0));
         st = chunk_resolve(e, now_ns, b, n, part[i & 1], dnode + b, dscore + b, false, i ? dnode + prev_b : nullptr,
-                           i ? prev_n : 0);
+                           i ? prev_n : 0, pvkeys);
         if (st) return fail(st);
         HIP_TRY(e, hipEventRecord(e->ev_res[i % 3], main_s));
         prev_b = b;
