@@ -4505,9 +4505,11 @@ kg_status ncache_build(kg_engine *e, int64_t now_ns) {
     e->ctr = ctr0;
     if (st) return st;
     const int64_t total = (int64_t)U * stride;
-    hipLaunchKernelGGL(k_ncache_init, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, e->stream, mask, numa, U,
-                       (int32_t)words, stride, width, cache);
-    HIP_TRY(e, hipGetLastError());
+    if (total > 0) {   // (an empty shard has no cache columns)
+        hipLaunchKernelGGL(k_ncache_init, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, e->stream, mask, numa, U,
+                           (int32_t)words, stride, width, cache);
+        HIP_TRY(e, hipGetLastError());
+    }
     e->ncache = cache;
     e->ncache_stride = stride;
     return KG_OK;
