@@ -4562,8 +4562,12 @@ kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64
         kg_engine *e;
         ~NcacheScope() { e->ncache_live = false; }
     } ncache_scope{e};
+    // (the refresh re-evaluates U pairs per committed node where a chunk evaluation takes one per node: worth it while
+    // the distinct rows are a fraction of the shard's nodes; the build's matrix outputs stay within 8 GiB)
+    const int64_t ncache_width = e->shard_end - e->shard_begin;
     if ((e->consts.plugins & KG_PLUGIN_NUMA) && e->eq_on && !e->consts.numa_bz && !(e->forms & KG_FORM_NUMA_NO_CACHE) &&
-        P > 2 * chunk && chunk <= e->numa_chunk_pods) {
+        P > 2 * chunk && chunk <= e->numa_chunk_pods && 4 * (int64_t)e->eq_n <= ncache_width &&
+        (int64_t)e->eq_n * ((ncache_width + 63) / 64 * 64) * 7 <= (int64_t)8 << 30) {
         st = ncache_build(e, now_ns);
         if (st) return st;
         e->ncache_live = true;
