@@ -1587,42 +1587,34 @@ __global__ __launch_bounds__(256) void k_ncache_init(const unsigned long long *_
     cache[i] = ok ? numa[i] : (uint8_t)KG_NCACHE_NO;
 }
 
-// the committed nodes of one chunk (nodes[0..n), −1 for an unplaced pod; host-checked n ≤ KG_NUMA_CHUNK_PODS) re-evaluated
-// for every distinct row: workgroup b takes rows [16b, 16b + 16), a thread per (row, node), both staged in LDS; the same
-// pair functions as k_eval_numa2 (its zone-table provider derives every value with the functions kg_zone_calc calls, so
-// the results are identical)
-__global__ __launch_bounds__(256) void k_ncache_refresh(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ rows,
-                                                        int32_t U, const int32_t *__restrict__ nodes, int32_t n,
-                                                        int64_t now_ns, uint8_t *__restrict__ cache, int64_t stride,
-                                                        int64_t col_begin, int64_t col_end) {
-    constexpr int G = KG_NUMA_CHUNK_PODS;
-    static_assert(G * G == 256, "a thread per (row, node) of a 16 × 16 block");
-    __shared__ __attribute__((aligned(16))) kg_node_row lrow[G];
-    __shared__ __attribute__((aligned(16))) kg_pod_dev lpd[G];
+// the committed nodes of one chunk (nodes[0..n), −1 for an unplaced pod) re-evaluated for every distinct row: one
+// single-wave workgroup per (row, node), every lane on that pair, its node and pod rows staged in LDS (k_prev_keys'
+// form); the same pair functions as k_eval_numa2 (its zone-table provider derives every value with the functions
+// kg_zone_calc calls, so the results are identical)
+__global__ __launch_bounds__(64) void k_ncache_refresh(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ rows,
+                                                       int32_t U, const int32_t *__restrict__ nodes, int32_t n,
+                                                       int64_t now_ns, uint8_t *__restrict__ cache, int64_t stride,
+                                                       int64_t col_begin, int64_t col_end) {
+    __shared__ __attribute__((aligned(16))) kg_node_row lrow;
+    __shared__ __attribute__((aligned(16))) kg_pod_dev lpd;
     constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16), POD_DW = (int)(sizeof(kg_pod_dev) / 4);
+    const int64_t i = blockIdx.x;
     const int tid = threadIdx.x;
-    const int u0 = blockIdx.x * G, nu = U - u0 < G ? U - u0 : G;
-    for (int x = tid; x < n * ROW_U4; x += 256) {
-        const int q = x / ROW_U4, w = x - q * ROW_U4;
-        const int64_t nd = nodes[q];
-        if (nd >= col_begin && nd < col_end) reinterpret_cast<uint4 *>(&lrow[q])[w] = reinterpret_cast<const uint4 *>(pl.rows + nd)[w];
-    }
-    for (int x = tid; x < nu * POD_DW; x += 256)
-        reinterpret_cast<uint32_t *>(lpd)[x] = reinterpret_cast<const uint32_t *>(rows + u0)[x];
-    __syncthreads();
-    const int ul = tid / G, k = tid % G;
-    if (ul >= nu || k >= n) return;
+    if (n <= 0 || i >= (int64_t)U * n) return;   // block-uniform
+    const int32_t u = (int32_t)(i / n), k = (int32_t)(i % n);
     const int64_t node = nodes[k];
     if (node < col_begin || node >= col_end) return;
-    const kg_pod_dev &pd = lpd[ul];
+    for (int x = tid; x < ROW_U4; x += 64) reinterpret_cast<uint4 *>(&lrow)[x] = reinterpret_cast<const uint4 *>(pl.rows + node)[x];
+    for (int x = tid; x < POD_DW; x += 64) reinterpret_cast<uint32_t *>(&lpd)[x] = reinterpret_cast<const uint32_t *>(rows + u)[x];
+    __syncthreads();
     NodeRegs nr;
     load_node(c, pl, node, true, BatchMasks{0xFFu, 0xFFu}, now_ns, nr);
     uint32_t fit, la;
-    bool ok = eval_pair(c, pl, pd, nr, node, now_ns, fit, la);
+    bool ok = eval_pair(c, pl, lpd, nr, node, now_ns, fit, la);
     kg_numa_out o;
-    kg_numa_pair_z<kg_zone_calc, false, false>(c, lrow[k], pd, o, kg_zone_calc{lrow[k]});
+    kg_numa_pair_z<kg_zone_calc, false, false>(c, lrow, lpd, o, kg_zone_calc{lrow});
     ok = ok && o.feasible;
-    cache[(int64_t)(u0 + ul) * stride + (node - col_begin)] = ok ? (uint8_t)o.score : (uint8_t)KG_NCACHE_NO;
+    if (tid == 0) cache[(int64_t)u * stride + (node - col_begin)] = ok ? (uint8_t)o.score : (uint8_t)KG_NCACHE_NO;
 }
 
 // k_eval_numa_chunk with the pair's Filter + NodeNUMAResource outcome read from the cache row of the pod's distinct
@@ -2131,42 +2123,38 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
 }
 
 // NodeNUMAResource, pipelined placement: the keys of every (chunk pod j, previous-chunk node q) pair, keys[j · n_prev + q],
-// after the previous chunk's resolve and before this chunk's (k_resolve's pvkeys).  One workgroup, a thread per pair
-// (host-checked: n, n_prev ≤ KG_NUMA_CHUNK_PODS); the nodes' canonical rows and the pods' rows staged in LDS first
-// (the hint enumeration re-reads the zone fields in every loop: from global memory it was a 187k-cycle chain).
-__global__ __launch_bounds__(256) void k_prev_keys(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t n,
-                                                   const int32_t *__restrict__ prev_nodes, int32_t n_prev, int64_t n_nodes,
-                                                   int64_t now_ns, unsigned long long *__restrict__ keys) {
-    __shared__ __attribute__((aligned(16))) kg_node_row lrow[KG_NUMA_CHUNK_PODS];
-    __shared__ __attribute__((aligned(16))) kg_pod_dev lpd[KG_NUMA_CHUNK_PODS];
+// after the previous chunk's resolve and before this chunk's (k_resolve's pvkeys).  One single-wave workgroup per pair,
+// every lane on the same pair (the node's row and the pod's row staged in LDS): lanes of one wave on different pairs
+// ran the union of their hint enumerations (r05 PMC: ≈ 13k instructions per wave at ≈ 12 cycles each), the slowest
+// wave setting the launch's length.
+__global__ __launch_bounds__(64) void k_prev_keys(kg_consts c, kg_planes pl, const kg_pod_dev *__restrict__ pods, int32_t n,
+                                                  const int32_t *__restrict__ prev_nodes, int32_t n_prev, int64_t n_nodes,
+                                                  int64_t now_ns, unsigned long long *__restrict__ keys) {
+    __shared__ __attribute__((aligned(16))) kg_node_row lrow;
+    __shared__ __attribute__((aligned(16))) kg_pod_dev lpd;
     constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16), POD_DW = (int)(sizeof(kg_pod_dev) / 4);
-    const int tid = threadIdx.x;
-    for (int x = tid; x < n_prev * ROW_U4; x += 256) {
-        const int q = x / ROW_U4, w = x - q * ROW_U4;
-        const int64_t node = prev_nodes[q];
-        if (node >= 0 && node < n_nodes) reinterpret_cast<uint4 *>(&lrow[q])[w] = reinterpret_cast<const uint4 *>(pl.rows + node)[w];
-    }
-    for (int x = tid; x < n * POD_DW; x += 256)
-        reinterpret_cast<uint32_t *>(lpd)[x] = reinterpret_cast<const uint32_t *>(pods)[x];
-    __syncthreads();
-    if (tid >= n * n_prev) return;
-    const int j = tid / n_prev, q = tid - j * n_prev;
+    const int i = blockIdx.x, tid = threadIdx.x;
+    if (i >= n * n_prev) return;   // block-uniform
+    const int j = i / n_prev, q = i - j * n_prev;
     const int64_t node = prev_nodes[q];
-    const kg_pod_dev &pd = lpd[j];
+    const bool in = node >= 0 && node < n_nodes;
+    for (int x = tid; in && x < ROW_U4; x += 64) reinterpret_cast<uint4 *>(&lrow)[x] = reinterpret_cast<const uint4 *>(pl.rows + node)[x];
+    for (int x = tid; x < POD_DW; x += 64) reinterpret_cast<uint32_t *>(&lpd)[x] = reinterpret_cast<const uint32_t *>(pods + j)[x];
+    __syncthreads();
     unsigned long long key = 0;
-    if (node >= 0 && node < n_nodes && !(pd.flags & KGP_RSV_REQUIRED)) {
+    if (in && !(lpd.flags & KGP_RSV_REQUIRED)) {
         NodeRegs nr;
         load_node(c, pl, node, true, BatchMasks{0xFFu, 0xFFu}, now_ns, nr);
         uint32_t fit, la;
-        if (eval_pair(c, pl, pd, nr, node, now_ns, fit, la)) {
+        if (eval_pair(c, pl, lpd, nr, node, now_ns, fit, la)) {
             // inlined (kg_numa_eval_any is a call: its frame in scratch); placement pipelines carry no cpuset binds
             kg_numa_out o;
-            kg_numa_pair_z<kg_zone_calc, false, false>(c, lrow[q], pd, o, kg_zone_calc{lrow[q]});
+            kg_numa_pair_z<kg_zone_calc, false, false>(c, lrow, lpd, o, kg_zone_calc{lrow});
             if (o.feasible)
                 key = ((unsigned long long)(total_of(c, fit, la, o.score) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
         }
     }
-    keys[tid] = key;
+    if (tid == 0) keys[i] = key;
 }
 
 // Sequential commit of pods [pod_begin, pod_begin + n) given their per-tile partial keys (kslots per
@@ -4281,8 +4269,7 @@ kg_status chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t
     // NodeNUMAResource: the previous chunk's nodes keyed for every pod at once (pvkeys: n × n_prev, the caller's)
     const bool pv = numa && pvkeys && n_prev > 0 && !ra.rsv && n <= KG_NUMA_CHUNK_PODS && n_prev <= KG_NUMA_CHUNK_PODS;
     if (pv) {
-        static_assert(KG_NUMA_CHUNK_PODS * KG_NUMA_CHUNK_PODS <= 256, "one thread per pair in one workgroup");
-        hipLaunchKernelGGL(k_prev_keys, dim3(1), dim3(256), 0, e->stream, e->consts, e->pl,
+        hipLaunchKernelGGL(k_prev_keys, dim3((unsigned)(n * n_prev)), dim3(64), 0, e->stream, e->consts, e->pl,
                            e->pods + pod_begin, n, prev_nodes_dev, n_prev, e->n_nodes, now_ns, pvkeys);
         HIP_TRY(e, hipGetLastError());
     }
@@ -4520,8 +4507,7 @@ kg_status ncache_refresh(kg_engine *e, int64_t now_ns, const int32_t *nodes, int
     const int64_t total = (int64_t)e->eq_n * n;
     if (total <= 0) return KG_OK;
     if (n > KG_NUMA_CHUNK_PODS) return set_err(e, KG_ERR_RANGE, "cache refresh of more than %d nodes", KG_NUMA_CHUNK_PODS);
-    hipLaunchKernelGGL(k_ncache_refresh, dim3((unsigned)((e->eq_n + KG_NUMA_CHUNK_PODS - 1) / KG_NUMA_CHUNK_PODS)), dim3(256), 0, s,
-                       e->consts, e->pl,
+    hipLaunchKernelGGL(k_ncache_refresh, dim3((unsigned)total), dim3(64), 0, s, e->consts, e->pl,
                        e->eq_pods, e->eq_n, nodes, n, now_ns, e->ncache, e->ncache_stride, e->shard_begin, e->shard_end);
     HIP_TRY(e, hipGetLastError());
     return KG_OK;
