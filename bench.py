@@ -48,7 +48,10 @@ def parse():
     ap.add_argument("--nodes", type=int, default=100_000,
                     help="global nodes (strong) or nodes per GPU (weak); config4 uses 1M")
     ap.add_argument("--scaling", choices=("strong", "config4", "weak"), default="strong")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: CPU rehearsal of N > 1)")
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend (gloo: CPU rehearsal of N > 1); loopback: gloo for the matrix-mode "
+                         "merge and kg_place_sharded's native loop over the host shared-memory communicator "
+                         "(kg_comm_init_loopback), so N ranks can share one GPU")
     ap.add_argument("--no-placement", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-distinct", action="store_true", help="skip the config2_distinct section")
@@ -60,6 +63,8 @@ def parse():
     ap.add_argument("--c5-pods", type=int, default=100_000,
                     help="config-5 (Reservation + ElasticQuota) pods placed in sequence; 0 skips it")
     ap.add_argument("--c5-matrix-pods", type=int, default=1_000, help="config-5 matrix-mode pods")
+    ap.add_argument("--dropin-cycles", type=int, default=1_000,
+                    help="one-pod scheduling cycles through the C-ABI (kg_pods_set, kg_eval to host, kg_commit); 0 skips")
     ap.add_argument("--la-extra-pods", type=int, default=1_000,
                     help="matrix-mode pods with LoadAware resourceWeights beyond cpu / memory (k_eval_exact); 0 skips")
     return ap.parse_args()
@@ -286,6 +291,60 @@ def bench_host_outputs(args, engine, eng, P, N, now, dev):
             "top1_only": {"evals_per_s": round(P * N / dt2, 1), "ms_per_step": round(dt2 * 1e3, 3)}}
 
 
+def bench_dropin_cycle(args, engine, eng, node_rows, pod_rows, now, ref_nodes):
+    """The drop-in boundary as the Go scheduler drives it: scheduleOne is per pod, so every
+    cycle is one pod — PreFilter uploads its row (kg_pods_set, P = 1), Filter / Score read the pod's planes from one
+    kg_eval over all nodes into pinned host memory (feasibility bits + {Fit, LoadAware} u8 scores + top-1: what the
+    plugins' O(1) lookups read), selectHost takes the best node, Reserve commits it (kg_commit).  µs per cycle over
+    `--dropin-cycles` pods of the config-2 queue, from the same snapshot as kg_place; the placements must equal
+    kg_place's (the sequential cycle) pod for pod."""
+    import torch
+
+    C = min(args.dropin_cycles, len(pod_rows))
+    N = len(node_rows)
+    W = (N + 63) // 64
+    mask = torch.empty((1, W), dtype=torch.int64, pin_memory=True)
+    scores = torch.empty((1, W * 64, 2), dtype=torch.uint8, pin_memory=True)
+    top1 = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+    top_np = top1.numpy().view(np.uint64)
+    eng.load_snapshot(node_rows)
+
+    def cycles(planes: bool, n: int, out=None):
+        t0 = time.perf_counter()
+        for p in range(n):
+            eng.set_pods(pod_rows[p:p + 1])
+            eng.eval_host(now, mask.data_ptr() if planes else 0, scores.data_ptr() if planes else 0, top1.data_ptr())
+            node = -1 if top_np[0] == 0 else int(0xFFFFFFFF - (int(top_np[0]) & 0xFFFFFFFF))
+            if node >= 0:
+                eng.commit(0, node)
+            if out is not None:
+                out.append(node)
+        return time.perf_counter() - t0
+
+    cycles(True, 8)   # warm-up (first-use allocations), then from the fresh snapshot
+    eng.load_snapshot(node_rows)
+    got = []
+    dt = cycles(True, C, got)
+    eng.load_snapshot(node_rows)
+    dt_top = cycles(False, C)
+    eng.load_snapshot(node_rows)
+    # the batch upload alone (kg_pods_set's class / equivalence grouping of the 10k headline batch, host work outside
+    # every other timer)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        eng.set_pods(pod_rows)
+        ts.append(time.perf_counter() - t0)
+    return {"workload": f"config2: {C} pods, one scheduling cycle each over {N} nodes (kg_pods_set P = 1 -> kg_eval "
+                        "into pinned host planes -> selectHost -> kg_commit)",
+            "cycles": C, "us_per_cycle": round(dt / C * 1e6, 1), "pods_per_s": round(C / dt, 1),
+            "top1_only": {"us_per_cycle": round(dt_top / C * 1e6, 1), "pods_per_s": round(C / dt_top, 1)},
+            "host_bytes_per_cycle": int(W * 8 + W * 64 * 2 + 8),
+            "matches_kg_place": bool(np.array_equal(np.asarray(got), np.asarray(ref_nodes[:C]))),
+            "pods_set_10k_ms": {"median": round(float(np.median(ts)) * 1e3, 2), "runs": [round(t * 1e3, 2) for t in ts],
+                                "pods": int(len(pod_rows))}}
+
+
 def bench_la_extra(args, engine, synth, shipped_profile, dev, stream):
     """Matrix mode with LoadAware resourceWeights beyond cpu / memory (ephemeral-storage, an extended resource,
     batch-cpu; estimatedScalingFactors for the first two): k_eval2's LAX form reads fp64 planes of the weighted
@@ -447,13 +506,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
-    gpu = local % ndev if args.backend == "gloo" else local
+    gpu = local % ndev if args.backend != "nccl" else local
     if world > 1:
         torch.cuda.set_device(gpu)
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
-            dist.init_process_group(args.backend)
+            dist.init_process_group("gloo" if args.backend == "loopback" else args.backend)
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
@@ -555,8 +614,10 @@ def main():
         from koordinator_amd import dist as kdist
         all_rows = global_rows if global_rows is not None else np.concatenate(
             [engine.build_node_rows(cfg, synth.make_cluster(N, 1, seed=2 + 7919 * r)) for r in range(world)])
-        native = args.backend == "nccl"   # kg_place_sharded on the engine's own RCCL communicator
-        deng = (kdist.native_engine(cfg, all_rows, pod_rows, dev, stream=stream) if native
+        # kg_place_sharded on the engine's own communicator: RCCL, or the loopback one (ranks sharing a GPU)
+        native = args.backend in ("nccl", "loopback")
+        comm = "loopback" if args.backend == "loopback" else "rccl"
+        deng = (kdist.native_engine(cfg, all_rows, pod_rows, dev, stream=stream, comm=comm) if native
                 else kdist.sharded_engine(cfg, all_rows, pod_rows, dev))
         dist.barrier()
         torch.cuda.synchronize(dev)
@@ -567,11 +628,12 @@ def main():
             nodes, tot = kdist.place_sharded(deng, now, dev, chunk=kdist.place_chunk_of(cfg))
         dist.barrier()
         tp1 = time.perf_counter()
+        deng_kind = deng.comm_kind() if native else None
         deng.close()
         placement = {"pods": P, "nodes": total, "seconds": round(tp1 - tp0, 6),
                      "pods_placed_per_s": round(P / (tp1 - tp0), 1), "placed": int((nodes >= 0).sum()),
                      "chunk": int(cfg["place_chunk"]),
-                     "mode": (f"kg_place_sharded over {world} ranks (RCCL)" if native
+                     "mode": (f"kg_place_sharded over {world} ranks ({deng_kind})" if native
                               else f"dist.place_sharded over {world} ranks ({args.backend})")}
 
     cpu_baseline = None
@@ -605,6 +667,14 @@ def main():
                                        f"over nodes per pod (kgo_schedule_parallel); median of {len(t2s)} runs",
                              "runs_s": t2s},
                 "host": host_info()}
+
+    dropin = None
+    if args.dropin_cycles > 0 and world == 1 and placement is not None:
+        dropin = bench_dropin_cycle(args, engine, eng, node_rows, pod_rows, now, nodes)
+        if placement.get("cpu_baseline"):
+            seq = placement["cpu_baseline"]["sequential"]
+            dropin["cpu_baseline"] = {"us_per_cycle": round(1e6 / seq["value"], 1), "kind": "port", "cores": 1,
+                                      "sample": "the oracle's sequential cycle per pod (placement.cpu_baseline.sequential)"}
 
     distinct = None
     if not args.no_distinct and world == 1:
@@ -661,6 +731,7 @@ def main():
             "cpu_baseline": cpu_baseline,
             "placement": placement,
             "host_outputs": host_out,
+            "dropin_cycle": dropin,
             "config2_distinct": distinct,
             "config3": config3,
             "config5": config5,

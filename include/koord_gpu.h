@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 11
+#define KG_ABI_VERSION 12
 #define KG_QUOTA_MAX_DEPTH 64 /* longest kg_quota parent chain (cycles are rejected) */
 
 /* largest kg_config.place_chunk / kg_place_chunk_resolve chunk (the resolve kernel's touched list) */
@@ -668,6 +668,21 @@ kg_status kg_place(kg_engine *eng, int64_t now_ns, int32_t *out_node, int64_t *o
 #define KG_COMM_ID_BYTES 128
 kg_status kg_comm_unique_id(void *out /* KG_COMM_ID_BYTES */);
 kg_status kg_comm_init(kg_engine *eng, int32_t rank, int32_t world, const void *unique_id);
+/* The loopback communicator: the ranks (processes of one host, on one GPU or several) merge the partial keys
+ * through a POSIX shared-memory segment `name` ("/…", the same on every rank; unlinked once every rank has joined)
+ * instead of RCCL, running the same chunk loop — the rehearsal of kg_place_sharded where RCCL cannot form a
+ * communicator (two ranks on one device).  Needs the snapshot loaded (the slots follow its tile count); a rank that
+ * does not arrive within 120 s fails the others' waits with KG_ERR_STATE instead of hanging them. */
+kg_status kg_comm_init_loopback(kg_engine *eng, int32_t rank, int32_t world, const char *name);
+#define KG_COMM_NONE 0
+#define KG_COMM_RCCL 1
+#define KG_COMM_LOOPBACK 2
+int32_t kg_comm_kind(const kg_engine *eng);
+/* Failure contract: the ranks first agree (one status all-reduce) that each set up its loop; if any failed, none
+ * enters it — that rank returns its error, the others KG_ERR_STATE, nothing is placed.  A step that fails inside
+ * the loop (not a HIP fault) turns the rest of that rank's loop into merges of zero keys flagged as failed, so no
+ * peer blocks in a collective; every rank then returns an error and is stale (reload the snapshot).  A HIP fault
+ * leaves the device unusable: RCCL peers may then block in their next collective (loopback peers time out). */
 kg_status kg_place_sharded(kg_engine *eng, int64_t now_ns, int32_t *out_node, int64_t *out_score);
 
 /* Multi-GPU building blocks of kg_place (see koordinator_amd/dist.py); pods that bind cpusets are refused
@@ -686,7 +701,8 @@ kg_status kg_place_chunk_resolve(kg_engine *eng, int64_t now_ns, int32_t pod_beg
  * and re-scores them like nodes this chunk touches (their keys in the lists are not trusted), exactly as the
  * one-GPU kg_place pipeline does.  The caller orders the streams: eval(i + 1) after resolve(i − 1), resolve(i)
  * after eval(i) and its merge.  Not with reservations (their per-pod entries are written by chunk_eval).
- * kg_set_eval_stream: the stream kg_place_chunk_eval launches on (NULL ⇒ the engine stream); no sync. */
+ * kg_set_eval_stream: the stream kg_place_chunk_eval launches on (NULL ⇒ the engine stream); no sync.  A resolve
+ * waits (on the device) for the kg_place_chunk_eval that last wrote its partial_dev, not for later evaluations. */
 kg_status kg_place_chunk_resolve_prev(kg_engine *eng, int64_t now_ns, int32_t pod_begin, int32_t n,
                                       const uint32_t *partial_dev, int32_t *out_node_dev, int64_t *out_score_dev,
                                       const int32_t *prev_nodes_dev, int32_t n_prev);

@@ -15,8 +15,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ENGINE_SO = os.environ.get("KG_ENGINE_SO") or os.path.join(_HERE, "lib", "libkoordgpu.so")
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 COMM_ID_BYTES = 128   # KG_COMM_ID_BYTES
+COMM_NONE, COMM_RCCL, COMM_LOOPBACK = 0, 1, 2   # kg_comm_kind
 # kg_set_forms bits (include/koord_gpu.h)
 FORM_PLACE_PIPELINE, FORM_PLACE_SEQUENTIAL, FORM_NUMA_QUEUED, FORM_NUMA_CHUNK_TILE = 0x1, 0x2, 0x4, 0x8
 FORM_NUMA_NO_CACHE = 0x10
@@ -215,7 +216,7 @@ EXPORTED = [
     "kg_rsv_set", "kg_rsv_download", "kg_quota_set", "kg_quota_download", "kg_row_eval_rsv", "kg_row_rsv_restore",
     "kg_snapshot_generation", "kg_cpuset_take", "kg_row_reserve", "kg_cpus_set", "kg_cpus_download",
     "kg_place_chunk_resolve_prev", "kg_set_eval_stream", "kg_set_forms", "kg_comm_unique_id", "kg_comm_init",
-    "kg_place_sharded", "kg_counters_get", "kg_counters_reset",
+    "kg_place_sharded", "kg_counters_get", "kg_counters_reset", "kg_comm_init_loopback", "kg_comm_kind",
 ]
 
 _lib = None
@@ -265,6 +266,7 @@ def lib() -> ctypes.CDLL:
         "kg_set_eval_stream": (i32, [vp, vp]), "kg_set_forms": (i32, [vp, ctypes.c_uint32]),
         "kg_comm_unique_id": (i32, [vp]), "kg_comm_init": (i32, [vp, i32, i32, vp]),
         "kg_place_sharded": (i32, [vp, ctypes.c_int64, vp, vp]), "kg_counters_get": (i32, [vp, vp]), "kg_counters_reset": (i32, [vp]),
+        "kg_comm_init_loopback": (i32, [vp, i32, i32, ctypes.c_char_p]), "kg_comm_kind": (i32, [vp]),
     }
     for name, (res, args) in sig.items():
         if host_only and not hasattr(L, name):

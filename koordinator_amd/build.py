@@ -35,11 +35,13 @@ def _newer(target: str, sources: list[str]) -> bool:
 
 
 def engine_sources() -> list[str]:
-    names = ["kg_engine.hip", "kg_host.cpp", "kg_cpuset.cpp", "kg_common.h", "kg_host.h"]
+    names = ["kg_engine.hip", "kg_host.cpp", "kg_cpuset.cpp", "kg_comm.cpp", "kg_common.h", "kg_host.h", "kg_comm.h"]
     return [os.path.join(CSRC, n) for n in names] + [os.path.join(ROOT, "include", "koord_gpu.h")]
 
 
 def build_engine(force: bool = False) -> str:
+    """Each object is rebuilt only when its own sources are newer (the device object takes minutes; the host
+    objects seconds), then the library is linked."""
     os.makedirs(LIB_DIR, exist_ok=True)
     if not force and not _newer(ENGINE_SO, engine_sources()):
         return ENGINE_SO
@@ -47,16 +49,44 @@ def build_engine(force: bool = False) -> str:
     obj_dir = os.path.join(LIB_DIR, "obj")
     os.makedirs(obj_dir, exist_ok=True)
     common = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
-    host_obj = os.path.join(obj_dir, "kg_host.o")
-    _run(["g++", *common, "-c", os.path.join(CSRC, "kg_host.cpp"), "-o", host_obj])
-    cpuset_obj = os.path.join(obj_dir, "kg_cpuset.o")
-    _run(["g++", *common, "-c", os.path.join(CSRC, "kg_cpuset.cpp"), "-o", cpuset_obj])
+    hdr = [os.path.join(ROOT, "include", "koord_gpu.h"), os.path.join(CSRC, "kg_common.h"), os.path.join(CSRC, "kg_host.h")]
+    objs = []
+    for src, extra in (("kg_host.cpp", []), ("kg_cpuset.cpp", []), ("kg_comm.cpp", [os.path.join(CSRC, "kg_comm.h")])):
+        obj = os.path.join(obj_dir, src.rsplit(".", 1)[0] + ".o")
+        if force or _newer(obj, [os.path.join(CSRC, src), *hdr, *extra]):
+            _run(["g++", *common, "-c", os.path.join(CSRC, src), "-o", obj])
+        objs.append(obj)
     dev_obj = os.path.join(obj_dir, "kg_engine.o")
-    _run([hipcc, *common, f"--offload-arch={ARCH}", "-c", os.path.join(CSRC, "kg_engine.hip"), "-o", dev_obj])
+    if force or _newer(dev_obj, [os.path.join(CSRC, "kg_engine.hip"), os.path.join(CSRC, "kg_comm.h"), *hdr]):
+        _run([hipcc, *common, f"--offload-arch={ARCH}", "-c", os.path.join(CSRC, "kg_engine.hip"), "-o", dev_obj])
     tmp = ENGINE_SO + ".tmp"
-    _run([hipcc, "-shared", f"--offload-arch={ARCH}", dev_obj, host_obj, cpuset_obj, "-o", tmp])
+    _run([hipcc, "-shared", f"--offload-arch={ARCH}", dev_obj, *objs, "-lrt", "-o", tmp])
     os.replace(tmp, ENGINE_SO)
     return ENGINE_SO
+
+
+BOUNDS_SO = os.path.join(LIB_DIR, "libkoordgpu_bounds.so")
+
+
+def build_bounds(force: bool = False) -> str:
+    """The bounds-checked engine (-DKG_BOUNDS_CHECK): every index into the pipelined placement's shared buffers is
+    checked on the device and a violation is reported by the next kg_place / kg_eval instead of faulting.  A debug
+    library beside the product one (loaded through KG_ENGINE_SO by tests/test_bounds_gpu.py); not built by default."""
+    if not force and not _newer(BOUNDS_SO, engine_sources()):
+        return BOUNDS_SO
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    common = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
+    dev_obj = os.path.join(obj_dir, "kg_engine_bounds.o")
+    _run([hipcc, *common, "-DKG_BOUNDS_CHECK", f"--offload-arch={ARCH}", "-c", os.path.join(CSRC, "kg_engine.hip"),
+          "-o", dev_obj])
+    objs = [os.path.join(obj_dir, n) for n in ("kg_host.o", "kg_cpuset.o", "kg_comm.o")]
+    if not all(os.path.exists(o) for o in objs):
+        raise RuntimeError("build the product engine first (its host objects are linked into the bounds build)")
+    tmp = BOUNDS_SO + ".tmp"
+    _run([hipcc, "-shared", f"--offload-arch={ARCH}", dev_obj, *objs, "-lrt", "-o", tmp])
+    os.replace(tmp, BOUNDS_SO)
+    return BOUNDS_SO
 
 
 def oracle_sources() -> list[str]:
@@ -104,4 +134,7 @@ def build_all(force: bool = False) -> None:
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
+    if "--bounds" in sys.argv:
+        build_bounds(force="--force" in sys.argv)
+    else:
+        build_all(force="--force" in sys.argv)

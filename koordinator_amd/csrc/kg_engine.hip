@@ -35,6 +35,7 @@
 #include <string>
 #include <vector>
 
+#include "kg_comm.h"
 #include "kg_common.h"
 #include "kg_host.h"
 
@@ -46,6 +47,27 @@
 #define KG_MAX_TILES 4096        // max tiles per snapshot in k_resolve (2M nodes)
 #define KG_LAX 4                 // LoadAware extra resources k_eval2's LAX form carries (more: k_eval_exact)
 #define KG_XCDS 8                // workgroup b of a 1-D grid runs on XCD b % 8 (each XCD has its own L2)
+
+// Bounds-checked build (-DKG_BOUNDS_CHECK, koordinator_amd/build.py build_bounds → lib/libkoordgpu_bounds.so): the
+// indices of the pipelined placement's shared buffers (previous-chunk lists, pvkeys, the outcome cache, the touched
+// lists, the partial keys) are checked before use; a violation is recorded (count, first site / index / bound) and
+// the access skipped, and the next kg_place / kg_eval returns KG_ERR_STATE naming it — a test reads the violation
+// instead of faulting the GPU.  The product build compiles every check to `true`.
+#ifdef KG_BOUNDS_CHECK
+__device__ unsigned long long g_kg_oob[4];   // count, first site, first index, first bound
+__device__ __noinline__ bool kg_oob_ok(int site, int64_t idx, int64_t bound) {
+    if (idx >= 0 && idx < bound) return true;
+    if (atomicAdd(&g_kg_oob[0], 1ull) == 0ull) {
+        g_kg_oob[1] = (unsigned long long)site;
+        g_kg_oob[2] = (unsigned long long)idx;
+        g_kg_oob[3] = (unsigned long long)bound;
+    }
+    return false;
+}
+#define KG_IN(site, idx, bound) kg_oob_ok((site), (int64_t)(idx), (int64_t)(bound))
+#else
+#define KG_IN(site, idx, bound) true
+#endif
 
 // ---------------------------------------------------------------------------------------
 // wave reductions
@@ -1604,6 +1626,7 @@ __global__ __launch_bounds__(64) void k_ncache_refresh(kg_consts c, kg_planes pl
     const int32_t u = (int32_t)(i / n), k = (int32_t)(i % n);
     const int64_t node = nodes[k];
     if (node < col_begin || node >= col_end) return;
+    if (!KG_IN(20, (int64_t)u * stride + (node - col_begin), (int64_t)U * stride)) return;   // (block-uniform)
     for (int x = tid; x < ROW_U4; x += 64) reinterpret_cast<uint4 *>(&lrow)[x] = reinterpret_cast<const uint4 *>(pl.rows + node)[x];
     for (int x = tid; x < POD_DW; x += 64) reinterpret_cast<uint32_t *>(&lpd)[x] = reinterpret_cast<const uint32_t *>(rows + u)[x];
     __syncthreads();
@@ -1623,7 +1646,7 @@ __global__ __launch_bounds__(64) void k_ncache_refresh(kg_consts c, kg_planes pl
 __global__ __launch_bounds__(256) void k_eval_numa_cached(kg_consts c, kg_planes pl, HotArgs a,
                                                           const kg_pod_dev *__restrict__ pods, int32_t shard_tiles,
                                                           uint32_t *__restrict__ partials, const uint8_t *__restrict__ cache,
-                                                          const int32_t *__restrict__ cls_of, int64_t stride) {
+                                                          const int32_t *__restrict__ cls_of, int64_t stride, int32_t U) {
     __shared__ __attribute__((aligned(16))) kg_pod_dev lp;
     __shared__ __attribute__((aligned(16))) uint32_t kbuf[KG_TILE];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1635,8 +1658,9 @@ __global__ __launch_bounds__(256) void k_eval_numa_cached(kg_consts c, kg_planes
     for (int k = tid; k < POD_DW; k += 256)
         reinterpret_cast<uint32_t *>(&lp)[k] = reinterpret_cast<const uint32_t *>(pods + p)[k];
     __syncthreads();
-    const uint8_t *crow = cache + (int64_t)cls_of[p] * stride - a.col_begin;
     const int tile = a.tile_begin + tile_rel;
+    if (!KG_IN(30, cls_of[p], U) || !KG_IN(31, (int64_t)tile * KG_TILE - a.col_begin, stride)) return;   // (block-uniform)
+    const uint8_t *crow = cache + (int64_t)cls_of[p] * stride - a.col_begin;
     const BatchMasks bm{0xFFu, 0xFFu};
 #pragma unroll 1
     for (int v = 0; v < KG_TILE / 256; v++) {
@@ -2136,6 +2160,7 @@ __global__ __launch_bounds__(64) void k_prev_keys(kg_consts c, kg_planes pl, con
     const int i = blockIdx.x, tid = threadIdx.x;
     if (i >= n * n_prev) return;   // block-uniform
     const int j = i / n_prev, q = i - j * n_prev;
+    if (!KG_IN(10, q, n_prev) || !KG_IN(11, j, n)) return;   // (block-uniform)
     const int64_t node = prev_nodes[q];
     const bool in = node >= 0 && node < n_nodes;
     for (int x = tid; in && x < ROW_U4; x += 64) reinterpret_cast<uint4 *>(&lrow)[x] = reinterpret_cast<const uint4 *>(pl.rows + node)[x];
@@ -2290,6 +2315,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             const int32_t node = prev_nodes[q];
             if (node < 0) continue;
             const int slot = atomicAdd(&n_prevt, 1);
+            if (!KG_IN(40, slot, KG_MAX_CHUNK) || !KG_IN(46, node, n_nodes)) continue;
             prevt[slot] = node;
             prevq[slot] = q;
         }
@@ -2350,7 +2376,10 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 if (!k) continue;
                 const int32_t node = (int32_t)(0xFFFFFFFFull - (k & 0xFFFFFFFFull));
                 const bool hit = is_touched(ttile[t], node, nt, np_prev);
-                if (hit) rescan[atomicAdd(&n_rescan[par], 1)] = t;
+                if (hit) {
+                    const int ri = atomicAdd(&n_rescan[par], 1);
+                    if (KG_IN(42, ri, KG_MAX_TILES)) rescan[ri] = t;
+                }
                 else best = best > k ? best : k;
                 continue;
             }
@@ -2395,7 +2424,10 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 }
             }
             const bool need = !found && !ended;
-            if (need) rescan[atomicAdd(&n_rescan[par], 1)] = t;
+            if (need) {
+                const int ri = atomicAdd(&n_rescan[par], 1);
+                if (KG_IN(42, ri, KG_MAX_TILES)) rescan[ri] = t;
+            }
             else best = best > cand ? best : cand;
         }
         KG_RT_AT(0, 9);
@@ -2413,16 +2445,18 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
         KG_RT_AT(128, 8);
         // the previous chunk's nodes, on the upper half of the workgroup (the tile scan and the touched re-scores
         // run on the lower threads: each NodeNUMAResource re-score is a long single-lane chain)
+        // A node an earlier pod of this chunk committed again is left to the touched re-score above: its key in pvkeys
+        // predates that commit, and in the plain form (LDSB) its global row and planes may still be in flight behind
+        // the LDS-only barriers (a global re-read would see the node before the commit, with more free capacity).
         for (int q = tid - KG_RESOLVE_THREADS / 2; q >= 0 && q < np_prev && plain_ok; q += KG_RESOLVE_THREADS / 2) {
-            unsigned long long k;
-            if (pv_pre) {
-                const int32_t nd = prevt[q];
-                bool again = false;
+            const int32_t nd = prevt[q];
+            bool again = false;
+            if (pv_pre || LDSB)
                 for (int z = 0; z < nt; z++) again |= touched[z] == nd;
-                k = again ? 0ull : pvkeys[(int64_t)j * n_prev + prevq[q]];
-            } else {
-                k = pair_key<NUMA>(c, pl, pd, prevt[q], n_nodes, now_ns);
-            }
+            unsigned long long k = 0ull;
+            if (again) k = 0ull;
+            else if (pv_pre && KG_IN(41, prevq[q], n_prev)) k = pvkeys[(int64_t)j * n_prev + prevq[q]];
+            else k = pair_key<NUMA>(c, pl, pd, nd, n_nodes, now_ns);
             best = best > k ? best : k;
         }
         // nodes outside the fp64 bounds are not in the lists: re-scored exactly, every pod
@@ -2467,8 +2501,9 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             wb = wb > rk ? wb : rk;
         }
         const unsigned long long w = gate_ok[par] ? wb : 0ull;   // a pod failing the quota gate is unschedulable
-        const int32_t node = w ? (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull)) : -1;
-        if (!w || (defer_last && j == n - 1)) {
+        int32_t node = w ? (int32_t)(0xFFFFFFFFull - (w & 0xFFFFFFFFull)) : -1;
+        if (w && !KG_IN(44, node, n_nodes)) node = -1;   // (every thread decodes the same w)
+        if (node < 0 || (defer_last && j == n - 1)) {
             // no feasible node; or the chunk's last pod may bind a cpuset: it is selected here and reserved by
             // the host (the CPU accumulator) after the launch
             if (tid == 0) {
@@ -2627,7 +2662,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             fl_pods_full = (int64_t)pc + 1 > (int64_t)srow.allowed_pods ? 1 : 0;
             fl_old_df = old_df;
             if (ce) ce->metric_ns = old_metric;
-            if (slot == nt) {
+            if (slot == nt && KG_IN(43, n_touched, KG_MAX_CHUNK)) {
                 touched[n_touched++] = node;
                 mark(node);
                 const int32_t rk = rsv_on && ra.M ? pl.rsv_of[node] : -1;
@@ -2668,7 +2703,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             const uint32_t df = (old & ~KGD_DYNAMIC) | dyn;
             pl.dflags[node] = df;
             pl.fit_mask[node] = fmask;
-            if ((df & KGD_SLOW) && !(old & KGD_SLOW)) {   // the node left the fast paths: list it
+            if ((df & KGD_SLOW) && !(old & KGD_SLOW) && KG_IN(45, n_slow, pl.cap)) {   // the node left the fast paths: list it
                 slow_list[n_slow++] = node;
                 *slow_count = n_slow;
                 if (lds_only) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the list entry is read next pod
@@ -2816,10 +2851,18 @@ struct kg_engine {
     kg_counters ctr{};                  // kg_counters_get
     int64_t ev_acc = 0;                 // profiled launches already summed into ctr.kernel_ns
     ncclComm_t comm = nullptr;          // kg_comm_init: this rank's RCCL communicator (kg_place_sharded)
+    kg_shm_comm *shm = nullptr;         // kg_comm_init_loopback: the host shared-memory communicator (kg_comm.cpp)
+    uint32_t *shm_stage = nullptr;      // its pinned staging buffer (the slot size)
+    uint32_t *comm_word = nullptr;      // device word of the status all-reduce (comm_agree)
     int32_t comm_rank = 0, comm_world = 0;
     hipStream_t eval_stream = nullptr;  // kg_set_eval_stream (kg_place_chunk_eval), nullptr ⇒ stream
-    hipEvent_t ev_eval = nullptr;       // recorded on eval_stream after each kg_place_chunk_eval; the chunk resolve
-                                        // entries make the engine stream wait on its latest record
+    // recorded on eval_stream after each kg_place_chunk_eval, one per partial buffer (keyed by its address): a chunk
+    // resolve makes the engine stream wait for the evaluation that wrote the partials it reads, whatever the caller
+    // enqueued on the eval stream since
+    static constexpr int kEvalEvents = 4;
+    hipEvent_t ev_eval[kEvalEvents] = {};
+    const void *ev_eval_buf[kEvalEvents] = {};
+    int32_t ev_eval_next = 0;
     static constexpr int kRing = 256;   // event pairs: one per profiled k_eval launch
     hipEvent_t ev0[kRing] = {}, ev1[kRing] = {};
     int64_t ev_count = 0;               // launches recorded since kg_set_profiling
@@ -2879,6 +2922,23 @@ kg_status set_err(kg_engine *e, kg_status code, const char *fmt, ...) {
         hipError_t _st = (expr);                                                                 \
         if (_st != hipSuccess) return set_err(e, KG_ERR_HIP, "%s: %s", #expr, hipGetErrorString(_st)); \
     } while (0)
+
+// the bounds-checked build's verdict (KG_BOUNDS_CHECK): the violations the kernels recorded since the last call
+kg_status bounds_verdict(kg_engine *e) {
+#ifdef KG_BOUNDS_CHECK
+    unsigned long long v[4] = {};
+    HIP_TRY(e, hipDeviceSynchronize());
+    HIP_TRY(e, hipMemcpyFromSymbol(v, HIP_SYMBOL(g_kg_oob), sizeof(v)));
+    if (v[0]) {
+        const unsigned long long z[4] = {};
+        HIP_TRY(e, hipMemcpyToSymbol(HIP_SYMBOL(g_kg_oob), z, sizeof(z)));
+        return set_err(e, KG_ERR_STATE, "bounds check: %llu violations, the first at site %llu: index %lld outside [0, %lld)",
+                       v[0], v[1], (long long)v[2], (long long)v[3]);
+    }
+#endif
+    (void)e;
+    return KG_OK;
+}
 
 // host → device copies go through here (kg_counters.h2d_bytes)
 hipError_t h2d(kg_engine *e, void *dst, const void *src, size_t bytes, hipStream_t s) {
@@ -3388,7 +3448,7 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
         if (e->ncache_live && !e->consts.numa_bz)
             hipLaunchKernelGGL(k_eval_numa_cached, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
                                e->pods + pod_begin, (int32_t)shard_tiles, partials, e->ncache, e->eq_of + pod_begin,
-                               e->ncache_stride);
+                               e->ncache_stride, e->eq_n);
         else if (e->consts.numa_bz)
             hipLaunchKernelGGL(k_eval_numa_chunk<true>, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
                                e->pods + pod_begin, (int32_t)shard_tiles, partials);
@@ -3665,6 +3725,9 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->numa_perm) (void)hipFree(e->numa_perm);
     if (e->numa_queue) (void)hipFree(e->numa_queue);
     if (e->comm) (void)rccl().comm_destroy(e->comm);
+    if (e->shm) kg_shm_comm_close(e->shm);
+    if (e->shm_stage) (void)hipHostFree(e->shm_stage);
+    if (e->comm_word) (void)hipFree(e->comm_word);
     if (e->hot_lax) (void)hipFree(e->hot_lax);
     if (e->eq_pods) (void)hipFree(e->eq_pods);
     if (e->eq_perm) (void)hipFree(e->eq_perm);
@@ -3674,7 +3737,8 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-    if (e->ev_eval) (void)hipEventDestroy(e->ev_eval);
+    for (int k = 0; k < kg_engine::kEvalEvents; k++)
+        if (e->ev_eval[k]) (void)hipEventDestroy(e->ev_eval[k]);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     for (int k = 0; k < 3; k++)
         if (e->ev_res[k]) (void)hipEventDestroy(e->ev_res[k]);
@@ -4362,8 +4426,15 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
     e->stream = main_s;
     if (st) return st;
     if (e->eval_stream) {   // the resolve that reads these partials waits for them (eval_join)
-        if (!e->ev_eval) HIP_TRY(e, hipEventCreateWithFlags(&e->ev_eval, hipEventDisableTiming));
-        HIP_TRY(e, hipEventRecord(e->ev_eval, e->eval_stream));
+        int k = 0;
+        while (k < kg_engine::kEvalEvents && e->ev_eval_buf[k] != partial_dev) k++;
+        if (k == kg_engine::kEvalEvents) {   // a new buffer: the least recently assigned slot
+            k = e->ev_eval_next;
+            e->ev_eval_next = (k + 1) % kg_engine::kEvalEvents;
+            e->ev_eval_buf[k] = partial_dev;
+        }
+        if (!e->ev_eval[k]) HIP_TRY(e, hipEventCreateWithFlags(&e->ev_eval[k], hipEventDisableTiming));
+        HIP_TRY(e, hipEventRecord(e->ev_eval[k], e->eval_stream));
     }
     return KG_OK;
 }
@@ -4371,10 +4442,14 @@ kg_status kg_place_chunk_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, i
 }  // extern "C"
 
 namespace {
-// a chunk resolve after kg_place_chunk_eval on the eval stream: the engine stream waits for the latest such eval
-// (in the pipelined order resolve(i) is enqueued before eval(i + 1), so that is the chunk's own)
-kg_status eval_join(kg_engine *e) {
-    if (e->eval_stream && e->ev_eval) HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev_eval, 0));
+// a chunk resolve after kg_place_chunk_eval on the eval stream: the engine stream waits for the evaluation that wrote
+// partial_dev (its latest record), not for whatever the caller enqueued on the eval stream after it — a caller that
+// enqueues eval(i + 1) before resolve(i) keeps its overlap.  Partials no evaluation wrote (the caller's own) join
+// nothing.
+kg_status eval_join(kg_engine *e, const void *partial_dev) {
+    if (!e->eval_stream) return KG_OK;
+    for (int k = 0; k < kg_engine::kEvalEvents; k++)
+        if (e->ev_eval_buf[k] == partial_dev && e->ev_eval[k]) HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev_eval[k], 0));
     return KG_OK;
 }
 }  // namespace
@@ -4423,7 +4498,7 @@ kg_status kg_place_chunk_resolve_prev(kg_engine *e, int64_t now_ns, int32_t pod_
         return set_err(e, KG_ERR_RANGE, "bad previous-chunk node list");
     if (n_prev > 0 && rsv_args(e).rsv)
         return set_err(e, KG_ERR_UNSUPPORTED, "pipelined resolve with reservations (chunk_eval writes their entries)");
-    st = eval_join(e);
+    st = eval_join(e, partial_dev);
     if (st) return st;
     return chunk_resolve(e, now_ns, pod_begin, n, partial_dev, out_node_dev, out_score_dev, false, prev_nodes_dev, n_prev);
 }
@@ -4434,7 +4509,7 @@ kg_status kg_place_chunk_resolve(kg_engine *e, int64_t now_ns, int32_t pod_begin
     if (st) return st;
     st = bind_ready(e, true);
     if (st) return st;
-    st = eval_join(e);
+    st = eval_join(e, partial_dev);
     if (st) return st;
     return chunk_resolve(e, now_ns, pod_begin, n, partial_dev, out_node_dev, out_score_dev, false);
 }
@@ -4449,7 +4524,9 @@ namespace {
 // skipped and they are re-scored exactly, while every other node's key is exact (its planes did not change).
 // Partial buffers alternate; a buffer is rewritten only after the resolve that read it (eval i + 2 waits for
 // resolve i).  Not used with reservations (one entry buffer) or cpuset pods (host Reserve between chunks).
-kg_status merge_partials(kg_engine *e, uint32_t *part, int32_t n, hipStream_t s);
+kg_status merge_partials(kg_engine *e, uint32_t *part, int32_t n, hipStream_t s, bool failed = false);
+kg_status merge_verdict(kg_engine *e, const uint32_t *part, int32_t n);
+kg_status comm_agree(kg_engine *e, kg_status mine);
 
 // the NodeNUMAResource cache of the batch's distinct rows over the shard (kg_engine::ncache), on the engine stream:
 // matrix mode (k_eval_numa2) over eq_pods into the buffer's tail, then k_ncache_init
@@ -4516,80 +4593,107 @@ kg_status ncache_refresh(kg_engine *e, int64_t now_ns, const int32_t *nodes, int
 kg_status place_pipelined(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score, int32_t chunk,
                           bool merge = false) {
     const int32_t P = e->n_pods;
-    const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS;
+    const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS + 4;   // + the status word
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t pvk_b = up((size_t)chunk * (size_t)chunk * 8);
-    kg_status st = ensure_scratch(e, 2 * up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + pvk_b + 256);
-    if (st) return st;
-    char *s = (char *)e->scratch;
-    uint32_t *part[2] = {(uint32_t *)s, (uint32_t *)(s + up(part_b))};
-    int32_t *dnode = (int32_t *)(s + 2 * up(part_b));
-    int64_t *dscore = (int64_t *)(s + 2 * up(part_b) + up((size_t)P * 4));
-    unsigned long long *pvkeys = (unsigned long long *)(s + 2 * up(part_b) + up((size_t)P * 4) + up((size_t)P * 8));
-    if (!e->stream2) {
-        HIP_TRY(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
-        HIP_TRY(e, hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
-        HIP_TRY(e, hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
-    }
-    if (!e->ev_res[0])
-        for (int k = 0; k < 3; k++) HIP_TRY(e, hipEventCreateWithFlags(&e->ev_res[k], hipEventDisableTiming));
-    hipStream_t main_s = e->stream, eval_s = e->stream2;
-    HIP_TRY(e, hipEventRecord(e->ev_fork, main_s));   // the eval stream starts after everything queued so far
-    HIP_TRY(e, hipStreamWaitEvent(eval_s, e->ev_fork, 0));
-    // an error return leaves no evaluation in flight behind the engine stream (it may write the scratch buffer)
-    auto fail = [&](kg_status code) {
-        (void)hipEventRecord(e->ev_join, eval_s);
-        (void)hipStreamWaitEvent(main_s, e->ev_join, 0);
-        return code;
-    };
+    hipStream_t main_s = e->stream;
     // NodeNUMAResource over a batch of repeated rows: the chunks read the distinct rows' cached outcomes (built on the
     // engine stream before the fork below; ncache_live off again on every return)
     struct NcacheScope {
         kg_engine *e;
         ~NcacheScope() { e->ncache_live = false; }
     } ncache_scope{e};
-    // (the refresh re-evaluates U pairs per committed node where a chunk evaluation takes one per node: worth it while
-    // the distinct rows are a fraction of the shard's nodes; the build's matrix outputs stay within 8 GiB)
-    const int64_t ncache_width = e->shard_end - e->shard_begin;
-    if ((e->consts.plugins & KG_PLUGIN_NUMA) && e->eq_on && !e->consts.numa_bz && !(e->forms & KG_FORM_NUMA_NO_CACHE) &&
-        P > 2 * chunk && chunk <= e->numa_chunk_pods && 4 * (int64_t)e->eq_n <= ncache_width &&
-        (int64_t)e->eq_n * ((ncache_width + 63) / 64 * 64) * 7 <= (int64_t)8 << 30) {
-        st = ncache_build(e, now_ns);
+    // this rank's setup (scratch, streams, events, the outcome cache); sharded (merge): the ranks agree on it before
+    // the first collective of the loop
+    auto setup = [&]() -> kg_status {
+        kg_status st = ensure_scratch(e, 2 * up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + pvk_b + 256);
         if (st) return st;
-        e->ncache_live = true;
-        HIP_TRY(e, hipEventRecord(e->ev_fork, main_s));
-        HIP_TRY(e, hipStreamWaitEvent(eval_s, e->ev_fork, 0));
-    }
-    int32_t prev_b = 0, prev_n = 0;
+        if (!e->stream2) {
+            HIP_TRY(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+            HIP_TRY(e, hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+            HIP_TRY(e, hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+        }
+        if (!e->ev_res[0])
+            for (int k = 0; k < 3; k++) HIP_TRY(e, hipEventCreateWithFlags(&e->ev_res[k], hipEventDisableTiming));
+        // (the refresh re-evaluates U pairs per committed node where a chunk evaluation takes one per node: worth it
+        // while the distinct rows are a fraction of the shard's nodes; the build's matrix outputs stay within 8 GiB)
+        const int64_t ncache_width = e->shard_end - e->shard_begin;
+        if ((e->consts.plugins & KG_PLUGIN_NUMA) && e->eq_on && !e->consts.numa_bz && !(e->forms & KG_FORM_NUMA_NO_CACHE) &&
+            P > 2 * chunk && chunk <= e->numa_chunk_pods && 4 * (int64_t)e->eq_n <= ncache_width &&
+            (int64_t)e->eq_n * ((ncache_width + 63) / 64 * 64) * 7 <= (int64_t)8 << 30) {
+            st = ncache_build(e, now_ns);
+            if (st) return st;
+            e->ncache_live = true;
+        }
+        return KG_OK;
+    };
+    kg_status st = setup();
+    if (merge) st = comm_agree(e, st);
+    if (st) return st;
+    char *s = (char *)e->scratch;
+    uint32_t *part[2] = {(uint32_t *)s, (uint32_t *)(s + up(part_b))};
+    int32_t *dnode = (int32_t *)(s + 2 * up(part_b));
+    int64_t *dscore = (int64_t *)(s + 2 * up(part_b) + up((size_t)P * 4));
+    unsigned long long *pvkeys = (unsigned long long *)(s + 2 * up(part_b) + up((size_t)P * 4) + up((size_t)P * 8));
+    hipStream_t eval_s = e->stream2;
+    HIP_TRY(e, hipEventRecord(e->ev_fork, main_s));   // the eval stream starts after everything queued so far
+    HIP_TRY(e, hipStreamWaitEvent(eval_s, e->ev_fork, 0));
+    // an error return leaves no evaluation in flight behind the engine stream (it may write the scratch buffer)
+    auto fail = [&](kg_status code) {
+        (void)hipEventRecord(e->ev_join, eval_s);
+        (void)hipStreamWaitEvent(main_s, e->ev_join, 0);
+        if (merge) e->stale = true;   // the replicas stopped at different chunks
+        return code;
+    };
+    // sharded: a step of this rank that fails (not the collective itself) turns the rest of the loop into merges of
+    // zero keys flagged as failed, so that no peer waits in a collective this rank never issues; every rank then
+    // returns an error (this one its own, the others KG_ERR_STATE from the last chunk's status word)
+    kg_status local = KG_OK;
+    int32_t prev_b = 0, prev_n = 0, last_n = 0;
     int32_t i = 0;
     for (int32_t b = 0; b < P; b += chunk, i++) {
         const int32_t n = P - b < chunk ? P - b : chunk;
+        last_n = n;
         if (i >= 2) HIP_TRY(e, hipStreamWaitEvent(eval_s, e->ev_res[(i - 2) % 3], 0));
-        if (i >= 2 && e->ncache_live) {   // chunk i − 2 (full-size) resolved: its nodes' cache entries re-evaluated
+        if (!local && i >= 2 && e->ncache_live) {   // chunk i − 2 (full-size) resolved: its nodes' cache entries re-evaluated
             st = ncache_refresh(e, now_ns, dnode + (b - 2 * chunk), chunk, eval_s);
-            if (st) return fail(st);
+            if (st) local = st;
         }
-        e->stream = eval_s;   // chunk_eval launches on e->stream
-        st = chunk_eval(e, now_ns, b, n, part[i & 1]);
-        e->stream = main_s;
-        if (st) return fail(st);
+        if (!local) {
+            e->stream = eval_s;   // chunk_eval launches on e->stream
+            st = chunk_eval(e, now_ns, b, n, part[i & 1]);
+            e->stream = main_s;
+            if (st) local = st;
+        }
+        if (local && !merge) return fail(local);
         if (merge) {   // the shards' partials merged beside the resolve (kg_place_sharded)
-            st = merge_partials(e, part[i & 1], n, eval_s);
+            st = merge_partials(e, part[i & 1], n, eval_s, local != KG_OK);
             if (st) return fail(st);
         }
+        if (local) continue;
         HIP_TRY(e, hipEventRecord(e->ev_join, eval_s));
         HIP_TRY(e, hipStreamWaitEvent(main_s, e->ev_join, 0));
         st = chunk_resolve(e, now_ns, b, n, part[i & 1], dnode + b, dscore + b, false, i ? dnode + prev_b : nullptr,
                            i ? prev_n : 0, pvkeys);
-        if (st) return fail(st);
+        if (st) {
+            if (!merge) return fail(st);
+            local = st;
+            continue;
+        }
         HIP_TRY(e, hipEventRecord(e->ev_res[i % 3], main_s));
         prev_b = b;
         prev_n = n;
+    }
+    if (local) {
+        (void)fail(local);
+        (void)hipStreamSynchronize(eval_s);
+        return local;
     }
     HIP_TRY(e, hipMemcpyAsync(out_node, dnode, (size_t)P * 4, hipMemcpyDeviceToHost, main_s));
     HIP_TRY(e, hipMemcpyAsync(out_score, dscore, (size_t)P * 8, hipMemcpyDeviceToHost, main_s));
     HIP_TRY(e, hipStreamSynchronize(main_s));
     HIP_TRY(e, hipStreamSynchronize(eval_s));
+    if (merge && i > 0) return merge_verdict(e, part[(i - 1) & 1], last_n);
     return KG_OK;
 }
 
@@ -4599,6 +4703,51 @@ extern "C" {
 
 kg_status place_impl(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score);
 kg_status place_loop(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score, bool sharded);
+
+}  // extern "C"
+
+namespace {
+// the engine's communicator (either kind) released
+void comm_drop(kg_engine *e) {
+    if (e->comm) (void)rccl().comm_destroy(e->comm);
+    e->comm = nullptr;
+    if (e->shm) kg_shm_comm_close(e->shm);
+    e->shm = nullptr;
+    if (e->shm_stage) (void)hipHostFree(e->shm_stage);
+    e->shm_stage = nullptr;
+    e->comm_world = 0;
+}
+}  // namespace
+
+extern "C" {
+
+kg_status kg_comm_init_loopback(kg_engine *e, int32_t rank, int32_t world, const char *name) {
+    kg_status st = check_engine(e);
+    if (st) return st;
+    if (!name || world < 1 || rank < 0 || rank >= world) return set_err(e, KG_ERR_INVALID_ARG, "bad rank / world / name");
+    if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "kg_comm_init_loopback sizes its slots from the snapshot: load it first");
+    comm_drop(e);
+    // one slot holds the largest merge: a chunk's partial keys + the status word (merge_partials)
+    const size_t slot = ((size_t)KG_MAX_CHUNK * (size_t)tiles_total(e) * KG_PARTIAL_SLOTS + 1) * 4;
+    std::string err;
+    kg_shm_comm *c = kg_shm_comm_open(name, rank, world, slot, 120.0, err);
+    if (!c) return set_err(e, KG_ERR_STATE, "%s", err.c_str());
+    if (hipHostMalloc((void **)&e->shm_stage, slot, hipHostMallocDefault) != hipSuccess) {
+        kg_shm_comm_abort(c);   // the peers' next wait fails instead of hanging
+        kg_shm_comm_close(c);
+        e->shm_stage = nullptr;
+        return set_err(e, KG_ERR_STATE, "hipHostMalloc(%zu) for the loopback staging buffer failed", slot);
+    }
+    e->shm = c;
+    e->comm_rank = rank;
+    e->comm_world = world;
+    return KG_OK;
+}
+
+int32_t kg_comm_kind(const kg_engine *e) {
+    if (!e) return KG_COMM_NONE;
+    return e->comm ? KG_COMM_RCCL : e->shm ? KG_COMM_LOOPBACK : KG_COMM_NONE;
+}
 
 kg_status kg_comm_unique_id(void *out) {
     if (!out) return KG_ERR_INVALID_ARG;
@@ -4616,10 +4765,7 @@ kg_status kg_comm_init(kg_engine *e, int32_t rank, int32_t world, const void *un
     if (!unique_id || world < 1 || rank < 0 || rank >= world) return set_err(e, KG_ERR_INVALID_ARG, "bad rank / world");
     Rccl &r = rccl();
     if (!r.h) return set_err(e, KG_ERR_UNSUPPORTED, "librccl not found");
-    if (e->comm) {
-        (void)r.comm_destroy(e->comm);
-        e->comm = nullptr;
-    }
+    comm_drop(e);
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof(id));
     const ncclResult_t res = r.comm_init_rank(&e->comm, world, id, rank);
@@ -4638,8 +4784,9 @@ kg_status kg_place_sharded(kg_engine *e, int64_t now_ns, int32_t *out_node, int6
     if (st) return st;
     if (!out_node || !out_score) return set_err(e, KG_ERR_INVALID_ARG, "null outputs");
     if (!e->plane_mem) return set_err(e, KG_ERR_STATE, "snapshot not initialised");
-    if (!e->comm) return set_err(e, KG_ERR_STATE, "kg_place_sharded needs kg_comm_init");
+    if (!e->comm && !e->shm) return set_err(e, KG_ERR_STATE, "kg_place_sharded needs kg_comm_init or kg_comm_init_loopback");
     st = place_loop(e, now_ns, out_node, out_score, true);
+    if (st == KG_OK) st = bounds_verdict(e);
     if (st == KG_OK) {
         e->ctr.resolved = resolved0 + (uint64_t)e->n_pods;
         for (int32_t p = 0; p < e->n_pods; p++) e->ctr.placed += out_node[p] >= 0 ? 1u : 0u;
@@ -4649,7 +4796,8 @@ kg_status kg_place_sharded(kg_engine *e, int64_t now_ns, int32_t *out_node, int6
 
 kg_status kg_place(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score) {
     const uint64_t resolved0 = e ? e->ctr.resolved : 0;
-    const kg_status st = place_impl(e, now_ns, out_node, out_score);
+    kg_status st = place_impl(e, now_ns, out_node, out_score);
+    if (st == KG_OK) st = bounds_verdict(e);
     if (st == KG_OK) {
         e->ctr.resolved = resolved0 + (uint64_t)e->n_pods;   // (the chunk resolves inside counted the same pods)
         for (int32_t p = 0; p < e->n_pods; p++) e->ctr.placed += out_node[p] >= 0 ? 1u : 0u;
@@ -4672,12 +4820,71 @@ kg_status place_impl(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *o
 }  // extern "C"
 
 namespace {
+// dev[0..count) := max over the ranks, in place, on stream s: ncclAllReduce on the RCCL communicator; through the host
+// shared-memory segment on the loopback one (device → pinned staging, the exchange, back; synchronous on s)
+kg_status comm_allreduce_max(kg_engine *e, uint32_t *dev, size_t count, hipStream_t s) {
+    if (e->comm) {
+        const ncclResult_t r = rccl().all_reduce(dev, dev, count, ncclUint32, ncclMax, e->comm, s);
+        if (r != ncclSuccess) return set_err(e, KG_ERR_HIP, "ncclAllReduce: %s", rccl().error_string(r));
+        return KG_OK;
+    }
+    if (!e->shm) return set_err(e, KG_ERR_STATE, "no communicator");
+    if (count * 4 > kg_shm_comm_slot_bytes(e->shm)) return set_err(e, KG_ERR_RANGE, "merge larger than the loopback slot");
+    HIP_TRY(e, hipMemcpyAsync(e->shm_stage, dev, count * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(e, hipStreamSynchronize(s));
+    std::string err;
+    if (!kg_shm_comm_allreduce_max_u32(e->shm, e->shm_stage, count, err)) return set_err(e, KG_ERR_STATE, "%s", err.c_str());
+    HIP_TRY(e, hipMemcpyAsync(dev, e->shm_stage, count * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(e, hipStreamSynchronize(s));
+    return KG_OK;
+}
+
+// the partial-key buffer of a chunk carries one status word after its n rows: 0 from a healthy rank, 1 from a rank
+// whose own steps failed (it keeps joining the merges with zero keys so that no peer blocks in a collective), merged
+// by the same max — a rank learns from the last chunk's word that a peer failed
+size_t merge_count(const kg_engine *e, int32_t n) { return (size_t)n * (size_t)tiles_total(e) * KG_PARTIAL_SLOTS; }
+
 // every rank's partial keys of a chunk merged in place (max over ranks: a tile's slots come from one rank, the
-// others hold zeros), on stream s
-kg_status merge_partials(kg_engine *e, uint32_t *part, int32_t n, hipStream_t s) {
-    const size_t count = (size_t)n * (size_t)tiles_total(e) * KG_PARTIAL_SLOTS;
-    const ncclResult_t r = rccl().all_reduce(part, part, count, ncclUint32, ncclMax, e->comm, s);
-    if (r != ncclSuccess) return set_err(e, KG_ERR_HIP, "ncclAllReduce: %s", rccl().error_string(r));
+// others hold zeros), on stream s; failed: this rank's step failed (its keys zeroed, the status word set)
+kg_status merge_partials(kg_engine *e, uint32_t *part, int32_t n, hipStream_t s, bool failed) {
+    const size_t count = merge_count(e, n);
+    if (failed) HIP_TRY(e, hipMemsetAsync(part, 0, count * 4, s));
+    HIP_TRY(e, hipMemsetD32Async((hipDeviceptr_t)(part + count), failed ? 1 : 0, 1, s));
+    return comm_allreduce_max(e, part, count + 1, s);
+}
+
+// the merged status word of the last chunk (after the loop's final synchronisation): a peer failed ⇒ this rank's
+// placements came from incomplete keys — an error, and the replicas may differ (stale until reloaded)
+kg_status merge_verdict(kg_engine *e, const uint32_t *part, int32_t n) {
+    uint32_t w = 0;
+    HIP_TRY(e, hipMemcpy(&w, part + merge_count(e, n), 4, hipMemcpyDeviceToHost));
+    if (w) {
+        e->stale = true;
+        return set_err(e, KG_ERR_STATE, "a peer rank failed during kg_place_sharded: placements are not valid and the "
+                                        "snapshot replicas may differ (reload with kg_snapshot_reset)");
+    }
+    return KG_OK;
+}
+
+// the ranks agree that every one of them is ready for the chunk loop (one all-reduce of a status flag after each
+// rank's own allocations and checks): a rank that failed returns its error, the others KG_ERR_STATE, none enters
+// the loop, so no rank waits in a collective its peer never issues
+kg_status comm_agree(kg_engine *e, kg_status mine) {
+    uint32_t v = mine != KG_OK ? 1u : 0u;
+    kg_status st = KG_OK;
+    if (!e->comm_word && hipMalloc((void **)&e->comm_word, 256) != hipSuccess) {
+        e->comm_word = nullptr;
+        return mine ? mine : set_err(e, KG_ERR_HIP, "hipMalloc of the status word");
+    }
+    if (hipMemcpyAsync(e->comm_word, &v, 4, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+        return mine ? mine : set_err(e, KG_ERR_HIP, "status word upload");
+    st = comm_allreduce_max(e, e->comm_word, 1, e->stream);
+    if (st) return mine ? mine : st;
+    if (hipMemcpyAsync(&v, e->comm_word, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+        return mine ? mine : set_err(e, KG_ERR_HIP, "status word download");
+    if (mine) return mine;
+    if (v) return set_err(e, KG_ERR_STATE, "a peer rank failed to set up kg_place_sharded (nothing was placed)");
     return KG_OK;
 }
 }  // namespace
@@ -4687,40 +4894,46 @@ extern "C" {
 // kg_place's chunk loop; sharded: this rank evaluates its node shard and the chunk's partial keys are merged over
 // the communicator before the (replicated, identical) resolve and host Reserve steps
 kg_status place_loop(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *out_score, bool sharded) {
-    kg_status st = bind_ready(e, true, true);
-    if (st) return st;
     const int32_t P = e->n_pods;
-    if (P == 0) return KG_OK;
+    kg_status st = bind_ready(e, true, true);
+    if (P == 0) return st;   // (the same batch on every rank: no rank enters a collective)
     int32_t chunk = e->cfg.place_chunk > 0 ? e->cfg.place_chunk : 16;
     if (chunk > KG_MAX_CHUNK) chunk = KG_MAX_CHUNK;
-    const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS;
-    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
-    // the host Reserve's row upload uses the head of the scratch buffer: the partials live after it
-    const size_t head = kHostReserveHead;
-    st = ensure_scratch(e, head + up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + 256);
-    if (st) return st;
-    char *s = (char *)e->scratch + head;
-    uint32_t *part = (uint32_t *)s;
-    int32_t *dnode = (int32_t *)(s + up(part_b));
-    int64_t *dscore = (int64_t *)(s + up(part_b) + up((size_t)P * 4));
     // a pod that may bind a cpuset (its own PreFilter decision, or a cpu request where nodes have a CPU bind
     // policy) ends its chunk, and its Reserve runs on the host before the next chunk is evaluated
     const bool bind_mode = (e->consts.plugins & KG_PLUGIN_NUMA) && (e->batch_bind || e->n_node_bind_nodes > 0);
     const uint8_t may_mask = e->n_node_bind_nodes > 0 ? 3 : 1;
     // the pipeline pays two cross-stream event hops per chunk: it wins where the chunk evaluation is long
     // (NodeNUMAResource: config 3 5.0k → 6.1k pods/s) and loses where it is short (config 2: 82k → 61k)
-    st = quota_ready(e);   // (before the pipeline: chunk_resolve checks it too, with an evaluation in flight)
+    const bool pipelined = !bind_mode && !rsv_args(e).rsv && !(e->forms & KG_FORM_PLACE_SEQUENTIAL) &&
+                           ((e->forms & KG_FORM_PLACE_PIPELINE) || (e->consts.plugins & KG_PLUGIN_NUMA));
+    if (!st) st = quota_ready(e);   // (before the pipeline: chunk_resolve checks it too, with an evaluation in flight)
+    if (st) {
+        if (sharded) (void)comm_agree(e, st);   // the peers' one agreement of this call (here or in place_pipelined)
+        return st;
+    }
+    if (pipelined) return place_pipelined(e, now_ns, out_node, out_score, chunk, sharded);
+    const size_t part_b = (size_t)chunk * (size_t)tiles_total(e) * 4 * KG_PARTIAL_SLOTS + 4;   // + the status word
+    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+    // the host Reserve's row upload uses the head of the scratch buffer: the partials live after it
+    const size_t head = kHostReserveHead;
+    st = ensure_scratch(e, head + up(part_b) + up((size_t)P * 4) + up((size_t)P * 8) + 256);
+    if (sharded) st = comm_agree(e, st);
     if (st) return st;
-    if (!bind_mode && !rsv_args(e).rsv &&
-        !(e->forms & KG_FORM_PLACE_SEQUENTIAL) &&
-        ((e->forms & KG_FORM_PLACE_PIPELINE) || (e->consts.plugins & KG_PLUGIN_NUMA)))
-        return place_pipelined(e, now_ns, out_node, out_score, chunk, sharded);
+    char *s = (char *)e->scratch + head;
+    uint32_t *part = (uint32_t *)s;
+    int32_t *dnode = (int32_t *)(s + up(part_b));
+    int64_t *dscore = (int64_t *)(s + up(part_b) + up((size_t)P * 4));
     // the placement kernels answer cpusets on NUMA-policy nodes for this batch (kg_consts.numa_bz)
     struct BzScope {
         kg_consts &k;
         BzScope(kg_consts &c, bool on) : k(c) { k.numa_bz = on ? 1 : 0; }
         ~BzScope() { k.numa_bz = 0; }
     } bz_scope(e->consts, bind_mode && e->n_numa_policy_nodes > 0);
+    // sharded: a failing step of this rank turns the rest of its loop into flagged merges of zero keys (see
+    // place_pipelined); chunk boundaries depend only on the batch, so every rank issues the same merges
+    kg_status local = KG_OK;
+    int32_t last_n = 0;
     for (int32_t b = 0; b < P;) {
         int32_t n = P - b < chunk ? P - b : chunk;
         bool defer = false;
@@ -4731,37 +4944,61 @@ kg_status place_loop(kg_engine *e, int64_t now_ns, int32_t *out_node, int64_t *o
                     defer = true;
                     break;
                 }
-        st = chunk_eval(e, now_ns, b, n, part);
-        if (st) return st;
-        if (sharded) {
-            st = merge_partials(e, part, n, e->stream);
-            if (st) return st;
+        last_n = n;
+        if (!local) {
+            st = chunk_eval(e, now_ns, b, n, part);
+            if (st) {
+                if (!sharded) return st;
+                local = st;
+            }
         }
-        st = chunk_resolve(e, now_ns, b, n, part, dnode + b, dscore + b, defer);
-        if (st) return st;
-        if (defer) {
+        if (sharded) {
+            st = merge_partials(e, part, n, e->stream, local != KG_OK);
+            if (st) {
+                e->stale = true;
+                return st;
+            }
+        }
+        if (!local) {
+            st = chunk_resolve(e, now_ns, b, n, part, dnode + b, dscore + b, defer);
+            if (st) {
+                if (!sharded) return st;
+                local = st;
+            }
+        }
+        if (defer && !local) {
             const int32_t j = b + n - 1;
             int32_t node = -1;
-            HIP_TRY(e, hipMemcpyAsync(&node, dnode + j, 4, hipMemcpyDeviceToHost, e->stream));
-            HIP_TRY(e, hipStreamSynchronize(e->stream));
-            if (node >= 0) {
+            st = KG_OK;
+            if (hipMemcpyAsync(&node, dnode + j, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+                hipStreamSynchronize(e->stream) != hipSuccess)
+                st = set_err(e, KG_ERR_HIP, "download of a deferred placement");
+            if (!st && node >= 0) {
                 bool failed = false;
                 st = host_reserve(e, j, node, &failed);
-                if (st) return st;
-                if (failed) {   // the Reserve failed: the pod is not placed
+                if (!st && failed) {   // the Reserve failed: the pod is not placed
                     const int32_t no = -1;
                     const int64_t ns = -1;
-                    HIP_TRY(e, h2d(e, dnode + j, &no, 4, e->stream));
-                    HIP_TRY(e, h2d(e, dscore + j, &ns, 8, e->stream));
-                    HIP_TRY(e, hipStreamSynchronize(e->stream));
+                    if (h2d(e, dnode + j, &no, 4, e->stream) != hipSuccess || h2d(e, dscore + j, &ns, 8, e->stream) != hipSuccess ||
+                        hipStreamSynchronize(e->stream) != hipSuccess)
+                        st = set_err(e, KG_ERR_HIP, "upload of a failed Reserve's outcome");
                 }
+            }
+            if (st) {
+                if (!sharded) return st;
+                local = st;
             }
         }
         b += n;
     }
+    if (local) {
+        e->stale = true;   // the replicas stopped at different chunks
+        return local;
+    }
     HIP_TRY(e, hipMemcpyAsync(out_node, dnode, (size_t)P * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipMemcpyAsync(out_score, dscore, (size_t)P * 8, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (sharded) return merge_verdict(e, part, last_n);
     return KG_OK;
 }
 

@@ -21,6 +21,8 @@ before and after the max (an order-preserving map from unsigned to signed).
 from __future__ import annotations
 
 import math
+import os
+import uuid
 from typing import Optional, Protocol, Tuple
 
 import numpy as np
@@ -206,15 +208,22 @@ def sharded_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray,
 
 def native_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, device: torch.device, group=None,
                   reservations: Optional[np.ndarray] = None, quotas: Optional[np.ndarray] = None,
-                  stream: Optional[torch.cuda.Stream] = None):
-    """A HIP engine holding the full snapshot, restricted to this rank's shard, with its own RCCL communicator
-    over the group (kg_comm_init; rank 0's unique id is broadcast through torch.distributed): the engine then
-    runs the whole sharded placement natively (Engine.place_sharded = kg_place_sharded), the chunk loop, the
-    partial-key ncclAllReduce and the replicated resolve / host Reserve steps in C++."""
+                  stream: Optional[torch.cuda.Stream] = None, comm: str = "rccl", rank: Optional[int] = None,
+                  world: Optional[int] = None, shm_name: Optional[str] = None):
+    """A HIP engine holding the full snapshot, restricted to this rank's shard, with its own communicator: the
+    engine then runs the whole sharded placement natively (Engine.place_sharded = kg_place_sharded), the chunk loop,
+    the partial-key merges and the replicated resolve / host Reserve steps in C++.
+
+    comm="rccl": an RCCL communicator over the group (kg_comm_init; rank 0's unique id is broadcast through
+    torch.distributed).  comm="loopback": the host shared-memory communicator (kg_comm_init_loopback) — several ranks
+    on ONE GPU (RCCL refuses two ranks on a device) run the same C++ loop; its segment name is rank 0's, broadcast
+    through torch.distributed, or `shm_name` when the caller starts the processes itself (rank / world given)."""
     from .engine import Engine
 
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if rank is None:
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if world is None:
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
     cfg = cfg.copy()
     cfg["device"] = device.index or 0
     eng = Engine(cfg)
@@ -228,6 +237,14 @@ def native_engine(cfg: np.ndarray, node_rows: np.ndarray, pod_rows: np.ndarray, 
     eng.set_pods(pod_rows)
     begin, end = shard_range(len(node_rows), rank, world)
     eng.set_shard(begin, end)
+    if comm == "loopback":
+        name = [shm_name or (f"/kg_loopback_{os.getpid()}_{uuid.uuid4().hex[:8]}" if rank == 0 else None)]
+        if shm_name is None and world > 1:
+            dist.broadcast_object_list(name, src=0, group=group)
+        eng.comm_init_loopback(rank, world, name[0])
+        return eng
+    if comm != "rccl":
+        raise ValueError(f"unknown communicator {comm!r}")
     uid = [Engine.comm_unique_id() if rank == 0 else None]
     if world > 1:
         dist.broadcast_object_list(uid, src=0, group=group)

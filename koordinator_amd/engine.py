@@ -252,9 +252,18 @@ class Engine:
         buf = ctypes.create_string_buffer(bytes(unique_id), nat.COMM_ID_BYTES)
         _check(nat.lib().kg_comm_init(self._h, int(rank), int(world), buf), self, "kg_comm_init")
 
+    def comm_init_loopback(self, rank: int, world: int, name: str) -> None:
+        """kg_comm_init_loopback: the ranks merge partial keys through the host shared-memory segment `name`
+        (the same "/…" on every rank) instead of RCCL — several ranks on one GPU run kg_place_sharded's own loop."""
+        _check(nat.lib().kg_comm_init_loopback(self._h, int(rank), int(world), name.encode()), self,
+               "kg_comm_init_loopback")
+
+    def comm_kind(self) -> str:
+        return {nat.COMM_NONE: "none", nat.COMM_RCCL: "rccl", nat.COMM_LOOPBACK: "loopback"}[nat.lib().kg_comm_kind(self._h)]
+
     def place_sharded(self, now_ns: int):
-        """kg_place over the ranks' node shards (kg_place_sharded): per chunk one ncclAllReduce of the partial
-        keys, the resolve and host Reserve steps replicated.  Same outputs as place()."""
+        """kg_place over the ranks' node shards (kg_place_sharded): per chunk one max-merge of the partial keys over
+        the communicator (RCCL or loopback), the resolve and host Reserve steps replicated.  Same outputs as place()."""
         P = self.n_pods
         nodes = np.zeros(P, dtype=np.int32)
         scores = np.zeros(P, dtype=np.int64)

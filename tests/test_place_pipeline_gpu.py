@@ -74,16 +74,22 @@ def test_fit_loadaware_place_pipeline_on_off(pipeline):
     np.testing.assert_array_equal(scores, ref_s)
 
 
-@pytest.mark.parametrize("kind", ["fit_la", "numa", "quota"])
+@pytest.mark.parametrize("kind", ["fit_la", "fit_la_pipe_most", "numa", "quota"])
 def test_resolve_small_clusters(kind):
     """k_resolve against the oracle's cycle on small clusters, so pods keep landing on nodes the previous pod
     took (the touched-node re-score right after a Reserve); an ElasticQuota tree without Reservation (the gate
-    after each Reserve)."""
+    after each Reserve).  "fit_la_pipe_most": the plain form pipelined (KG_FORM_PLACE_PIPELINE) under MostAllocated,
+    so a node the previous chunk committed is committed again by an earlier pod of the chunk and then scored by a
+    later one (the previous-chunk loop must leave it to the touched re-score: its global row may still be in flight
+    behind the plain form's LDS-only barriers)."""
     from rsv_cases import rsv_cluster
     P = 300
     if kind == "fit_la":
         cl = synth.make_cluster(1024, P, seed=95)
         cfg = shipped_profile(place_chunk=16)
+    elif kind == "fit_la_pipe_most":
+        cl = synth.make_cluster(1024, P, seed=98)
+        cfg = shipped_profile(place_chunk=16, fit_strategy="MostAllocated")
     elif kind == "numa":
         cl = synth.make_numa_cluster(1500, P, seed=96)
         cfg = shipped_profile()
@@ -94,6 +100,8 @@ def test_resolve_small_clusters(kind):
                               eq_check_parent_quota=1)
     idx = np.arange(P)
     with engine.Engine(cfg) as eng:
+        if kind == "fit_la_pipe_most":
+            eng.set_forms(nat.FORM_PLACE_PIPELINE)
         eng.load_snapshot(engine.build_node_rows(cfg, cl))
         if kind == "quota":
             eng.set_quotas(cl.quota_arr)
@@ -111,4 +119,11 @@ def test_resolve_small_clusters(kind):
     np.testing.assert_array_equal(scores, ref_s)
     if kind == "fit_la":
         assert (np.diff(nodes[nodes >= 0]) == 0).any()   # back-to-back pods on one node
+    if kind == "fit_la_pipe_most":
+        # the shape the previous-chunk loop must handle: a node of chunk i − 1 committed twice in chunk i
+        hits = 0
+        for b in range(16, P, 16):
+            prev, cur = set(nodes[b - 16:b].tolist()) - {-1}, nodes[b:b + 16].tolist()
+            hits += sum(1 for n in set(cur) if n in prev and cur.count(n) >= 2)
+        assert hits > 3, hits
     np.testing.assert_array_equal(after, _replay(cfg, cl, idx, nodes))
