@@ -60,6 +60,8 @@ def parse():
                     help="CPU-baseline budget per baseline: one timed run ≈ budget / 6 (warm-up + median of 5)")
     ap.add_argument("--c3-pods", type=int, default=1_000, help="config-3 (NodeNUMAResource) pods; 0 skips it")
     ap.add_argument("--c3-large-pods", type=int, default=10_000, help="config-3 matrix run at this many pods; 0 skips")
+    ap.add_argument("--c3-distinct-pods", type=int, default=1_000,
+                    help="config-3 matrix run over pairwise distinct pod rows (no equivalence); 0 skips")
     ap.add_argument("--c5-pods", type=int, default=100_000,
                     help="config-5 (Reservation + ElasticQuota) pods placed in sequence; 0 skips it")
     ap.add_argument("--c5-matrix-pods", type=int, default=1_000, help="config-5 matrix-mode pods")
@@ -202,6 +204,36 @@ def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
         del mask, scores, numa
         out["large"] = {"pods": PL, "evals_per_s": round(PL * N / tl, 1), "ms_per_step": round(tl * 1e3, 3),
                         "kernel_ms": round(kl, 3)}
+    if args.c3_distinct_pods > 0:
+        # the same config-3 nodes with pairwise distinct pod rows (continuous cpu / memory requests): no pod
+        # equivalence, every (pod, node) pair through k_eval_numa2's hint enumeration
+        PD = args.c3_distinct_pods
+        cl_d = synth.make_numa_cluster(N, PD, seed=3, distinct_pods=True)
+        prow_d = engine.build_pod_rows(cfg, cl_d, np.arange(PD))
+        eng = engine.Engine(cfg)
+        eng.set_stream(stream.cuda_stream)
+        eng.load_snapshot(rows)
+        eng.set_pods(prow_d)
+        mask = torch.empty((PD, W), dtype=torch.int64, device=dev)
+        scores = torch.empty((PD, W * 64, 2), dtype=torch.uint8, device=dev)
+        numa = torch.empty((PD, W * 64), dtype=torch.uint8, device=dev)
+        top1 = torch.zeros(PD, dtype=torch.int64, device=dev)
+        step = lambda: eng.eval_device(cl.now_ns, mask.data_ptr(), scores.data_ptr(), top1.data_ptr(), numa.data_ptr())
+        step()
+        torch.cuda.synchronize(dev)
+        eng.set_profiling(True)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize(dev)
+        td = (time.perf_counter() - t0) / 3
+        kd = float(np.mean(eng.eval_kernel_times(3)))
+        eng.close()
+        del mask, scores, numa
+        distinct_rows = len({r.tobytes() for r in prow_d})
+        out["distinct"] = {"pods": PD, "distinct_rows": distinct_rows, "evals_per_s": round(PD * N / td, 1),
+                           "ms_per_step": round(td * 1e3, 3), "kernel_ms": round(kd, 3),
+                           "roofline_frac": round(PD * N * 3.125 / (kd * 1e-3) / HBM_PEAK, 4)}
     if not args.no_cpu_baseline:
         from oracle import oracle  # CPU restatement, timed as the baseline only
         workers = min(16, os.cpu_count() or 1)
@@ -416,11 +448,17 @@ def bench_config5(args, engine, synth, shipped_profile, dev, stream, cpu_model):
     step = lambda: eng.eval_device(cl.now_ns, mask.data_ptr(), scores.data_ptr(), top1.data_ptr())
     step()
     torch.cuda.synchronize(dev)
+    # device time of the whole pass (every launch of kg_eval is on the engine stream: the Fit / LoadAware kernel
+    # over the plain nodes, k_rsv_eval / k_rsv_reduce over the reservation nodes, the quota gate)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t0 = time.perf_counter()
+    ev[0].record(stream)
     for _ in range(3):
         step()
+    ev[1].record(stream)
     torch.cuda.synchronize(dev)
     tm = (time.perf_counter() - t0) / 3
+    dev_ms = ev[0].elapsed_time(ev[1]) / 3
     # placement of the whole burst
     reset(pods)
     torch.cuda.synchronize(dev)
@@ -438,7 +476,9 @@ def bench_config5(args, engine, synth, shipped_profile, dev, stream, cpu_model):
                          "placed": int((nodes >= 0).sum()), "placed_on_reservation_nodes": on_rsv,
                          "reservation_assignments": int((rsv_after["n_assigned"] - cl.rsv_arr["n_assigned"]).sum()),
                          "mode": "kg_place (greedy sequential commit, touched-node re-score)"},
-           "matrix": {"pods": PM, "evals_per_s": round(PM * N / tm, 1), "ms_per_step": round(tm * 1e3, 3)}}
+           "matrix": {"pods": PM, "evals_per_s": round(PM * N / tm, 1), "ms_per_step": round(tm * 1e3, 3),
+                      "device_ms": round(dev_ms, 3),
+                      "roofline_frac": round((PM * N * BYTES_PER_PAIR + N * BYTES_PER_NODE) / (dev_ms * 1e-3) / HBM_PEAK, 4)}}
     if not args.no_cpu_baseline:
         from oracle import oracle  # CPU restatement of the sequential cycle, timed as the baseline only
         k, med, ts = cpu_median(lambda k: oracle.schedule2(cfg, cl, np.arange(k), cl.now_ns), P,

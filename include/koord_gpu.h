@@ -86,7 +86,9 @@ typedef int32_t kg_status;
 /* ------------------------------------------------------------------ */
 /* resources                                                             */
 /* ------------------------------------------------------------------ */
-#define KG_NUM_RES 8
+#define KG_NUM_RES 12
+#define KG_NUM_EXT_RES 5          /* named scalar slots KG_RES_EXT0 .. KG_RES_EXT4 */
+#define KG_RES_NAME_MAX 64        /* bytes of a slot name in kg_config.ext_resource_names, NUL included */
 enum kg_resource {
     KG_RES_CPU = 0,               /* "cpu"                         MilliValue */
     KG_RES_MEMORY = 1,            /* "memory"                      Value      */
@@ -95,10 +97,16 @@ enum kg_resource {
     KG_RES_BATCH_MEMORY = 4,      /* "kubernetes.io/batch-memory"  Value      */
     KG_RES_MID_CPU = 5,           /* "kubernetes.io/mid-cpu"       Value      */
     KG_RES_MID_MEMORY = 6,        /* "kubernetes.io/mid-memory"    Value      */
-    KG_RES_EXTENDED = 7           /* one extended resource, e.g. "example.com/gpu" Value */
+    /* the named scalar slots: extended resources (nvidia.com/gpu, koordinator.sh/gpu-core, koordinator.sh/rdma,
+     * ...) and hugepages-<size>, named by kg_config.ext_resource_names (default: slot 0 "example.com/gpu", the
+     * others unused).  Every plugin on the path treats them as the ScalarResources of framework.Resource:
+     * NodeResourcesFit compares each requested one (fitsRequest), scores those its ScoringStrategy weighs,
+     * LoadAware weighs those its resourceWeights name, Reservation / ElasticQuota add them up. */
+    KG_RES_EXT0 = 7, KG_RES_EXT1 = 8, KG_RES_EXT2 = 9, KG_RES_EXT3 = 10, KG_RES_EXT4 = 11,
+    KG_RES_EXTENDED = KG_RES_EXT0
 };
 /* resources that upstream schedutil.IsScalarResourceName() treats as scalar */
-#define KG_SCALAR_RES_MASK 0xF8u
+#define KG_SCALAR_RES_MASK 0xFF8u
 
 /* A corev1.ResourceList restricted to the resources above: `present` is the
  * key set (bit r ⇔ key r exists in the map), v[r] the converted value. */
@@ -236,6 +244,10 @@ typedef struct kg_config {
     /* ElasticQuotaArgs.EnableCheckParentQuota: PreFilter also checks every ancestor group below the root
      * (plugin.go:250-252, plugin_helper.go:281-297 checkQuotaRecursive) */
     int32_t eq_check_parent_quota;
+    /* names of the scalar slots KG_RES_EXT0 + i ("" ⇔ unused): the resource-name keys the ingest maps to them,
+     * and their place in the sorted-name order the topology merge walks (policy.go:108: Go map order, fixed to
+     * sorted names here).  Distinct, not one of the fixed names above. */
+    char ext_resource_names[KG_NUM_EXT_RES][KG_RES_NAME_MAX];
 } kg_config;
 
 /* ------------------------------------------------------------------ */
@@ -438,7 +450,7 @@ typedef struct kg_pod_row {
     int32_t rsv_affinity_class;         /* kg_pod_spec.rsv_affinity_class */
     int32_t quota;                      /* kg_pod_spec.quota */
     int32_t _pad2;
-    int64_t la_estimate_x[KG_NUM_RES - 2]; /* EstimatePod(pod)[r] for r = 2..7 (0 unless resourceWeights name r) */
+    int64_t la_estimate_x[KG_NUM_RES - 2]; /* EstimatePod(pod)[r] for r = 2..11 (0 unless resourceWeights name r) */
 } kg_pod_row;
 
 #define KG_NODE_VALID 0x1u
@@ -484,7 +496,7 @@ typedef struct kg_node_row {
     int32_t cpus_per_core;              /* CPUTopology.CPUsPerCore() (0 ⇔ no CPU detail) */
     int32_t cpuset_full_free_cpus;      /* CPUs of the cores whose every CPU is available (getAvailableCPUs) */
     int32_t cpuset_free_cores;          /* cores with at least one available CPU */
-    /* LoadAwareScheduling resourceWeights beyond cpu / memory (resources 2..7; zero unless weighted):
+    /* LoadAwareScheduling resourceWeights beyond cpu / memory (resources 2..11; zero unless weighted):
        EstimateNode(node)[r] and the [nonProd, prod] node terms of r */
     int64_t la_alloc_x[KG_NUM_RES - 2];
     int64_t la_used_x[2][KG_NUM_RES - 2];

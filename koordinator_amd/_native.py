@@ -21,9 +21,14 @@ COMM_NONE, COMM_RCCL, COMM_LOOPBACK = 0, 1, 2   # kg_comm_kind
 # kg_set_forms bits (include/koord_gpu.h)
 FORM_PLACE_PIPELINE, FORM_PLACE_SEQUENTIAL, FORM_NUMA_QUEUED, FORM_NUMA_CHUNK_TILE = 0x1, 0x2, 0x4, 0x8
 FORM_NUMA_NO_CACHE = 0x10
-NUM_RES = 8
+NUM_RES = 12
+NUM_EXT_RES = 5        # KG_NUM_EXT_RES: the named scalar slots RES_EXT0 .. RES_EXT4
+RES_NAME_MAX = 64      # KG_RES_NAME_MAX
 (RES_CPU, RES_MEMORY, RES_EPHEMERAL_STORAGE, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY,
- RES_EXTENDED) = range(8)
+ RES_EXT0, RES_EXT1, RES_EXT2, RES_EXT3, RES_EXT4) = range(12)
+RES_EXTENDED = RES_EXT0   # the default name of slot 0: "example.com/gpu"
+FIXED_RES_NAMES = ("cpu", "memory", "ephemeral-storage", "kubernetes.io/batch-cpu", "kubernetes.io/batch-memory",
+                   "kubernetes.io/mid-cpu", "kubernetes.io/mid-memory")
 PRIO_NONE, PRIO_PROD, PRIO_MID, PRIO_BATCH, PRIO_FREE = range(5)
 QOS_NONE, QOS_LSE, QOS_LSR, QOS_LS, QOS_BE, QOS_SYSTEM = range(6)
 KUBE_QOS_UNSET, KUBE_QOS_GUARANTEED, KUBE_QOS_BURSTABLE, KUBE_QOS_BESTEFFORT = range(4)
@@ -68,6 +73,7 @@ CONFIG = np.dtype([
     ("numa_resource_weight", "<i8", (NUM_RES,)),
     ("device", "<i4"), ("place_chunk", "<i4"),
     ("weight_reservation", "<i4"), ("eq_check_parent_quota", "<i4"),
+    ("ext_resource_names", f"S{RES_NAME_MAX}", (NUM_EXT_RES,)),
 ], align=True)
 
 CONTAINER = np.dtype([("requests", RESOURCE_LIST), ("limits", RESOURCE_LIST)], align=True)

@@ -12,18 +12,19 @@ from typing import Dict, Optional
 import numpy as np
 
 from . import _native as nat
-from .objects import AGG, RES
+from . import objects
+from .objects import AGG
 
 DEFAULT_USAGE_THRESHOLDS = {"cpu": 65, "memory": 95}
 DEFAULT_RESOURCE_WEIGHTS = {"cpu": 1, "memory": 1}
 DEFAULT_SCALING_FACTORS = {"cpu": 85, "memory": 70}
 
 
-def _rl(d: Optional[Dict[str, int]]) -> np.ndarray:
+def _rl(d: Optional[Dict[str, int]], res: Dict[str, int]) -> np.ndarray:
     out = np.zeros((), dtype=nat.RESOURCE_LIST)
     for k, v in (d or {}).items():
-        out["v"][RES[k]] = int(v)
-        out["present"] |= np.uint32(1 << RES[k])
+        out["v"][res[k]] = int(v)
+        out["present"] |= np.uint32(1 << res[k])
     return out
 
 
@@ -42,8 +43,15 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
                 numa_hint_strategy: str = "LeastAllocated", numa_resources: Optional[Dict[str, int]] = None,
                 numa_default_cpu_bind_policy: str = "FullPCPUs",
                 weight_reservation: int = 1, eq_check_parent_quota: int = 0, device: int = 0,
-                place_chunk: int = 16) -> np.ndarray:
+                place_chunk: int = 16, extended_resources=None) -> np.ndarray:
+    """extended_resources: the names of the named scalar slots (kg_config.ext_resource_names, ≤ 5; default the
+    flattening's current ones, objects.EXTENDED — "example.com/gpu" unless set_extended_resources changed it).
+    Flatten clusters for this config under objects.extended_resources(the same names)."""
+    ext = tuple(objects.EXTENDED if extended_resources is None else extended_resources)
+    RES = objects.resource_map(ext)
     c = np.zeros((), dtype=nat.CONFIG)
+    for i, n in enumerate(ext):
+        c["ext_resource_names"][i] = n.encode()
     c["abi_version"] = nat.ABI_VERSION
     bits = 0
     for p in plugins:
@@ -63,8 +71,8 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
     c["la_expiration_seconds"] = 180 if node_metric_expiration_seconds is None else node_metric_expiration_seconds
     for k, w in (resource_weights or DEFAULT_RESOURCE_WEIGHTS).items():
         c["la_resource_weight"][RES[k]] = w
-    c["la_usage_thresholds"] = _rl(usage_thresholds if usage_thresholds else DEFAULT_USAGE_THRESHOLDS)
-    c["la_prod_usage_thresholds"] = _rl(prod_usage_thresholds)
+    c["la_usage_thresholds"] = _rl(usage_thresholds if usage_thresholds else DEFAULT_USAGE_THRESHOLDS, RES)
+    c["la_prod_usage_thresholds"] = _rl(prod_usage_thresholds, RES)
     sf = dict(estimated_scaling_factors or {})
     for k, v in DEFAULT_SCALING_FACTORS.items():
         sf.setdefault(k, v)
@@ -73,7 +81,7 @@ def make_config(*, plugins=("NodeResourcesFit", "LoadAwareScheduling"), weight_f
     c["la_score_according_prod_usage"] = int(score_according_prod_usage)
     if aggregated is not None:
         c["la_has_aggregated"] = 1
-        c["la_agg_usage_thresholds"] = _rl(aggregated.get("usageThresholds"))
+        c["la_agg_usage_thresholds"] = _rl(aggregated.get("usageThresholds"), RES)
         c["la_agg_usage_type"] = AGG[aggregated.get("usageAggregationType", "")]
         c["la_agg_score_type"] = AGG[aggregated.get("scoreAggregationType", "")]
         c["la_agg_usage_duration_ns"] = int(aggregated.get("usageAggregatedDuration", 0) * 10**9)

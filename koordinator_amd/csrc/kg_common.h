@@ -103,7 +103,9 @@ struct kg_consts {
     int32_t numa_w[KG_NUM_RES];  // ScoringStrategy.Resources weights
     int32_t weight_rsv;          // Reservation profile weight
     int32_t la_extra;            // LoadAware weights beyond cpu / memory: every node takes kg_pair_exact
-    int32_t la_wx[KG_NUM_RES - 2]; // their weights (resources 2..7; included in la_wsum)
+    int32_t la_wx[KG_NUM_RES - 2]; // their weights (resources 2..11; included in la_wsum)
+    int8_t res_sorted[KG_NUM_RES]; // resource ids in sorted resource-name order (kg_res_sorted_order: the fixed names
+                                   // and kg_config.ext_resource_names), the order the topology merge walks the lists
     int32_t numa_bz;             // placement of a batch that binds cpusets on NUMA-policy nodes: the chunk and
                                  // resolve kernels answer those pairs (kg_numa_pair_bz) instead of leaving them out
 };
@@ -892,8 +894,7 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
     }
     const uint32_t full = (1u << Z) - 1u;
     // hint lists (generateResourceHints) in sorted resource-name order
-    const int sorted[KG_NUM_RES] = {KG_RES_CPU, KG_RES_EPHEMERAL_STORAGE, KG_RES_EXTENDED, KG_RES_BATCH_CPU,
-                                    KG_RES_BATCH_MEMORY, KG_RES_MID_CPU, KG_RES_MID_MEMORY, KG_RES_MEMORY};
+    const int8_t *sorted = c.res_sorted;   // sorted resource names (the fixed ones and the named scalar slots)
     kg_numa_list L[KG_NUMA_MAX_LISTS];
     int nl = 0;
     for (int j = 0; j < KG_NUM_RES; j++) {

@@ -3971,10 +3971,20 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
     };
     static const int32_t native_map[2] = {KG_RES_CPU, KG_RES_MEMORY};
     static const int32_t coloc_map[4] = {KG_RES_CPU, KG_RES_MEMORY, KG_RES_BATCH_CPU, KG_RES_BATCH_MEMORY};
-    static const int32_t all_map[8] = {0, 1, 2, 3, 4, 5, 6, 7};
     build(kg_pod_hot_t<2>(), 2, native_map);
     if (need & ~0x3u) build(kg_pod_hot_t<4>(), 4, coloc_map);
-    if (need & ~0x1Bu) build(kg_pod_hot_t<8>(), 8, all_map);
+    if (need & ~0x1Bu) {   // 8 slots: cpu, memory and every other resource the batch compares or scores (≤ 6 more)
+        int32_t map8[8] = {KG_RES_CPU, KG_RES_MEMORY, -1, -1, -1, -1, -1, -1};
+        int ns8 = 2;
+        for (int r = 2; r < KG_NUM_RES; r++) {
+            if (!((need >> r) & 1u)) continue;
+            if (ns8 == 8)
+                return set_err(e, KG_ERR_UNSUPPORTED, "the batch compares or scores more than 8 resources (%d)",
+                               __builtin_popcount(need | 3u));
+            map8[ns8++] = r;
+        }
+        build(kg_pod_hot_t<8>(), 8, map8);
+    }
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     if (n > e->pods_cap || hot.size() > e->hot_bytes) {
         if (e->pods) HIP_TRY(e, hipFree(e->pods));

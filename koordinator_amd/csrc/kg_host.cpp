@@ -367,7 +367,32 @@ void kg_config_default(kg_config *c) {
     c->numa_resource_weight[KG_RES_CPU] = 1;
     c->numa_resource_weight[KG_RES_MEMORY] = 1;
     c->place_chunk = 16;
+    snprintf(c->ext_resource_names[0], KG_RES_NAME_MAX, "%s", "example.com/gpu");
 }
+
+}  // extern "C"
+
+// the resource-name keys of the slots: the fixed ones, then kg_config.ext_resource_names ("" ⇔ unused)
+const char *kg_res_name(const kg_config &c, int r) {
+    static const char *const fixed[KG_RES_EXT0] = {"cpu", "memory", "ephemeral-storage", "kubernetes.io/batch-cpu",
+                                                   "kubernetes.io/batch-memory", "kubernetes.io/mid-cpu",
+                                                   "kubernetes.io/mid-memory"};
+    return r < KG_RES_EXT0 ? fixed[r] : c.ext_resource_names[r - KG_RES_EXT0];
+}
+
+// resource ids by name (Go string order, bytewise); unused slots last
+void kg_res_sorted_order(const kg_config &c, int8_t out[KG_NUM_RES]) {
+    int ids[KG_NUM_RES];
+    for (int r = 0; r < KG_NUM_RES; r++) ids[r] = r;
+    std::stable_sort(ids, ids + KG_NUM_RES, [&](int a, int b) {
+        const char *na = kg_res_name(c, a), *nb = kg_res_name(c, b);
+        if (!na[0] || !nb[0]) return na[0] && !nb[0];
+        return strcmp(na, nb) < 0;
+    });
+    for (int r = 0; r < KG_NUM_RES; r++) out[r] = (int8_t)ids[r];
+}
+
+extern "C" {
 
 void kg_config_shipped_profile(kg_config *c) {
     // config/manager/scheduler-config.yaml:17-45
@@ -419,6 +444,17 @@ kg_status kg_config_validate(const kg_config *c, char *err, int32_t err_len) {
         return fail("unsupported NodeResourcesFit scoring strategy");
     // kg_place: 0 ⇒ the default chunk (8); at most the resolve kernel's touched-list capacity
     if (c->place_chunk < 0 || c->place_chunk > KG_PLACE_CHUNK_MAX) return fail("place_chunk out of range (0..1024)");
+    // the named scalar slots: NUL-terminated, printable, distinct, none a fixed name
+    for (int i = 0; i < KG_NUM_EXT_RES; i++) {
+        const char *n = c->ext_resource_names[i];
+        if (!memchr(n, 0, KG_RES_NAME_MAX)) return fail("ext_resource_names: a name is not NUL-terminated");
+        for (const char *q = n; *q; q++)
+            if ((unsigned char)*q <= ' ' || (unsigned char)*q >= 127) return fail("ext_resource_names: unprintable name");
+        if (!n[0]) continue;
+        for (int r = 0; r < KG_NUM_RES; r++)
+            if (r != KG_RES_EXT0 + i && !strcmp(n, kg_res_name(*c, r)))
+                return fail("ext_resource_names: a name repeats or is a fixed resource name");
+    }
     return KG_OK;
 }
 
@@ -827,6 +863,7 @@ void kg_consts_from_config(const kg_config &c, kg_consts &k) {
     k.numa_hint_most = c.numa_hint_strategy == KG_STRATEGY_MOST_ALLOCATED;
     for (int r = 0; r < KG_NUM_RES; r++) k.numa_w[r] = (int32_t)c.numa_resource_weight[r];
     k.weight_rsv = (c.enabled_plugins & KG_PLUGIN_RESERVATION) ? c.weight_reservation : 0;
+    kg_res_sorted_order(c, k.res_sorted);
 }
 
 void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &d) {

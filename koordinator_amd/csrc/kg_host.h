@@ -3,6 +3,8 @@
 #include "kg_common.h"
 
 void kg_consts_from_config(const kg_config &c, kg_consts &k);
+const char *kg_res_name(const kg_config &c, int r);   // the resource-name key of slot r ("" ⇔ an unused named slot)
+void kg_res_sorted_order(const kg_config &c, int8_t out[KG_NUM_RES]);
 void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &d);
 bool kg_pod_row_in_bounds(const kg_pod_row &row);
 int kg_numa_list_count(const kg_pod_row &row);   // NodeNUMAResource hint lists the pod can produce

@@ -8,6 +8,7 @@ LoadAware podAssignCache).  Quantities follow k8s ``resource.Quantity``: cpu is 
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import math
 import re
@@ -18,16 +19,53 @@ import numpy as np
 
 from . import _native as nat
 
-RES = {
-    "cpu": nat.RES_CPU,
-    "memory": nat.RES_MEMORY,
-    "ephemeral-storage": nat.RES_EPHEMERAL_STORAGE,
-    "kubernetes.io/batch-cpu": nat.RES_BATCH_CPU,
-    "kubernetes.io/batch-memory": nat.RES_BATCH_MEMORY,
-    "kubernetes.io/mid-cpu": nat.RES_MID_CPU,
-    "kubernetes.io/mid-memory": nat.RES_MID_MEMORY,
-    "example.com/gpu": nat.RES_EXTENDED,
-}
+# The engine's resource slots: the fixed names, then the named scalar slots (kg_config.ext_resource_names) —
+# extended resources and hugepages-<size> the deployment's pods request.  RES maps a resource name to its slot for
+# the flattening and the config builders; the Go shim keeps the same map per profile.  Names outside it are dropped
+# from nodes and make a pod that requests them unsupported (ingest.UnsupportedResource).
+DEFAULT_EXTENDED = ("example.com/gpu",)
+
+
+def resource_map(extended=DEFAULT_EXTENDED) -> Dict[str, int]:
+    """name → slot for the fixed resources and `extended` (≤ NUM_EXT_RES names, slot RES_EXT0 + i; "" skips one)."""
+    extended = tuple(extended)
+    if len(extended) > nat.NUM_EXT_RES:
+        raise ValueError(f"at most {nat.NUM_EXT_RES} named scalar resources, got {len(extended)}")
+    out = {n: r for r, n in enumerate(nat.FIXED_RES_NAMES)}
+    for i, n in enumerate(extended):
+        if not n:
+            continue
+        if n in out:
+            raise ValueError(f"named scalar resource {n!r} repeats or is a fixed resource")
+        out[n] = nat.RES_EXT0 + i
+    return out
+
+
+RES: Dict[str, int] = {}
+EXTENDED = DEFAULT_EXTENDED
+
+
+def set_extended_resources(names=DEFAULT_EXTENDED) -> None:
+    """Point the flattening (and the config builders' defaults) at the profile's named scalar slots."""
+    global EXTENDED
+    m = resource_map(names)
+    RES.clear()
+    RES.update(m)
+    EXTENDED = tuple(names)
+
+
+@contextlib.contextmanager
+def extended_resources(names):
+    """set_extended_resources for a block (tests and tools building clusters for one profile)."""
+    old = EXTENDED
+    set_extended_resources(names)
+    try:
+        yield
+    finally:
+        set_extended_resources(old)
+
+
+set_extended_resources()
 BATCH_CPU = "kubernetes.io/batch-cpu"
 BATCH_MEMORY = "kubernetes.io/batch-memory"
 

@@ -265,7 +265,7 @@ def make_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, dec
 
 
 def make_numa_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS, zones=(4, 6, 8),
-                      ls_frac: float = 0.6) -> SynthView:
+                      ls_frac: float = 0.6, distinct_pods: bool = False) -> SynthView:
     """BASELINE config 3: nodes with Z ∈ `zones` NUMA zones (equal split of the node's
     cpu / memory allocatable; zone allocated uniform 0–70 %), policy mix 40 % SingleNUMANode, 30 %
     Restricted, 30 % None; pods 60 % LS (cpu / memory requests) and 40 % batch (batch-cpu /
@@ -303,7 +303,7 @@ def make_numa_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS
     nodes["nonzero_requested"][:, 0] = rv[:, nat.RES_CPU]
     nodes["nonzero_requested"][:, 1] = rv[:, nat.RES_MEMORY]
     nodes["numa"] = np.arange(n_nodes)
-    pods, cont = make_pods(n_pods, seed)
+    pods, cont = make_pods(n_pods, seed, distinct=distinct_pods)   # distinct: continuous requests, no repeated rows
     # 60 % LS / 40 % batch mix
     rng2 = np.random.default_rng(seed + 991)
     batch = rng2.random(n_pods) >= ls_frac
@@ -509,4 +509,40 @@ def make_la_extra_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NO
         _rl_fill(pm["usage"], nat.RES_BATCH_CPU, rng.integers(0, 4000, m), rng.random(m) < 0.4)
         _rl_fill(pm["usage"], nat.RES_EXTENDED, rng.integers(0, 3, m), rng.random(m) < 0.2)
     return SynthView(base.pods, cont, nodes, now_ns, aggregated=base.aggregated_arr, pod_metrics=pm,
+                     assigned=base.assigned_arr)
+
+
+SCALAR_NAMES = ("nvidia.com/gpu", "koordinator.sh/gpu-core", "koordinator.sh/rdma", "hugepages-2Mi")
+
+
+def make_scalar_cluster(n_nodes: int, n_pods: int, seed: int, now_ns: int = NOW_NS) -> SynthView:
+    """A config-2 cluster whose nodes and pods also carry the named scalar slots RES_EXT0..3 (the profile names them
+    SCALAR_NAMES: GPUs, GPU cores, RDMA devices, 2 MiB hugepages): every node reports each with probability 0.6 (some
+    already partly requested, some fully: Insufficient), 40 % of the pods request one to three of them at once (a
+    zero-valued key now and then: a scalar key with a zero request still takes part in the compare)."""
+    base = make_cluster(n_nodes, n_pods, seed, now_ns)
+    rng = np.random.default_rng(seed + 5151)
+    nodes = base.nodes.copy()
+    n = len(nodes)
+    caps = {nat.RES_EXT0: (0, 9), nat.RES_EXT1: (0, 801), nat.RES_EXT2: (0, 5), nat.RES_EXT3: (0, 65)}
+    for r, (lo, hi) in caps.items():
+        has = rng.random(n) < 0.6
+        a = rng.integers(lo, hi, n)
+        if r == nat.RES_EXT3:
+            a = a * 2 * MI
+        _rl_fill(nodes["allocatable"], r, a, has)
+        _rl_fill(nodes["requested"], r, (a * rng.integers(0, 5, n)) // 4, has & (rng.random(n) < 0.7))
+    cont = base.containers.copy()
+    c = len(cont)
+    rq, lm = cont["requests"], cont["limits"]
+    wants = rng.random(c) < 0.4
+    k = rng.integers(1, 4, c)
+    for j, (r, (lo, hi)) in enumerate(caps.items()):
+        pick = wants & (rng.random(c) < k / 4.0)
+        v = rng.integers(0, max(2, hi // 3), c)
+        if r == nat.RES_EXT3:
+            v = v * 2 * MI
+        _rl_fill(rq, r, v, pick)
+        _rl_fill(lm, r, v, pick)
+    return SynthView(base.pods, cont, nodes, now_ns, aggregated=base.aggregated_arr, pod_metrics=base.pod_metrics_arr,
                      assigned=base.assigned_arr)

@@ -572,10 +572,37 @@ int64_t kgo_fit_score(const kg_config *c, const kg_cluster_view *v, const kg_pod
 /* ---------------------------------------------------------------- */
 typedef struct { uint64_t mask; int nil; int pref; int64_t score; } numa_hint;
 
-/* resource ids in sorted resource-name order: cpu, ephemeral-storage, example.com/gpu,
- * kubernetes.io/batch-cpu, batch-memory, mid-cpu, mid-memory, memory */
-static const int kSortedRes[KG_NUM_RES] = {KG_RES_CPU, KG_RES_EPHEMERAL_STORAGE, KG_RES_EXTENDED, KG_RES_BATCH_CPU,
-                                           KG_RES_BATCH_MEMORY, KG_RES_MID_CPU, KG_RES_MID_MEMORY, KG_RES_MEMORY};
+/* resource ids in sorted resource-name order (Go string order): the fixed names — cpu, ephemeral-storage,
+ * kubernetes.io/{batch,mid}-{cpu,memory}, memory — and the named scalar slots (kg_config.ext_resource_names,
+ * e.g. example.com/gpu, hugepages-2Mi, nvidia.com/gpu) where their names fall; unused slots last */
+static const char *res_name(const kg_config *c, int r) {
+    static const char *const fixed[KG_RES_EXT0] = {"cpu", "memory", "ephemeral-storage", "kubernetes.io/batch-cpu",
+                                                   "kubernetes.io/batch-memory", "kubernetes.io/mid-cpu",
+                                                   "kubernetes.io/mid-memory"};
+    return r < KG_RES_EXT0 ? fixed[r] : c->ext_resource_names[r - KG_RES_EXT0];
+}
+static void sorted_res(const kg_config *c, int out[KG_NUM_RES]) {
+    int n = 0;
+    for (int r = 0; r < KG_NUM_RES; r++) {   /* insertion sort of the named resources */
+        const char *nm = res_name(c, r);
+        if (!nm[0]) continue;
+        int k = n++;
+        while (k > 0 && strcmp(res_name(c, out[k - 1]), nm) > 0) {
+            out[k] = out[k - 1];
+            k--;
+        }
+        out[k] = r;
+    }
+    for (int r = 0; r < KG_NUM_RES; r++)
+        if (!res_name(c, r)[0]) out[n++] = r;
+}
+
+/* test hook: the order above */
+void kgo_sorted_res(const kg_config *c, int32_t *out) {
+    int o[KG_NUM_RES];
+    sorted_res(c, o);
+    for (int r = 0; r < KG_NUM_RES; r++) out[r] = o[r];
+}
 
 static int popcount64(uint64_t m) { return __builtin_popcountll(m); }
 
@@ -866,8 +893,10 @@ static int numa_admit(const kg_config *c, const numa_zones *z, int policy, const
     numa_hint *plist[KG_NUM_RES];
     int plen[KG_NUM_RES];
     int nl = 0, any_list = 0;
+    int order[KG_NUM_RES];
+    sorted_res(c, order);
     for (int k = 0; k < KG_NUM_RES; k++) {
-        const hint_list *l = &lists[kSortedRes[k]];
+        const hint_list *l = &lists[order[k]];
         if (!l->present) continue;
         any_list = 1;
         if (l->n == 0) {

@@ -148,10 +148,11 @@ def numa_hint_lists(cfg, view, pod_i, node_j, bind=False, required=0):
     """GetTopologyHints of one pair → {resource id: [(mask bits, preferred), ...]} for the resources with a
     list (possibly empty)."""
     MAX_HINTS = 256
-    present = np.zeros(8, np.uint8)
-    count = np.zeros(8, np.int32)
-    masks = np.zeros((8, MAX_HINTS), np.uint64)
-    pref = np.zeros((8, MAX_HINTS), np.uint8)
+    NR = 12   # KG_NUM_RES
+    present = np.zeros(NR, np.uint8)
+    count = np.zeros(NR, np.int32)
+    masks = np.zeros((NR, MAX_HINTS), np.uint64)
+    pref = np.zeros((NR, MAX_HINTS), np.uint8)
     L = lib()
     L.kgo_numa_hint_lists.restype = ctypes.c_int
     L.kgo_numa_hint_lists.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4
@@ -159,7 +160,7 @@ def numa_hint_lists(cfg, view, pod_i, node_j, bind=False, required=0):
                              int(required), present.ctypes.data, count.ctypes.data, masks.ctypes.data,
                              pref.ctypes.data) != 0:
         raise RuntimeError("kgo_numa_hint_lists failed")
-    return {r: [(int(masks[r, k]), bool(pref[r, k])) for k in range(count[r])] for r in range(8) if present[r]}
+    return {r: [(int(masks[r, k]), bool(pref[r, k])) for k in range(count[r])] for r in range(NR) if present[r]}
 
 
 def filter_single_numa_hints(lists):
@@ -390,3 +391,10 @@ def schedule_cpus(cfg, view, pod_index, now_ns):
     if st != 0:
         raise RuntimeError("kgo_schedule3 failed")
     return nodes, scores, cpus
+
+
+def sorted_res_order(cfg):
+    """Resource ids in sorted resource-name order (the fixed names and cfg's named scalar slots; unused last)."""
+    out = np.zeros(12, np.int32)   # KG_NUM_RES
+    lib().kgo_sorted_res(_cfg(cfg), out.ctypes.data_as(ctypes.c_void_p))
+    return out
