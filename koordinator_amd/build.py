@@ -68,6 +68,21 @@ def build_engine(force: bool = False) -> str:
 BOUNDS_SO = os.path.join(LIB_DIR, "libkoordgpu_bounds.so")
 
 
+def build_variant(tag: str, defines: list) -> str:
+    """A measurement build of the engine (lib/libkoordgpu_<tag>.so, the device object compiled with `defines`),
+    loaded through KG_ENGINE_SO by tools; never by the product or the tests."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    common = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
+    dev_obj = os.path.join(obj_dir, f"kg_engine_{tag}.o")
+    _run([hipcc, *common, *defines, f"--offload-arch={ARCH}", "-c", os.path.join(CSRC, "kg_engine.hip"), "-o", dev_obj])
+    objs = [os.path.join(obj_dir, n) for n in ("kg_host.o", "kg_cpuset.o", "kg_comm.o")]
+    so = os.path.join(LIB_DIR, f"libkoordgpu_{tag}.so")
+    _run([hipcc, "-shared", f"--offload-arch={ARCH}", dev_obj, *objs, "-lrt", "-o", so + ".tmp"])
+    os.replace(so + ".tmp", so)
+    return so
+
+
 def build_bounds(force: bool = False) -> str:
     """The bounds-checked engine (-DKG_BOUNDS_CHECK): every index into the pipelined placement's shared buffers is
     checked on the device and a violation is reported by the next kg_place / kg_eval instead of faulting.  A debug
@@ -134,7 +149,10 @@ def build_all(force: bool = False) -> None:
 
 
 if __name__ == "__main__":
-    if "--bounds" in sys.argv:
+    if "--variant" in sys.argv:   # python koordinator_amd/build.py --variant <tag> -DX=1 ...
+        i = sys.argv.index("--variant")
+        build_variant(sys.argv[i + 1], sys.argv[i + 2:])
+    elif "--bounds" in sys.argv:
         build_bounds(force="--force" in sys.argv)
     else:
         build_all(force="--force" in sys.argv)

@@ -1389,6 +1389,15 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
             const kg_node_row &row = lrow;
             const bool zoned = (row.flags & KG_NODE_NUMA_OPTIONS) && row.numa_policy != KG_NUMA_NONE &&
                                row.n_zones > 0;   // n_zones ≤ KG_MAX_ZONES (kg_build_node_rows)
+#if defined(KG_NUMA2_ABLATE) && KG_NUMA2_ABLATE >= 1   // measurement builds (tools: the cost split of a node-wave)
+            if (KG_NUMA2_ABLATE == 1 && zoned) {
+                kg_zone_tab_fill(row, lane, 64, zt, [] { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); },
+                                 row.n_zones != succ_z);
+                succ_z = row.n_zones;
+            }
+            nsc = (uint32_t)zt.succ[lane & 255] & 1u;
+            if (false)
+#endif
             if (zoned) {  // wave-uniform; the previous node's reads precede these writes (in-order LDS per wave)
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
@@ -1400,10 +1409,12 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
             }
+#if !defined(KG_NUMA2_ABLATE) || KG_NUMA2_ABLATE == 0
             kg_numa_out o;   // a node without zones returns before the hint enumeration reads the table
             kg_numa_pair_z<kg_zone_tab, false, false>(c, row, pd, o, kg_zone_tab{zt});
             ok = ok && o.feasible;
             nsc = o.score;
+#endif
         }
         const uint32_t local = (uint32_t)(node - tile * KG_TILE);
         if (ok) {
