@@ -104,13 +104,17 @@ struct kg_consts {
     int32_t weight_rsv;          // Reservation profile weight
     int32_t la_extra;            // LoadAware weights beyond cpu / memory: every node takes kg_pair_exact
     int32_t la_wx[KG_NUM_RES - 2]; // their weights (resources 2..11; included in la_wsum)
-    int8_t res_sorted[KG_NUM_RES]; // resource ids in sorted resource-name order (kg_res_sorted_order: the fixed names
-                                   // and kg_config.ext_resource_names), the order the topology merge walks the lists
+    int8_t res_rank[KG_NUM_RES];   // each resource's rank in sorted resource-name order (kg_res_sorted_order: the fixed
+                                   // names and kg_config.ext_resource_names), the order the topology merge walks the lists
     int32_t numa_bz;             // placement of a batch that binds cpusets on NUMA-policy nodes: the chunk and
                                  // resolve kernels answer those pairs (kg_numa_pair_bz) instead of leaving them out
 };
 
 #define KG_NEUTRAL_REQ INT64_MIN  // request that passes every Fit compare
+
+// The fast per-pair paths keep resources 0 .. KG_FAST_RES − 1 (the fixed ones and the first named slot) in registers;
+// the later named slots are read from memory where a pod uses them (kg_pair_view) or take the exact path (eval_pair)
+#define KG_FAST_RES 8
 
 // per-pod data of the hot kernel (k_eval2), over S resource "slots" (the launch's resource
 // profile maps slot s → resource id).  Read as whole 64-byte blocks with s_load_dwordx16.
@@ -501,6 +505,7 @@ KG_HD uint32_t kg_numa_score_node(const kg_consts &c, const kg_node_row &row, co
                                   bool amplified = false, const int64_t *requested = nullptr, int64_t pod_cpu = -1) {
     if (!requested) requested = row.requested;
     int64_t s = 0, w = 0;
+#pragma unroll   // constant indices into the pod row (a private copy in k_eval_numa2)
     for (int r = 0; r < KG_NUM_RES; r++) {
         if (c.numa_w[r] <= 0) continue;
         const bool scalar = (KG_SCALAR_RES_MASK >> r) & 1u;
@@ -893,12 +898,13 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
         return;
     }
     const uint32_t full = (1u << Z) - 1u;
-    // hint lists (generateResourceHints) in sorted resource-name order
-    const int8_t *sorted = c.res_sorted;   // sorted resource names (the fixed ones and the named scalar slots)
+    // hint lists (generateResourceHints), ordered by resource name: the resources are visited in slot order with
+    // constant indices into the pod row (a run-time resource index would move the row to scratch memory) and each
+    // list takes its place by the name rank of its resource (kg_consts.res_rank; at most two lists)
     kg_numa_list L[KG_NUMA_MAX_LISTS];
-    int nl = 0;
-    for (int j = 0; j < KG_NUM_RES; j++) {
-        const int r = sorted[j];
+    int nl = 0, rank0 = 0;
+#pragma unroll
+    for (int r = 0; r < KG_NUM_RES; r++) {
         if (!((p.numa_present >> r) & 1u)) continue;
         const int64_t q = r == KG_RES_CPU ? pcpu : p.numa_req[r];
         kg_numa_list l{r, Z, false, q};
@@ -919,8 +925,16 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
             return;
         }
         // constant indices only: the two lists stay in registers
-        if (nl == 0) L[0] = l;
-        else L[1] = l;
+        const int rk = c.res_rank[r];
+        if (nl == 0) {
+            L[0] = l;
+            rank0 = rk;
+        } else if (rk < rank0) {
+            L[1] = L[0];
+            L[0] = l;
+        } else {
+            L[1] = l;
+        }
         nl++;
     }
     const bool single = policy == KG_NUMA_SINGLE_NUMA_NODE;
@@ -1064,6 +1078,7 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
         o.score = kg_numa_score_zones(c, c.numa_most != 0, z_used, z_tot, p, pcpu);
     } else if (bd) {
         int64_t rq[KG_NUM_RES];
+        #pragma unroll
         for (int r = 0; r < KG_NUM_RES; r++) rq[r] = requested[r];
         rq[KG_RES_CPU] = row.cpuset_amp_milli;
         o.score = kg_numa_score_node(c, row, p, false, rq, pcpu);
@@ -1203,10 +1218,11 @@ KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_
                         int64_t pod_count, uint32_t df, const kg_pod_dev &p, int64_t now_ns, bool &feasible,
                         uint32_t &fit, uint32_t &la) {
     // every row field first, as independent loads (on the device the row is in global memory: loads
-    // interleaved with the compares below would each wait for the previous one)
-    int64_t al[KG_NUM_RES], rq[KG_NUM_RES];
+    // interleaved with the compares below would each wait for the previous one); the later named slots
+    // (KG_FAST_RES.., rare) are read where a pod uses them, so they cost the common pairs no registers
+    int64_t al[KG_FAST_RES], rq[KG_FAST_RES];
 #pragma unroll
-    for (int r = 0; r < KG_NUM_RES; r++) {
+    for (int r = 0; r < KG_FAST_RES; r++) {
         al[r] = row.alloc[r];
         rq[r] = requested[r];
     }
@@ -1221,10 +1237,14 @@ KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_
     if (c.plugins & KG_PLUGIN_FIT) {
         if (pod_count + 1 > allowed) ok = false;
         if (p.flags & KG_POD_HAS_REQUEST) {
-            for (int r = 0; r < KG_NUM_RES; r++) {
+#pragma unroll
+            for (int r = 0; r < KG_FAST_RES; r++) {
                 bool chk = r < 3 || ((p.request_present >> r) & 1u);
                 if (chk && p.req[r] > al[r] - rq[r]) ok = false;
             }
+#pragma unroll   // (constant indices: the pod row may be a private copy)
+            for (int r = KG_FAST_RES; r < KG_NUM_RES; r++)
+                if (((p.request_present >> r) & 1u) && p.req[r] > row.alloc[r] - requested[r]) ok = false;
         }
     }
     if (c.plugins & KG_PLUGIN_LOADAWARE) {
@@ -1235,12 +1255,13 @@ KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_
     la = 0;
     if (c.plugins & KG_PLUGIN_FIT) {
         int64_t s = 0, w = 0;
+#pragma unroll
         for (int r = 0; r < KG_NUM_RES; r++) {
             if (!((p.fit_mask >> r) & 1u)) continue;
             bool present = r < 3 || ((apresent >> r) & 1u);
-            int64_t a = al[r];
+            int64_t a = r < KG_FAST_RES ? al[r] : row.alloc[r];
             if (!present || a == 0) continue;
-            int64_t base = r < 2 ? nz[r] : rq[r];
+            int64_t base = r < 2 ? nz[r] : r < KG_FAST_RES ? rq[r] : requested[r];
             int64_t req = base + p.fit_pr_i[r];
             int64_t q;
             if (c.fit_most) q = (req > a ? a : req) * 100 / a;
@@ -1301,6 +1322,7 @@ struct kg_rsv_view {
 // updateNodeInfoRequested / NodeInfo.RemovePod of a pod requesting `l` (calculateResource with
 // GetNonzeroRequests' 100m / 200Mi defaults for absent cpu / memory keys)
 KG_HD void kg_rsv_update(kg_rsv_view &v, const kg_resource_list &l, int64_t sign) {
+    #pragma unroll
     for (int r = 0; r < KG_NUM_RES; r++) v.requested[r] += sign * kg_rl_get(l, r);
     v.nonzero[0] += sign * ((l.present & 1u) ? l.v[0] : 100);
     v.nonzero[1] += sign * ((l.present & 2u) ? l.v[1] : KG_MIB200);
@@ -1323,6 +1345,7 @@ KG_HD void kg_rsv_restore(const kg_node_row &row, const kg_reservation *rs, int 
     v.has_state = false;
     v.n_matched = 0;
     v.matched = 0;
+    #pragma unroll
     for (int r = 0; r < KG_NUM_RES; r++) {
         v.requested[r] = row.requested[r];
         v.pod_requested[r] = row.requested[r];
@@ -1352,17 +1375,20 @@ KG_HD void kg_rsv_restore(const kg_node_row &row, const kg_reservation *rs, int 
         rem.present = r.allocatable.present | r.allocated.present;
         rem._pad = 0;
         bool zero = true;
+        #pragma unroll
         for (int q = 0; q < KG_NUM_RES; q++) {
             rem.v[q] = ((rem.present >> q) & 1u) ? kg_rsv_remained(r, q) : 0;
             if (rem.v[q] != 0) zero = false;
         }
         if (!zero) kg_rsv_update(v, rem, +1);
     }
+    #pragma unroll
     for (int q = 0; q < KG_NUM_RES; q++) v.pod_requested[q] = v.requested[q];
     for (uint32_t m = v.matched; m; m &= m - 1u) {  // restoreMatchedReservation → RemovePod(reserve pod)
         const kg_reservation &r = rs[__builtin_ctz(m)];
         kg_rsv_update(v, r.allocatable, -1);
         v.pod_count -= 1;
+        #pragma unroll
         for (int q = 0; q < KG_NUM_RES; q++) v.r_allocated[q] += kg_rl_get(r.allocated, q);
     }
 }
@@ -1372,6 +1398,7 @@ KG_HD bool kg_rsv_fits_node(const kg_node_row &row, const kg_rsv_view &v, const 
     if (v.pod_count - v.n_matched + 1 > (int64_t)row.allowed_pods) return false;
     const uint32_t scal = p.numa_present & KG_SCALAR_RES_MASK;
     if (p.numa_req[0] == 0 && p.numa_req[1] == 0 && p.numa_req[2] == 0 && scal == 0) return true;
+    #pragma unroll
     for (int q = 0; q < KG_NUM_RES; q++) {
         if (q >= 3 && !((scal >> q) & 1u)) continue;
         const int64_t free_q = row.alloc[q] - (v.pod_requested[q] - kg_rsv_remained(r, q) - v.r_allocated[q]);
@@ -1392,6 +1419,7 @@ KG_HD bool kg_rsv_filter_with(const kg_node_row &row, const kg_rsv_view &v, cons
             ok = node_fits;
         } else if (r.policy == KG_RSV_POLICY_RESTRICTED) {
             bool fits = true;  // Mask(podRequests, names) ≤ Allocatable − Mask(Allocated, names)
+            #pragma unroll
             for (int q = 0; q < KG_NUM_RES; q++) {
                 if (!((r.allocatable.present >> q) & 1u) || !((p.numa_present >> q) & 1u)) continue;
                 const int64_t rem = r.allocatable.v[q] - kg_rl_get(r.allocated, q);
@@ -1422,6 +1450,7 @@ KG_HD int kg_rsv_most_preferred(const kg_reservation *rs, uint32_t set, int64_t 
 // scoreReservation (scoring.go:183-203): MostAllocated over RemoveZeros(Allocatable) in MilliValue
 KG_HD uint32_t kg_rsv_score(const kg_reservation &r, const kg_pod_dev &p) {
     int64_t w = 0, s = 0;
+    #pragma unroll
     for (int q = 0; q < KG_NUM_RES; q++) {
         if (!((r.allocatable.present >> q) & 1u) || r.allocatable.v[q] == 0) continue;
         w++;
@@ -1465,7 +1494,9 @@ struct kg_rsv_out {
     int32_t nominated;      // slot of the nominated reservation, −1 none
 };
 
-// Filter + Score of one (pod, node-with-reservations) pair.
+// Filter + Score of one (pod, node-with-reservations) pair.  NUMA = false: a form without the NodeNUMAResource call
+// (the device kernels of a profile without that plugin: its call frame would otherwise cost them scratch memory).
+template <bool NUMA = true>
 KG_HD void kg_rsv_pair(const kg_consts &c, const kg_node_row &row, uint32_t df, const kg_reservation *rs, int nr,
                        const kg_pod_dev &p, int64_t now_ns, kg_rsv_out &o) {
     kg_rsv_view v;
@@ -1473,7 +1504,7 @@ KG_HD void kg_rsv_pair(const kg_consts &c, const kg_node_row &row, uint32_t df, 
     bool feas;
     kg_pair_view(c, row, v.requested, v.nonzero, v.pod_count, df, p, now_ns, feas, o.fit, o.la);
     o.numa = 0;
-    if (c.plugins & KG_PLUGIN_NUMA) {
+    if (NUMA && (c.plugins & KG_PLUGIN_NUMA)) {
         // NodeNUMAResource on the restored NodeInfo; its own RestoreReservation hands back only the
         // reservations' cpusets (reservation.go:68-122), which reservations of non-binding pods do not hold
         kg_numa_out no;

@@ -121,10 +121,14 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 // ---------------------------------------------------------------------------------------
 // per-lane node registers and the pair evaluation
 // ---------------------------------------------------------------------------------------
+// The fast per-pair path keeps the planes of resources 0 .. KG_FAST_RES − 1 in registers (the fixed resources and
+// the first named slot); a pod that compares or scores a later named slot takes the exact int64 path on the node's
+// canonical row (kg_pair_exact), so those slots cost the common batches no registers (eval_pair, pair_key_cached).
+static_assert(KG_FAST_RES <= KG_NUM_RES, "fast resources are a prefix of the resource slots");
 struct NodeRegs {
-    int64_t free_[KG_NUM_RES];
-    double fit_R[KG_NUM_RES];
-    double fit_F[KG_NUM_RES];
+    int64_t free_[KG_FAST_RES];
+    double fit_R[KG_FAST_RES];
+    double fit_F[KG_FAST_RES];
     double la_R[2];
     double la_F0[2];           // LoadAware offset, non-prod usage variant
     double la_F1[2];           // LoadAware offset, prod usage variant
@@ -164,7 +168,7 @@ __device__ __forceinline__ void load_node(const kg_consts &c, const kg_planes &p
     uint32_t df = in_range ? pl.dflags[i] : 0u;
     n.df = df;
 #pragma unroll
-    for (int r = 0; r < KG_NUM_RES; r++) {
+    for (int r = 0; r < KG_FAST_RES; r++) {
         n.free_[r] = 0;
         n.fit_R[r] = 0.0;
         n.fit_F[r] = 0.0;
@@ -215,11 +219,11 @@ __device__ __forceinline__ bool eval_fast(const kg_consts &c, const kg_pod_dev &
                               ((p.zero_native_mask & 4u) ? KGD_OVER_EPH : 0u);
         ok = ok && !(n.df & over);
 #pragma unroll
-        for (int r = 0; r < KG_NUM_RES; r++)
+        for (int r = 0; r < KG_FAST_RES; r++)
             if ((p.cmp_mask >> r) & 1u) ok = ok && (p.req[r] <= n.free_[r]);
         uint32_t s = 0;
 #pragma unroll
-        for (int r = 0; r < KG_NUM_RES; r++) {
+        for (int r = 0; r < KG_FAST_RES; r++) {
             if ((p.fit_mask >> r) & 1u) {
                 int q = lr_q(p.fit_pr[r], n.fit_R[r], n.fit_F[r]);
                 if (c.fit_most) q = q < 100 ? q : 100;
@@ -231,7 +235,7 @@ __device__ __forceinline__ bool eval_fast(const kg_consts &c, const kg_pod_dev &
         } else {
             uint32_t w = 0;
 #pragma unroll
-            for (int r = 0; r < KG_NUM_RES; r++)
+            for (int r = 0; r < KG_FAST_RES; r++)
                 if (((n.fit_mask & p.fit_mask) >> r) & 1u) w += (uint32_t)c.fit_w[r];
             fit = w ? s / w : 0u;
         }
@@ -249,7 +253,7 @@ __device__ __forceinline__ bool eval_fast(const kg_consts &c, const kg_pod_dev &
 
 __device__ __forceinline__ bool eval_pair(const kg_consts &c, const kg_planes &pl, const kg_pod_dev &p,
                                           const NodeRegs &n, int64_t node, int64_t now_ns, uint32_t &fit, uint32_t &la) {
-    if (n.df & KGD_SLOW) {
+    if ((n.df & KGD_SLOW) || ((p.cmp_mask | p.fit_mask) >> KG_FAST_RES)) {   // (a later named slot: exact path)
         bool feas;
         kg_pair_exact(c, pl.rows[node], n.df, p, now_ns, feas, fit, la);
         return feas;
@@ -1741,11 +1745,12 @@ __device__ __forceinline__ unsigned long long rsv_base_key(unsigned long long e,
 }
 
 // `row` / `df`: the node's canonical row and dflags (global, or the resolve's LDS copies)
+template <bool NUMA = true>
 __device__ __forceinline__ void rsv_entry(const kg_consts &c, const kg_node_row &row, uint32_t df, const RsvArgs &ra,
                                           const kg_pod_dev &p, int32_t k, int64_t now_ns, kg_rsv_out *keep,
                                           unsigned long long &e, int64_t &o) {
     kg_rsv_out r;
-    kg_rsv_pair(c, row, df, ra.rsv + ra.rfirst[k], ra.rfirst[k + 1] - ra.rfirst[k], p, now_ns, r);
+    kg_rsv_pair<NUMA>(c, row, df, ra.rsv + ra.rfirst[k], ra.rfirst[k + 1] - ra.rfirst[k], p, now_ns, r);
     const uint32_t base = total_of(c, r.fit, r.la, r.numa);
     e = r.feasible ? ((unsigned long long)(base + 1u) << 32) | ((unsigned long long)r.raw << 16) |
                          (unsigned long long)(uint32_t)(r.nominated + 1)
@@ -2012,6 +2017,7 @@ __device__ unsigned long long rsv_best_resolve(const kg_consts &c, const kg_plan
 }
 
 // entries of pods [0, P) × every reservation node; matrix mode also writes their planes
+template <bool NUMA>
 __global__ __launch_bounds__(256) void k_rsv_eval(kg_consts c, kg_planes pl, RsvArgs ra, const kg_pod_dev *pods,
                                                   int32_t P, int64_t now_ns, unsigned long long *mask,
                                                   uint16_t *scores, uint8_t *numa_scores, int64_t col_begin,
@@ -2025,7 +2031,7 @@ __global__ __launch_bounds__(256) void k_rsv_eval(kg_consts c, kg_planes pl, Rsv
     const bool live = k < ra.n_rn;
     const int32_t nd = live ? ra.rnode[k] : 0;
     if (live) {
-        rsv_entry(c, pl.rows[nd], pl.dflags[nd], ra, pods[p], k, now_ns, &r, e, o);
+        rsv_entry<NUMA>(c, pl.rows[nd], pl.dflags[nd], ra, pods[p], k, now_ns, &r, e, o);
         ra.E[(int64_t)p * ra.n_rn + k] = e;
         ra.O[(int64_t)p * ra.n_rn + k] = o;
     }
@@ -2142,8 +2148,9 @@ __device__ __forceinline__ unsigned long long pair_key_cached(const kg_consts &c
     const bool expired = (c.plugins & KG_PLUGIN_LOADAWARE) ? kg_metric_expired(c, n.df, ce.metric_ns, now_ns) : false;
     node_regs_status(c, n.df, expired, n);
     uint32_t fit, la, numa = 0;
-    if (n.df & KGD_SLOW) {   // the exact pair path on the LDS copy of the committed row (its global stores may
-        bool feas;           // still be in flight: the plain resolve orders pods by LDS-only barriers)
+    if ((n.df & KGD_SLOW) || ((p.cmp_mask | p.fit_mask) >> KG_FAST_RES)) {   // the exact pair path on the LDS copy of
+        bool feas;   // the committed row (its global stores may still be in flight: the plain resolve orders pods by
+                     // LDS-only barriers); a pod on a later named slot always takes it
         kg_pair_exact(c, crow, n.df, p, now_ns, feas, fit, la);
         if (!feas) return 0ull;
     } else if (!eval_fast(c, p, n, fit, la)) {
@@ -2365,9 +2372,9 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
                 const int32_t k = pl.rsv_of[nd];
                 if (k < 0) continue;
                 if (q < KG_NCACHE)   // the committed row and flags cached in LDS
-                    rsv_entry(c, nrow[q], ncache[q].n.df, ra, pd, k, now_ns, nullptr, E[k], O[k]);
+                    rsv_entry<NUMA>(c, nrow[q], ncache[q].n.df, ra, pd, k, now_ns, nullptr, E[k], O[k]);
                 else
-                    rsv_entry(c, pl.rows[nd], pl.dflags[nd], ra, pd, k, now_ns, nullptr, E[k], O[k]);
+                    rsv_entry<NUMA>(c, pl.rows[nd], pl.dflags[nd], ra, pd, k, now_ns, nullptr, E[k], O[k]);
             }
         }
         // a pod that requires a reservation can only land on reservation nodes (rsv part below)
@@ -2597,7 +2604,7 @@ __global__ __launch_bounds__(KG_RESOLVE_THREADS) void k_resolve(kg_consts c, kg_
             double R, F;
             fin[r] = kg_finalize_fit_r(c, pl, node, srow, r, &fr, &R, &F);
             KG_RT_AT(64 + 1, 7);
-            if (ce) {
+            if (ce && r < KG_FAST_RES) {
                 ce->n.free_[r] = fr;
                 ce->n.fit_R[r] = R;
                 ce->n.fit_F[r] = F;
@@ -3669,7 +3676,8 @@ kg_status rsv_eval_chunk(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_
     if (!split) ra.M = nullptr;
     if (ra.M) HIP_TRY(e, hipMemsetAsync(ra.Mn, 0, 4 * (size_t)n, e->stream));
     dim3 grid((unsigned)((ra.n_rn + 255) / 256), (unsigned)n);
-    hipLaunchKernelGGL(k_rsv_eval, grid, dim3(256), 0, e->stream, e->consts, e->pl, ra, e->pods + pod_begin, n, now_ns,
+    auto *kre = (e->consts.plugins & KG_PLUGIN_NUMA) ? k_rsv_eval<true> : k_rsv_eval<false>;
+    hipLaunchKernelGGL(kre, grid, dim3(256), 0, e->stream, e->consts, e->pl, ra, e->pods + pod_begin, n, now_ns,
                        (unsigned long long *)mask, scores, numa_scores, e->shard_begin, e->shard_end, mask_words,
                        score_stride);
     HIP_TRY(e, hipGetLastError());

@@ -863,7 +863,9 @@ void kg_consts_from_config(const kg_config &c, kg_consts &k) {
     k.numa_hint_most = c.numa_hint_strategy == KG_STRATEGY_MOST_ALLOCATED;
     for (int r = 0; r < KG_NUM_RES; r++) k.numa_w[r] = (int32_t)c.numa_resource_weight[r];
     k.weight_rsv = (c.enabled_plugins & KG_PLUGIN_RESERVATION) ? c.weight_reservation : 0;
-    kg_res_sorted_order(c, k.res_sorted);
+    int8_t order[KG_NUM_RES];
+    kg_res_sorted_order(c, order);
+    for (int i = 0; i < KG_NUM_RES; i++) k.res_rank[order[i]] = (int8_t)i;
 }
 
 void kg_pod_dev_from_row(const kg_config &c, const kg_pod_row &row, kg_pod_dev &d) {
