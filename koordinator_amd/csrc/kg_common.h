@@ -781,6 +781,9 @@ struct kg_zone_trim {
 template <class ZS, bool REC = true>
 KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                          const ZS &zs, const int64_t *requested, int policy, int64_t pcpu, const kg_numa_bind *bd);
+template <class ZS>
+KG_HD void kg_numa_zoned_one(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
+                             const ZS &zs, const int64_t *requested, int64_t pcpu);
 
 // the cpuset path with its own (trimmed) zone provider, out of line on the device: the hint enumeration
 // of k_eval_numa2 keeps its register budget for the common, unbound pods
@@ -803,9 +806,11 @@ void kg_numa_bind_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod
 // and leave those pairs infeasible for the fix-up kernel, so they carry no call into the cpuset path.
 // REC: record the allocation (o.zone / o.alloc, what Reserve needs); Filter / Score callers pass false and
 // get o.feasible, o.score and o.n_alloc only (no per-lane arrays written at a run-time index)
+// `one` (Filter / Score callers, REC false): the pair meets kg_numa_one_node and kg_numa_one_pair, so the zoned part
+// takes kg_numa_zoned_one (the single-zone hints only) instead of the whole enumeration
 template <class ZS, bool BZ = true, bool REC = true>
 KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
-                          const ZS &zs, const int64_t *requested = nullptr, bool reserve = false) {
+                          const ZS &zs, const int64_t *requested = nullptr, bool reserve = false, bool one = false) {
     if (!requested) requested = row.requested;
     o.feasible = true;
     o.score = 0;
@@ -884,7 +889,8 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
         else o.feasible = false;   // the caller re-evaluates these pairs (k_numa_bind_fix)
         return;
     }
-    kg_numa_zoned<ZS, REC>(c, row, p, o, zs, requested, policy, pcpu, (const kg_numa_bind *)nullptr);
+    if (!REC && one) kg_numa_zoned_one(c, row, p, o, zs, requested, pcpu);
+    else kg_numa_zoned<ZS, REC>(c, row, p, o, zs, requested, policy, pcpu, (const kg_numa_bind *)nullptr);
 }
 
 // hint generation, merge, Admit, allocateResourcesByHint and the zone score (the part of Filter / Score
@@ -1082,6 +1088,101 @@ KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_po
         for (int r = 0; r < KG_NUM_RES; r++) rq[r] = requested[r];
         rq[KG_RES_CPU] = row.cpuset_amp_milli;
         o.score = kg_numa_score_node(c, row, p, false, rq, pcpu);
+    } else {
+        o.score = kg_numa_score_node(c, row, p, false, requested);
+    }
+}
+
+// The common NodeNUMAResource pair, answered without the hint enumeration: the node has ≥ 2 zones with distinct
+// affinity ids, every zone carries cpu and memory totals, and its policy is SingleNUMANode or Restricted
+// (kg_numa_one_node); the pod's hint lists are at most cpu and memory (no zero request of another resource makes a
+// list of its own) and each list's minimum affinity is one zone (kg_numa_one_pair: the request is within the largest
+// zone total).  Then kg_numa_zoned's preferred pass visits exactly the single zones that fit every list, in index
+// order, each merging to itself with its own hint score (the k = 1 branch: visit(a, a) / visit(a, full)); the fold
+// keeps the first of the narrowest, replaced by a smaller id mask or a higher score; no fitting zone is a
+// non-preferred merge, which Admit rejects under both policies; the allocation takes the chosen zone alone.
+KG_HD bool kg_numa_one_node(const kg_node_row &row) {
+    const int Z = row.n_zones;
+    if (Z < 2 || Z > KG_MAX_ZONES || (row.numa_policy != KG_NUMA_SINGLE_NUMA_NODE && row.numa_policy != KG_NUMA_RESTRICTED))
+        return false;
+    uint64_t ids = 0;
+    for (int i = 0; i < KG_MAX_ZONES; i++)
+        if (i < Z) ids |= 1ull << (row.zone_id[i] & 63);
+    const uint32_t keys = row.zone_keys & ((1u << (2 * Z)) - 1u);
+    return __builtin_popcountll(ids) == Z && keys == ((1u << (2 * Z)) - 1u);
+}
+// the pod side that does not depend on the node (once per pod): no resource beyond cpu / memory makes a hint list
+KG_HD bool kg_numa_one_pod(const kg_pod_dev &p) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 2; r < KG_NUM_RES; r++) ok = ok && !(((p.numa_present >> r) & 1u) && p.numa_req[r] == 0);
+    return ok;
+}
+// `mx[r]`: the node's largest zone total of cpu / memory (kg_zone_total)
+KG_HD bool kg_numa_one_pair(const kg_pod_dev &p, const int64_t mx[2]) {
+    return (!(p.numa_present & 1u) || p.numa_req[KG_RES_CPU] <= mx[0]) &&
+           (!(p.numa_present & 2u) || p.numa_req[KG_RES_MEMORY] <= mx[1]);
+}
+
+template <class ZS>
+KG_HD void kg_numa_zoned_one(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
+                             const ZS &zs, const int64_t *requested, int64_t pcpu) {
+    const int Z = row.n_zones;
+    const bool hc = (p.numa_present & 1u) != 0, hm = (p.numa_present & 2u) != 0;
+    if (!hc && !hm) {   // no hint lists: any affinity, preferred; nothing to allocate in zones
+        o.score = kg_numa_score_node(c, row, p, false, requested);
+        return;
+    }
+    const int64_t qc = pcpu, qm = p.numa_req[KG_RES_MEMORY];
+    bool pref = false;
+    uint64_t bmask = 0;
+    uint32_t bscore = 0;
+    int bi = 0;
+    for (int i = 0; i < KG_MAX_ZONES; i++) {
+        if (i >= Z) break;
+        int64_t tot[2], av[2];
+        zs.sums(1u << i, tot, av);
+        const bool fit = (!hc || qc == 0 || (tot[0] >= qc && av[0] >= qc)) && (!hm || qm == 0 || (tot[1] >= qm && av[1] >= qm));
+        if (!fit) continue;
+        const int64_t used[2] = {tot[0] - av[0], tot[1] - av[1]};
+        const uint32_t sc = kg_numa_score_zones(c, c.numa_hint_most != 0, used, tot, p, pcpu);
+        const uint64_t m = zs.idmask(1u << i);
+        if (!pref || m < bmask || sc > bscore) {   // kg_numa_fold between preferred single-zone masks
+            pref = true;
+            bmask = m;
+            bscore = sc;
+            bi = i;
+        }
+    }
+    if (!pref) {   // Admit (SingleNUMANode / Restricted)
+        o.feasible = false;
+        return;
+    }
+    // allocateResourcesByHint on the one zone (kg_numa_zoned's allocation loop)
+    const uint32_t keys = row.zone_keys | kg_zone_alloc_keys(row);
+    int64_t got[2] = {0, 0};
+    bool short_ = false;
+    const int64_t req[2] = {p.numa_req[0], p.numa_req[1]};
+    const bool want[2] = {hc, hm};
+    for (int r = 0; r < 2; r++) {
+        if (!want[r] || !((keys >> (2 * bi + r)) & 1u)) continue;
+        const int64_t a = kg_zone_avail(row, bi, r);
+        got[r] = a < req[r] ? a : req[r];
+        short_ = short_ || req[r] - got[r] != 0;
+    }
+    if (short_) {
+        o.feasible = false;
+        return;
+    }
+    if (got[0] != 0 || got[1] != 0) {
+        o.n_alloc = 1;
+        int64_t z_tot[2], z_used[2];
+        for (int r = 0; r < 2; r++) {
+            z_tot[r] = kg_zone_total(row, bi, r);
+            const int64_t u = kg_zone_alloc(row, bi, r);
+            z_used[r] = u > 0 ? u : 0;
+        }
+        o.score = kg_numa_score_zones(c, c.numa_most != 0, z_used, z_tot, p, pcpu);
     } else {
         o.score = kg_numa_score_node(c, row, p, false, requested);
     }

@@ -1359,21 +1359,54 @@ __global__ __launch_bounds__(256) void k_numa_bind_fix(kg_consts c, kg_planes pl
 #define KG_NUMA2_SEG 32   // nodes per work item of the queued form (whole 32-bit halves of the mask words)
 #define KG_NUMA2_SEG_TOPK 8   // ... of a placement chunk (keys only: no mask or score planes)
 #define KG_NUMA2_WPE 3   // waves per SIMD the register budget is sized for (r02 A/B)
+typedef uint32_t kg_u32x4 __attribute__((ext_vector_type(4)));
+#ifndef KG_NUMA2_FLUSH
+#define KG_NUMA2_FLUSH 32   // nodes per output flush of k_eval_numa2 (a multiple of 16; r6 A/B against 16)
+#endif
 // one wave's run of `npw` nodes from `base` (inside tile `tile`) for the 64 pods of its lanes; npw is a
 // multiple of 32, runs start on a 32-node boundary
+#ifndef KG_NUMA2_PREFETCH
+#define KG_NUMA2_PREFETCH 1
+#endif
+// one 16-byte LDS-DMA piece per lane into `slot` + lane·16 (a wave-uniform LDS address): issued from inline assembly,
+// so the compiler adds no wait of its own before the wave's next LDS reads (it cannot tell the slots apart); the
+// reader waits vmcnt(0) for the piece before it reads the slot
+__device__ __forceinline__ void kg_glds16(const uint4 *src, uint4 *slot) {
+    const uint32_t lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)slot);
+    int keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+}
 __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &pl, const HotArgs &a,
-                                          const kg_pod_dev &pd, int p, bool live, int64_t tile, int64_t base, int npw,
+                                          const kg_pod_dev &pd,
+                                          int p, bool live, int64_t tile, int64_t base, int npw,
                                           const kg_node_row *__restrict__ rows, unsigned long long *__restrict__ mask,
                                           uint16_t *__restrict__ scores, uint8_t *__restrict__ numa_scores,
                                           uint32_t *__restrict__ partials, const BatchMasks &bm,
-                                          kg_zone_tab_data &zt, kg_node_row &lrow) {
+                                          kg_zone_tab_data &zt, uint4 *__restrict__ lrow_w) {
     const int lane = threadIdx.x & 63;
     uint32_t best = 0;
     uint64_t mword = 0;
-    uint32_t sacc[4] = {0u, 0u, 0u, 0u};
-    uint32_t nacc[4] = {0u, 0u, 0u, 0u};
+    // output segments of KG_NUMA2_FLUSH nodes per pod, held in registers and written by back-to-back stores: each
+    // lane writes its own pod's row, so a store instruction touches 64 rows; one 16-byte piece every 8 nodes left
+    // partial lines in L2 that reached HBM as partial writes (r6 PMC: 5.4 GB written for 0.31 GB of planes on a
+    // 1k-pod pass); whole 64-byte (scores) / 32-byte (NodeNUMAResource) segments per flush
+    constexpr int FL = KG_NUMA2_FLUSH;
+    static_assert(FL % 16 == 0 && KG_NUMA2_SEG % FL == 0, "flush segments are whole 16-byte pieces of a run");
+    uint32_t sacc[FL / 2], nacc[FL / 4];
+#pragma unroll
+    for (int i = 0; i < FL / 2; i++) sacc[i] = 0u;
+#pragma unroll
+    for (int i = 0; i < FL / 4; i++) nacc[i] = 0u;
     constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16);
     int succ_z = -1;   // the zone count the wave's table holds combination successors for
+    const bool pod_one = kg_numa_one_pod(pd);
+#if KG_NUMA2_PREFETCH
+    // the canonical rows reach LDS by LDS-DMA one node ahead (two 1 KiB slots per wave): node k + 1's row is in
+    // flight while node k's hint enumeration runs, instead of a load → LDS → read chain at the head of every node
+    const int src_u4 = lane < ROW_U4 ? lane : ROW_U4 - 1;   // lanes past the row re-read its last piece into the pad
+    if (base < a.node_end) kg_glds16(reinterpret_cast<const uint4 *>(rows + base) + src_u4, lrow_w);
+#endif
     for (int k = 0; k < npw; k++) {
         const int64_t node = base + k;
         const bool in_range = node < a.node_end;
@@ -1385,14 +1418,23 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
             ok = eval_pair(c, pl, pd, n, node, a.now_ns, fit, la);
             // the node's canonical row, staged once into the wave's LDS: the hint enumeration re-reads
             // its zone fields in every loop of every lane
+#if KG_NUMA2_PREFETCH
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this node's row has landed (and the last flush)
+            __builtin_amdgcn_wave_barrier();
+            if (k + 1 < npw && node + 1 < a.node_end)   // the other slot: its node's reads are done (in-order LDS)
+                kg_glds16(reinterpret_cast<const uint4 *>(rows + node + 1) + src_u4, lrow_w + 64 * ((k + 1) & 1));
+            const kg_node_row &row = *reinterpret_cast<const kg_node_row *>(lrow_w + 64 * (k & 1));
+#else
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
-            if (lane < ROW_U4) reinterpret_cast<uint4 *>(&lrow)[lane] = reinterpret_cast<const uint4 *>(rows + node)[lane];
+            if (lane < ROW_U4) lrow_w[lane] = reinterpret_cast<const uint4 *>(rows + node)[lane];
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
-            const kg_node_row &row = lrow;
+            const kg_node_row &row = *reinterpret_cast<const kg_node_row *>(lrow_w);
+#endif
             const bool zoned = (row.flags & KG_NODE_NUMA_OPTIONS) && row.numa_policy != KG_NUMA_NONE &&
                                row.n_zones > 0;   // n_zones ≤ KG_MAX_ZONES (kg_build_node_rows)
+            bool one = false;   // this lane's pair takes kg_numa_zoned_one
 #if defined(KG_NUMA2_ABLATE) && KG_NUMA2_ABLATE >= 1   // measurement builds (tools: the cost split of a node-wave)
             if (KG_NUMA2_ABLATE == 1 && zoned) {
                 kg_zone_tab_fill(row, lane, 64, zt, [] { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); },
@@ -1403,19 +1445,43 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
             if (false)
 #endif
             if (zoned) {  // wave-uniform; the previous node's reads precede these writes (in-order LDS per wave)
-                __builtin_amdgcn_wave_barrier();
-                asm volatile("" ::: "memory");
-                kg_zone_tab_fill(row, lane, 64, zt, [] {
+                const auto wsync = [] {
                     __builtin_amdgcn_wave_barrier();
                     asm volatile("" ::: "memory");
-                }, row.n_zones != succ_z);
-                succ_z = row.n_zones;
-                __builtin_amdgcn_wave_barrier();
-                asm volatile("" ::: "memory");
+                };
+                wsync();
+                // the single-zone entries of the table (what kg_numa_zoned_one reads); the whole table only when some
+                // lane's pair takes the full enumeration
+                const int Z = row.n_zones;
+                if (lane < 2 * KG_MAX_ZONES) {
+                    const int i = lane & (KG_MAX_ZONES - 1), r = lane >> 3;
+                    if (i < Z) {
+                        zt.tot[r][1u << i] = kg_zone_total(row, i, r);
+                        zt.av[r][1u << i] = kg_zone_avail(row, i, r);
+                    }
+                } else if (lane < 3 * KG_MAX_ZONES) {
+                    const int i = lane - 2 * KG_MAX_ZONES;
+                    if (i < Z) zt.idm[1u << i] = 1ull << row.zone_id[i];
+                }
+                int64_t mx[2] = {0, 0};
+#pragma unroll
+                for (int i = 0; i < KG_MAX_ZONES; i++) {
+                    if (i >= Z) break;
+                    const int64_t t0 = kg_zone_total(row, i, 0), t1 = kg_zone_total(row, i, 1);
+                    mx[0] = t0 > mx[0] ? t0 : mx[0];
+                    mx[1] = t1 > mx[1] ? t1 : mx[1];
+                }
+                one = pod_one && kg_numa_one_node(row) && kg_numa_one_pair(pd, mx);
+                wsync();
+                if (__builtin_amdgcn_ballot_w64(!one)) {
+                    kg_zone_tab_fill(row, lane, 64, zt, wsync, row.n_zones != succ_z);
+                    succ_z = row.n_zones;
+                    wsync();
+                }
             }
 #if !defined(KG_NUMA2_ABLATE) || KG_NUMA2_ABLATE == 0
             kg_numa_out o;   // a node without zones returns before the hint enumeration reads the table
-            kg_numa_pair_z<kg_zone_tab, false, false>(c, row, pd, o, kg_zone_tab{zt});
+            kg_numa_pair_z<kg_zone_tab, false, false>(c, row, pd, o, kg_zone_tab{zt}, nullptr, false, one);
             ok = ok && o.feasible;
             nsc = o.score;
 #endif
@@ -1426,22 +1492,33 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
             best = best > key ? best : key;
         }
         mword |= (uint64_t)ok << (k & 63);
-        sacc[(k & 7) >> 1] |= (fit | (la << 8)) << ((k & 1) * 16);
-        nacc[(k & 15) >> 2] |= nsc << ((k & 3) * 8);
-        const int64_t col = node - a.col_begin;
-        if ((k & 7) == 7) {
-            const int64_t c0 = col - 7;
-            if (live && scores && c0 < a.score_stride)
-                *reinterpret_cast<uint4 *>(scores + (int64_t)p * a.score_stride + c0) =
-                    make_uint4(sacc[0], sacc[1], sacc[2], sacc[3]);
-            sacc[0] = sacc[1] = sacc[2] = sacc[3] = 0u;
+        {   // (selects with constant indices: the segments stay in registers)
+            const int si = (k & (FL - 1)) >> 1, ni = (k & (FL - 1)) >> 2;
+            const uint32_t sv = (fit | (la << 8)) << ((k & 1) * 16), nv = nsc << ((k & 3) * 8);
+#pragma unroll
+            for (int i = 0; i < FL / 2; i++) sacc[i] |= i == si ? sv : 0u;
+#pragma unroll
+            for (int i = 0; i < FL / 4; i++) nacc[i] |= i == ni ? nv : 0u;
         }
-        if ((k & 15) == 15) {
-            const int64_t c0 = col - 15;
-            if (live && numa_scores && c0 < a.score_stride)
-                *reinterpret_cast<uint4 *>(numa_scores + (int64_t)p * a.score_stride + c0) =
-                    make_uint4(nacc[0], nacc[1], nacc[2], nacc[3]);
-            nacc[0] = nacc[1] = nacc[2] = nacc[3] = 0u;
+        const int64_t col = node - a.col_begin;
+        if ((k & (FL - 1)) == FL - 1) {
+            const int64_t c0 = col - (FL - 1);
+            if (live && scores && c0 < a.score_stride) {
+                kg_u32x4 *d = reinterpret_cast<kg_u32x4 *>(scores + (int64_t)p * a.score_stride + c0);
+#pragma unroll
+                for (int i = 0; i < FL / 8; i++)
+                    __builtin_nontemporal_store(kg_u32x4{sacc[4 * i], sacc[4 * i + 1], sacc[4 * i + 2], sacc[4 * i + 3]}, d + i);
+            }
+            if (live && numa_scores && c0 < a.score_stride) {
+                kg_u32x4 *d = reinterpret_cast<kg_u32x4 *>(numa_scores + (int64_t)p * a.score_stride + c0);
+#pragma unroll
+                for (int i = 0; i < FL / 16; i++)
+                    __builtin_nontemporal_store(kg_u32x4{nacc[4 * i], nacc[4 * i + 1], nacc[4 * i + 2], nacc[4 * i + 3]}, d + i);
+            }
+#pragma unroll
+            for (int i = 0; i < FL / 2; i++) sacc[i] = 0u;
+#pragma unroll
+            for (int i = 0; i < FL / 4; i++) nacc[i] = 0u;
         }
         if ((k & 63) == 63) {
             const int64_t c0 = col - 63;
@@ -1482,8 +1559,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WP
     // per-wave zone table of the current node (every index mask's sums and id mask, prefix sums of
     // the descending totals): filled by the wave's 64 lanes, read by the hint enumeration of its pods
     __shared__ kg_zone_tab_data ztab[256 / 64];
-    __shared__ __attribute__((aligned(16))) kg_node_row lrow_s[256 / 64];
-    static_assert(sizeof(kg_node_row) % 16 == 0, "rows are staged as 16-byte words");
+    // each wave's row slots: 64 × 16 B (one LDS-DMA wave-instruction) per slot, two slots with KG_NUMA2_PREFETCH
+    __shared__ __attribute__((aligned(16))) uint4 lrow_s[256 / 64][KG_NUMA2_PREFETCH ? 2 : 1][64];
+    static_assert(sizeof(kg_node_row) % 16 == 0 && sizeof(kg_node_row) <= 64 * 16, "rows are staged as 16-byte words");
     const int n_pb = (a.n_pods + 63) / 64;
     for (int it = 0;; it++) {   // grid form: one pass; queued: every wave leaves once the counter passes n_items
         int64_t tile, base;
@@ -1510,7 +1588,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WP
         const int p = live && perm ? perm[slot] : slot;   // the pod row this lane evaluates and writes
         const kg_pod_dev pd = pods[live ? p : 0];
         numa2_run(c, pl, a, pd, p, live, tile, base, npw, rows, mask, scores, numa_scores, partials, bm, ztab[wave],
-                  lrow_s[wave]);
+                  &lrow_s[wave][0][0]);
     }
 }
 
