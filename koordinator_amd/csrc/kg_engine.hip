@@ -1435,7 +1435,7 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
             const bool zoned = (row.flags & KG_NODE_NUMA_OPTIONS) && row.numa_policy != KG_NUMA_NONE &&
                                row.n_zones > 0;   // n_zones ≤ KG_MAX_ZONES (kg_build_node_rows)
             bool one = false;   // this lane's pair takes kg_numa_zoned_one
-#if defined(KG_NUMA2_ABLATE) && KG_NUMA2_ABLATE >= 1   // measurement builds (tools: the cost split of a node-wave)
+#if defined(KG_NUMA2_ABLATE) && KG_NUMA2_ABLATE >= 1 && KG_NUMA2_ABLATE <= 2   // measurement builds (the cost split of a node-wave)
             if (KG_NUMA2_ABLATE == 1 && zoned) {
                 kg_zone_tab_fill(row, lane, 64, zt, [] { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); },
                                  row.n_zones != succ_z);
@@ -1472,6 +1472,9 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
                     mx[1] = t1 > mx[1] ? t1 : mx[1];
                 }
                 one = pod_one && kg_numa_one_node(row) && kg_numa_one_pair(pd, mx);
+#if defined(KG_NUMA2_ABLATE) && KG_NUMA2_ABLATE == 3   // measurement build: every pair on the single-zone path
+                one = true;
+#endif
                 wsync();
                 if (__builtin_amdgcn_ballot_w64(!one)) {
                     kg_zone_tab_fill(row, lane, 64, zt, wsync, row.n_zones != succ_z);
@@ -1479,7 +1482,7 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
                     wsync();
                 }
             }
-#if !defined(KG_NUMA2_ABLATE) || KG_NUMA2_ABLATE == 0
+#if !defined(KG_NUMA2_ABLATE) || KG_NUMA2_ABLATE == 0 || KG_NUMA2_ABLATE == 3
             kg_numa_out o;   // a node without zones returns before the hint enumeration reads the table
             kg_numa_pair_z<kg_zone_tab, false, false>(c, row, pd, o, kg_zone_tab{zt}, nullptr, false, one);
             ok = ok && o.feasible;
@@ -4106,17 +4109,31 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
         HIP_TRY(e, h2d(e, e->hot, hot.data(), hot.size(), e->stream));
     }
     // k_eval_numa2 runs a wave's 64 pods in lockstep through the hint enumeration, whose trip counts
-    // depend on the pod's hint lists: matrix mode visits the pods grouped by (list count, cpu,
-    // memory request), so a wave's lanes mostly share one loop shape (outputs stay in pod-row order)
-    // (of the pods `ids`, as positions into ids)
+    // depend on the pod's hint lists: matrix mode visits the pods (of `ids`, as positions into ids) grouped by list count
+    // and request size, so a wave's lanes mostly share one loop shape (outputs stay in pod-row order).  Within a list
+    // count the key is the larger of the pod's cpu and memory request ranks: a wave takes the single-zone path on a
+    // node only when every lane's requests fit its largest zone, so the pods large in either resource share waves
     auto numa_order = [&](const std::vector<int32_t> &ids) {
-        std::vector<int32_t> order(ids.size());
-        for (size_t i = 0; i < ids.size(); i++) order[i] = (int32_t)i;
+        const size_t m = ids.size();
+        std::vector<int32_t> order(m);
+        for (size_t i = 0; i < m; i++) order[i] = (int32_t)i;
         auto lists = [&](int32_t i) { return (rows[i].flags & KG_POD_NUMA_SKIP) ? 0 : kg_numa_list_count(rows[i]); };
+        std::vector<int32_t> rank_max(m, 0), by(order);
+        for (int r = 0; r < 2; r++) {   // dense rank of the request among the pods (equal requests share a rank)
+            std::sort(by.begin(), by.end(), [&](int32_t a, int32_t b) {
+                return dev[ids[(size_t)a]].numa_req[r] < dev[ids[(size_t)b]].numa_req[r];
+            });
+            int32_t rk = 0;
+            for (size_t i = 0; i < m; i++) {
+                if (i > 0 && dev[ids[(size_t)by[i]]].numa_req[r] != dev[ids[(size_t)by[i - 1]]].numa_req[r]) rk++;
+                rank_max[(size_t)by[i]] = std::max(rank_max[(size_t)by[i]], rk);
+            }
+        }
         std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
             const int32_t x = ids[(size_t)a], y = ids[(size_t)b];
             const int lx = lists(x), ly = lists(y);
             if (lx != ly) return lx < ly;
+            if (rank_max[(size_t)a] != rank_max[(size_t)b]) return rank_max[(size_t)a] < rank_max[(size_t)b];
             if (dev[x].numa_req[KG_RES_CPU] != dev[y].numa_req[KG_RES_CPU])
                 return dev[x].numa_req[KG_RES_CPU] < dev[y].numa_req[KG_RES_CPU];
             return dev[x].numa_req[KG_RES_MEMORY] < dev[y].numa_req[KG_RES_MEMORY];
