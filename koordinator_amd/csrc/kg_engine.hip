@@ -1358,7 +1358,9 @@ __global__ __launch_bounds__(256) void k_numa_bind_fix(kg_consts c, kg_planes pl
 #define KG_NUMA2_NODES 256
 #define KG_NUMA2_SEG 32   // nodes per work item of the queued form (whole 32-bit halves of the mask words)
 #define KG_NUMA2_SEG_TOPK 8   // ... of a placement chunk (keys only: no mask or score planes)
-#define KG_NUMA2_WPE 3   // waves per SIMD the register budget is sized for (r02 A/B)
+#ifndef KG_NUMA2_WPE
+#define KG_NUMA2_WPE 3   // waves per SIMD the register budget is sized for (r02 A/B; r06: 2 is slower, 6.9 vs 5.9 ms)
+#endif
 typedef uint32_t kg_u32x4 __attribute__((ext_vector_type(4)));
 #ifndef KG_NUMA2_FLUSH
 #define KG_NUMA2_FLUSH 32   // nodes per output flush of k_eval_numa2 (a multiple of 16; r6 A/B against 16)
