@@ -731,12 +731,16 @@ kg_status kg_set_eval_stream(kg_engine *eng, void *hip_stream);
  *                            (by size: chunks above 16 pods; smaller ones take per-tile top-16 lists)
  *  KG_FORM_NUMA_NO_CACHE     pipelined NodeNUMAResource placement evaluates every chunk pair by pair (by size: a
  *                            batch of repeated pod rows reads the distinct rows' outcomes from a per-node cache,
- *                            refreshed for each chunk's committed nodes) */
+ *                            refreshed for each chunk's committed nodes)
+ *  KG_FORM_NUMA_FUSED        NodeNUMAResource matrix launches evaluate Fit + LoadAware inside k_eval_numa2 (by size:
+ *                            a matrix launch with planes runs the Fit + LoadAware pass first and k_eval_numa2
+ *                            adds the NodeNUMAResource term to its planes) */
 #define KG_FORM_PLACE_PIPELINE 0x1u
 #define KG_FORM_PLACE_SEQUENTIAL 0x2u
 #define KG_FORM_NUMA_QUEUED 0x4u
 #define KG_FORM_NUMA_CHUNK_TILE 0x8u
 #define KG_FORM_NUMA_NO_CACHE 0x10u
+#define KG_FORM_NUMA_FUSED 0x20u
 kg_status kg_set_forms(kg_engine *eng, uint32_t forms);
 
 /* Reservation cache (KG_PLUGIN_RESERVATION): replaces every reservation slot; a node holds at most

@@ -21,6 +21,7 @@ COMM_NONE, COMM_RCCL, COMM_LOOPBACK = 0, 1, 2   # kg_comm_kind
 # kg_set_forms bits (include/koord_gpu.h)
 FORM_PLACE_PIPELINE, FORM_PLACE_SEQUENTIAL, FORM_NUMA_QUEUED, FORM_NUMA_CHUNK_TILE = 0x1, 0x2, 0x4, 0x8
 FORM_NUMA_NO_CACHE = 0x10
+FORM_NUMA_FUSED = 0x20
 NUM_RES = 12
 NUM_EXT_RES = 5        # KG_NUM_EXT_RES: the named scalar slots RES_EXT0 .. RES_EXT4
 RES_NAME_MAX = 64      # KG_RES_NAME_MAX

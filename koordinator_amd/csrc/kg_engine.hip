@@ -1379,6 +1379,10 @@ __device__ __forceinline__ void kg_glds16(const uint4 *src, uint4 *slot) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
 }
+// COMBINE: the Fit + LoadAware planes (mask bits, score pairs) of the lane's pod row are already written (the class /
+// slot kernels' pass); the run reads them per 32-node segment, adds the NodeNUMAResource term to the mask and keys and
+// writes the NodeNUMAResource plane, without touching the score pairs
+template <bool COMBINE>
 __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &pl, const HotArgs &a,
                                           const kg_pod_dev &pd,
                                           int p, bool live, int64_t tile, int64_t base, int npw,
@@ -1402,6 +1406,7 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
     for (int i = 0; i < FL / 4; i++) nacc[i] = 0u;
     constexpr int ROW_U4 = (int)(sizeof(kg_node_row) / 16);
     int succ_z = -1;   // the zone count the wave's table holds combination successors for
+    uint32_t sin[COMBINE ? FL / 2 : 1], min32 = 0;   // COMBINE: the segment's score pairs and feasibility bits
     const bool pod_one = kg_numa_one_pod(pd);
 #if KG_NUMA2_PREFETCH
     // the canonical rows reach LDS by LDS-DMA one node ahead (two 1 KiB slots per wave): node k + 1's row is in
@@ -1414,10 +1419,44 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
         const bool in_range = node < a.node_end;
         uint32_t fit = 0, la = 0, nsc = 0;
         bool ok = false;
+        if (COMBINE && (k & (FL - 1)) == 0) {   // (runs start on a 32-node boundary: k = 0 begins a segment)
+            const int64_t c0 = node - a.col_begin;
+            const bool have = live && in_range && c0 < a.score_stride;
+            const kg_u32x4 *src = reinterpret_cast<const kg_u32x4 *>(scores + (int64_t)p * a.score_stride + c0);
+#pragma unroll
+            for (int i = 0; i < FL / 8; i++) {
+                const kg_u32x4 v = have ? src[i] : kg_u32x4{0u, 0u, 0u, 0u};
+                sin[4 * i] = v.x;
+                sin[4 * i + 1] = v.y;
+                sin[4 * i + 2] = v.z;
+                sin[4 * i + 3] = v.w;
+            }
+        }
+        if (COMBINE && (k & 31) == 0) {
+            const int64_t c0 = node - a.col_begin;
+            min32 = live && in_range && c0 < (int64_t)a.mask_words * 64
+                        ? reinterpret_cast<const uint32_t *>(mask + (int64_t)p * a.mask_words)[c0 >> 5] : 0u;
+        }
         if (in_range) {  // wave-uniform branch
-            NodeRegs n;
-            load_node(c, pl, node, true, bm, a.now_ns, n);
-            ok = eval_pair(c, pl, pd, n, node, a.now_ns, fit, la);
+#if defined(KG_NUMA2_ABLATE) && KG_NUMA2_ABLATE == 4   // measurement build: NodeNUMAResource term only
+            ok = true;
+            fit = la = 0;
+#else
+            if constexpr (COMBINE) {
+                const int si = (k & (FL - 1)) >> 1;
+                uint32_t w = 0;
+#pragma unroll
+                for (int i = 0; i < FL / 2; i++) w |= i == si ? sin[i] : 0u;
+                const uint32_t sv = (w >> ((k & 1) * 16)) & 0xFFFFu;
+                fit = sv & 0xFFu;
+                la = sv >> 8;
+                ok = (min32 >> (k & 31)) & 1u;
+            } else {
+                NodeRegs n;
+                load_node(c, pl, node, true, bm, a.now_ns, n);
+                ok = eval_pair(c, pl, pd, n, node, a.now_ns, fit, la);
+            }
+#endif
             // the node's canonical row, staged once into the wave's LDS: the hint enumeration re-reads
             // its zone fields in every loop of every lane
 #if KG_NUMA2_PREFETCH
@@ -1484,7 +1523,7 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
                     wsync();
                 }
             }
-#if !defined(KG_NUMA2_ABLATE) || KG_NUMA2_ABLATE == 0 || KG_NUMA2_ABLATE == 3
+#if !defined(KG_NUMA2_ABLATE) || KG_NUMA2_ABLATE == 0 || KG_NUMA2_ABLATE >= 3
             kg_numa_out o;   // a node without zones returns before the hint enumeration reads the table
             kg_numa_pair_z<kg_zone_tab, false, false>(c, row, pd, o, kg_zone_tab{zt}, nullptr, false, one);
             ok = ok && o.feasible;
@@ -1500,15 +1539,17 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
         {   // (selects with constant indices: the segments stay in registers)
             const int si = (k & (FL - 1)) >> 1, ni = (k & (FL - 1)) >> 2;
             const uint32_t sv = (fit | (la << 8)) << ((k & 1) * 16), nv = nsc << ((k & 3) * 8);
+            if constexpr (!COMBINE) {
 #pragma unroll
-            for (int i = 0; i < FL / 2; i++) sacc[i] |= i == si ? sv : 0u;
+                for (int i = 0; i < FL / 2; i++) sacc[i] |= i == si ? sv : 0u;
+            }
 #pragma unroll
             for (int i = 0; i < FL / 4; i++) nacc[i] |= i == ni ? nv : 0u;
         }
         const int64_t col = node - a.col_begin;
         if ((k & (FL - 1)) == FL - 1) {
             const int64_t c0 = col - (FL - 1);
-            if (live && scores && c0 < a.score_stride) {
+            if (!COMBINE && live && scores && c0 < a.score_stride) {
                 kg_u32x4 *d = reinterpret_cast<kg_u32x4 *>(scores + (int64_t)p * a.score_stride + c0);
 #pragma unroll
                 for (int i = 0; i < FL / 8; i++)
@@ -1552,6 +1593,7 @@ __device__ __forceinline__ void numa2_run(const kg_consts &c, const kg_planes &p
 //    (tile, 32-node run, pod block), pod block fastest, from a device counter until `n_items` are taken —
 //    the whole-workgroup grid of the first form leaves a last partial round of workgroups on a few CUs
 //    (1568 workgroups over 768 resident slots is 3 rounds for 2.04 rounds of work).
+template <bool COMBINE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WPE))) void k_eval_numa2(kg_consts c, kg_planes pl, HotArgs a,
                                                     const kg_pod_dev *__restrict__ pods,
                                                     const kg_node_row *__restrict__ rows,
@@ -1592,7 +1634,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_NUMA2_WP
         const bool live = slot < a.n_pods;
         const int p = live && perm ? perm[slot] : slot;   // the pod row this lane evaluates and writes
         const kg_pod_dev pd = pods[live ? p : 0];
-        numa2_run(c, pl, a, pd, p, live, tile, base, npw, rows, mask, scores, numa_scores, partials, bm, ztab[wave],
+        numa2_run<COMBINE>(c, pl, a, pd, p, live, tile, base, npw, rows, mask, scores, numa_scores, partials, bm, ztab[wave],
                   &lrow_s[wave][0][0]);
     }
 }
@@ -2858,6 +2900,8 @@ struct kg_engine {
     bool eq_on = false;
     int32_t eq_n = 0;                  // distinct rows
     kg_pod_dev *eq_pods = nullptr;     // [eq_n]
+    void *eq_hot = nullptr;            // [eq_n] their hot rows (the batch's slot map), for the Fit + LoadAware pass
+    bool reps_in = false;              // pods / hot hold the distinct rows (eval_eq, ncache_build)
     int32_t *eq_perm = nullptr;        // [eq_n] their NodeNUMAResource visiting order (as numa_perm)
     bool eq_perm_on = false;
     int32_t *eq_of = nullptr;          // [n_pods] the distinct row of each pod
@@ -2873,6 +2917,7 @@ struct kg_engine {
     BatchMasks bm{0, 0};
     uint32_t forms = 0;             // kg_set_forms: size-chosen kernel forms forced (KG_FORM_*), 0 = by size
     int64_t numa_resident_wgs = 0;  // resident k_eval_numa2 workgroups of the device (queried at first use)
+    int64_t numa_resident_wgs_c = 0;  // ... of its COMBINE form
     int32_t *numa_queue = nullptr;  // its work-item counter
     int32_t numa_chunk_pods = KG_NUMA_CHUNK_PODS;   // placement chunks up to this many pods take k_eval_numa_chunk
                                                     // (0 under KG_FORM_NUMA_CHUNK_TILE: k_eval_numa2 for every chunk)
@@ -3525,90 +3570,10 @@ kg_status slow_refresh(kg_engine *e) {
 
 // topk: placement chunk (partials of KG_PARTIAL_SLOTS per (pod, tile) on the non-NUMA path; the NUMA
 // kernel writes one key per (pod, tile), slot 0 of a dense [n][tiles] layout — see partial_slots)
-kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
-                      uint32_t *partials, bool use_cls = false, uint8_t *numa_scores = nullptr, bool topk = false) {
-    if (n <= 0) return KG_OK;
-    if ((mask == nullptr) != (scores == nullptr)) return set_err(e, KG_ERR_INVALID_ARG, "mask and scores go together");
-    const int64_t shard_tiles = (e->shard_end - e->shard_begin + KG_TILE - 1) / KG_TILE;
-    if (shard_tiles <= 0) return KG_OK;
-    HotArgs a;
-    a.n_pods = n;
-    a.pods_per_block = pods_per_block_for(n, shard_tiles);
-    a.tile_begin = (int32_t)(e->shard_begin / KG_TILE);
-    a.tiles_total = (int32_t)tiles_total(e);
-    a.node_end = e->shard_end;
-    a.col_begin = e->shard_begin;
-    a.mask_words = (int32_t)((e->shard_end - e->shard_begin + 63) / 64);
-    a.score_stride = (e->shard_end - e->shard_begin + 63) / 64 * 64;
-    a.fit_cap = e->consts.fit_most ? 100u : 0xFFFFFFFFu;
-    for (int s = 0; s < 8; s++) a.slot_res[s] = s < e->nslot ? e->slot_res[s] : -1;
-    a.now_ns = now_ns;
-    if ((e->consts.plugins & KG_PLUGIN_NUMA) && topk && n <= e->numa_chunk_pods) {
-        if (e->profiling) HIP_TRY(e, prof_begin(e));
-        const unsigned blocks = (unsigned)((shard_tiles + KG_XCDS - 1) / KG_XCDS * KG_XCDS * n);
-        if (e->ncache_live && !e->consts.numa_bz)
-            hipLaunchKernelGGL(k_eval_numa_cached, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
-                               e->pods + pod_begin, (int32_t)shard_tiles, partials, e->ncache, e->eq_of + pod_begin,
-                               e->ncache_stride, e->eq_n);
-        else if (e->consts.numa_bz)
-            hipLaunchKernelGGL(k_eval_numa_chunk<true>, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
-                               e->pods + pod_begin, (int32_t)shard_tiles, partials);
-        else
-            hipLaunchKernelGGL(k_eval_numa_chunk<false>, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
-                               e->pods + pod_begin, (int32_t)shard_tiles, partials);
-        HIP_TRY(e, hipGetLastError());
-        if (e->profiling) HIP_TRY(e, prof_end(e));
-        return KG_OK;
-    }
-    if (e->consts.plugins & KG_PLUGIN_NUMA) {
-        if (e->profiling) HIP_TRY(e, prof_begin(e));
-        {  // pod per lane; queued 32-node items when they fill every resident wave slot several times over,
-           // else a grid where a single pod block splits each wave's node run 4 ways
-            // segment: 32 nodes (half mask words); 8 for a placement chunk's keys-only launch
-            const int32_t seg = mask == nullptr && scores == nullptr && numa_scores == nullptr ? KG_NUMA2_SEG_TOPK : KG_NUMA2_SEG;
-            const int64_t n_items = shard_tiles * (KG_TILE / seg) * ((n + 63) / 64);
-            const int32_t *perm = e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr;
-            const BatchMasks bm = e->bm;
-            if (e->numa_resident_wgs == 0) {
-                int dev_cus = 0, per_cu = 0;
-                HIP_TRY(e, hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->device));
-                HIP_TRY(e, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_eval_numa2, 256, 0));
-                e->numa_resident_wgs = (int64_t)dev_cus * (per_cu > 0 ? per_cu : 1);
-                HIP_TRY(e, hipMalloc(&e->numa_queue, sizeof(int32_t)));
-            }
-            // queued when the items give every resident wave one at least; else the grid, each wave's 256-node run
-            // split z ways so that the grid covers the resident slots twice (a 70-row distinct batch of config 3:
-            // 98 tiles × 2 pod blocks would otherwise be 196 workgroups for 768 slots)
-            const bool queued = (e->forms & KG_FORM_NUMA_QUEUED) || topk || n_items >= 4 * e->numa_resident_wgs;
-            if (queued && n_items < INT32_MAX) {
-                HIP_TRY(e, hipMemsetAsync(e->numa_queue, 0, sizeof(int32_t), e->stream));
-                const int64_t wgs = std::min<int64_t>(e->numa_resident_wgs, (n_items + 3) / 4);
-                hipLaunchKernelGGL(k_eval_numa2, dim3((unsigned)wgs), dim3(256), 0, e->stream, e->consts, e->pl, a,
-                                   e->pods + pod_begin, e->pl.rows, (unsigned long long *)mask, scores, numa_scores,
-                                   partials, perm, bm, e->numa_queue, (int32_t)n_items, seg);
-            } else {
-                const int64_t blocks = shard_tiles * ((n + 63) / 64);
-                unsigned z = 1;
-                while (z < KG_NUMA2_NODES / 32 && blocks * z < 2 * e->numa_resident_wgs) z *= 2;
-                dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), z);
-                hipLaunchKernelGGL(k_eval_numa2, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
-                                   e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials, perm, bm,
-                                   (int32_t *)nullptr, 0, 0);
-            }
-        }
-        HIP_TRY(e, hipGetLastError());
-        // cpusets on NUMA-policy nodes: patched in after the hot kernel (matrix planes, or the one-key-per-tile
-        // partials of a large placement chunk)
-        if ((!topk || e->consts.numa_bz) && e->n_numa_policy_nodes > 0 && (e->batch_bind || e->n_node_bind_nodes > 0)) {
-            const int64_t width = e->shard_end - e->shard_begin;
-            dim3 grid((unsigned)((width + 255) / 256), (unsigned)(n < 65535 ? n : 65535));
-            hipLaunchKernelGGL(k_numa_bind_fix, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
-                               (unsigned long long *)mask, scores, numa_scores, partials);
-            HIP_TRY(e, hipGetLastError());
-        }
-        if (e->profiling) HIP_TRY(e, prof_end(e));
-        return KG_OK;
-    }
+// Fit + LoadAware over the launch's pods (every form but NodeNUMAResource's): the LAX / exact forms for LoadAware
+// weights beyond cpu / memory, the class kernels, the slot kernels, then the slow-node fix-up
+kg_status launch_eval_plain(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
+                            uint32_t *partials, bool use_cls, bool topk, HotArgs a, int64_t shard_tiles) {
     if (e->consts.la_extra && !topk && e->lax_ok) {
         // LoadAware weights beyond cpu / memory, at most KG_LAX of them: k_eval2's LAX form reads their planes too;
         // the nodes outside the fp64 bounds of any plane (KGD_XSLOW) are re-evaluated exactly after it
@@ -3665,7 +3630,7 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
         if (e->profiling) HIP_TRY(e, prof_end(e));
         return KG_OK;
     }
-    use_cls = use_cls && e->cls_ok && pod_begin == 0 && n == e->n_pods;
+    use_cls = use_cls && e->cls_ok && !e->reps_in && pod_begin == 0 && n == e->n_pods;
     if (use_cls) {
         kg_status st = cls_layout(e, e->shard_end - e->shard_begin, shard_tiles);
         if (st) return st;
@@ -3690,6 +3655,117 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
         HIP_TRY(e, hipGetLastError());
     }
     return KG_OK;
+}
+
+kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
+                      uint32_t *partials, bool use_cls = false, uint8_t *numa_scores = nullptr, bool topk = false) {
+    if (n <= 0) return KG_OK;
+    if ((mask == nullptr) != (scores == nullptr)) return set_err(e, KG_ERR_INVALID_ARG, "mask and scores go together");
+    const int64_t shard_tiles = (e->shard_end - e->shard_begin + KG_TILE - 1) / KG_TILE;
+    if (shard_tiles <= 0) return KG_OK;
+    HotArgs a;
+    a.n_pods = n;
+    a.pods_per_block = pods_per_block_for(n, shard_tiles);
+    a.tile_begin = (int32_t)(e->shard_begin / KG_TILE);
+    a.tiles_total = (int32_t)tiles_total(e);
+    a.node_end = e->shard_end;
+    a.col_begin = e->shard_begin;
+    a.mask_words = (int32_t)((e->shard_end - e->shard_begin + 63) / 64);
+    a.score_stride = (e->shard_end - e->shard_begin + 63) / 64 * 64;
+    a.fit_cap = e->consts.fit_most ? 100u : 0xFFFFFFFFu;
+    for (int s = 0; s < 8; s++) a.slot_res[s] = s < e->nslot ? e->slot_res[s] : -1;
+    a.now_ns = now_ns;
+    if ((e->consts.plugins & KG_PLUGIN_NUMA) && topk && n <= e->numa_chunk_pods) {
+        if (e->profiling) HIP_TRY(e, prof_begin(e));
+        const unsigned blocks = (unsigned)((shard_tiles + KG_XCDS - 1) / KG_XCDS * KG_XCDS * n);
+        if (e->ncache_live && !e->consts.numa_bz)
+            hipLaunchKernelGGL(k_eval_numa_cached, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                               e->pods + pod_begin, (int32_t)shard_tiles, partials, e->ncache, e->eq_of + pod_begin,
+                               e->ncache_stride, e->eq_n);
+        else if (e->consts.numa_bz)
+            hipLaunchKernelGGL(k_eval_numa_chunk<true>, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                               e->pods + pod_begin, (int32_t)shard_tiles, partials);
+        else
+            hipLaunchKernelGGL(k_eval_numa_chunk<false>, dim3(blocks), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                               e->pods + pod_begin, (int32_t)shard_tiles, partials);
+        HIP_TRY(e, hipGetLastError());
+        if (e->profiling) HIP_TRY(e, prof_end(e));
+        return KG_OK;
+    }
+    if (e->consts.plugins & KG_PLUGIN_NUMA) {
+        // matrix launches with planes: Fit + LoadAware by the class / slot kernels first (node per lane, pods uniform:
+        // the per-pair form costs 0.08 ms per 1e8 pairs), their tile keys cleared, then k_eval_numa2 reads the two
+        // score bytes and the feasibility bit back and adds the NodeNUMAResource term — the pod-per-lane kernel then
+        // carries no node planes and no Fit / LoadAware pair code
+        const bool combine = mask && scores && partials && !topk && !(e->forms & KG_FORM_NUMA_FUSED) &&
+                             !(e->reps_in && (e->consts.la_extra || !e->eq_hot));
+        if (combine) {
+            kg_status st = launch_eval_plain(e, now_ns, pod_begin, n, mask, scores, partials, use_cls, false, a, shard_tiles);
+            if (st) return st;
+            HIP_TRY(e, hipMemsetAsync(partials, 0, (size_t)n * (size_t)a.tiles_total * 4, e->stream));
+        }
+        if (e->profiling) HIP_TRY(e, prof_begin(e));
+        {  // pod per lane; queued 32-node items when they fill every resident wave slot several times over,
+           // else a grid where a single pod block splits each wave's node run 4 ways
+            // segment: 32 nodes (half mask words); 8 for a placement chunk's keys-only launch
+            const int32_t seg = mask == nullptr && scores == nullptr && numa_scores == nullptr ? KG_NUMA2_SEG_TOPK : KG_NUMA2_SEG;
+            const int64_t n_items = shard_tiles * (KG_TILE / seg) * ((n + 63) / 64);
+            const int32_t *perm = e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr;
+            const BatchMasks bm = e->bm;
+            if (e->numa_resident_wgs == 0) {
+                int dev_cus = 0, per_cu = 0;
+                HIP_TRY(e, hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->device));
+                HIP_TRY(e, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_eval_numa2<false>, 256, 0));
+                e->numa_resident_wgs = (int64_t)dev_cus * (per_cu > 0 ? per_cu : 1);
+                per_cu = 0;
+                HIP_TRY(e, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_eval_numa2<true>, 256, 0));
+                e->numa_resident_wgs_c = (int64_t)dev_cus * (per_cu > 0 ? per_cu : 1);
+                HIP_TRY(e, hipMalloc(&e->numa_queue, sizeof(int32_t)));
+            }
+            // queued when the items give every resident wave one at least; else the grid, each wave's 256-node run
+            // split z ways so that the grid covers the resident slots twice (a 70-row distinct batch of config 3:
+            // 98 tiles × 2 pod blocks would otherwise be 196 workgroups for 768 slots)
+            const bool queued = (e->forms & KG_FORM_NUMA_QUEUED) || topk || n_items >= 4 * e->numa_resident_wgs;
+            if (queued && n_items < INT32_MAX) {
+                HIP_TRY(e, hipMemsetAsync(e->numa_queue, 0, sizeof(int32_t), e->stream));
+                const int64_t wgs = std::min<int64_t>(combine ? e->numa_resident_wgs_c : e->numa_resident_wgs, (n_items + 3) / 4);
+                if (combine)
+                    hipLaunchKernelGGL(k_eval_numa2<true>, dim3((unsigned)wgs), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                                       e->pods + pod_begin, e->pl.rows, (unsigned long long *)mask, scores, numa_scores,
+                                       partials, perm, bm, e->numa_queue, (int32_t)n_items, seg);
+                else
+                    hipLaunchKernelGGL(k_eval_numa2<false>, dim3((unsigned)wgs), dim3(256), 0, e->stream, e->consts, e->pl, a,
+                                       e->pods + pod_begin, e->pl.rows, (unsigned long long *)mask, scores, numa_scores,
+                                       partials, perm, bm, e->numa_queue, (int32_t)n_items, seg);
+            } else {
+                const int64_t blocks = shard_tiles * ((n + 63) / 64);
+                unsigned z = 1;
+                while (z < KG_NUMA2_NODES / 32 && blocks * z < 2 * e->numa_resident_wgs) z *= 2;
+                dim3 grid((unsigned)shard_tiles, (unsigned)((n + 63) / 64), z);
+                if (combine)
+                    hipLaunchKernelGGL(k_eval_numa2<true>, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
+                                       e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials, perm, bm,
+                                       (int32_t *)nullptr, 0, 0);
+                else
+                    hipLaunchKernelGGL(k_eval_numa2<false>, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
+                                       e->pl.rows, (unsigned long long *)mask, scores, numa_scores, partials, perm, bm,
+                                       (int32_t *)nullptr, 0, 0);
+            }
+        }
+        HIP_TRY(e, hipGetLastError());
+        // cpusets on NUMA-policy nodes: patched in after the hot kernel (matrix planes, or the one-key-per-tile
+        // partials of a large placement chunk)
+        if ((!topk || e->consts.numa_bz) && e->n_numa_policy_nodes > 0 && (e->batch_bind || e->n_node_bind_nodes > 0)) {
+            const int64_t width = e->shard_end - e->shard_begin;
+            dim3 grid((unsigned)((width + 255) / 256), (unsigned)(n < 65535 ? n : 65535));
+            hipLaunchKernelGGL(k_numa_bind_fix, grid, dim3(256), 0, e->stream, e->consts, e->pl, a, e->pods + pod_begin,
+                               (unsigned long long *)mask, scores, numa_scores, partials);
+            HIP_TRY(e, hipGetLastError());
+        }
+        if (e->profiling) HIP_TRY(e, prof_end(e));
+        return KG_OK;
+    }
+    return launch_eval_plain(e, now_ns, pod_begin, n, mask, scores, partials, use_cls, topk, a, shard_tiles);
 }
 
 #define KG_RSV_POD_CHUNK 1024   // pods per reservation-entry pass (E/O hold [chunk][n_rn])
@@ -3819,6 +3895,7 @@ void kg_engine_destroy(kg_engine *e) {
     if (e->plane_mem) (void)hipFree(e->plane_mem);
     if (e->pods) (void)hipFree(e->pods);
     if (e->hot) (void)hipFree(e->hot);
+    if (e->eq_hot) (void)hipFree(e->eq_hot);
     if (e->scratch) (void)hipFree(e->scratch);
     if (e->cls_mem) (void)hipFree(e->cls_mem);
     if (e->rsv_mem) (void)hipFree(e->rsv_mem);
@@ -4199,6 +4276,15 @@ kg_status kg_pods_set(kg_engine *e, const kg_pod_row *rows, int32_t n) {
             for (int32_t k = 0; k < u; k++) udev[(size_t)k] = dev[(size_t)reps[(size_t)k]];
             HIP_TRY(e, h2d(e, e->eq_pods, udev.data(), sizeof(kg_pod_dev) * (size_t)u, e->stream));
             HIP_TRY(e, h2d(e, e->eq_of, of.data(), sizeof(int32_t) * (size_t)n, e->stream));
+            {   // the distinct rows' hot rows (the batch's slot map) for the Fit + LoadAware pass over them
+                const size_t hs = hot.size() / (size_t)n;
+                std::vector<char> uh(hs * (size_t)u);
+                for (int32_t k = 0; k < u; k++) memcpy(uh.data() + hs * (size_t)k, hot.data() + hs * (size_t)reps[(size_t)k], hs);
+                if (e->eq_hot) HIP_TRY(e, hipFree(e->eq_hot));
+                e->eq_hot = nullptr;
+                HIP_TRY(e, hipMalloc(&e->eq_hot, uh.size()));
+                HIP_TRY(e, h2d(e, e->eq_hot, uh.data(), uh.size(), e->stream));
+            }
             e->eq_perm_on = (e->cfg.enabled_plugins & KG_PLUGIN_NUMA) && u > 64;
             if (e->eq_perm_on) {
                 const std::vector<int32_t> order = numa_order(reps);
@@ -4379,14 +4465,18 @@ kg_status eval_eq(kg_engine *e, int64_t now_ns, const kg_eval_out *out) {
     // the distinct batch in place of the batch for the inner call (restored on every path)
     const kg_counters ctr0 = e->ctr;
     std::swap(e->pods, e->eq_pods);
+    std::swap(e->hot, e->eq_hot);
     std::swap(e->numa_perm, e->eq_perm);
     std::swap(e->numa_perm_on, e->eq_perm_on);
     e->n_pods = U;
     e->eq_on = false;
+    e->reps_in = true;
     kg_status st = kg_eval(e, now_ns, &cout);
+    e->reps_in = false;
     e->eq_on = true;
     e->n_pods = P;
     std::swap(e->pods, e->eq_pods);
+    std::swap(e->hot, e->eq_hot);
     std::swap(e->numa_perm, e->eq_perm);
     std::swap(e->numa_perm_on, e->eq_perm_on);
     e->ctr = ctr0;   // counted as the whole batch below
@@ -4597,7 +4687,7 @@ kg_status kg_set_forms(kg_engine *e, uint32_t forms) {
     kg_status st = check_engine(e);
     if (st) return st;
     if (forms & ~(KG_FORM_PLACE_PIPELINE | KG_FORM_PLACE_SEQUENTIAL | KG_FORM_NUMA_QUEUED | KG_FORM_NUMA_CHUNK_TILE |
-                  KG_FORM_NUMA_NO_CACHE))
+                  KG_FORM_NUMA_NO_CACHE | KG_FORM_NUMA_FUSED))
         return set_err(e, KG_ERR_INVALID_ARG, "unknown kernel form bits 0x%x", forms);
     if ((forms & KG_FORM_PLACE_PIPELINE) && (forms & KG_FORM_PLACE_SEQUENTIAL))
         return set_err(e, KG_ERR_INVALID_ARG, "pipelined and sequential placement together");
@@ -4684,12 +4774,16 @@ kg_status ncache_build(kg_engine *e, int64_t now_ns) {
     const kg_counters ctr0 = e->ctr;
     const int32_t P = e->n_pods;
     std::swap(e->pods, e->eq_pods);
+    std::swap(e->hot, e->eq_hot);
     std::swap(e->numa_perm, e->eq_perm);
     std::swap(e->numa_perm_on, e->eq_perm_on);
     e->n_pods = U;
+    e->reps_in = true;
     kg_status st = launch_eval(e, now_ns, 0, U, (uint64_t *)mask, scores, part, false, numa);
+    e->reps_in = false;
     e->n_pods = P;
     std::swap(e->pods, e->eq_pods);
+    std::swap(e->hot, e->eq_hot);
     std::swap(e->numa_perm, e->eq_perm);
     std::swap(e->numa_perm_on, e->eq_perm_on);
     e->ctr = ctr0;

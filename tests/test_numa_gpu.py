@@ -138,6 +138,17 @@ def test_matrix_numa_queued_form(pods, begin, end):
                    forms=nat.FORM_NUMA_QUEUED)
 
 
+@pytest.mark.parametrize("forms", [nat.FORM_NUMA_FUSED, nat.FORM_NUMA_FUSED | nat.FORM_NUMA_QUEUED, 0])
+@pytest.mark.parametrize("pods,begin,end,dup", [(97, 0, None, False), (333, 1024, 2500, False), (700, 0, None, True)])
+def test_matrix_numa_fused_and_combined(forms, pods, begin, end, dup):
+    """The two matrix forms of NodeNUMAResource: Fit + LoadAware inside k_eval_numa2 (KG_FORM_NUMA_FUSED), and the
+    default for launches with planes — the class / slot kernels' Fit + LoadAware pass, then k_eval_numa2 adding the
+    NodeNUMAResource term to those planes (also over the distinct rows of an equivalent-pod batch, `dup`)."""
+    cl = make_numa_edge_cluster(2_500, 120 if dup else pods, seed=61 + pods)
+    idx = np.random.default_rng(61).integers(0, 120, pods) if dup else None
+    _check_matrix3(numa_config(), cl, pods, begin=begin, end=end, idx=idx, forms=forms)
+
+
 @pytest.mark.parametrize("case", SCORE["cases"], ids=lambda c: c["name"])
 def test_kat_numa_node_score(case):
     """TestNUMANodeScore (nodenumaresource/scoring_test.go) through kg_eval."""
