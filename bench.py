@@ -175,7 +175,8 @@ def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
     out = {"workload": f"config3: {P} pods x {N} nodes, 4/6/8 NUMA zones, policy mix 40% SingleNUMANode / 30% "
                        "Restricted / 30% None, 60% LS / 40% batch pods, shipped profile + NodeNUMAResource",
            "evals_per_s": round(P * N / ((t1 - t0) / steps), 1), "ms_per_step": round((t1 - t0) / steps * 1e3, 3),
-           "kernel": "k_eval_numa2", "kernel_ms": round(k_ms, 3), "feasible_frac_sample": round(feasible, 4),
+           "kernel": "Fit + LoadAware pass (slot kernels) + k_eval_numa2<COMBINE> over the distinct rows (kernel_ms; the k_eq_rows copies are in ms_per_step)",
+           "kernel_ms": round(k_ms, 3), "feasible_frac_sample": round(feasible, 4),
            "placement": {"pods": P, "seconds": round(tp1 - tp0, 4), "pods_placed_per_s": round(P / (tp1 - tp0), 1),
                          "placed": int((nodes >= 0).sum())}}
     del mask, scores, numa
@@ -206,7 +207,7 @@ def bench_config3(args, engine, synth, shipped_profile, dev, stream, cpu_model):
                         "kernel_ms": round(kl, 3)}
     if args.c3_distinct_pods > 0:
         # the same config-3 nodes with pairwise distinct pod rows (continuous cpu / memory requests): no pod
-        # equivalence, every (pod, node) pair through k_eval_numa2's hint enumeration
+        # equivalence: the class kernels' Fit + LoadAware pass, then k_eval_numa2<COMBINE> on every (pod, node) pair
         PD = args.c3_distinct_pods
         cl_d = synth.make_numa_cluster(N, PD, seed=3, distinct_pods=True)
         prow_d = engine.build_pod_rows(cfg, cl_d, np.arange(PD))

@@ -3572,8 +3572,9 @@ kg_status slow_refresh(kg_engine *e) {
 // kernel writes one key per (pod, tile), slot 0 of a dense [n][tiles] layout — see partial_slots)
 // Fit + LoadAware over the launch's pods (every form but NodeNUMAResource's): the LAX / exact forms for LoadAware
 // weights beyond cpu / memory, the class kernels, the slot kernels, then the slow-node fix-up
+// `prof`: its own profiled interval (false inside the NodeNUMAResource launch's, which covers both passes)
 kg_status launch_eval_plain(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n, uint64_t *mask, uint16_t *scores,
-                            uint32_t *partials, bool use_cls, bool topk, HotArgs a, int64_t shard_tiles) {
+                            uint32_t *partials, bool use_cls, bool topk, HotArgs a, int64_t shard_tiles, bool prof = true) {
     if (e->consts.la_extra && !topk && e->lax_ok) {
         // LoadAware weights beyond cpu / memory, at most KG_LAX of them: k_eval2's LAX form reads their planes too;
         // the nodes outside the fp64 bounds of any plane (KGD_XSLOW) are re-evaluated exactly after it
@@ -3583,7 +3584,7 @@ kg_status launch_eval_plain(kg_engine *e, int64_t now_ns, int32_t pod_begin, int
             a.lax_w[k] = k < e->lax_n ? (uint32_t)e->consts.la_wx[e->lax_x[k]] : 0u;
         }
         a.lax_est = e->hot_lax + (int64_t)pod_begin * KG_LAX;
-        if (e->profiling) HIP_TRY(e, prof_begin(e));
+        if (prof && e->profiling) HIP_TRY(e, prof_begin(e));
         dim3 grid((unsigned)shard_tiles, (unsigned)((n + a.pods_per_block - 1) / a.pods_per_block));
         const bool prod = e->la_prod;
 #define KG_LAX_LAUNCH(S_)                                                                                               \
@@ -3607,7 +3608,7 @@ kg_status launch_eval_plain(kg_engine *e, int64_t now_ns, int32_t pod_begin, int
         else KG_LAX_LAUNCH(8);
 #undef KG_LAX_LAUNCH
         HIP_TRY(e, hipGetLastError());
-        if (e->profiling) HIP_TRY(e, prof_end(e));
+        if (prof && e->profiling) HIP_TRY(e, prof_end(e));
         HIP_TRY(e, hipMemsetAsync(e->xslow_count, 0, sizeof(int32_t), e->stream));
         if (e->n_nodes > 0)
             hipLaunchKernelGGL(k_slow_list, dim3((unsigned)((e->n_nodes + 255) / 256)), dim3(256), 0, e->stream, e->pl.dflags,
@@ -3620,14 +3621,14 @@ kg_status launch_eval_plain(kg_engine *e, int64_t now_ns, int32_t pod_begin, int
         return KG_OK;
     }
     if (e->consts.la_extra && !topk) {   // every node is on the exact path: no fast kernel, no slow list
-        if (e->profiling) HIP_TRY(e, prof_begin(e));
+        if (prof && e->profiling) HIP_TRY(e, prof_begin(e));
         const int64_t width = e->shard_end - e->shard_begin;
         dim3 grid((unsigned)((width + 255) / 256), (unsigned)(n < 65535 ? n : 65535));
         hipLaunchKernelGGL(k_eval_exact, grid, dim3(256), 0, e->stream, e->consts, e->pl, e->pods + pod_begin, n,
                            e->shard_begin, e->shard_end, a.mask_words, a.score_stride, a.tiles_total, now_ns,
                            (unsigned long long *)mask, scores, partials);
         HIP_TRY(e, hipGetLastError());
-        if (e->profiling) HIP_TRY(e, prof_end(e));
+        if (prof && e->profiling) HIP_TRY(e, prof_end(e));
         return KG_OK;
     }
     use_cls = use_cls && e->cls_ok && !e->reps_in && pod_begin == 0 && n == e->n_pods;
@@ -3636,13 +3637,13 @@ kg_status launch_eval_plain(kg_engine *e, int64_t now_ns, int32_t pod_begin, int
         if (st) return st;
     }
     dim3 grid((unsigned)shard_tiles, use_cls ? (unsigned)e->cls_nwork : (unsigned)((n + a.pods_per_block - 1) / a.pods_per_block));
-    if (e->profiling) HIP_TRY(e, prof_begin(e));
+    if (prof && e->profiling) HIP_TRY(e, prof_begin(e));
     if (use_cls) launch_cls(e, grid, a, mask, scores, partials);
     else if (e->nslot == 2) launch_hot<2>(e, grid, a, pod_begin, mask, scores, partials, topk);
     else if (e->nslot == 4) launch_hot<4>(e, grid, a, pod_begin, mask, scores, partials, topk);
     else launch_hot<8>(e, grid, a, pod_begin, mask, scores, partials, topk);
     HIP_TRY(e, hipGetLastError());
-    if (e->profiling) HIP_TRY(e, prof_end(e));
+    if (prof && e->profiling) HIP_TRY(e, prof_end(e));
     // exact re-evaluation of the (rare) nodes outside the fp64 fast-path bounds; a placement chunk
     // leaves them to the resolve, which re-scores the slow-node list itself
     kg_status st = slow_refresh(e);
@@ -3699,17 +3700,17 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
         // carries no node planes and no Fit / LoadAware pair code
         const bool combine = mask && scores && partials && !topk && !(e->forms & KG_FORM_NUMA_FUSED) &&
                              !(e->reps_in && (e->consts.la_extra || !e->eq_hot));
+        if (e->profiling) HIP_TRY(e, prof_begin(e));   // one profiled interval for both passes
         if (combine) {
-            kg_status st = launch_eval_plain(e, now_ns, pod_begin, n, mask, scores, partials, use_cls, false, a, shard_tiles);
+            kg_status st = launch_eval_plain(e, now_ns, pod_begin, n, mask, scores, partials, use_cls, false, a, shard_tiles,
+                                             false);
             if (st) return st;
             HIP_TRY(e, hipMemsetAsync(partials, 0, (size_t)n * (size_t)a.tiles_total * 4, e->stream));
         }
-        if (e->profiling) HIP_TRY(e, prof_begin(e));
         {  // pod per lane; queued 32-node items when they fill every resident wave slot several times over,
            // else a grid where a single pod block splits each wave's node run 4 ways
             // segment: 32 nodes (half mask words); 8 for a placement chunk's keys-only launch
             const int32_t seg = mask == nullptr && scores == nullptr && numa_scores == nullptr ? KG_NUMA2_SEG_TOPK : KG_NUMA2_SEG;
-            const int64_t n_items = shard_tiles * (KG_TILE / seg) * ((n + 63) / 64);
             const int32_t *perm = e->numa_perm_on && pod_begin == 0 && n == e->n_pods ? e->numa_perm : nullptr;
             const BatchMasks bm = e->bm;
             if (e->numa_resident_wgs == 0) {
@@ -3725,6 +3726,7 @@ kg_status launch_eval(kg_engine *e, int64_t now_ns, int32_t pod_begin, int32_t n
             // queued when the items give every resident wave one at least; else the grid, each wave's 256-node run
             // split z ways so that the grid covers the resident slots twice (a 70-row distinct batch of config 3:
             // 98 tiles × 2 pod blocks would otherwise be 196 workgroups for 768 slots)
+            const int64_t n_items = shard_tiles * (KG_TILE / seg) * ((n + 63) / 64);
             const bool queued = (e->forms & KG_FORM_NUMA_QUEUED) || topk || n_items >= 4 * e->numa_resident_wgs;
             if (queued && n_items < INT32_MAX) {
                 HIP_TRY(e, hipMemsetAsync(e->numa_queue, 0, sizeof(int32_t), e->stream));

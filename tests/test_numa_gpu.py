@@ -138,7 +138,7 @@ def test_matrix_numa_queued_form(pods, begin, end):
                    forms=nat.FORM_NUMA_QUEUED)
 
 
-@pytest.mark.parametrize("forms", [nat.FORM_NUMA_FUSED, nat.FORM_NUMA_FUSED | nat.FORM_NUMA_QUEUED, 0])
+@pytest.mark.parametrize("forms", [nat.FORM_NUMA_FUSED, nat.FORM_NUMA_FUSED | nat.FORM_NUMA_QUEUED, 0, nat.FORM_NUMA_QUEUED])
 @pytest.mark.parametrize("pods,begin,end,dup", [(97, 0, None, False), (333, 1024, 2500, False), (700, 0, None, True)])
 def test_matrix_numa_fused_and_combined(forms, pods, begin, end, dup):
     """The two matrix forms of NodeNUMAResource: Fit + LoadAware inside k_eval_numa2 (KG_FORM_NUMA_FUSED), and the
