@@ -1124,6 +1124,20 @@ KG_HD bool kg_numa_one_pair(const kg_pod_dev &p, const int64_t mx[2]) {
            (!(p.numa_present & 2u) || p.numa_req[KG_RES_MEMORY] <= mx[1]);
 }
 
+// the three conditions for one pair on its own (the per-pair kernels: k_resolve's re-scores, the cache refresh, the
+// placement chunks), the largest zone totals taken from the row
+KG_HD bool kg_numa_one(const kg_node_row &row, const kg_pod_dev &p) {
+    if (!(row.flags & KG_NODE_NUMA_OPTIONS) || !kg_numa_one_node(row) || !kg_numa_one_pod(p)) return false;
+    int64_t mx[2] = {0, 0};
+    for (int i = 0; i < KG_MAX_ZONES; i++) {
+        if (i >= row.n_zones) break;
+        const int64_t t0 = kg_zone_total(row, i, 0), t1 = kg_zone_total(row, i, 1);
+        mx[0] = t0 > mx[0] ? t0 : mx[0];
+        mx[1] = t1 > mx[1] ? t1 : mx[1];
+    }
+    return kg_numa_one_pair(p, mx);
+}
+
 template <class ZS>
 KG_HD void kg_numa_zoned_one(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                              const ZS &zs, const int64_t *requested, int64_t pcpu) {
@@ -1228,8 +1242,9 @@ inline
 #endif
 uint64_t kg_numa_eval_any(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p) {
     kg_numa_out o;
-    if (c.numa_bz) kg_numa_pair_z<kg_zone_calc, true, false>(c, row, p, o, kg_zone_calc{row});
-    else kg_numa_pair_z<kg_zone_calc, false, false>(c, row, p, o, kg_zone_calc{row});
+    const bool one = kg_numa_one(row, p);
+    if (c.numa_bz) kg_numa_pair_z<kg_zone_calc, true, false>(c, row, p, o, kg_zone_calc{row}, nullptr, false, one);
+    else kg_numa_pair_z<kg_zone_calc, false, false>(c, row, p, o, kg_zone_calc{row}, nullptr, false, one);
     return ((uint64_t)(o.feasible ? 1u : 0u) << 32) | o.score;
 }
 

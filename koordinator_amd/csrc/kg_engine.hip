@@ -1719,7 +1719,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KG_CHUNK_WP
         if (in_range && eval_pair(c, pl, lp, nr, node, a.now_ns, fit, la)) {
             kg_numa_out o;
             const kg_node_row &row = pl.rows[node];
-            kg_numa_pair_z<kg_zone_calc, BZ, false>(c, row, lp, o, kg_zone_calc{row});
+            kg_numa_pair_z<kg_zone_calc, BZ, false>(c, row, lp, o, kg_zone_calc{row}, nullptr, false, kg_numa_one(row, lp));
             if (o.feasible)
                 key = ((total_of(c, fit, la, o.score) + 1u) << KG_TILE_SHIFT) | (uint32_t)(KG_TILE - 1 - local);
         }
@@ -1775,7 +1775,7 @@ __global__ __launch_bounds__(64) void k_ncache_refresh(kg_consts c, kg_planes pl
     uint32_t fit, la;
     bool ok = eval_pair(c, pl, lpd, nr, node, now_ns, fit, la);
     kg_numa_out o;
-    kg_numa_pair_z<kg_zone_calc, false, false>(c, lrow, lpd, o, kg_zone_calc{lrow});
+    kg_numa_pair_z<kg_zone_calc, false, false>(c, lrow, lpd, o, kg_zone_calc{lrow}, nullptr, false, kg_numa_one(lrow, lpd));
     ok = ok && o.feasible;
     if (tid == 0) cache[(int64_t)u * stride + (node - col_begin)] = ok ? (uint8_t)o.score : (uint8_t)KG_NCACHE_NO;
 }
@@ -2317,7 +2317,7 @@ __global__ __launch_bounds__(64) void k_prev_keys(kg_consts c, kg_planes pl, con
         if (eval_pair(c, pl, lpd, nr, node, now_ns, fit, la)) {
             // inlined (kg_numa_eval_any is a call: its frame in scratch); placement pipelines carry no cpuset binds
             kg_numa_out o;
-            kg_numa_pair_z<kg_zone_calc, false, false>(c, lrow, lpd, o, kg_zone_calc{lrow});
+            kg_numa_pair_z<kg_zone_calc, false, false>(c, lrow, lpd, o, kg_zone_calc{lrow}, nullptr, false, kg_numa_one(lrow, lpd));
             if (o.feasible)
                 key = ((unsigned long long)(total_of(c, fit, la, o.score) + 1u) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
         }
