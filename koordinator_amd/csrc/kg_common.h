@@ -781,7 +781,7 @@ struct kg_zone_trim {
 template <class ZS, bool REC = true>
 KG_HD void kg_numa_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                          const ZS &zs, const int64_t *requested, int policy, int64_t pcpu, const kg_numa_bind *bd);
-template <class ZS>
+template <class ZS, bool REC = false>
 KG_HD void kg_numa_zoned_one(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                              const ZS &zs, const int64_t *requested, int64_t pcpu);
 
@@ -806,8 +806,8 @@ void kg_numa_bind_zoned(const kg_consts &c, const kg_node_row &row, const kg_pod
 // and leave those pairs infeasible for the fix-up kernel, so they carry no call into the cpuset path.
 // REC: record the allocation (o.zone / o.alloc, what Reserve needs); Filter / Score callers pass false and
 // get o.feasible, o.score and o.n_alloc only (no per-lane arrays written at a run-time index)
-// `one` (Filter / Score callers, REC false): the pair meets kg_numa_one_node and kg_numa_one_pair, so the zoned part
-// takes kg_numa_zoned_one (the single-zone hints only) instead of the whole enumeration
+// `one`: the pair meets kg_numa_one_node, kg_numa_one_pod and kg_numa_one_pair, so the zoned part takes
+// kg_numa_zoned_one (the single-zone hints only, recording the allocation when REC) instead of the whole enumeration
 template <class ZS, bool BZ = true, bool REC = true>
 KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                           const ZS &zs, const int64_t *requested = nullptr, bool reserve = false, bool one = false) {
@@ -889,7 +889,7 @@ KG_HD void kg_numa_pair_z(const kg_consts &c, const kg_node_row &row, const kg_p
         else o.feasible = false;   // the caller re-evaluates these pairs (k_numa_bind_fix)
         return;
     }
-    if (!REC && one) kg_numa_zoned_one(c, row, p, o, zs, requested, pcpu);
+    if (one) kg_numa_zoned_one<ZS, REC>(c, row, p, o, zs, requested, pcpu);
     else kg_numa_zoned<ZS, REC>(c, row, p, o, zs, requested, policy, pcpu, (const kg_numa_bind *)nullptr);
 }
 
@@ -1138,7 +1138,7 @@ KG_HD bool kg_numa_one(const kg_node_row &row, const kg_pod_dev &p) {
     return kg_numa_one_pair(p, mx);
 }
 
-template <class ZS>
+template <class ZS, bool REC>
 KG_HD void kg_numa_zoned_one(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                              const ZS &zs, const int64_t *requested, int64_t pcpu) {
     const int Z = row.n_zones;
@@ -1189,6 +1189,11 @@ KG_HD void kg_numa_zoned_one(const kg_consts &c, const kg_node_row &row, const k
         return;
     }
     if (got[0] != 0 || got[1] != 0) {
+        if constexpr (REC) {   // what Reserve records (kg_numa_apply)
+            o.zone[0] = bi;
+            o.alloc[0][0] = got[0];
+            o.alloc[0][1] = got[1];
+        }
         o.n_alloc = 1;
         int64_t z_tot[2], z_used[2];
         for (int r = 0; r < 2; r++) {
@@ -1212,7 +1217,7 @@ inline
 void kg_numa_pair(const kg_consts &c, const kg_node_row &row, const kg_pod_dev &p, kg_numa_out &o,
                   const int64_t *requested = nullptr, bool reserve = false) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    kg_numa_pair_z<kg_zone_calc, false>(c, row, p, o, kg_zone_calc{row}, requested, reserve);
+    kg_numa_pair_z<kg_zone_calc, false>(c, row, p, o, kg_zone_calc{row}, requested, reserve, kg_numa_one(row, p));
 #else
     kg_numa_pair_z(c, row, p, o, kg_zone_calc{row}, requested, reserve);
 #endif
@@ -1324,7 +1329,7 @@ void kg_numa_commit_tab(const kg_consts &c, kg_node_row &row, const kg_pod_dev &
         return;
     }
     kg_numa_out o;
-    kg_numa_pair_z<kg_zone_tab, false, true>(c, row, p, o, kg_zone_tab{zt}, nullptr, true);
+    kg_numa_pair_z<kg_zone_tab, false, true>(c, row, p, o, kg_zone_tab{zt}, nullptr, true, kg_numa_one(row, p));
     kg_numa_apply(row, o);
 }
 
