@@ -1385,12 +1385,13 @@ KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_
             int64_t base = r < 2 ? nz[r] : r < KG_FAST_RES ? rq[r] : requested[r];
             int64_t req = base + p.fit_pr_i[r];
             int64_t q;
-            if (c.fit_most) q = (req > a ? a : req) * 100 / a;
-            else q = req > a ? 0 : (a - req) * 100 / a;
+            // kg_qdiv: the exact quotient by one fp64 division on the device (a software int64 division otherwise)
+            if (c.fit_most) q = kg_qdiv((req > a ? a : req) * 100, a);
+            else q = req > a ? 0 : kg_qdiv((a - req) * 100, a);
             s += q * c.fit_w[r];
             w += c.fit_w[r];
         }
-        fit = w ? (uint32_t)(s / w) : 0;
+        fit = w ? (uint32_t)kg_qdiv(s, w) : 0;
     }
     if ((c.plugins & KG_PLUGIN_LOADAWARE) && kg_la_valid(c, df, expired)) {
         int64_t s = 0;
@@ -1398,7 +1399,7 @@ KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_
             if (c.la_w[r] == 0) continue;
             int64_t a = la_a[r];
             int64_t req = p.la_est_i[r] + la_u[r];
-            int64_t q = (a == 0 || req > a) ? 0 : (a - req) * 100 / a;
+            int64_t q = (a == 0 || req > a) ? 0 : kg_qdiv((a - req) * 100, a);
             s += q * c.la_w[r];
         }
         if (c.la_extra) {
@@ -1409,7 +1410,7 @@ KG_HD void kg_pair_view(const kg_consts &c, const kg_node_row &row, const int64_
                 s += ((a == 0 || req > a) ? 0 : kg_qdiv((a - req) * 100, a)) * c.la_wx[r];
             }
         }
-        la = c.la_wsum ? (uint32_t)(s / c.la_wsum) : 0;
+        la = c.la_wsum ? (uint32_t)kg_qdiv(s, c.la_wsum) : 0;
     }
 }
 
@@ -1578,9 +1579,9 @@ KG_HD uint32_t kg_rsv_score(const kg_reservation &r, const kg_pod_dev &p) {
         const int64_t cap = r.allocatable.v[q];
         const int64_t req = (((p.numa_present >> q) & 1u) ? p.numa_req[q] : 0) + kg_rl_get(r.allocated, q);
         const int64_t m = q == KG_RES_CPU ? 1 : 1000;  // Quantity.MilliValue of the stored unit
-        if (req <= cap) s += 100 * (req * m) / (cap * m);
+        if (req <= cap) s += kg_qdiv(100 * (req * m), cap * m);
     }
-    return w <= 0 ? 0u : (uint32_t)(s / w);
+    return w <= 0 ? 0u : (uint32_t)kg_qdiv(s, w);
 }
 
 // NominateReservation (nominator.go:76-135): slot index or −1
