@@ -1970,7 +1970,7 @@ __device__ unsigned long long rsv_best_block(const kg_consts &c, const unsigned 
             uint32_t sn = 0;
             if (e[u]) {
                 const unsigned long long raw = k == pref ? 1000ull : ((e[u] >> 16) & 0xFFFFull);
-                sn = mx ? (uint32_t)(100ull * raw / mx) : 0u;
+                sn = mx ? 100u * (uint32_t)raw / (uint32_t)mx : 0u;   // (raw ≤ 0xFFFF, mx ≤ 0xFFFF: a 32-bit quotient)
                 const unsigned long long total = (e[u] >> 32) - 1ull + (unsigned long long)c.weight_rsv * sn;
                 const unsigned long long key = ((total + 1ull) << 32) | (0xFFFFFFFFull - (unsigned long long)node);
                 best = best > key ? best : key;
@@ -2115,7 +2115,7 @@ __device__ unsigned long long rsv_best_resolve(const kg_consts &c, const kg_plan
         get(q, k, node, e, o);
         if (!e) continue;
         const unsigned long long raw = k == pref ? 1000ull : ((e >> 16) & 0xFFFFull);
-        const uint32_t sn = mx ? (uint32_t)(100ull * raw / mx) : 0u;
+        const uint32_t sn = mx ? 100u * (uint32_t)raw / (uint32_t)mx : 0u;   // (raw ≤ 0xFFFF, mx ≤ 0xFFFF: a 32-bit quotient)
         const unsigned long long total = (e >> 32) - 1ull + (unsigned long long)c.weight_rsv * sn;
         const unsigned long long key = ((total + 1ull) << 32) | (0xFFFFFFFFull - (unsigned long long)(uint32_t)node);
         best = best > key ? best : key;
